@@ -1,0 +1,194 @@
+/*
+ * posu.h — C ABI of libposeu.so, the MI355X (gfx950) kernels behind the
+ * pose-unsupervised hot path:
+ *
+ *   PoseResNet forward (ResNet-18..152 backbone + 3x ConvTranspose head)
+ *     -> heatmap soft-argmax / argmax decoding (+ crop affine back to image px)
+ *     -> epipolar (fundamental-matrix) consistency loss
+ *     -> multi-view DLT triangulation.
+ *
+ * The reference (LouisNUST/pose-unsupervised) is pure Python/PyTorch; these
+ * entry points replace the framework ops its Python functions call.  Each
+ * declaration cites the reference interface it replaces (file:line relative to
+ * the reference repo root).
+ *
+ * Conventions (all entry points):
+ *   - Every tensor argument is a caller-owned DEVICE pointer (e.g. from
+ *     torch.Tensor.data_ptr()).  Shapes are explicit ints; layouts are stated.
+ *   - `stream` is a hipStream_t passed as void* (PyTorch's current stream).
+ *     Calls only enqueue work; none synchronises, allocates or frees, so every
+ *     call is hipGraph-capturable.
+ *   - Return value: 0 (POSU_OK) or a POSU_ERR_* code; posu_last_error() then
+ *     returns a thread-local message.
+ *   - dtype codes: POSU_F32 (fp32 operands, exact-f32 MFMA, the parity mode)
+ *                  POSU_BF16 (bf16 operands, f32 accumulate, the fast mode).
+ */
+#ifndef POSU_H_
+#define POSU_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POSU_OK 0
+#define POSU_ERR_ARG 1          /* invalid shape / pointer / unsupported config */
+#define POSU_ERR_HIP 2          /* a HIP launch failed */
+
+#define POSU_F32 0
+#define POSU_BF16 1
+#define POSU_F64 2
+
+/* ---------------------------------------------------------------- runtime */
+const char* posu_last_error(void);
+int posu_abi_version(void);
+
+/* ------------------------------------------------------------ input prep */
+/* NCHW fp32 image batch -> NHWC activations with Cpad (>= C) channels,
+ * zero-filled above C.  Replaces the implicit layout of the first
+ * nn.Conv2d call in PoseResNet.forward (lib/models/pose_resnet.py:192).
+ * x: [N, C, H, W] f32.  y: [N, H, W, Cpad] of `dtype`. */
+int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W,
+                           void* y, int Cpad, void* stream);
+
+/* NHWC activations -> NCHW fp32 (for returning x1 / f in the reference
+ * layout: lib/models/pose_resnet.py:205). */
+int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
+                          float* y, void* stream);
+
+/* ---------------------------------------------------------- convolutions */
+/* Implicit-GEMM convolution on MFMA (NHWC), fused eval-mode BatchNorm
+ * (per-channel scale/shift), optional residual add and ReLU:
+ *     y = act( conv(x, w) * scale[co] + shift[co] + residual )
+ * Replaces nn.Conv2d + nn.BatchNorm2d (+ `out += residual`) + nn.ReLU in
+ * Bottleneck.forward / BasicBlock.forward (lib/models/pose_resnet.py:42-58,
+ * 79-99), the stem (pose_resnet.py:192-194) and the downsample branch
+ * (pose_resnet.py:136-141).
+ *   x: [N, H, W, C] dtype, C % 8 == 0.
+ *   w: packed [CoutPad][Kpad] dtype, k = (kh*KW + kw)*C + ci, zero padded;
+ *      CoutPad = round_up(Cout, 64), Kpad = round_up(KH*KW*C, posu_conv_bk(dtype)).
+ *   scale/shift: [Cout] f32 (may be NULL: scale 1, shift 0).
+ *   residual: NULL or [N, Ho, Wo, Cout] dtype.
+ *   y: [N, Ho, Wo, Cout] dtype. */
+int posu_conv_bk(int dtype);
+int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                    const void* w, int Cout, int KH, int KW, int stride, int pad,
+                    const float* scale, const float* shift, const void* residual,
+                    int relu, void* y, int Ho, int Wo, void* stream);
+
+/* ConvTranspose2d(kernel 4, stride 2, padding 1, output_padding 0) as four
+ * stride-1 2x2 sub-pixel convolutions (one per output parity class) in one
+ * launch, + fused BN + ReLU.  Replaces _make_deconv_layer's
+ * ConvTranspose2d/BatchNorm2d/ReLU triples (lib/models/pose_resnet.py:164-189).
+ *   x: [N, H, W, C] dtype.
+ *   w: packed [4 classes][CoutPad][Kpad] dtype (see posu_pack_deconv4x4 in
+ *      the Python layer), class = py*2 + px, k = (ty*2 + tx)*C + ci.
+ *   y: [N, 2H, 2W, Cout] dtype. */
+int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                         const void* w, int Cout, const float* scale,
+                         const float* shift, int relu, void* y, void* stream);
+
+/* 1x1 convolution (+bias) writing NCHW fp32 heatmaps: PoseResNet.final_layer
+ * (lib/models/pose_resnet.py:126-132, 203).
+ *   x: [N, H, W, C] dtype; w: packed [CoutPad][Kpad]; bias: [Cout] f32;
+ *   y: [N, Cout, H, W] f32. */
+int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                          const void* w, int Cout, const float* bias, float* y,
+                          void* stream);
+
+/* MaxPool2d(3, stride 2, padding 1) on NHWC (lib/models/pose_resnet.py:113,195).
+ * y: [N, Ho, Wo, C], Ho = (H - 1) / 2 + 1. */
+int posu_maxpool3x3s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                          void* y, void* stream);
+
+/* ---------------------------------------------------- heatmap -> coords */
+/* Soft-argmax (generate_integral_preds_2d_th, lib/utils/transforms.py:149-171):
+ *   p = softmax(beta * h) over H*W (beta = 100 in the reference),
+ *   x = sum p * col, y = sum p * row,
+ * optionally followed by the per-sample crop affine of transform_back_th
+ * (lib/utils/transforms.py:174-198): [x, y, 1] @ T^T.
+ *   hm: [N, J, H, W] f32 contiguous; affine: NULL or [N, 2, 3] f32;
+ *   out: [N, J, 2] f32.  stats: NULL or [N, J, 4] f32 = (max of beta*h,
+ *   sum of exp, x, y in heatmap px) kept for the backward pass. */
+int posu_softargmax2d_fwd(const float* hm, int N, int J, int H, int W, float beta,
+                          const float* affine, float* out, float* stats, void* stream);
+
+/* Gradient of posu_softargmax2d_fwd w.r.t. hm, given gout [N, J, 2]:
+ *   dh = beta * p * ((col - x) * gx' + (row - y) * gy'), g' = T_lin^T g.
+ * ghm: [N, J, H, W] f32 (overwritten). */
+int posu_softargmax2d_bwd(const float* hm, const float* stats, int N, int J, int H, int W,
+                          float beta, const float* affine, const float* gout, float* ghm,
+                          void* stream);
+
+/* Argmax decoding + quarter-pixel post-process + crop affine back
+ * (get_max_preds / get_final_preds, lib/core/inference.py:19-75).
+ *   First maximum wins (np.argmax); coords zeroed when maxval <= 0;
+ *   post_process != 0 applies the +-0.25 px shift (inference.py:57-66);
+ *   affine: NULL or [N, 2, 3] f64 (transform_preds, transforms.py:67-73, which
+ *   applies the cv2 float64 matrix in float64 before storing float32).
+ *   preds: [N, J, 2] f32; maxvals: [N, J] f32. */
+int posu_argmax2d_fwd(const float* hm, int N, int J, int H, int W, int post_process,
+                      const double* affine, float* preds, float* maxvals, void* stream);
+
+/* Per-sample 2-D affine of joint coordinates (transform_back_th's
+ * `[x, y, 1] @ T^T`, lib/utils/transforms.py:190-195):
+ *   transpose == 0: out = [x, y, 1] @ T^T            (forward)
+ *   transpose == 1: out = g @ T[:, :, 0:2]            (its gradient w.r.t. pts)
+ *   pts: [N, J, 2] f32; T: [N, 2, 3] f32; out: [N, J, 2] f32. */
+int posu_affine2d_apply(const float* pts, const float* T, int N, int J, int transpose,
+                        float* out, void* stream);
+
+/* Weighted heatmap MSE (JointsMSELoss.forward, lib/core/loss.py:70-86):
+ *   loss = sum_j mean_{n,p} (pred*w_nj - gt*w_nj)^2 = sum_{n,j,p} (w (pred-gt))^2 / (N*HW)
+ *   pred, gt: [N, J, HW] f32; w: NULL (use_target_weight False) or [N, J] f32;
+ *   ws: workspace [N*J] f32 (per-map partial sums, fixed-order final sum);
+ *   loss: [1] f32. */
+int posu_joints_mse_fwd(const float* pred, const float* gt, const float* w, int N, int J, int HW,
+                        float* ws, float* loss, void* stream);
+
+/* Gradient of posu_joints_mse_fwd w.r.t. pred given gloss [1] (device):
+ *   gpred = gloss * 2 w^2 (pred - gt) / (N*HW).  gpred: [N, J, HW] f32. */
+int posu_joints_mse_bwd(const float* pred, const float* gt, const float* w, int N, int J, int HW,
+                        const float* gloss, float* gpred, void* stream);
+
+/* ------------------------------------------------------------- geometry */
+/* Epipolar consistency loss (FundamentalLoss.__call__, lib/core/loss.py:101-133):
+ *   loss = sum_{b, (i,j) in permutations(V,2), k} |x~_j^T F_{s(b),i,j} x~_i| * w_i w_j
+ *          / (N * V*(V-1) * J)
+ *   x: [V, N, J, 2] f32 (image px); w: NULL or [V, N, J] f32 (target weights,
+ *   used when non-NULL, i.e. USE_TARGET_WEIGHT_FUND);
+ *   F: [S, V*(V-1), 3, 3] f32, pair index p enumerates itertools.permutations
+ *   order; subj: [N] int32 in [0, S).
+ *   loss: [1] f32 (written, not accumulated); resid: NULL or [N, P, J] f32. */
+int posu_epipolar_loss_fwd(const float* x, const float* w, const float* F,
+                           const int* subj, int V, int N, int J, int S,
+                           float* loss, float* resid, void* stream);
+
+/* d loss / d x given the scalar upstream gradient gloss [1] (device).
+ * gx: [V, N, J, 2] f32 (overwritten). */
+int posu_epipolar_loss_bwd(const float* x, const float* w, const float* F,
+                           const int* subj, int V, int N, int J, int S,
+                           const float* gloss, float* gx, void* stream);
+
+/* Multi-view linear triangulation (triangulate_poses / pymvg
+ * MultiCameraSystem.find3d, lib/multiviews/triangulate.py:43-99): per
+ * (group, joint), undistort each visible view's point with the OpenCV
+ * fixed-point model (5 iterations), build 2 DLT rows per view
+ * (x*M[2]-M[0], y*M[2]-M[1]) and take the right singular vector of the
+ * smallest singular value (one-sided Jacobi SVD, fp64).  Joints seen in < 2
+ * views give (0,0,0) (triangulate.py:95-96).
+ *   M:    [G, V, 3, 4] f64 projection matrices K[R | -R C];
+ *   intr: [G, V, 9] f64 = fx, fy, cx, cy, k1, k2, p1, p2, k3;
+ *   xy:   pixel coords in xy_dtype (POSU_F32 or POSU_F64); joint k of view v of
+ *         group g at xy[g*xy_stride_g + v*xy_stride_v + 2k] (elements):
+ *         [G, V, J, 2] -> (V*J*2, J*2); view-major [V, G, J, 2] -> (J*2, G*J*2);
+ *   vis:  NULL (all visible) or [G, V, J] uint8;
+ *   undistort: 0 = no_distortion cameras (distortion ignored);
+ *   X:    [G, J, 3] f64. */
+int posu_triangulate_dlt(const double* M, const double* intr, const void* xy, int xy_dtype,
+                         int xy_stride_g, int xy_stride_v, const unsigned char* vis, int G,
+                         int V, int J, int undistort, double* X, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POSU_H_ */

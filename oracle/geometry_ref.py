@@ -1,0 +1,215 @@
+"""CPU ORACLE (test infrastructure only): restatement of the reference's heatmap
+decoding, losses, camera model and triangulation.
+
+Sources (paths relative to the reference repo):
+  softargmax2d        lib/utils/transforms.py:149-171 (torch-CPU fp32, same op order)
+  crop affine         lib/utils/transforms.py:76-135 (+ cv2.getAffineTransform's 6x6 solve)
+  transform_back      lib/utils/transforms.py:174-198
+  get_max_preds       lib/core/inference.py:19-47
+  get_final_preds     lib/core/inference.py:50-75, transforms.py:67-73, 112-120
+  fundamental_loss    lib/core/loss.py:101-133
+  joints_mse          lib/core/loss.py:70-86
+  project_point_radial lib/multiviews/cameras.py:25-49
+  triangulate_poses   lib/multiviews/triangulate.py:17-99 with pymvg's
+                      CameraModel.undistort (OpenCV fixed point, 5 iterations) and
+                      MultiCameraSystem.find3d (DLT rows, numpy SVD) restated
+                      (pymvg is an unpinned, un-vendored dependency).
+"""
+import itertools
+import math
+
+import numpy as np
+import torch
+
+
+# ---------------------------------------------------------------- heatmaps
+def softargmax2d(hm):
+    """[N, J, h, w] f32 CPU tensor -> [N, J, 2] (x, y)."""
+    n, j, h, w = hm.shape
+    p = torch.softmax((hm * 100).view(n, j, -1), dim=-1).view(n, j, h, w)
+    accu_w = p.sum(dim=2)
+    accu_h = p.sum(dim=3)
+    xs = torch.sum(accu_w * torch.arange(w, dtype=torch.float32).view(1, 1, -1), dim=2)
+    ys = torch.sum(accu_h * torch.arange(h, dtype=torch.float32).view(1, 1, -1), dim=2)
+    return torch.stack([xs, ys], dim=2)
+
+
+def _solve_affine(src, dst):
+    a = np.zeros((6, 6))
+    b = np.zeros(6)
+    src = np.asarray(src, np.float32).astype(np.float64)
+    dst = np.asarray(dst, np.float32).astype(np.float64)
+    for i in range(3):
+        a[2 * i, :3] = [src[i, 0], src[i, 1], 1]
+        a[2 * i + 1, 3:] = [src[i, 0], src[i, 1], 1]
+        b[2 * i:2 * i + 2] = dst[i]
+    return np.linalg.solve(a, b).reshape(2, 3)
+
+
+def crop_affine(center, scale, output_size, inv=1):
+    scale = np.asarray(scale, dtype=np.float64) * 200.0
+    half = scale[0] * -0.5
+    src = np.zeros((3, 2), np.float32)
+    dst = np.zeros((3, 2), np.float32)
+    src[0] = center
+    src[1] = np.asarray(center) + np.array([0.0, half])  # rot = 0
+    dst[0] = [output_size[0] * 0.5, output_size[1] * 0.5]
+    dst[1] = np.array([output_size[0] * 0.5, output_size[1] * 0.5]) + np.array([0, output_size[0] * -0.5],
+                                                                                 np.float32)
+    for m in (src, dst):
+        d = m[0] - m[1]
+        m[2] = m[1] + np.array([-d[1], d[0]], np.float32)
+    return _solve_affine(dst, src) if inv else _solve_affine(src, dst)
+
+
+def transform_back(coords, centers, scales, hm_size):
+    """coords [N, J, 2] f32 tensor (heatmap px) -> image px (fp32 matrices, like the reference)."""
+    out = []
+    for i in range(coords.shape[0]):
+        T = torch.from_numpy(crop_affine(centers[i], scales[i], hm_size)).float()
+        p = torch.cat([coords[i], torch.ones(coords.shape[1], 1)], dim=1)
+        out.append(p @ T.t())
+    return torch.stack(out, 0)
+
+
+def get_max_preds(hm):
+    n, j, h, w = hm.shape
+    flat = hm.reshape(n, j, -1)
+    idx = np.argmax(flat, 2).reshape(n, j, 1)
+    maxvals = np.amax(flat, 2).reshape(n, j, 1)
+    preds = np.tile(idx, (1, 1, 2)).astype(np.float32)
+    preds[:, :, 0] = preds[:, :, 0] % w
+    preds[:, :, 1] = np.floor(preds[:, :, 1] / w)
+    preds *= np.tile(np.greater(maxvals, 0.0), (1, 1, 2)).astype(np.float32)
+    return preds, maxvals
+
+
+def get_final_preds(hm, centers, scales, post_process=True):
+    coords, maxvals = get_max_preds(hm)
+    h, w = hm.shape[2], hm.shape[3]
+    if post_process:
+        for n in range(coords.shape[0]):
+            for p in range(coords.shape[1]):
+                m = hm[n][p]
+                px = int(math.floor(coords[n][p][0] + 0.5))
+                py = int(math.floor(coords[n][p][1] + 0.5))
+                if 1 < px < w - 1 and 1 < py < h - 1:
+                    diff = np.array([m[py][px + 1] - m[py][px - 1], m[py + 1][px] - m[py - 1][px]])
+                    coords[n][p] += np.sign(diff) * .25
+    preds = coords.copy()
+    for i in range(coords.shape[0]):
+        T = crop_affine(centers[i], scales[i], [w, h])
+        pt = np.concatenate((coords[i][:, :2], np.ones((coords.shape[1], 1))), axis=-1)
+        preds[i][:, :2] = np.dot(pt, T.T)
+    return preds, maxvals
+
+
+# ------------------------------------------------------------------ losses
+def fundamental_loss(joints, weights, subjects, F_dict, use_target_weight=True):
+    """joints: V x [B, J, 2] f32 tensors; weights: V x [B, J, 1]; subjects [B]."""
+    nv = len(joints)
+    b, j = joints[0].shape[:2]
+    homo = [torch.cat([p, torch.ones(b, j, 1)], dim=2) for p in joints]
+    pairs = list(itertools.permutations(range(nv), 2))
+    loss = 0
+    for idx, s in enumerate(subjects):
+        for (pi, pj) in pairs:
+            Fm = torch.as_tensor(np.asarray(F_dict[(int(s), pi, pj)]), dtype=torch.float32)
+            r = torch.abs(torch.sum(torch.mm(homo[pj][idx], Fm) * homo[pi][idx], dim=1))
+            if use_target_weight:
+                r = r * torch.squeeze(weights[pj][idx] * weights[pi][idx])
+            loss = loss + r.sum()
+    return loss / (b * len(pairs) * j)
+
+
+def joints_mse(pred, gt, w=None):
+    n, j = pred.shape[:2]
+    hp = pred.reshape(n, j, -1)
+    hg = gt.reshape(n, j, -1)
+    loss = 0
+    for k in range(j):
+        a, c = hp[:, k], hg[:, k]
+        if w is not None:
+            a = a * w[:, k]
+            c = c * w[:, k]
+        loss = loss + torch.mean((a - c) ** 2)
+    return loss
+
+
+# ------------------------------------------------------------------ camera
+def project_point_radial(x, R, T, f, c, k, p):
+    xcam = R.dot(x.T - T)
+    y = xcam[:2] / xcam[2]
+    r2 = np.sum(y ** 2, axis=0)
+    k = np.asarray(k).reshape(-1)
+    p = np.asarray(p).reshape(-1)
+    radial = 1 + (k[0] * r2 + k[1] * r2 ** 2 + k[2] * r2 ** 3)
+    tan = p[0] * y[1] + p[1] * y[0]
+    y = y * np.tile(radial + tan, (2, 1)) + np.outer(np.array([p[1], p[0]]), r2)
+    return (f * y + np.asarray(c, np.float64).reshape(2, 1)).T
+
+
+def project_pose(x, cam):
+    f = 0.5 * (cam['fx'] + cam['fy'])
+    return project_point_radial(x, cam['R'], cam['T'], f, np.array([cam['cx'], cam['cy']]), cam['k'], cam['p'])
+
+
+# ------------------------------------------------------------- triangulate
+def _camera(cam, no_distortion):
+    f = [float(np.ravel(cam['fx'])[0]), float(np.ravel(cam['fy'])[0])]
+    c = [float(np.ravel(cam['cx'])[0]), float(np.ravel(cam['cy'])[0])]
+    K = np.array([[f[0], 0, c[0]], [0, f[1], c[1]], [0, 0, 1]], dtype=float)
+    R = np.asarray(cam['R'], float)
+    t = -np.matmul(R, np.asarray(cam['T'], float).reshape(3, 1))
+    M = K.dot(np.concatenate((R, t), axis=1))
+    k = np.ravel(cam['k'])
+    p = np.ravel(cam['p'])
+    D = np.zeros(5) if no_distortion else np.array([k[0], k[1], p[0], p[1], k[2]], float)
+    return M, K, D
+
+
+def undistort_point(xy, K, D):
+    """pymvg CameraModel.undistort restated (OpenCV cvUndistortPoints fixed point)."""
+    if np.sum(np.abs(D)) == 0.0:
+        return np.asarray(xy, dtype=np.float64)
+    fx, cx, fy, cy = K[0, 0], K[0, 2], K[1, 1], K[1, 2]
+    xd = (xy[0] - cx) / fx
+    yd = (xy[1] - cy) / fy
+    k1, k2, t1, t2, k3 = D
+    x, y = xd, yd
+    for _ in range(5):
+        r2 = x * x + y * y
+        icdist = 1.0 / (1 + ((k3 * r2 + k2) * r2 + k1) * r2)
+        dx = 2 * t1 * x * y + t2 * (r2 + 2 * x * x)
+        dy = t1 * (r2 + 2 * y * y) + 2 * t2 * x * y
+        x = (xd - dx) * icdist
+        y = (yd - dy) * icdist
+    return np.array([x * fx + cx, y * fy + cy])
+
+
+def find3d(Ms, Ks, Ds, pts):
+    A = []
+    for M, K, D, xy in zip(Ms, Ks, Ds, pts):
+        u, v = undistort_point(np.asarray(xy, dtype=np.float64), K, D)
+        A.append(u * M[2] - M[0])
+        A.append(v * M[2] - M[1])
+    _, _, vt = np.linalg.svd(np.array(A))
+    return vt[-1, :3] / vt[-1, 3]
+
+
+def triangulate_poses(cameras, poses2d, joints_vis=None, no_distortion=False):
+    nviews = 4
+    nj = poses2d.shape[1]
+    g = len(cameras) // nviews
+    if joints_vis is None:
+        joints_vis = np.ones(poses2d.shape[:2])
+    out = np.zeros((g, nj, 3))
+    for i in range(g):
+        cams = [_camera(cameras[i * nviews + v], no_distortion) for v in range(nviews)]
+        for k in range(nj):
+            sel = [v for v in range(nviews) if joints_vis[i * nviews + v, k]]
+            if len(sel) < 2:
+                continue
+            out[i, k] = find3d([cams[v][0] for v in sel], [cams[v][1] for v in sel], [cams[v][2] for v in sel],
+                               [poses2d[i * nviews + v, k] for v in sel])
+    return out

@@ -1,0 +1,286 @@
+// Multi-view geometry kernels: epipolar (fundamental-matrix) loss forward/backward
+// and fp64 DLT triangulation.  Latency-bound, tiny working sets: no MFMA, no LDS
+// tiling beyond the block reductions.
+//
+// Epipolar loss (FundamentalLoss.__call__, lib/core/loss.py:101-133): residual of
+// ordered view pair p = (i, j) (itertools.permutations order, loss.py:123) at joint k
+// of sample b is |x~_j^T F_{subj(b), i, j} x~_i| (loss.py:128), weighted by
+// w_i * w_j when target weights are given (loss.py:129-130), summed and divided by
+// N * P * J (loss.py:132).  One 256-thread block does the whole reduction in a fixed
+// order, so the value is deterministic (no atomics).
+//
+// Triangulation (triangulate_poses -> pymvg MultiCameraSystem.find3d,
+// lib/multiviews/triangulate.py:43-99): one thread per (group, joint); OpenCV-model
+// fixed-point undistortion (5 iterations) of each visible view's pixel, two DLT rows
+// per view, and the right singular vector of the smallest singular value from a
+// one-sided (Hestenes) Jacobi SVD in fp64.
+#include "posu_common.h"
+
+namespace posu {
+namespace {
+
+__device__ __forceinline__ void pair_of(int p, int V, int& i, int& j) {
+  // permutations(range(V), 2): i major, j over the remaining views ascending
+  i = p / (V - 1);
+  const int r = p - i * (V - 1);
+  j = r < i ? r : r + 1;
+}
+
+// signed epipolar residual x~_j^T F x~_i  (row vector h_j times F, dotted with h_i)
+__device__ __forceinline__ float epi_residual(const float* F, float xi, float yi, float xj, float yj) {
+  const float a0 = xj * F[0] + yj * F[3] + F[6];
+  const float a1 = xj * F[1] + yj * F[4] + F[7];
+  const float a2 = xj * F[2] + yj * F[5] + F[8];
+  return a0 * xi + a1 * yi + a2;
+}
+
+__global__ __launch_bounds__(256) void epipolar_fwd_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ F,
+                                                           const int* __restrict__ subj, int V, int N, int J,
+                                                           float* __restrict__ loss, float* __restrict__ resid) {
+  const int P = V * (V - 1);
+  const int total = N * P * J;
+  float acc = 0.f;
+  for (int t = threadIdx.x; t < total; t += 256) {
+    const int k = t % J;
+    const int bp = t / J;
+    const int p = bp % P, b = bp / P;
+    int i, j;
+    pair_of(p, V, i, j);
+    const float* xi = x + (static_cast<size_t>(i) * N + b) * J * 2 + 2 * k;
+    const float* xj = x + (static_cast<size_t>(j) * N + b) * J * 2 + 2 * k;
+    const float* Fm = F + (static_cast<size_t>(subj[b]) * P + p) * 9;
+    float r = fabsf(epi_residual(Fm, xi[0], xi[1], xj[0], xj[1]));
+    if (w) r *= w[(static_cast<size_t>(j) * N + b) * J + k] * w[(static_cast<size_t>(i) * N + b) * J + k];
+    if (resid) resid[t] = r;
+    acc += r;
+  }
+  __shared__ float part[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float s = (part[0] + part[1]) + (part[2] + part[3]);
+    loss[0] = s / static_cast<float>(static_cast<long long>(N) * P * J);
+  }
+}
+
+// one thread per (view v, sample b, joint k): sums d|r|/dx over the 2(V-1) pairs
+// in which view v takes part (as i with F^T h_j, as j with F h_i)
+__global__ __launch_bounds__(256) void epipolar_bwd_kernel(const float* __restrict__ x,
+                                                           const float* __restrict__ w,
+                                                           const float* __restrict__ F,
+                                                           const int* __restrict__ subj, int V, int N, int J,
+                                                           const float* __restrict__ gloss,
+                                                           float* __restrict__ gx) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int total = V * N * J;
+  if (t >= total) return;
+  const int k = t % J;
+  const int vb = t / J;
+  const int b = vb % N, v = vb / N;
+  const int P = V * (V - 1);
+  const float g = gloss[0] / static_cast<float>(static_cast<long long>(N) * P * J);
+  float dx = 0.f, dy = 0.f;
+  for (int p = 0; p < P; ++p) {
+    int i, j;
+    pair_of(p, V, i, j);
+    if (i != v && j != v) continue;
+    const float* Fm = F + (static_cast<size_t>(subj[b]) * P + p) * 9;
+    const float* xi = x + (static_cast<size_t>(i) * N + b) * J * 2 + 2 * k;
+    const float* xj = x + (static_cast<size_t>(j) * N + b) * J * 2 + 2 * k;
+    const float r = epi_residual(Fm, xi[0], xi[1], xj[0], xj[1]);
+    float sg = r > 0.f ? g : (r < 0.f ? -g : 0.f);
+    if (w) sg *= w[(static_cast<size_t>(j) * N + b) * J + k] * w[(static_cast<size_t>(i) * N + b) * J + k];
+    if (i == v) {  // d/dx_i (h_j^T F h_i) = F^T h_j
+      dx += sg * (xj[0] * Fm[0] + xj[1] * Fm[3] + Fm[6]);
+      dy += sg * (xj[0] * Fm[1] + xj[1] * Fm[4] + Fm[7]);
+    } else {  // d/dx_j = F h_i
+      dx += sg * (Fm[0] * xi[0] + Fm[1] * xi[1] + Fm[2]);
+      dy += sg * (Fm[3] * xi[0] + Fm[4] * xi[1] + Fm[5]);
+    }
+  }
+  gx[2 * t] = dx;
+  gx[2 * t + 1] = dy;
+}
+
+constexpr int kMaxViews = 16;
+
+__global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ Mall,
+                                                         const double* __restrict__ intr,
+                                                         const void* __restrict__ xyv, int xy_dtype, int sg,
+                                                         int sv, const unsigned char* __restrict__ vis, int G, int V,
+                                                         int J, int undistort, double* __restrict__ X) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= G * J) return;
+  const int g = t / J, k = t - g * J;
+  double A[2 * kMaxViews][4];
+  int rows = 0;
+  for (int v = 0; v < V; ++v) {
+    const size_t gv = static_cast<size_t>(g) * V + v;
+    if (vis && !vis[gv * J + k]) continue;
+    double u, vv;
+    const size_t xoff = static_cast<size_t>(g) * sg + static_cast<size_t>(v) * sv + 2 * k;
+    if (xy_dtype == POSU_F64) {
+      const double* p = static_cast<const double*>(xyv) + xoff;
+      u = p[0];
+      vv = p[1];
+    } else {
+      const float* p = static_cast<const float*>(xyv) + xoff;
+      u = p[0];
+      vv = p[1];
+    }
+    const double* c = intr + gv * 9;
+    if (undistort) {
+      const double fx = c[0], fy = c[1], cx = c[2], cy = c[3];
+      const double k1 = c[4], k2 = c[5], p1 = c[6], p2 = c[7], k3 = c[8];
+      // pymvg returns the input untouched when every coefficient is zero
+      if (fabs(k1) + fabs(k2) + fabs(p1) + fabs(p2) + fabs(k3) != 0.0) {
+        const double xd = (u - cx) / fx, yd = (vv - cy) / fy;
+        double xx = xd, yy = yd;
+        for (int it = 0; it < 5; ++it) {
+          const double r2 = xx * xx + yy * yy;
+          const double icdist = 1.0 / (1.0 + ((k3 * r2 + k2) * r2 + k1) * r2);
+          const double dX = 2.0 * p1 * xx * yy + p2 * (r2 + 2.0 * xx * xx);
+          const double dY = p1 * (r2 + 2.0 * yy * yy) + 2.0 * p2 * xx * yy;
+          xx = (xd - dX) * icdist;
+          yy = (yd - dY) * icdist;
+        }
+        u = xx * fx + cx;
+        vv = yy * fy + cy;
+      }
+    }
+    const double* M = Mall + gv * 12;
+#pragma unroll
+    for (int cidx = 0; cidx < 4; ++cidx) {
+      A[rows][cidx] = u * M[8 + cidx] - M[cidx];
+      A[rows + 1][cidx] = vv * M[8 + cidx] - M[4 + cidx];
+    }
+    rows += 2;
+  }
+  double* out = X + static_cast<size_t>(t) * 3;
+  if (rows < 4) {  // fewer than two views: the reference leaves zeros
+    out[0] = out[1] = out[2] = 0.0;
+    return;
+  }
+  // one-sided Jacobi: rotate column pairs of A until mutually orthogonal; V accumulates
+  double Vm[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rotated = false;
+    for (int p = 0; p < 3; ++p) {
+      for (int q = p + 1; q < 4; ++q) {
+        double alpha = 0, beta = 0, gamma = 0;
+        for (int r = 0; r < rows; ++r) {
+          alpha += A[r][p] * A[r][p];
+          beta += A[r][q] * A[r][q];
+          gamma += A[r][p] * A[r][q];
+        }
+        if (fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0) continue;
+        rotated = true;
+        const double zeta = (beta - alpha) / (2.0 * gamma);
+        const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
+        for (int r = 0; r < rows; ++r) {
+          const double ap = A[r][p], aq = A[r][q];
+          A[r][p] = cs * ap - sn * aq;
+          A[r][q] = sn * ap + cs * aq;
+        }
+        for (int r = 0; r < 4; ++r) {
+          const double vp = Vm[r][p], vq = Vm[r][q];
+          Vm[r][p] = cs * vp - sn * vq;
+          Vm[r][q] = sn * vp + cs * vq;
+        }
+      }
+    }
+    if (!rotated) break;
+  }
+  int best = 0;
+  double bn = INFINITY;
+  for (int cidx = 0; cidx < 4; ++cidx) {
+    double nrm = 0;
+    for (int r = 0; r < rows; ++r) nrm += A[r][cidx] * A[r][cidx];
+    if (nrm < bn) {
+      bn = nrm;
+      best = cidx;
+    }
+  }
+  const double h = Vm[3][best];
+  out[0] = Vm[0][best] / h;
+  out[1] = Vm[1][best] / h;
+  out[2] = Vm[2][best] / h;
+}
+
+}  // namespace
+}  // namespace posu
+
+using namespace posu;
+
+extern "C" int posu_epipolar_loss_fwd(const float* x, const float* w, const float* F, const int* subj, int V, int N,
+                                      int J, int S, float* loss, float* resid, void* stream) {
+  POSU_REQUIRE(x && F && subj && loss, "posu_epipolar_loss_fwd: null pointer");
+  POSU_REQUIRE(V >= 2 && N >= 0 && J > 0 && S > 0, "posu_epipolar_loss_fwd: bad shape");
+  if (N == 0) {
+    set_error("posu_epipolar_loss_fwd: empty batch (the reference divides by zero)");
+    return POSU_ERR_ARG;
+  }
+  hipLaunchKernelGGL(epipolar_fwd_kernel, dim3(1), dim3(256), 0, as_stream(stream), x, w, F, subj, V, N, J, loss,
+                     resid);
+  return check_launch("posu_epipolar_loss_fwd");
+}
+
+extern "C" int posu_epipolar_loss_bwd(const float* x, const float* w, const float* F, const int* subj, int V, int N,
+                                      int J, int S, const float* gloss, float* gx, void* stream) {
+  POSU_REQUIRE(x && F && subj && gloss && gx, "posu_epipolar_loss_bwd: null pointer");
+  POSU_REQUIRE(V >= 2 && N > 0 && J > 0 && S > 0, "posu_epipolar_loss_bwd: bad shape");
+  const int total = V * N * J;
+  hipLaunchKernelGGL(epipolar_bwd_kernel, dim3((total + 255) / 256), dim3(256), 0, as_stream(stream), x, w, F,
+                     subj, V, N, J, gloss, gx);
+  return check_launch("posu_epipolar_loss_bwd");
+}
+
+extern "C" int posu_triangulate_dlt(const double* M, const double* intr, const void* xy, int xy_dtype,
+                                    int xy_stride_g, int xy_stride_v, const unsigned char* vis, int G, int V,
+                                    int J, int undistort, double* X, void* stream) {
+  POSU_REQUIRE(M && intr && xy && X, "posu_triangulate_dlt: null pointer");
+  POSU_REQUIRE(G >= 0 && V >= 1 && V <= kMaxViews && J > 0, "posu_triangulate_dlt: bad shape (V <= 16)");
+  POSU_REQUIRE(xy_dtype == POSU_F32 || xy_dtype == POSU_F64, "posu_triangulate_dlt: xy dtype must be F32 or F64");
+  POSU_REQUIRE(xy_stride_g >= 0 && xy_stride_v >= 0, "posu_triangulate_dlt: negative xy stride");
+  if (G == 0) return POSU_OK;
+  const int total = G * J;
+  hipLaunchKernelGGL(triangulate_kernel, dim3((total + 63) / 64), dim3(64), 0, as_stream(stream), M, intr, xy,
+                     xy_dtype, xy_stride_g, xy_stride_v, vis, G, V, J, undistort, X);
+  return check_launch("posu_triangulate_dlt");
+}
+
+// ------------------------------------------------------- per-sample 2-D affine
+namespace posu {
+namespace {
+
+__global__ __launch_bounds__(256) void affine_kernel(const float* __restrict__ pts, const float* __restrict__ T,
+                                                     int N, int J, int transpose, float* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= N * J) return;
+  const float* A = T + static_cast<size_t>(t / J) * 6;
+  const float x = pts[2 * t], y = pts[2 * t + 1];
+  if (!transpose) {
+    out[2 * t] = x * A[0] + y * A[1] + A[2];
+    out[2 * t + 1] = x * A[3] + y * A[4] + A[5];
+  } else {
+    out[2 * t] = x * A[0] + y * A[3];
+    out[2 * t + 1] = x * A[1] + y * A[4];
+  }
+}
+
+}  // namespace
+}  // namespace posu
+
+extern "C" int posu_affine2d_apply(const float* pts, const float* T, int N, int J, int transpose, float* out,
+                                   void* stream) {
+  POSU_REQUIRE(pts && T && out, "posu_affine2d_apply: null pointer");
+  POSU_REQUIRE(N >= 0 && J > 0, "posu_affine2d_apply: bad shape");
+  if (N == 0) return POSU_OK;
+  hipLaunchKernelGGL(affine_kernel, dim3((N * J + 255) / 256), dim3(256), 0, as_stream(stream), pts, T, N, J,
+                     transpose, out);
+  return check_launch("posu_affine2d_apply");
+}

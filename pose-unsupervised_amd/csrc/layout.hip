@@ -1,0 +1,192 @@
+// HBM-bound layout kernels around the conv stack: NCHW f32 -> NHWC packing of the
+// input crops, NHWC -> NCHW f32 unpacking of returned feature maps, and the stem
+// max-pool.  One 16-byte channel chunk per thread, vectorised loads/stores.
+#include "posu_common.h"
+
+namespace posu {
+namespace {
+
+template <typename T>
+struct Vec;
+template <>
+struct Vec<uint16_t> {
+  static constexpr int E = 8;
+  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ uint4 pack(const float* v) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      w[i] = static_cast<uint32_t>(f2bf(v[2 * i])) | (static_cast<uint32_t>(f2bf(v[2 * i + 1])) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+};
+template <>
+struct Vec<float> {
+  static constexpr int E = 4;
+  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
+    v[0] = __uint_as_float(u.x);
+    v[1] = __uint_as_float(u.y);
+    v[2] = __uint_as_float(u.z);
+    v[3] = __uint_as_float(u.w);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* v) {
+    return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                      __float_as_uint(v[3]));
+  }
+};
+
+// one thread per (pixel, 16-B output chunk)
+template <typename T>
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                                   T* __restrict__ y, int Cpad) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = Cpad / E;
+  const long long total = static_cast<long long>(N) * H * W * chunks;
+  const long long HW = static_cast<long long>(H) * W;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const long long n = pix / HW, p = pix - n * HW;
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int c = ch * E + e;
+      v[e] = c < C ? x[(n * C + c) * HW + p] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(y + pix * Cpad + ch * E) = Vec<T>::pack(v);
+  }
+}
+
+// one thread per (pixel, 16-B input chunk); writes E channel planes
+template <typename T>
+__global__ __launch_bounds__(256) void unpack_kernel(const T* __restrict__ x, int N, int H, int W, int C,
+                                                     float* __restrict__ y) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = C / E;
+  const long long HW = static_cast<long long>(H) * W;
+  const long long total = N * HW * chunks;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    // pixel-fastest thread order so the NCHW stores coalesce
+    const long long p = i % HW;
+    const long long rest = i / HW;
+    const int ch = static_cast<int>(rest % chunks);
+    const long long n = rest / chunks;
+    float v[E];
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(x + (n * HW + p) * C + ch * E), v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) y[(n * C + ch * E + e) * HW + p] = v[e];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ x, int N, int H, int W, int C,
+                                                      T* __restrict__ y, int Ho, int Wo) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = C / E;
+  const long long total = static_cast<long long>(N) * Ho * Wo * chunks;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const int ox = static_cast<int>(pix % Wo);
+    const long long t = pix / Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const long long n = t / Ho;
+    float m[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) m[e] = -INFINITY;
+    for (int dy = 0; dy < 3; ++dy) {
+      const int iy = oy * 2 - 1 + dy;
+      if (iy < 0 || iy >= H) continue;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int ix = ox * 2 - 1 + dx;
+        if (ix < 0 || ix >= W) continue;
+        float v[E];
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(x + ((n * H + iy) * W + ix) * C + ch * E), v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) m[e] = fmaxf(m[e], v[e]);
+      }
+    }
+    *reinterpret_cast<uint4*>(y + pix * C + ch * E) = Vec<T>::pack(m);
+  }
+}
+
+inline int grid_for(long long total) {
+  long long g = (total + 255) / 256;
+  return static_cast<int>(g < 8192 ? (g > 0 ? g : 1) : 8192);
+}
+
+}  // namespace
+}  // namespace posu
+
+using namespace posu;
+
+extern "C" int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, void* y, int Cpad,
+                                      void* stream) {
+  POSU_REQUIRE(x && y, "posu_pack_nchw_to_nhwc: null pointer");
+  POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && Cpad >= C, "posu_pack_nchw_to_nhwc: bad shape");
+  hipStream_t s = as_stream(stream);
+  const long long pix = static_cast<long long>(N) * H * W;
+  if (dtype == POSU_BF16) {
+    POSU_REQUIRE(Cpad % 8 == 0, "posu_pack_nchw_to_nhwc: Cpad % 8 != 0");
+    hipLaunchKernelGGL(pack_kernel<uint16_t>, dim3(grid_for(pix * Cpad / 8)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<uint16_t*>(y), Cpad);
+  } else if (dtype == POSU_F32) {
+    POSU_REQUIRE(Cpad % 4 == 0, "posu_pack_nchw_to_nhwc: Cpad % 4 != 0");
+    hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(pix * Cpad / 4)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<float*>(y), Cpad);
+  } else {
+    set_error("posu_pack_nchw_to_nhwc: unsupported dtype");
+    return POSU_ERR_ARG;
+  }
+  return check_launch("posu_pack_nchw_to_nhwc");
+}
+
+extern "C" int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C, float* y,
+                                     void* stream) {
+  POSU_REQUIRE(x && y, "posu_nhwc_to_nchw_f32: null pointer");
+  POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, "posu_nhwc_to_nchw_f32: bad shape");
+  hipStream_t s = as_stream(stream);
+  const long long el = static_cast<long long>(N) * H * W * C;
+  if (dtype == POSU_BF16) {
+    POSU_REQUIRE(C % 8 == 0, "posu_nhwc_to_nchw_f32: C % 8 != 0");
+    hipLaunchKernelGGL(unpack_kernel<uint16_t>, dim3(grid_for(el / 8)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), N, H, W, C, y);
+  } else if (dtype == POSU_F32) {
+    POSU_REQUIRE(C % 4 == 0, "posu_nhwc_to_nchw_f32: C % 4 != 0");
+    hipLaunchKernelGGL(unpack_kernel<float>, dim3(grid_for(el / 4)), dim3(256), 0, s,
+                       static_cast<const float*>(x), N, H, W, C, y);
+  } else {
+    set_error("posu_nhwc_to_nchw_f32: unsupported dtype");
+    return POSU_ERR_ARG;
+  }
+  return check_launch("posu_nhwc_to_nchw_f32");
+}
+
+extern "C" int posu_maxpool3x3s2_fwd(int dtype, const void* x, int N, int H, int W, int C, void* y,
+                                     void* stream) {
+  POSU_REQUIRE(x && y, "posu_maxpool3x3s2_fwd: null pointer");
+  POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, "posu_maxpool3x3s2_fwd: bad shape");
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipStream_t s = as_stream(stream);
+  const long long el = static_cast<long long>(N) * Ho * Wo * C;
+  if (dtype == POSU_BF16) {
+    POSU_REQUIRE(C % 8 == 0, "posu_maxpool3x3s2_fwd: C % 8 != 0");
+    hipLaunchKernelGGL(maxpool_kernel<uint16_t>, dim3(grid_for(el / 8)), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), N, H, W, C, static_cast<uint16_t*>(y), Ho, Wo);
+  } else if (dtype == POSU_F32) {
+    POSU_REQUIRE(C % 4 == 0, "posu_maxpool3x3s2_fwd: C % 4 != 0");
+    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_for(el / 4)), dim3(256), 0, s,
+                       static_cast<const float*>(x), N, H, W, C, static_cast<float*>(y), Ho, Wo);
+  } else {
+    set_error("posu_maxpool3x3s2_fwd: unsupported dtype");
+    return POSU_ERR_ARG;
+  }
+  return check_launch("posu_maxpool3x3s2_fwd");
+}

@@ -1,0 +1,107 @@
+"""ctypes binding of libposeu.so (the C ABI declared in include/posu.h).
+
+The library is built in-tree (``make -C pose-unsupervised_amd`` or
+``__graft_entry__.build()``) and loaded from this directory.  There is no
+fallback: if the library is missing, or no GPU is visible when an op runs,
+the op raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- loads PyTorch's HIP runtime before libposeu.so binds to it
+
+F32 = 0
+BF16 = 1
+F64 = 2
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
+_lock = threading.Lock()
+_lib = None
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+_SIGNATURES = {
+    'posu_last_error': [],
+    'posu_abi_version': [],
+    'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _p],
+    'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
+    'posu_conv_bk': [_i],
+    'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _p],
+    'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],
+    'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],
+    'posu_maxpool3x3s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _p],
+    'posu_softargmax2d_fwd': [_p, _i, _i, _i, _i, _f, _p, _p, _p, _p],
+    'posu_softargmax2d_bwd': [_p, _p, _i, _i, _i, _i, _f, _p, _p, _p, _p],
+    'posu_argmax2d_fwd': [_p, _i, _i, _i, _i, _i, _p, _p, _p, _p],
+    'posu_affine2d_apply': [_p, _p, _i, _i, _i, _p, _p],
+    'posu_epipolar_loss_fwd': [_p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p],
+    'posu_epipolar_loss_bwd': [_p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p],
+    'posu_triangulate_dlt': [_p, _p, _p, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p],
+    'posu_joints_mse_fwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
+    'posu_joints_mse_bwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
+}
+_RESTYPES = {'posu_last_error': ctypes.c_char_p}
+
+
+def library_path():
+    return _LIB_PATH
+
+
+def load():
+    """Load libposeu.so once and declare every exported signature."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError(
+                'libposeu.so is not built (%s); run `make -C pose-unsupervised_amd` '
+                'or __graft_entry__.build()' % _LIB_PATH)
+        lib = ctypes.CDLL(_LIB_PATH)
+        for name, args in _SIGNATURES.items():
+            fn = getattr(lib, name)  # AttributeError = a declared symbol is missing
+            fn.argtypes = args
+            fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return sorted(_SIGNATURES)
+
+
+def last_error():
+    return load().posu_last_error().decode('utf-8', 'replace')
+
+
+def call(name, *args):
+    """Invoke an entry point and raise on a non-zero status."""
+    status = getattr(load(), name)(*args)
+    if status != 0:
+        raise RuntimeError('%s failed (status %d): %s' % (name, status, last_error()))
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_cuda(*tensors):
+    """The product path runs only on the GPU: refuse CPU tensors loudly."""
+    for t in tensors:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                'pose-unsupervised_amd ops run only on the MI355X HIP path; '
+                'got a CPU tensor (move inputs to a cuda device)')

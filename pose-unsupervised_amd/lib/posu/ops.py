@@ -1,0 +1,269 @@
+"""Tensor-level wrappers over libposeu.so entry points.
+
+Every function here takes/returns torch tensors on a cuda (HIP) device, launches on
+PyTorch's current stream, and raises if given CPU tensors: there is no fallback
+path.  Autograd Functions wrap the kernels that the training step differentiates
+through (soft-argmax, crop affine, epipolar loss, heatmap MSE).
+"""
+import torch
+
+from . import _native as nat
+from ._native import F32, BF16, F64, ptr, call, stream_of, require_cuda
+
+_TORCH_OF = {F32: torch.float32, BF16: torch.bfloat16}
+
+
+def dtype_code(dtype):
+    if dtype in ('bf16', torch.bfloat16, BF16):
+        return BF16
+    if dtype in ('fp32', 'f32', torch.float32, F32):
+        return F32
+    raise ValueError('unsupported compute dtype %r (bf16 | fp32)' % (dtype,))
+
+
+def torch_dtype(code):
+    return _TORCH_OF[code]
+
+
+def conv_bk(code):
+    return nat.load().posu_conv_bk(code)
+
+
+# ---------------------------------------------------------------- layout ops
+def pack_nchw_to_nhwc(x, code, cpad, out=None):
+    """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C)."""
+    require_cuda(x)
+    x = x.contiguous().float()
+    n, c, h, w = x.shape
+    if out is None:
+        out = torch.empty((n, h, w, cpad), dtype=torch_dtype(code), device=x.device)
+    call('posu_pack_nchw_to_nhwc', code, ptr(x), n, c, h, w, ptr(out), cpad, stream_of(x.device))
+    return out
+
+
+def nhwc_to_nchw_f32(x, code):
+    require_cuda(x)
+    n, h, w, c = x.shape
+    out = torch.empty((n, c, h, w), dtype=torch.float32, device=x.device)
+    call('posu_nhwc_to_nchw_f32', code, ptr(x), n, h, w, c, ptr(out), stream_of(x.device))
+    return out
+
+
+# ------------------------------------------------------------------ conv ops
+def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None):
+    n, h, w, c = x.shape
+    ho = (h + 2 * pad - kh) // stride + 1
+    wo = (w + 2 * pad - kw) // stride + 1
+    if out is None:
+        out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
+    call('posu_conv2d_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, kh, kw, stride, pad,
+         ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, stream_of(x.device))
+    return out
+
+
+def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None):
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
+    call('posu_deconv4x4s2_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(scale), ptr(shift),
+         int(relu), ptr(out), stream_of(x.device))
+    return out
+
+
+def head1x1_nchw(x, wpk, cout, bias, code, out=None):
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
+    call('posu_head1x1_nchw_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(bias), ptr(out),
+         stream_of(x.device))
+    return out
+
+
+def maxpool3x3s2_nhwc(x, code, out=None):
+    n, h, w, c = x.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    if out is None:
+        out = torch.empty((n, ho, wo, c), dtype=x.dtype, device=x.device)
+    call('posu_maxpool3x3s2_fwd', code, ptr(x), n, h, w, c, ptr(out), stream_of(x.device))
+    return out
+
+
+# ------------------------------------------------------------ heatmap decode
+class _SoftArgmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, hm, beta, affine):
+        hm = hm.contiguous()
+        n, j, h, w = hm.shape
+        out = torch.empty((n, j, 2), dtype=torch.float32, device=hm.device)
+        stats = torch.empty((n, j, 4), dtype=torch.float32, device=hm.device)
+        call('posu_softargmax2d_fwd', ptr(hm), n, j, h, w, float(beta), ptr(affine), ptr(out), ptr(stats),
+             stream_of(hm.device))
+        ctx.save_for_backward(hm, stats, affine)
+        ctx.beta = beta
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        hm, stats, affine = ctx.saved_tensors
+        n, j, h, w = hm.shape
+        gout = gout.contiguous().float()
+        ghm = torch.empty_like(hm)
+        call('posu_softargmax2d_bwd', ptr(hm), ptr(stats), n, j, h, w, float(ctx.beta), ptr(affine), ptr(gout),
+             ptr(ghm), stream_of(hm.device))
+        return ghm, None, None
+
+
+def softargmax2d(hm, beta=100.0, affine=None):
+    """[N, J, H, W] f32 heatmaps -> [N, J, 2] (x=col, y=row); affine [N, 2, 3] maps to image px."""
+    require_cuda(hm, affine)
+    if hm.dtype != torch.float32:
+        raise TypeError('soft-argmax expects float32 heatmaps (got %s)' % hm.dtype)
+    if affine is not None:
+        affine = affine.to(device=hm.device, dtype=torch.float32).contiguous()
+    return _SoftArgmax.apply(hm, beta, affine)
+
+
+class _Affine2d(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pts, T):
+        pts = pts.contiguous().float()
+        n, j, _ = pts.shape
+        out = torch.empty_like(pts)
+        call('posu_affine2d_apply', ptr(pts), ptr(T), n, j, 0, ptr(out), stream_of(pts.device))
+        ctx.save_for_backward(T)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (T,) = ctx.saved_tensors
+        g = g.contiguous().float()
+        n, j, _ = g.shape
+        gin = torch.empty_like(g)
+        call('posu_affine2d_apply', ptr(g), ptr(T), n, j, 1, ptr(gin), stream_of(g.device))
+        return gin, None
+
+
+def affine2d(pts, T):
+    """[N, J, 2] @ per-sample [N, 2, 3] affine (homogeneous)."""
+    require_cuda(pts)
+    T = T.to(device=pts.device, dtype=torch.float32).contiguous()
+    return _Affine2d.apply(pts, T)
+
+
+def argmax2d(hm, post_process=True, affine64=None):
+    """get_final_preds on device: returns (preds [N, J, 2] f32, maxvals [N, J, 1] f32)."""
+    require_cuda(hm)
+    hm = hm.contiguous().float()
+    n, j, h, w = hm.shape
+    if affine64 is not None:
+        affine64 = affine64.to(device=hm.device, dtype=torch.float64).contiguous()
+    preds = torch.empty((n, j, 2), dtype=torch.float32, device=hm.device)
+    maxv = torch.empty((n, j, 1), dtype=torch.float32, device=hm.device)
+    call('posu_argmax2d_fwd', ptr(hm), n, j, h, w, int(bool(post_process)), ptr(affine64), ptr(preds), ptr(maxv),
+         stream_of(hm.device))
+    return preds, maxv
+
+
+# ----------------------------------------------------------------- losses
+class _Epipolar(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, F, subj):
+        x = x.contiguous().float()
+        v, n, j, _ = x.shape
+        s = F.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=x.device)
+        call('posu_epipolar_loss_fwd', ptr(x), ptr(w), ptr(F), ptr(subj), v, n, j, s, ptr(loss), None,
+             stream_of(x.device))
+        ctx.save_for_backward(x, w, F, subj)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        x, w, F, subj = ctx.saved_tensors
+        v, n, j, _ = x.shape
+        gloss = gloss.contiguous().float().reshape(1)
+        gx = torch.empty_like(x)
+        call('posu_epipolar_loss_bwd', ptr(x), ptr(w), ptr(F), ptr(subj), v, n, j, F.shape[0], ptr(gloss),
+             ptr(gx), stream_of(x.device))
+        return gx, None, None, None
+
+
+def epipolar_loss(x, w, F, subj):
+    """x [V, N, J, 2] image px; w [V, N, J] or None; F [S, V(V-1), 3, 3]; subj [N] int32."""
+    require_cuda(x, w, F, subj)
+    if w is not None:
+        w = w.contiguous().float()
+    return _Epipolar.apply(x, w, F.contiguous().float(), subj.contiguous().int())
+
+
+def epipolar_residuals(x, w, F, subj):
+    """Per (sample, pair, joint) weighted |x_j^T F x_i| [N, P, J] (no autograd)."""
+    require_cuda(x, w, F, subj)
+    x = x.contiguous().float()
+    v, n, j, _ = x.shape
+    p = v * (v - 1)
+    loss = torch.empty((), dtype=torch.float32, device=x.device)
+    resid = torch.empty((n, p, j), dtype=torch.float32, device=x.device)
+    call('posu_epipolar_loss_fwd', ptr(x), ptr(None if w is None else w.contiguous().float()),
+         ptr(F.contiguous().float()), ptr(subj.contiguous().int()), v, n, j, F.shape[0], ptr(loss), ptr(resid),
+         stream_of(x.device))
+    return resid, loss
+
+
+class _JointsMSE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, gt, w):
+        n, j = pred.shape[:2]
+        hw = pred[0, 0].numel()
+        pred = pred.contiguous().float()
+        gt = gt.contiguous().float()
+        ws = torch.empty((n * j,), dtype=torch.float32, device=pred.device)
+        loss = torch.empty((), dtype=torch.float32, device=pred.device)
+        call('posu_joints_mse_fwd', ptr(pred), ptr(gt), ptr(w), n, j, hw, ptr(ws), ptr(loss), stream_of(pred.device))
+        ctx.save_for_backward(pred, gt, w)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        pred, gt, w = ctx.saved_tensors
+        n, j = pred.shape[:2]
+        hw = pred[0, 0].numel()
+        gloss = gloss.contiguous().float().reshape(1)
+        gpred = torch.empty_like(pred)
+        call('posu_joints_mse_bwd', ptr(pred), ptr(gt), ptr(w), n, j, hw, ptr(gloss), ptr(gpred),
+             stream_of(pred.device))
+        return gpred, None, None
+
+
+def joints_mse(pred, gt, w=None):
+    require_cuda(pred, gt, w)
+    if w is not None:
+        w = w.reshape(pred.shape[0], pred.shape[1]).contiguous().float()
+    return _JointsMSE.apply(pred, gt, w)
+
+
+# -------------------------------------------------------------- triangulation
+def triangulate_dlt(M, intr, xy, vis=None, undistort=True, view_major=False):
+    """M [G, V, 3, 4] f64, intr [G, V, 9] f64, xy [G, V, J, 2] (or [V, G, J, 2] with view_major) f32|f64,
+    vis [G, V, J] u8 -> X [G, J, 3] f64."""
+    require_cuda(M, intr, xy, vis)
+    if view_major:
+        v, g, j, _ = xy.shape
+        sg, sv = j * 2, g * j * 2
+    else:
+        g, v, j, _ = xy.shape
+        sg, sv = v * j * 2, j * 2
+    M = M.contiguous().double()
+    intr = intr.contiguous().double()
+    xy = xy.contiguous()
+    if xy.dtype == torch.float64:
+        code = F64
+    else:
+        xy = xy.float()
+        code = F32
+    if vis is not None:
+        vis = vis.contiguous().to(torch.uint8)
+    X = torch.empty((g, j, 3), dtype=torch.float64, device=xy.device)
+    call('posu_triangulate_dlt', ptr(M), ptr(intr), ptr(xy), code, sg, sv, ptr(vis), g, v, j, int(bool(undistort)),
+         ptr(X), stream_of(xy.device))
+    return X

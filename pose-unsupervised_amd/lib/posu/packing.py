@@ -1,0 +1,57 @@
+"""Weight packing: reference (PyTorch NCHW) parameters -> the layouts the HIP kernels read.
+
+* Conv2d weight [Cout, Cin, KH, KW] -> [CoutPad][Kpad], k = (kh*KW + kw)*CinPad + ci
+  (K contiguous per output channel, the B^T operand of the implicit GEMM).
+* ConvTranspose2d(4, s2, p1) weight [Cin, Cout, 4, 4] -> [4 classes][CoutPad][Kpad]:
+  output parity class (py, px) is a 2x2 stride-1 convolution whose tap (ty, tx) is the
+  deconv tap (3 - py - 2ty, 3 - px - 2tx) (see csrc/conv_igemm.hip).
+* Eval-mode BatchNorm2d -> per-channel (scale, shift) f32, folded in fp64:
+  scale = gamma / sqrt(var + eps), shift = beta - mean * scale (+ conv bias * scale).
+"""
+import torch
+
+COUT_ALIGN = 64
+
+
+def round_up(x, m):
+    return (x + m - 1) // m * m
+
+
+def pack_conv_weight(w, cin_pad, bk, dtype):
+    cout, cin, kh, kw = w.shape
+    k = kh * kw * cin_pad
+    wt = torch.zeros((cout, kh, kw, cin_pad), dtype=torch.float32, device=w.device)
+    wt[..., :cin] = w.detach().float().permute(0, 2, 3, 1)
+    out = torch.zeros((round_up(cout, COUT_ALIGN), round_up(k, bk)), dtype=torch.float32, device=w.device)
+    out[:cout, :k] = wt.reshape(cout, k)
+    return out.to(dtype).contiguous()
+
+
+def pack_deconv4x4_weight(w, bk, dtype):
+    cin, cout, kh, kw = w.shape
+    if (kh, kw) != (4, 4):
+        raise NotImplementedError('sub-pixel deconv kernel supports kernel 4 / stride 2 / padding 1 only')
+    wf = w.detach().float()
+    k = 4 * cin
+    out = torch.zeros((4, round_up(cout, COUT_ALIGN), round_up(k, bk)), dtype=torch.float32, device=w.device)
+    for py in range(2):
+        for px in range(2):
+            taps = []
+            for ty in range(2):
+                for tx in range(2):
+                    taps.append(wf[:, :, 3 - py - 2 * ty, 3 - px - 2 * tx].t())  # [Cout, Cin]
+            out[py * 2 + px, :cout, :k] = torch.cat(taps, dim=1)
+    return out.to(dtype).contiguous()
+
+
+def fold_bn(bn, conv_bias=None):
+    """(scale, shift) f32 of an eval-mode BatchNorm2d (optionally after a biased conv)."""
+    gamma = bn.weight.detach().double() if bn.weight is not None else torch.ones_like(bn.running_mean.double())
+    beta = bn.bias.detach().double() if bn.bias is not None else torch.zeros_like(bn.running_mean.double())
+    mean = bn.running_mean.detach().double()
+    var = bn.running_var.detach().double()
+    scale = gamma / torch.sqrt(var + bn.eps)
+    shift = beta - mean * scale
+    if conv_bias is not None:
+        shift = shift + conv_bias.detach().double() * scale
+    return scale.float().contiguous(), shift.float().contiguous()

@@ -1,0 +1,123 @@
+"""Inference plan for PoseResNet on the HIP kernels.
+
+A plan is the packed, device-resident form of a PoseResNet (NHWC weights, folded BN)
+plus the ordered list of kernel launches of one forward pass
+(lib/models/pose_resnet.py:191-205 of the reference):
+
+    pack(NCHW f32 -> NHWC, C 3 -> 8)
+    stem conv 7x7/s2 + BN + ReLU          -> maxpool 3x3/s2
+    layer1..4: per block conv/BN/ReLU chain, residual (+ downsample conv/BN) fused
+               into the last conv's epilogue
+    3 x (deconv 4x4/s2 + BN + ReLU)       (sub-pixel, one launch each)
+    final 1x1 conv + bias                 -> NCHW f32 heatmaps
+
+All launches go to PyTorch's current stream, so a forward can be captured in a
+torch.cuda.CUDAGraph (hipGraph) by the caller.
+"""
+import torch
+
+from . import ops
+from .packing import fold_bn, pack_conv_weight, pack_deconv4x4_weight
+
+STEM_CIN_PAD = 8
+
+
+class _Conv:
+    __slots__ = ('w', 'scale', 'shift', 'cout', 'k', 'stride', 'pad', 'relu')
+
+    def __init__(self, conv, bn, relu, code, bk, cin_pad=None):
+        cin = conv.weight.shape[1]
+        self.w = pack_conv_weight(conv.weight, cin_pad or cin, bk, ops.torch_dtype(code))
+        self.scale, self.shift = fold_bn(bn, conv.bias)
+        self.cout = conv.weight.shape[0]
+        self.k = conv.kernel_size[0]
+        if conv.kernel_size[0] != conv.kernel_size[1]:
+            raise NotImplementedError('square kernels only')
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.relu = relu
+
+    def __call__(self, x, code, residual=None):
+        return ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale,
+                               self.shift, residual, self.relu, code)
+
+
+class _Block:
+    __slots__ = ('convs', 'down')
+
+    def __init__(self, blk, code, bk):
+        names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
+        self.convs = []
+        for i, nm in enumerate(names):
+            self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
+        self.down = None
+        if blk.downsample is not None:
+            self.down = _Conv(blk.downsample[0], blk.downsample[1], False, code, bk)
+
+    def __call__(self, x, code):
+        res = self.down(x, code) if self.down is not None else x
+        out = x
+        for c in self.convs[:-1]:
+            out = c(out, code)
+        return self.convs[-1](out, code, residual=res)
+
+
+class _Deconv:
+    __slots__ = ('w', 'scale', 'shift', 'cout')
+
+    def __init__(self, dc, bn, code, bk):
+        if dc.stride != (2, 2) or dc.padding != (1, 1) or dc.output_padding != (0, 0):
+            raise NotImplementedError('deconv supported for kernel 4, stride 2, padding 1')
+        self.w = pack_deconv4x4_weight(dc.weight, bk, ops.torch_dtype(code))
+        self.scale, self.shift = fold_bn(bn, dc.bias)
+        self.cout = dc.weight.shape[1]
+
+    def __call__(self, x, code):
+        return ops.deconv4x4s2_nhwc(x, self.w, self.cout, self.scale, self.shift, True, code)
+
+
+class PoseResNetPlan:
+    """Packed weights + forward launch sequence of one PoseResNet in one compute dtype."""
+
+    def __init__(self, net, code):
+        self.code = code
+        bk = ops.conv_bk(code)
+        self.stem = _Conv(net.conv1, net.bn1, True, code, bk, cin_pad=STEM_CIN_PAD)
+        self.layers = [[_Block(b, code, bk) for b in layer] for layer in
+                       (net.layer1, net.layer2, net.layer3, net.layer4)]
+        mods = list(net.deconv_layers)
+        self.deconvs = []
+        for i in range(0, len(mods), 3):
+            self.deconvs.append(_Deconv(mods[i], mods[i + 1], code, bk))
+        fl = net.final_layer
+        if fl.kernel_size != (1, 1):
+            raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
+        self.head_w = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, ops.torch_dtype(code))
+        self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None
+                       else torch.zeros(fl.weight.shape[0], device=fl.weight.device))
+        self.njoints = fl.weight.shape[0]
+
+    def pack_input(self, views):
+        """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N)."""
+        n, _, h, w = views[0].shape
+        x = torch.empty((n * len(views), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(self.code),
+                        device=views[0].device)
+        for i, v in enumerate(views):
+            ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n])
+        return x
+
+    def run(self, x):
+        """NHWC packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC)."""
+        code = self.code
+        x = self.stem(x, code)
+        x = ops.maxpool3x3s2_nhwc(x, code)
+        x1 = None
+        for li, layer in enumerate(self.layers):
+            for blk in layer:
+                x = blk(x, code)
+            if li == 0:
+                x1 = x
+        for dc in self.deconvs:
+            x = dc(x, code)
+        hm = ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code)
+        return hm, x1, x

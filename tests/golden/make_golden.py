@@ -1,0 +1,229 @@
+"""Generate the golden fixtures in tests/golden/ by importing the REFERENCE
+(/root/reference/lib) in this container.  Run once (not on the GPU box):
+
+    python tests/golden/make_golden.py
+
+What it imports and how (all in-process, nothing is copied into the repo):
+  * models.pose_resnet (imports as-is) -- PoseResNet R18/R50/R152 heatmaps; also a
+    train-mode calibration pass whose BN running statistics become
+    pose-unsupervised_amd/data/synthetic_bn_r*_*.npz (momentum 1.0 = one batch's stats);
+  * utils.transforms, core.inference, core.loss -- these import OpenCV, which is not
+    installed; a stand-in module provides only cv2.getAffineTransform (the 6x6 linear
+    solve OpenCV performs).  generate_integral_preds_2d_th calls Tensor.get_device(),
+    which is -1 on CPU tensors: it is patched to return 'cpu' while generating.
+    FundamentalLoss.__init__ needs torch.distributed + CUDA: the object is built with
+    __new__ and given its fundamental-matrix dict directly;
+  * multiviews.cameras (imports as-is) -- projection of known 3-D points, used as the
+    exact known-answer input of the triangulation tests (pymvg is not importable).
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF_LIB = '/root/reference/lib'
+
+def _load_synthetic():
+    # loaded by file path: the build's lib/ must not shadow the reference's packages here
+    import importlib.util
+    path = os.path.join(REPO, 'pose-unsupervised_amd', 'lib', 'posu', 'synthetic.py')
+    spec = importlib.util.spec_from_file_location('posu_synthetic', path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+syn = _load_synthetic()  # deterministic inputs, no reference code
+
+
+def _install_cv2_standin():
+    m = types.ModuleType('cv2')
+
+    def getAffineTransform(src, dst):
+        a = np.zeros((6, 6))
+        b = np.zeros(6)
+        src = np.asarray(src, np.float64)
+        dst = np.asarray(dst, np.float64)
+        for i in range(3):
+            a[2 * i, :3] = [src[i, 0], src[i, 1], 1]
+            a[2 * i + 1, 3:] = [src[i, 0], src[i, 1], 1]
+            b[2 * i:2 * i + 2] = dst[i]
+        return np.linalg.solve(a, b).reshape(2, 3)
+
+    m.getAffineTransform = getAffineTransform
+    m.INTER_LINEAR = 1
+    sys.modules['cv2'] = m
+
+
+def _import_reference():
+    _install_cv2_standin()
+    for p in (REF_LIB, os.path.join(REF_LIB, 'core')):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import models.pose_resnet as ref_pr  # noqa
+    import utils.transforms as ref_tf  # noqa
+    import core.inference as ref_inf  # noqa
+    import core.loss as ref_loss  # noqa
+    import multiviews.cameras as ref_cam  # noqa
+    return ref_pr, ref_tf, ref_inf, ref_loss, ref_cam
+
+
+def _patched_get_device():
+    orig = torch.Tensor.get_device
+
+    def gd(self):
+        return 'cpu' if not self.is_cuda else orig(self)
+    return orig, gd
+
+
+def pose_resnet_golden(ref_pr, num_layers, image_size, batch, seed):
+    cfg = syn.make_cfg(num_layers=num_layers, image_size=image_size)
+    block, layers = ref_pr.resnet_spec[num_layers]
+    net = ref_pr.PoseResNet(block, layers, cfg)
+    sd = syn.synthetic_state_dict(net.state_dict(), seed=seed)
+    net.load_state_dict(sd)
+    # calibration: one train-mode pass with momentum 1 sets running stats = batch stats
+    for m in net.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.momentum = 1.0
+    calib = torch.cat(syn.synthetic_views(1, 4, image_size, seed=777), 0)
+    net.train()
+    with torch.no_grad():
+        net(calib)
+    stats = {k: v.detach().numpy().copy() for k, v in net.state_dict().items()
+             if k.endswith('running_mean') or k.endswith('running_var')}
+    os.makedirs(syn.DATA_DIR, exist_ok=True)
+    np.savez_compressed(syn.bn_stats_file(num_layers, image_size), **stats)
+    net.eval()
+    x = torch.cat(syn.synthetic_views(1, batch, image_size, seed=seed + 1), 0)
+    with torch.no_grad():
+        hm, x1, f = net(x)
+    np.savez_compressed(os.path.join(HERE, 'pose_resnet_r%d_%d.npz' % (num_layers, image_size)),
+                        seed=seed, input_seed=seed + 1, batch=batch, heatmaps=hm.numpy(),
+                        x1_mean=x1.mean(dim=(0, 2, 3)).numpy(), x1_slice=x1[:, :8, :8, :8].numpy(),
+                        f_mean=f.mean(dim=(0, 2, 3)).numpy(), f_slice=f[:, :8, :8, :8].numpy())
+    print('pose_resnet r%d@%d: |hm| max %.3f' % (num_layers, image_size, hm.abs().max()))
+
+
+def peaked_heatmaps(n, j, h, w, seed):
+    r = np.random.default_rng(seed)
+    hm = 0.02 * r.standard_normal((n, j, h, w)).astype(np.float32)
+    ys, xs = np.mgrid[0:h, 0:w]
+    for a in range(n):
+        for b in range(j):
+            cy, cx = r.uniform(2, h - 3), r.uniform(2, w - 3)
+            hm[a, b] += np.exp(-((ys - cy) ** 2 + (xs - cx) ** 2) / (2 * 2.0 ** 2)).astype(np.float32)
+    return hm
+
+
+def decode_golden(ref_tf, ref_inf):
+    n, j, h, w = 6, 16, 64, 64
+    hm = peaked_heatmaps(n, j, h, w, seed=5)
+    hm[0, 0] = -1.0 - np.abs(hm[0, 0])          # all-negative map -> coords zeroed
+    hm[0, 1] = 0.0
+    hm[0, 1, 10, 20] = hm[0, 1, 30, 5] = 2.0    # tie -> first index wins
+    hm[0, 2] = 0.0
+    hm[0, 2, 0, 63] = 1.0                       # border peak -> no post-process shift
+    hm[0, 3] = 0.0
+    hm[0, 3, 1, 1] = 1.0                        # px == 1 -> no shift (strict 1 < px)
+    centers = np.random.default_rng(6).uniform(300, 700, size=(n, 2))
+    scales = np.random.default_rng(7).uniform(3.5, 6.0, size=(n, 2))
+    orig, gd = _patched_get_device()
+    torch.Tensor.get_device = gd
+    try:
+        t = torch.from_numpy(hm)
+        sa = ref_tf.generate_integral_preds_2d_th(t)
+        meta = [{'center': torch.from_numpy(centers), 'scale': torch.from_numpy(scales)}]
+        cfg = syn.make_cfg()
+        tb = ref_tf.transform_back_th(cfg, [sa], meta)[0]
+    finally:
+        torch.Tensor.get_device = orig
+    maxp, maxv = ref_inf.get_max_preds(hm.copy())
+    cfg = syn.make_cfg(post_process=True)
+    fp, fv = ref_inf.get_final_preds(cfg, hm.copy(), centers, scales)
+    cfg.TEST.POST_PROCESS = False
+    fp0, _ = ref_inf.get_final_preds(cfg, hm.copy(), centers, scales)
+    affs = np.stack([ref_tf.get_affine_transform(c, s, 0, [w, h], inv=1) for c, s in zip(centers, scales)])
+    np.savez_compressed(os.path.join(HERE, 'decode.npz'), heatmaps=hm, centers=centers, scales=scales,
+                        softargmax=sa.numpy(), transform_back=tb.numpy(), max_preds=maxp, max_vals=maxv,
+                        final_preds=fp, final_vals=fv, final_preds_nopost=fp0, inv_affines=affs)
+    print('decode: softargmax range', sa.min().item(), sa.max().item())
+
+
+def loss_golden(ref_loss):
+    V, B, J = 4, 6, 16
+    r = np.random.default_rng(11)
+    F_dict = syn.fundamental_dict()
+    joints = [torch.tensor(r.uniform(100, 900, size=(B, J, 2)).astype(np.float32), requires_grad=True)
+              for _ in range(V)]
+    weights = [torch.from_numpy((r.uniform(size=(B, J, 1)) > 0.2).astype(np.float32)) for _ in range(V)]
+    subjects = np.array([9, 11, 11, 9, 9, 11])
+    meta = [{'subject': torch.from_numpy(subjects)} for _ in range(V)]
+    out = {}
+    for utw in (True, False):
+        fl = ref_loss.FundamentalLoss.__new__(ref_loss.FundamentalLoss)
+        fl.use_target_weight = utw
+        fl.fundamental_matrix_dict = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in F_dict.items()}
+        for jt in joints:
+            jt.grad = None
+        loss = fl(joints, weights, meta)
+        loss.backward()
+        tag = 'w' if utw else 'nw'
+        out['fund_loss_' + tag] = loss.detach().numpy()
+        out['fund_grad_' + tag] = np.stack([jt.grad.numpy() for jt in joints])
+    pred = torch.tensor(r.standard_normal((B, J, 32, 32)).astype(np.float32), requires_grad=True)
+    gt = torch.from_numpy(r.standard_normal((B, J, 32, 32)).astype(np.float32))
+    tw = torch.from_numpy(r.uniform(size=(B, J, 1)).astype(np.float32))
+    for utw in (True, False):
+        pred.grad = None
+        crit = ref_loss.JointsMSELoss(use_target_weight=utw)
+        loss = crit(pred, gt, tw)
+        loss.backward()
+        tag = 'w' if utw else 'nw'
+        out['mse_loss_' + tag] = loss.detach().numpy()
+        out['mse_grad_' + tag] = pred.grad.numpy()
+    keys = sorted(F_dict)
+    np.savez_compressed(os.path.join(HERE, 'losses.npz'), joints=np.stack([j.detach().numpy() for j in joints]),
+                        weights=np.stack([w.numpy() for w in weights]), subjects=subjects,
+                        F_keys=np.array(keys), F_vals=np.stack([F_dict[k] for k in keys]),
+                        mse_pred=pred.detach().numpy(), mse_gt=gt.numpy(), mse_w=tw.numpy(), **out)
+    print('losses:', {k: float(v) for k, v in out.items() if 'loss' in k})
+
+
+def camera_golden(ref_cam):
+    G = 6
+    cams = syn.group_cameras(G, distortion=True)
+    cams_nd = syn.group_cameras(G, distortion=False)
+    poses = syn.synthetic_poses3d(G, seed=3)
+    proj = np.zeros((G * 4, 16, 2))
+    proj_nd = np.zeros((G * 4, 16, 2))
+    for g in range(G):
+        for v in range(4):
+            proj[g * 4 + v] = ref_cam.project_pose(poses[g], cams[g * 4 + v])
+            proj_nd[g * 4 + v] = ref_cam.project_pose(poses[g], cams_nd[g * 4 + v])
+    cam0 = cams[0]
+    xc = np.stack([ref_cam.world_to_camera_frame(poses[g], cam0['R'], cam0['T']) for g in range(G)])
+    back = np.stack([ref_cam.camera_to_world_frame(xc[g], cam0['R'], cam0['T']) for g in range(G)])
+    np.savez_compressed(os.path.join(HERE, 'cameras.npz'), poses3d=poses, proj=proj, proj_nodist=proj_nd,
+                        cam_frame=xc, world_back=back)
+    print('cameras: proj range', proj.min(), proj.max())
+
+
+def main():
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    ref_pr, ref_tf, ref_inf, ref_loss, ref_cam = _import_reference()
+    pose_resnet_golden(ref_pr, 50, 256, batch=2, seed=0)
+    pose_resnet_golden(ref_pr, 18, 128, batch=2, seed=1)
+    pose_resnet_golden(ref_pr, 152, 384, batch=1, seed=2)
+    decode_golden(ref_tf, ref_inf)
+    loss_golden(ref_loss)
+    camera_golden(ref_cam)
+
+
+if __name__ == '__main__':
+    main()

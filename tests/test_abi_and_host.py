@@ -1,0 +1,170 @@
+"""CPU-side checks: the C-ABI library loads and exports every declared symbol, and the
+host logic (weight packing / sub-pixel deconv decomposition, crop affines, camera
+tables, synthetic data determinism) is right.  No kernel is launched here."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from posu import _native, packing, synthetic as syn
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(REPO, 'include', 'posu.h')).read()
+    src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+    return sorted(set(re.findall(r'\b(posu_\w+)\s*\(', src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.load()
+    declared = _declared_symbols()
+    assert len(declared) >= 18
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert sorted(declared) == _native.exported_symbols()
+    assert lib.posu_abi_version() == 1
+    assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
+
+
+def test_argument_errors_are_reported_without_a_gpu():
+    # shape validation happens on the host before any launch
+    lib = _native.load()
+    st = lib.posu_conv2d_fwd(_native.BF16, None, 1, 8, 8, 8, None, 64, 3, 3, 1, 1, None, None, None, 1, None, 8, 8,
+                             None)
+    assert st == 1 and 'null pointer' in _native.last_error()
+    st = lib.posu_triangulate_dlt(None, None, None, _native.F32, 128, 32, None, 1, 4, 16, 1, None, None)
+    assert st == 1
+
+
+def _im2col_nhwc(x, kh, kw, stride, pad):
+    """[N, H, W, C] -> [N*Ho*Wo, kh*kw*C] with k = (kh, kw, c) (the kernel's A operand)."""
+    n, h, w, c = x.shape
+    xp = F.pad(x.permute(0, 3, 1, 2), (pad, pad, pad, pad)).permute(0, 2, 3, 1)
+    ho = (h + 2 * pad - kh) // stride + 1
+    wo = (w + 2 * pad - kw) // stride + 1
+    cols = []
+    for i in range(kh):
+        for j in range(kw):
+            cols.append(xp[:, i:i + stride * ho:stride, j:j + stride * wo:stride, :])
+    return torch.cat(cols, dim=3).reshape(n * ho * wo, kh * kw * c), ho, wo
+
+
+@pytest.mark.parametrize('cin,cout,k,stride,pad,cin_pad', [(3, 64, 7, 2, 3, 8), (64, 64, 3, 1, 1, 64),
+                                                           (128, 256, 1, 2, 0, 128), (256, 16, 1, 1, 0, 256)])
+def test_conv_weight_packing_is_the_implicit_gemm_B_operand(cin, cout, k, stride, pad, cin_pad):
+    torch.manual_seed(0)
+    w = torch.randn(cout, cin, k, k)
+    x = torch.randn(2, cin, 13, 11)
+    ref = F.conv2d(x, w, stride=stride, padding=pad)
+    bk = 64
+    wp = packing.pack_conv_weight(w, cin_pad, bk, torch.float32)
+    assert wp.shape[0] % 64 == 0 and wp.shape[1] % bk == 0
+    xn = torch.zeros(2, 13, 11, cin_pad)
+    xn[..., :cin] = x.permute(0, 2, 3, 1)
+    A, ho, wo = _im2col_nhwc(xn, k, k, stride, pad)
+    Kd = A.shape[1]
+    out = A @ wp[:cout, :Kd].t()
+    got = out.reshape(2, ho, wo, cout).permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_deconv_subpixel_decomposition_matches_conv_transpose():
+    torch.manual_seed(1)
+    cin, cout, h, w = 16, 24, 5, 7
+    wt = torch.randn(cin, cout, 4, 4)
+    x = torch.randn(2, cin, h, w)
+    ref = F.conv_transpose2d(x, wt, stride=2, padding=1)
+    wp = packing.pack_deconv4x4_weight(wt, 32, torch.float32)  # [4, CoutPad, Kpad]
+    xn = x.permute(0, 2, 3, 1)
+    out = torch.zeros(2, 2 * h, 2 * w, cout)
+    for py in range(2):
+        for px in range(2):
+            # class (py, px): inputs qy + py - 1 + ty -> pad (1-py) before, py after
+            xp = F.pad(xn.permute(0, 3, 1, 2), (1 - px, px, 1 - py, py)).permute(0, 2, 3, 1)
+            A, ho, wo = _im2col_nhwc(xp, 2, 2, 1, 0)
+            assert (ho, wo) == (h, w)
+            o = A @ wp[py * 2 + px, :cout, :4 * cin].t()
+            out[:, py::2, px::2, :] = o.reshape(2, h, w, cout)
+    torch.testing.assert_close(out.permute(0, 3, 1, 2), ref, atol=1e-4, rtol=1e-4)
+
+
+def test_bn_folding_matches_eval_batchnorm():
+    bn = torch.nn.BatchNorm2d(8)
+    bn.eval()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.normal_()
+        bn.running_mean.normal_()
+        bn.running_var.uniform_(0.5, 2)
+    bias = torch.randn(8)
+    x = torch.randn(3, 8, 4, 4)
+    sc, sh = packing.fold_bn(bn, bias)
+    torch.testing.assert_close(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1),
+                               bn(x + bias.view(1, -1, 1, 1)), atol=1e-5, rtol=1e-5)
+
+
+def test_crop_affine_matches_reference(golden):
+    from utils.transforms import get_affine_transform, transform_preds
+    g = golden('decode.npz')
+    for c, s, ref in zip(g['centers'], g['scales'], g['inv_affines']):
+        np.testing.assert_allclose(get_affine_transform(c, s, 0, [64, 64], inv=1), ref, rtol=1e-12, atol=1e-9)
+    pts = g['max_preds'][1]
+    out = transform_preds(pts, g['centers'][1], g['scales'][1], [64, 64])
+    np.testing.assert_allclose(out[:, :2], pts @ g['inv_affines'][1][:, :2].T + g['inv_affines'][1][:, 2],
+                               rtol=1e-9)
+
+
+def test_camera_tables_project_like_the_reference(golden):
+    from multiviews.triangulate import camera_tables
+    from multiviews.cameras import project_pose, camera_to_world_frame, world_to_camera_frame
+    g = golden('cameras.npz')
+    G_ = g['poses3d'].shape[0]
+    cams = syn.group_cameras(G_, distortion=False)
+    M, intr = camera_tables(cams, 4, no_distortion=True)
+    assert M.shape == (G_, 4, 3, 4) and intr.shape == (G_, 4, 9)
+    Xh = np.concatenate([g['poses3d'], np.ones((G_, 16, 1))], axis=2)
+    for gi in range(G_):
+        for v in range(4):
+            uvw = Xh[gi] @ M[gi, v].T
+            np.testing.assert_allclose(uvw[:, :2] / uvw[:, 2:], g['proj_nodist'][gi * 4 + v], rtol=1e-10)
+            np.testing.assert_allclose(project_pose(g['poses3d'][gi], cams[gi * 4 + v]),
+                                       g['proj_nodist'][gi * 4 + v], rtol=1e-12, atol=1e-9)
+    cams_d = syn.group_cameras(G_, distortion=True)
+    for gi in range(G_):
+        np.testing.assert_allclose(project_pose(g['poses3d'][gi], cams_d[gi * 4]), g['proj'][gi * 4], rtol=1e-12,
+                                   atol=1e-9)
+    c0 = cams_d[0]
+    np.testing.assert_allclose(world_to_camera_frame(g['poses3d'][0], c0['R'], c0['T']), g['cam_frame'][0],
+                               rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(camera_to_world_frame(g['cam_frame'][0], c0['R'], c0['T']), g['world_back'][0],
+                               rtol=1e-12, atol=1e-9)
+
+
+def test_synthetic_state_dict_is_deterministic_and_keyed_like_the_reference():
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=50), is_train=False)
+    sd1 = syn.synthetic_state_dict(net.state_dict(), seed=0)
+    sd2 = syn.synthetic_state_dict(net.state_dict(), seed=0)
+    assert list(sd1) == list(net.state_dict())
+    assert len(sd1) == 338  # reference R50 PoseResNet state entries
+    for k in sd1:
+        assert torch.equal(sd1[k], sd2[k])
+    net.load_state_dict(sd1)
+    assert 'deconv_layers.6.weight' in sd1 and 'final_layer.bias' in sd1
+    assert sum(p.numel() for p in net.parameters()) == 33_999_376 or \
+        abs(sum(p.numel() for p in net.parameters()) - 34.0e6) < 0.1e6
+
+
+def test_forward_refuses_cpu_tensors():
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=18, image_size=64), is_train=False).eval()
+    with pytest.raises(RuntimeError, match='cuda'):
+        net(torch.zeros(1, 3, 64, 64))
+    net.train()
+    with pytest.raises(NotImplementedError):
+        net(torch.zeros(1, 3, 64, 64))

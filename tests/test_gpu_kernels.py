@@ -1,0 +1,224 @@
+"""Kernel-level parity on the MI355X: every libposeu.so entry point against the CPU
+oracle / a torch fp32 reference of the same op, on seeded inputs."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import geometry_ref as G
+from posu import ops, packing, synthetic as syn
+from posu._native import BF16, F32
+
+pytestmark = pytest.mark.gpu
+
+
+def _conv_case(cuda, code, n, cin, h, w, cout, k, stride, pad, residual, relu, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    ref = F.conv2d(x, wt, stride=stride, padding=pad) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1)
+    res = None
+    if residual:
+        res = torch.randn_like(ref)
+        ref = ref + res
+    if relu:
+        ref = F.relu(ref)
+    dt = ops.torch_dtype(code)
+    cin_pad = max(8, cin)
+    xd = torch.zeros(n, h, w, cin_pad)
+    xd[..., :cin] = x.permute(0, 2, 3, 1)
+    xd = xd.to(cuda, dt)
+    wp = packing.pack_conv_weight(wt.to(cuda), cin_pad, ops.conv_bk(code), dt)
+    rd = res.permute(0, 2, 3, 1).contiguous().to(cuda, dt) if residual else None
+    out = ops.conv2d_nhwc(xd, wp, cout, k, k, stride, pad, sc.to(cuda), sh.to(cuda), rd, relu, code)
+    torch.cuda.synchronize()
+    return out.float().cpu().permute(0, 3, 1, 2), ref
+
+
+CONV_CASES = [
+    # n, cin, h, w, cout, k, stride, pad, residual, relu
+    (2, 3, 40, 36, 64, 7, 2, 3, False, True),      # stem (Cin padded to 8)
+    (2, 64, 16, 16, 64, 1, 1, 0, False, True),
+    (2, 64, 17, 15, 64, 3, 1, 1, False, True),     # ragged spatial
+    (2, 128, 16, 16, 128, 3, 2, 1, False, True),   # strided 3x3
+    (3, 64, 16, 16, 256, 1, 1, 0, True, True),     # bottleneck tail with residual
+    (2, 256, 8, 8, 512, 1, 2, 0, False, False),    # downsample
+    (1, 512, 4, 4, 512, 3, 1, 1, False, True),     # small M (< one tile)
+]
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv2d_fp32_matches_torch(cuda, case):
+    got, ref = _conv_case(cuda, F32, *case)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv2d_bf16_close_to_torch(cuda, case):
+    got, ref = _conv_case(cuda, BF16, *case)
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 0.03 * scale + 0.02, (err, scale)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+def test_deconv4x4s2_matches_conv_transpose(cuda, code, tol):
+    g = torch.Generator().manual_seed(3)
+    n, cin, h, w, cout = 2, 64, 6, 5, 64
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cin, cout, 4, 4, generator=g) * (2.0 / (cin * 4)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    ref = F.relu(F.conv_transpose2d(x, wt, stride=2, padding=1) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    dt = ops.torch_dtype(code)
+    wp = packing.pack_deconv4x4_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    out = ops.deconv4x4s2_nhwc(xd, wp, cout, sc.to(cuda), sh.to(cuda), True, code)
+    got = out.float().cpu().permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+def test_head1x1_writes_nchw_heatmaps(cuda, code, tol):
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(3, 256, 16, 16, generator=g)
+    wt = torch.randn(16, 256, 1, 1, generator=g) * 0.06
+    b = torch.randn(16, generator=g)
+    ref = F.conv2d(x, wt, b)
+    dt = ops.torch_dtype(code)
+    wp = packing.pack_conv_weight(wt.to(cuda), 256, ops.conv_bk(code), dt)
+    out = ops.head1x1_nchw(x.permute(0, 2, 3, 1).contiguous().to(cuda, dt), wp, 16, b.to(cuda), code)
+    torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_maxpool_pack_unpack(cuda, code):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(2, 3, 33, 30, generator=g)
+    dt = ops.torch_dtype(code)
+    xp = ops.pack_nchw_to_nhwc(x.to(cuda), code, 8)
+    assert xp.shape == (2, 33, 30, 8)
+    back = xp.float().cpu().permute(0, 3, 1, 2)
+    torch.testing.assert_close(back[:, :3], x.to(dt).float())
+    assert torch.all(back[:, 3:] == 0)
+    y = torch.randn(2, 64, 17, 16, generator=g).to(dt)
+    yn = y.permute(0, 2, 3, 1).contiguous().to(cuda)
+    mp = ops.maxpool3x3s2_nhwc(yn, code)
+    ref = F.max_pool2d(y.float(), 3, stride=2, padding=1)
+    torch.testing.assert_close(mp.float().cpu().permute(0, 3, 1, 2), ref)
+    un = ops.nhwc_to_nchw_f32(yn, code)
+    torch.testing.assert_close(un.cpu(), y.float())
+
+
+def test_softargmax_matches_reference_golden(cuda, golden):
+    g = golden('decode.npz')
+    hm = torch.from_numpy(g['heatmaps']).to(cuda)
+    sa = ops.softargmax2d(hm)
+    np.testing.assert_allclose(sa.cpu().numpy(), g['softargmax'], atol=2e-4, rtol=0)
+    T = torch.from_numpy(g['inv_affines']).float()
+    fused = ops.softargmax2d(hm, affine=T.to(cuda))
+    np.testing.assert_allclose(fused.cpu().numpy(), g['transform_back'], atol=5e-3, rtol=0)
+    tb = ops.affine2d(sa, T.to(cuda))
+    np.testing.assert_allclose(tb.cpu().numpy(), g['transform_back'], atol=5e-3, rtol=0)
+
+
+def test_softargmax_backward_matches_autograd(cuda):
+    r = np.random.default_rng(0)
+    hm = torch.from_numpy((0.03 * r.standard_normal((3, 5, 16, 12))).astype(np.float32))
+    T = torch.from_numpy(r.uniform(-2, 2, size=(3, 2, 3)).astype(np.float32))
+    gout = torch.from_numpy(r.standard_normal((3, 5, 2)).astype(np.float32))
+    a = hm.clone().requires_grad_(True)
+    ref = G.softargmax2d(a)
+    ref = torch.einsum('njc,nkc->njk', torch.cat([ref, torch.ones(3, 5, 1)], 2), T)
+    (ref * gout).sum().backward()
+    b = hm.to(cuda).requires_grad_(True)
+    out = ops.softargmax2d(b, affine=T.to(cuda))
+    (out * gout.to(cuda)).sum().backward()
+    torch.testing.assert_close(out.detach().cpu(), ref.detach(), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(b.grad.cpu(), a.grad, atol=1e-4, rtol=1e-3)
+
+
+def test_argmax_decoding_matches_reference_golden(cuda, golden):
+    g = golden('decode.npz')
+    hm = torch.from_numpy(g['heatmaps']).to(cuda)
+    p, v = ops.argmax2d(hm, post_process=False)
+    np.testing.assert_array_equal(p.cpu().numpy(), g['max_preds'])
+    np.testing.assert_array_equal(v.cpu().numpy(), g['max_vals'])
+    T = torch.from_numpy(g['inv_affines'])
+    fp, fv = ops.argmax2d(hm, post_process=True, affine64=T.to(cuda))
+    np.testing.assert_allclose(fp.cpu().numpy(), g['final_preds'], atol=1e-4, rtol=0)
+    np.testing.assert_array_equal(fv.cpu().numpy(), g['final_vals'])
+    fp0, _ = ops.argmax2d(hm, post_process=False, affine64=T.to(cuda))
+    np.testing.assert_allclose(fp0.cpu().numpy(), g['final_preds_nopost'], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize('tag,utw', [('w', True), ('nw', False)])
+def test_epipolar_loss_and_grad_match_reference_golden(cuda, golden, tag, utw):
+    from core.loss import FundamentalLoss
+    g = golden('losses.npz')
+    F_dict = {tuple(int(v) for v in k): f for k, f in zip(g['F_keys'], g['F_vals'])}
+    cfg = syn.make_cfg(use_target_weight_fund=utw)
+    crit = FundamentalLoss(cfg, fundamental_matrix_dict=F_dict, device=cuda)
+    joints = [torch.tensor(j, device=cuda, requires_grad=True) for j in g['joints']]
+    weights = [torch.from_numpy(w).to(cuda) for w in g['weights']]
+    meta = [{'subject': torch.from_numpy(g['subjects'])} for _ in range(4)]
+    loss = crit(joints, weights, meta)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g['fund_loss_' + tag], rtol=1e-5)
+    grad = np.stack([j.grad.cpu().numpy() for j in joints])
+    np.testing.assert_allclose(grad, g['fund_grad_' + tag], rtol=1e-5, atol=1e-9)
+
+
+@pytest.mark.parametrize('tag,utw', [('w', True), ('nw', False)])
+def test_joints_mse_matches_reference_golden(cuda, golden, tag, utw):
+    from core.loss import JointsMSELoss
+    g = golden('losses.npz')
+    pred = torch.tensor(g['mse_pred'], device=cuda, requires_grad=True)
+    loss = JointsMSELoss(utw)(pred, torch.from_numpy(g['mse_gt']).to(cuda), torch.from_numpy(g['mse_w']).to(cuda))
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g['mse_loss_' + tag], rtol=1e-5)
+    np.testing.assert_allclose(pred.grad.cpu().numpy(), g['mse_grad_' + tag], rtol=1e-5, atol=1e-9)
+
+
+def test_triangulation_known_answer_exact(cuda, golden):
+    """Noise-free pinhole projections from the reference camera code -> exact 3-D joints."""
+    from multiviews.triangulate import triangulate_poses
+    g = golden('cameras.npz')
+    n = g['poses3d'].shape[0]
+    cams = syn.group_cameras(n, distortion=False)
+    X = triangulate_poses(cams, g['proj_nodist'], no_distortion=True)
+    assert X.shape == (n, 16, 3) and X.dtype == np.float64
+    np.testing.assert_allclose(X, g['poses3d'], atol=1e-6, rtol=0)  # well inside the 1e-2 mm gate
+
+
+def test_triangulation_matches_oracle_on_noisy_distorted_views(cuda, golden):
+    from multiviews.triangulate import triangulate_poses
+    g = golden('cameras.npz')
+    n = g['poses3d'].shape[0]
+    cams = syn.group_cameras(n, distortion=True)
+    r = np.random.default_rng(1)
+    p2d = g['proj'] + r.normal(0, 3.0, size=g['proj'].shape)
+    vis = (r.uniform(size=p2d.shape[:2]) > 0.15).astype(np.float64)
+    vis[0:4, 2] = 0          # joint unseen everywhere
+    vis[4:7, 7] = 0          # seen by one view only
+    ref = G.triangulate_poses(cams, p2d, joints_vis=vis, no_distortion=False)
+    got = triangulate_poses(cams, p2d, joints_vis=vis, no_distortion=False)
+    np.testing.assert_allclose(got, ref, atol=1e-2, rtol=0)   # 1e-2 mm gate (BASELINE.json)
+    assert np.abs(got - ref).max() < 1e-5
+    assert np.all(got[0, 2] == 0) and np.all(got[1, 7] == 0)
+    # float32 inputs (as the h5 'locations' are) promote exactly
+    got32 = triangulate_poses(cams, p2d.astype(np.float32), joints_vis=vis)
+    ref32 = G.triangulate_poses(cams, p2d.astype(np.float32).astype(np.float64), joints_vis=vis)
+    np.testing.assert_allclose(got32, ref32, atol=1e-2, rtol=0)
+
+
+def test_triangulate_one_point_api(cuda, golden):
+    from multiviews.triangulate import build_multi_camera_system, triangulate_one_point
+    g = golden('cameras.npz')
+    cams = syn.group_cameras(1, distortion=False)
+    system = build_multi_camera_system([('camera_%d' % v, cams[v]) for v in range(4)], no_distortion=True)
+    pts = [('camera_%d' % v, g['proj_nodist'][v, 4]) for v in (0, 2, 3)]
+    X = triangulate_one_point(system, pts)
+    np.testing.assert_allclose(X, g['poses3d'][0, 4], atol=1e-6)

@@ -1,0 +1,90 @@
+"""Model-level parity on the MI355X: the HIP PoseResNet against heatmaps the reference
+produced (fp32 mode, 1e-3 gate from BASELINE.json), the bf16 deviation, the multi-view
+wrapper, and the full 4-view pipeline against the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import geometry_ref as G
+from oracle import pose_resnet_ref as PR
+from posu import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+HEATMAP_TOL = 1e-3  # BASELINE.json: heatmaps within 1e-3 of the reference CPU path
+
+
+def _model(num_layers, size, seed, precision, device):
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=num_layers, image_size=size), is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=seed,
+                                                 bn_stats=syn.load_bn_stats(num_layers, size)))
+    return net.to(device).eval()
+
+
+@pytest.mark.parametrize('num_layers,size', [(18, 128), (50, 256), (152, 384)])
+def test_pose_resnet_fp32_matches_reference_heatmaps(cuda, golden, num_layers, size):
+    g = golden('pose_resnet_r%d_%d.npz' % (num_layers, size))
+    net = _model(num_layers, size, int(g['seed']), 'fp32', cuda)
+    x = torch.cat(syn.synthetic_views(1, int(g['batch']), size, seed=int(g['input_seed'])), 0)
+    with torch.no_grad():
+        hm, x1, f = net(x.to(cuda))
+    assert hm.shape == g['heatmaps'].shape and hm.dtype == torch.float32
+    np.testing.assert_allclose(hm.cpu().numpy(), g['heatmaps'], atol=HEATMAP_TOL, rtol=0)
+    np.testing.assert_allclose(x1.float().mean(dim=(0, 2, 3)).cpu().numpy(), g['x1_mean'], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(x1[:, :8, :8, :8].float().cpu().numpy(), g['x1_slice'], atol=1e-4, rtol=1e-4)
+    np.testing.assert_allclose(f[:, :8, :8, :8].float().cpu().numpy(), g['f_slice'], atol=1e-4, rtol=1e-4)
+
+
+def test_pose_resnet_bf16_deviation_is_bounded(cuda, golden):
+    """bf16 operands / f32 accumulation: report-only gate (loose) on the heatmaps."""
+    g = golden('pose_resnet_r50_256.npz')
+    net = _model(50, 256, int(g['seed']), 'bf16', cuda)
+    x = torch.cat(syn.synthetic_views(1, int(g['batch']), 256, seed=int(g['input_seed'])), 0)
+    with torch.no_grad():
+        hm, _, _ = net(x.to(cuda))
+    err = np.abs(hm.cpu().numpy() - g['heatmaps'])
+    print('bf16 heatmap deviation vs reference: max %.4f mean %.5f' % (err.max(), err.mean()))
+    assert err.mean() < 0.05 and err.max() < 0.6
+
+
+def test_multiview_forward_equals_per_view_forward(cuda):
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    net = _model(18, 128, 1, 'fp32', cuda)
+    mv = get_multiview_pose_net(net, syn.make_cfg(num_layers=18, image_size=128))
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 3, 128, seed=9)]
+    with torch.no_grad():
+        single, multi, low, high = mv(views)
+        assert len(single) == 4 and multi == [] and len(low) == 4 and len(high) == 4
+        for v, hm in zip(views, single):
+            ref, _, _ = net(v)
+            torch.testing.assert_close(hm, ref, atol=1e-5, rtol=1e-5)
+        assert single[0].shape == (3, 16, 32, 32)
+        assert low[0].shape == (3, 256, 32, 32) and high[0].shape == (3, 256, 32, 32)
+
+
+def test_pipeline_matches_cpu_oracle(cuda):
+    """forward -> soft-argmax + affine -> epipolar loss -> triangulation vs the oracle chain."""
+    from posu.pipeline import MultiViewPipeline, synthetic_meta
+    ng, size = 4, 128
+    net = _model(18, size, 1, 'fp32', cuda)
+    meta, host = synthetic_meta(ng, cuda, image_size=size)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, ng, size, seed=21)]
+    with torch.no_grad():
+        hm, coords, loss, X = MultiViewPipeline(net).step(views, meta)
+    torch.cuda.synchronize()
+    # oracle chain on CPU
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    x_all = torch.cat([v.cpu() for v in views], 0)
+    hm_ref, _, _ = PR.pose_resnet_forward(x_all, sd, 18)
+    np.testing.assert_allclose(hm.cpu().numpy(), hm_ref.numpy(), atol=HEATMAP_TOL, rtol=0)
+    sa = G.softargmax2d(hm.cpu())  # decode the device heatmaps: isolates the decode/geometry stages
+    img = G.transform_back(sa, host['centers'].reshape(-1, 2), host['scales'].reshape(-1, 2), [32, 32])
+    np.testing.assert_allclose(coords.reshape(-1, 16, 2).cpu().numpy(), img.numpy(), atol=5e-3, rtol=0)
+    joints = [torch.from_numpy(coords[v].cpu().numpy()) for v in range(4)]
+    ones = [torch.ones(ng, 16, 1) for _ in range(4)]
+    lref = G.fundamental_loss(joints, ones, host['subjects'], host['F_dict'])
+    np.testing.assert_allclose(loss.item(), lref.item(), rtol=1e-4)
+    p2d = coords.permute(1, 0, 2, 3).reshape(ng * 4, 16, 2).double().cpu().numpy()
+    Xref = G.triangulate_poses(host['cams'], p2d.astype(np.float32).astype(np.float64))
+    np.testing.assert_allclose(X.cpu().numpy(), Xref, atol=1e-2, rtol=1e-9)

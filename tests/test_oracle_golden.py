@@ -1,0 +1,123 @@
+"""Pin the CPU oracle against golden vectors produced by the reference itself
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import geometry_ref as G
+from oracle import pose_resnet_ref as PR
+from posu import synthetic as syn
+
+
+def _model_inputs(golden, num_layers, size):
+    g = golden('pose_resnet_r%d_%d.npz' % (num_layers, size))
+    template = {k: v for k, v in _reference_shaped_state(num_layers, size).items()}
+    sd = syn.synthetic_state_dict(template, seed=int(g['seed']), bn_stats=syn.load_bn_stats(num_layers, size))
+    x = torch.cat(syn.synthetic_views(1, int(g['batch']), size, seed=int(g['input_seed'])), 0)
+    return g, sd, x
+
+
+def _reference_shaped_state(num_layers, size):
+    # the build's module tree has the reference's state_dict keys and shapes
+    from models.pose_resnet import get_pose_net
+    return get_pose_net(syn.make_cfg(num_layers=num_layers, image_size=size), is_train=False).state_dict()
+
+
+@pytest.mark.parametrize('num_layers,size', [(18, 128), (50, 256), (152, 384)])
+def test_oracle_pose_resnet_matches_reference(golden, num_layers, size):
+    torch.set_num_threads(8)
+    g, sd, x = _model_inputs(golden, num_layers, size)
+    hm, x1, f = PR.pose_resnet_forward(x, sd, num_layers)
+    assert hm.shape == g['heatmaps'].shape
+    np.testing.assert_allclose(hm.numpy(), g['heatmaps'], atol=2e-5, rtol=0)
+    np.testing.assert_allclose(x1.mean(dim=(0, 2, 3)).numpy(), g['x1_mean'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(x1[:, :8, :8, :8].numpy(), g['x1_slice'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(f.mean(dim=(0, 2, 3)).numpy(), g['f_mean'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(f[:, :8, :8, :8].numpy(), g['f_slice'], atol=1e-5, rtol=1e-5)
+
+
+def test_oracle_decode_matches_reference(golden):
+    g = golden('decode.npz')
+    hm = torch.from_numpy(g['heatmaps'])
+    sa = G.softargmax2d(hm)
+    np.testing.assert_allclose(sa.numpy(), g['softargmax'], atol=1e-5, rtol=0)
+    tb = G.transform_back(sa, g['centers'], g['scales'], [64, 64])
+    np.testing.assert_allclose(tb.numpy(), g['transform_back'], atol=1e-3, rtol=0)
+    mp, mv = G.get_max_preds(g['heatmaps'].copy())
+    np.testing.assert_array_equal(mp, g['max_preds'])
+    np.testing.assert_array_equal(mv, g['max_vals'])
+    fp, fv = G.get_final_preds(g['heatmaps'].copy(), g['centers'], g['scales'], post_process=True)
+    np.testing.assert_allclose(fp, g['final_preds'], atol=1e-4, rtol=0)
+    fp0, _ = G.get_final_preds(g['heatmaps'].copy(), g['centers'], g['scales'], post_process=False)
+    np.testing.assert_allclose(fp0, g['final_preds_nopost'], atol=1e-4, rtol=0)
+    for i in range(len(g['centers'])):
+        np.testing.assert_allclose(G.crop_affine(g['centers'][i], g['scales'][i], [64, 64]), g['inv_affines'][i],
+                                   rtol=1e-12, atol=1e-9)
+
+
+def _F_dict(g):
+    return {tuple(int(v) for v in k): f for k, f in zip(g['F_keys'], g['F_vals'])}
+
+
+@pytest.mark.parametrize('tag,utw', [('w', True), ('nw', False)])
+def test_oracle_losses_match_reference(golden, tag, utw):
+    g = golden('losses.npz')
+    joints = [torch.tensor(j, requires_grad=True) for j in g['joints']]
+    weights = [torch.from_numpy(w) for w in g['weights']]
+    loss = G.fundamental_loss(joints, weights, g['subjects'], _F_dict(g), use_target_weight=utw)
+    loss.backward()
+    np.testing.assert_allclose(loss.item(), g['fund_loss_' + tag], rtol=1e-5)
+    np.testing.assert_allclose(np.stack([j.grad.numpy() for j in joints]), g['fund_grad_' + tag], rtol=1e-5,
+                               atol=1e-9)
+    pred = torch.tensor(g['mse_pred'], requires_grad=True)
+    ml = G.joints_mse(pred, torch.from_numpy(g['mse_gt']), torch.from_numpy(g['mse_w']) if utw else None)
+    ml.backward()
+    np.testing.assert_allclose(ml.item(), g['mse_loss_' + tag], rtol=1e-5)
+    np.testing.assert_allclose(pred.grad.numpy(), g['mse_grad_' + tag], rtol=1e-5, atol=1e-9)
+
+
+def test_oracle_camera_projection_matches_reference(golden):
+    g = golden('cameras.npz')
+    G_ = g['poses3d'].shape[0]
+    cams = syn.group_cameras(G_, distortion=True)
+    cams_nd = syn.group_cameras(G_, distortion=False)
+    for gi in range(G_):
+        for v in range(4):
+            np.testing.assert_allclose(G.project_pose(g['poses3d'][gi], cams[gi * 4 + v]), g['proj'][gi * 4 + v],
+                                       rtol=1e-12, atol=1e-9)
+            np.testing.assert_allclose(G.project_pose(g['poses3d'][gi], cams_nd[gi * 4 + v]),
+                                       g['proj_nodist'][gi * 4 + v], rtol=1e-12, atol=1e-9)
+
+
+def test_oracle_triangulation_known_answer(golden):
+    """Noise-free pinhole projections (made by the reference's cameras.project_pose)
+    triangulate back to the known 3-D joints."""
+    g = golden('cameras.npz')
+    G_ = g['poses3d'].shape[0]
+    cams = syn.group_cameras(G_, distortion=False)
+    X = G.triangulate_poses(cams, g['proj_nodist'], no_distortion=True)
+    np.testing.assert_allclose(X, g['poses3d'], atol=1e-6, rtol=0)
+    # joints visible in fewer than two views stay at the origin (triangulate.py:95-96)
+    vis = np.ones((G_ * 4, 16))
+    vis[0:4, 3] = 0
+    vis[1:4, 5] = 0
+    X2 = G.triangulate_poses(cams, g['proj_nodist'], joints_vis=vis, no_distortion=True)
+    assert np.all(X2[0, 3] == 0) and np.all(X2[0, 5] == 0)
+    np.testing.assert_allclose(np.delete(X2[0], [3, 5], axis=0), np.delete(g['poses3d'][0], [3, 5], axis=0),
+                               atol=1e-6)
+
+
+def test_oracle_undistort_inverts_opencv_model():
+    """The restated pymvg undistortion inverts the OpenCV distortion model it targets."""
+    K = np.array([[1145.0, 0, 512.0], [0, 1145.0, 515.0], [0, 0, 1]])
+    D = np.array([-0.207, 0.247, -0.0009, -0.0016, -0.003])
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        x, y = rng.uniform(-0.2, 0.2, size=2)
+        r2 = x * x + y * y
+        rad = 1 + D[0] * r2 + D[1] * r2 ** 2 + D[4] * r2 ** 3
+        xd = x * rad + 2 * D[2] * x * y + D[3] * (r2 + 2 * x * x)
+        yd = y * rad + D[2] * (r2 + 2 * y * y) + 2 * D[3] * x * y
+        u = np.array([xd * K[0, 0] + K[0, 2], yd * K[1, 1] + K[1, 2]])
+        und = G.undistort_point(u, K, D)
+        np.testing.assert_allclose(und, [x * K[0, 0] + K[0, 2], y * K[1, 1] + K[1, 2]], atol=0.05)
