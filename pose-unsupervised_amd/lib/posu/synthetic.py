@@ -49,6 +49,14 @@ def bn_stats_file(num_layers, image_size):
     return os.path.join(DATA_DIR, 'synthetic_bn_r%d_%d.npz' % (num_layers, image_size))
 
 
+def _is_residual_tail(name, template):
+    parts = name.split('.')
+    if len(parts) != 4 or not parts[0].startswith('layer') or not parts[2].startswith('bn'):
+        return False
+    nxt = '%s.%s.bn%d.weight' % (parts[0], parts[1], int(parts[2][2:]) + 1)
+    return nxt not in template
+
+
 def synthetic_state_dict(template, seed=0, bn_stats=None):
     """template: a state_dict (names + shapes) of the reference-shaped model."""
     out = {}
@@ -70,7 +78,13 @@ def synthetic_state_dict(template, seed=0, bn_stats=None):
             gain = 1.0 if name.startswith('final_layer') else 2.0
             v = (r.standard_normal(shape) * np.sqrt(gain / fan_in)).astype(np.float32)
         elif name.endswith('weight'):  # BN gamma
-            v = r.uniform(0.5, 1.5, size=shape).astype(np.float32)
+            if _is_residual_tail(name, template):
+                # last BN of a residual branch: small gamma keeps every block close to the
+                # identity, so the random network is well conditioned (perturbations do
+                # not grow exponentially with depth, as they would not in a trained net)
+                v = r.uniform(0.1, 0.3, size=shape).astype(np.float32)
+            else:
+                v = r.uniform(0.5, 1.5, size=shape).astype(np.float32)
         else:  # BN beta / conv bias
             v = (0.1 * r.standard_normal(shape)).astype(np.float32)
         out[name] = torch.from_numpy(v)

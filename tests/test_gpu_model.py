@@ -31,9 +31,11 @@ def test_pose_resnet_fp32_matches_reference_heatmaps(cuda, golden, num_layers, s
         hm, x1, f = net(x.to(cuda))
     assert hm.shape == g['heatmaps'].shape and hm.dtype == torch.float32
     np.testing.assert_allclose(hm.cpu().numpy(), g['heatmaps'], atol=HEATMAP_TOL, rtol=0)
-    np.testing.assert_allclose(x1.float().mean(dim=(0, 2, 3)).cpu().numpy(), g['x1_mean'], atol=1e-4, rtol=1e-4)
-    np.testing.assert_allclose(x1[:, :8, :8, :8].float().cpu().numpy(), g['x1_slice'], atol=1e-4, rtol=1e-4)
-    np.testing.assert_allclose(f[:, :8, :8, :8].float().cpu().numpy(), g['f_slice'], atol=1e-4, rtol=1e-4)
+    # intermediate features: same 1e-3 gate as the heatmaps
+    np.testing.assert_allclose(x1.float().mean(dim=(0, 2, 3)).cpu().numpy(), g['x1_mean'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(x1[:, :8, :8, :8].float().cpu().numpy(), g['x1_slice'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(f.float().mean(dim=(0, 2, 3)).cpu().numpy(), g['f_mean'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(f[:, :8, :8, :8].float().cpu().numpy(), g['f_slice'], atol=1e-3, rtol=0)
 
 
 def test_pose_resnet_bf16_deviation_is_bounded(cuda, golden):
@@ -60,7 +62,7 @@ def test_multiview_forward_equals_per_view_forward(cuda):
             ref, _, _ = net(v)
             torch.testing.assert_close(hm, ref, atol=1e-5, rtol=1e-5)
         assert single[0].shape == (3, 16, 32, 32)
-        assert low[0].shape == (3, 256, 32, 32) and high[0].shape == (3, 256, 32, 32)
+        assert low[0].shape == (3, 64, 32, 32) and high[0].shape == (3, 256, 32, 32)  # BasicBlock: 64-ch layer1
 
 
 def test_pipeline_matches_cpu_oracle(cuda):
