@@ -50,6 +50,13 @@ int posu_abi_version(void);
 int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W,
                            void* y, int Cpad, void* stream);
 
+/* NCHW fp32 -> space-to-depth NHWC for the stem: y[n][i][j][(dy*2+dx)*C + c] =
+ * x[n][c][2i+dy][2j+dx], zero above 4C.  The 7x7/s2/p3 stem conv then runs as a
+ * 4x4/s1 conv with top/left padding 2 over this grid (K = 16 * Cpad instead of
+ * 49 * Cpad taps of a Cin-padded 7x7 window).  H, W even; y: [N, H/2, W/2, Cpad]. */
+int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W,
+                       void* y, int Cpad, void* stream);
+
 /* NHWC activations -> NCHW fp32 (for returning x1 / f in the reference
  * layout: lib/models/pose_resnet.py:205). */
 int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
@@ -68,12 +75,25 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *      CoutPad = round_up(Cout, 64), Kpad = round_up(KH*KW*C, posu_conv_bk(dtype)).
  *   scale/shift: [Cout] f32 (may be NULL: scale 1, shift 0).
  *   residual: NULL or [N, Ho, Wo, Cout] dtype.
- *   y: [N, Ho, Wo, Cout] dtype. */
+ *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
+ *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied). */
 int posu_conv_bk(int dtype);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,
                     int relu, void* y, int Ho, int Wo, void* stream);
+
+/* Two 1x1 convolutions summed into one output (Bottleneck conv3/bn3 + the
+ * downsample conv/bn residual branch, lib/models/pose_resnet.py:90-99, 136-141):
+ *   y[n,i,j,:] = act( W[:, :C] x[n,i,j,:] + W[:, C:] x2[n, i*stride2, j*stride2, :]
+ *                     * scale + shift )
+ * with the two BN scales pre-multiplied into W by the caller.
+ *   x: [N, H, W, C]; x2: [N, H2, W2, C2]; C, C2 multiples of posu_conv_bk(dtype);
+ *   w: [CoutPad][C + C2]; y: [N, H, W, Cout]. */
+int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                          const void* x2, int H2, int W2, int C2, int stride2,
+                          const void* w, int Cout, const float* scale, const float* shift,
+                          int relu, void* y, void* stream);
 
 /* ConvTranspose2d(kernel 4, stride 2, padding 1, output_padding 0) as four
  * stride-1 2x2 sub-pixel convolutions (one per output parity class) in one

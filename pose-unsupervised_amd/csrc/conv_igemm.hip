@@ -3,12 +3,13 @@
 // GEMM view of one launch:  rows m = output pixels (n, oy, ox) of the launch grid,
 //                           cols   = output channels,
 //                           k      = (kh, kw, ci) taps of the input window.
-// A[m][k] is gathered on the fly from the NHWC input (16-byte channel chunks),
-// B[k][co] is the packed weight [CoutPad][Kpad] (K contiguous, zero padded).
+// A[m][k] is gathered on the fly from the NHWC input (16-byte channel chunks,
+// out-of-window taps read as zeros through a buffer descriptor), B[k][co] is the
+// packed weight [CoutPad][Kpad] (K contiguous, zero padded).
 //
-// Block tile BM x BN, K-tile of 128 bytes per row (64 bf16 / 32 f32), 256 threads
-// = 4 waves in a 2x2 grid, each wave owning a (BM/2) x (BN/2) accumulator tile made
-// of 16x16 MFMA tiles:
+// Block tile BM x BN (BM in {64, 128}, BN in {64, 128}), K-tile of 128 bytes per row
+// (64 bf16 / 32 f32), 256 threads = 4 waves in a 2x2 grid, each wave owning a
+// (BM/2) x (BN/2) accumulator tile made of 16x16 MFMA tiles:
 //   bf16: v_mfma_f32_16x16x32_bf16 (one 16-B chunk per lane = one MFMA k-step)
 //   f32 : v_mfma_f32_16x16x4_f32   (one 16-B chunk per lane = four MFMA k-steps;
 //         the k order inside a chunk is permuted identically for A and B, which
@@ -19,9 +20,14 @@
 // XOR-swizzled by (row>>1)&7, which makes the 16-lane ds_read_b128 groups of the
 // fragment reads conflict-free.
 //
-// Epilogue: accumulators (+BN scale/shift) are staged through LDS as an f32 tile,
-// then written as 16-byte NHWC chunks with optional residual add + ReLU (Bottleneck
-// tail, lib/models/pose_resnet.py:90-99), or as NCHW f32 heatmaps (+bias) for the
+// DUAL variant (Bottleneck tail with a downsample branch, pose_resnet.py:90-99,
+// 136-141): two 1x1 sources share one accumulator,
+//   y = act( [W3*s3 | Wd*sd] . [conv2_out(m) ; block_in(n, oy*s, ox*s)] + (b3 + bd) ),
+// so the downsample output is never written to / re-read from HBM.
+//
+// Epilogue: residual chunks are prefetched into registers first; the accumulators
+// (+BN scale/shift) are staged through LDS as an f32 tile, then written as 16-byte
+// NHWC chunks with residual add + ReLU, or as NCHW f32 heatmaps (+bias) for the
 // final 1x1 layer (pose_resnet.py:126-132).
 //
 // ConvTranspose2d(4, s2, p1) runs as 4 sub-pixel 2x2 stride-1 convolutions, one per
@@ -35,13 +41,15 @@ namespace {
 
 struct ConvGeom {
   const void* x;
+  const void* x2;  // DUAL: second 1x1 source
   const void* w;
   const float* scale;
   const float* shift;
   const void* res;
   void* y;
   int N, H, W, C, logC;
-  int Ho, Wo, M;  // launch grid: rows = N*Ho*Wo
+  int H2, W2, C2, stride2, K1;  // DUAL: source-2 geometry, K offset where it starts
+  int Ho, Wo, M;                // launch grid: rows = N*Ho*Wo
   int Cout, CoutPad, K, Kpad;
   int KH, KW, stride, pad_h, pad_w;
   int relu;
@@ -108,12 +116,45 @@ constexpr int smem_bytes() {
   return (2 * (BM + BN) * 128) > (BM * (BN + 4) * 4) ? (2 * (BM + BN) * 128) : (BM * (BN + 4) * 4);
 }
 
-template <typename T, int BM, int BN>
+constexpr int kOOB = 0x7ffffff0;  // buffer offset past num_records: the load returns zeros
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource descriptor (base, num_records = bytes, raw dword format) built from
+// wave-uniform values, kept in SGPRs.
+__device__ __forceinline__ u32x4 make_srd(const void* base, int bytes) {
+  const unsigned long long p = reinterpret_cast<unsigned long long>(base);
+  u32x4 r;
+  r.x = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(p));
+  r.y = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(p >> 32));
+  r.z = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(bytes));
+  r.w = 0x00020000u;
+  return r;
+}
+
+// One 16-B-per-lane LDS-DMA: buffer_load_dwordx4 ... lds writes lane l's 16 bytes to
+// LDS address lds + 16*l (wave-uniform `lds` in M0); offsets past num_records load 0.
+// Issued from inline asm so hipcc neither waits for it before unrelated ds_reads of
+// the other LDS buffer nor drains it early: the kernel retires it itself with
+// s_waitcnt vmcnt(0) before the barrier that precedes the reads.
+__device__ __forceinline__ void dma16(u32x4 srd, int voff, unsigned lds) {
+  unsigned keep;
+  asm volatile(
+      "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(srd), "s"(lds)
+      : "memory");
+}
+
+template <typename T, int BM, int BN, int WGM, bool DUAL>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int E = O::E;
+  constexpr int ES = static_cast<int>(sizeof(T));
   constexpr int BK = 8 * E;  // 128-byte LDS rows
-  constexpr int WTM = BM / 2, WTN = BN / 2;
+  constexpr int WGN = 4 / WGM;                // wave grid WGM x WGN
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per K-tile
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
@@ -121,7 +162,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / WGN, wn = wid % WGN;
   const int r16 = lane & 15, q = lane >> 4;
 
   // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a
@@ -144,11 +185,22 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
     wp += static_cast<size_t>(cls) * g.CoutPad * g.Kpad;
   }
   const T* __restrict__ xp = reinterpret_cast<const T*>(g.x);
+  const u32x4 xrs = make_srd(xp, g.N * g.H * g.W * g.C * ES);
+  const u32x4 wrs = make_srd(wp, g.CoutPad * g.Kpad * ES);
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
 
-  // ---- per-thread A rows (pixel decode once)
-  const int cA = tid & 7;
-  int hb[RA], wb[RA], nb[RA];
+  // ---- LDS-DMA staging.  One buffer_load_dwordx4 ... lds per wave writes 1 KiB =
+  // 8 LDS rows x 8 chunks, lane l at byte 16*l: row (tid >> 3) + 32*i, physical
+  // chunk tid & 7.  The XOR swizzle of the fragment reads is applied on the SOURCE:
+  // that lane fetches logical chunk cL = (tid & 7) ^ ((row >> 1) & 7), which is the
+  // same for every i because 32*i does not touch bits 1..3 of the row.
+  const int cL = (tid & 7) ^ ((tid >> 4) & 7);
   const int HoWo = g.Ho * g.Wo;
+  int hb[RA], wb[RA], nb[RA];   // generic window gather
+  int o1[RA], o2[RA];           // DUAL: byte offsets of the two 1x1 sources
+  u32x4 x2rs = xrs;
+  if constexpr (DUAL) x2rs = make_srd(g.x2, g.N * g.H2 * g.W2 * g.C2 * ES);
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
     const int m = m0 + (tid >> 3) + 32 * i;
@@ -158,64 +210,73 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
       hb[i] = oy * g.stride - pad_h;
       wb[i] = ox * g.stride - pad_w;
       nb[i] = n * g.H * g.W * g.C;
+      if constexpr (DUAL) {
+        o1[i] = (m * g.C + cL * E) * ES;
+        o2[i] = (((n * g.H2 + oy * g.stride2) * g.W2 + ox * g.stride2) * g.C2 + cL * E) * ES;
+      }
     } else {
       hb[i] = -(1 << 28);
       wb[i] = 0;
       nb[i] = 0;
+      if constexpr (DUAL) {
+        o1[i] = kOOB;
+        o2[i] = kOOB;
+      }
     }
   }
+  // K-tile -> (kh, kw, ci) of this thread's chunk.  Three regimes:
+  //  tap_uniform: C % BK == 0, one tap per K-tile (all 3x3 / 1x1 / deconv layers);
+  //  row_uniform: KW*C == BK, one kernel row per K-tile (space-to-depth stem);
+  //  generic    : per-chunk tap decode (C = 8 direct stem, f32 stem).
   const bool tap_uniform = (g.C % BK) == 0;
+  const bool row_uniform = !tap_uniform && g.KW * g.C == BK;
+  const int kw_row = (cL * E) >> g.logC, ci_row = (cL * E) & (g.C - 1);
   const int nk = g.Kpad / BK;
+  const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;  // weight row offset (elements) for i = 0
 
-  // Out-of-window taps read through a buffer descriptor at an offset past
-  // num_records: the hardware returns zeros, so the gather needs no branches.
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<T*>(xp), static_cast<short>(0), g.N * g.H * g.W * g.C * static_cast<int>(sizeof(T)),
-      0x00020000);
-  constexpr int OOB = 0x7ffffff0;
-
-  uint4 ra[RA], rb[RB];
-  // global -> registers for K-tile KT (macro, so the staging arrays stay in VGPRs)
-#define POSU_LOAD_TILE(KT)                                                                          \
+  // global -> LDS (async DMA) for K-tile KT into buffer BUF
+#define POSU_DMA_TILE(KT, BUF)                                                                      \
   {                                                                                                 \
     const int kbase = (KT) * BK;                                                                    \
-    int kh, kw, ci;                                                                                 \
-    bool kvalid;                                                                                    \
-    if (tap_uniform) {                                                                              \
-      const int tap = kbase >> g.logC;                                                              \
-      kh = tap / g.KW;                                                                              \
-      kw = tap - kh * g.KW;                                                                         \
-      ci = (kbase & (g.C - 1)) + cA * E;                                                            \
-      kvalid = true;                                                                                \
+    const unsigned As_ = lds0 + (BUF) * STAGE + wid_u * 1024;                                       \
+    const unsigned Bs_ = As_ + A_BYTES;                                                             \
+    if constexpr (DUAL) {                                                                           \
+      const bool first = kbase < g.K1;                                                              \
+      _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                              \
+        const int o = first ? o1[i] : o2[i];                                                        \
+        const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;                 \
+        dma16(first ? xrs : x2rs, off, As_ + i * 4096);                                             \
+      }                                                                                             \
     } else {                                                                                        \
-      const int k = kbase + cA * E;                                                                 \
-      const int tap = k >> g.logC;                                                                  \
-      kh = tap / g.KW;                                                                              \
-      kw = tap - kh * g.KW;                                                                         \
-      ci = k & (g.C - 1);                                                                           \
-      kvalid = k < g.K;                                                                             \
+      int kh, kw, ci;                                                                               \
+      bool kvalid = true;                                                                           \
+      if (tap_uniform) {                                                                            \
+        const int tap = kbase >> g.logC;                                                            \
+        kh = tap / g.KW;                                                                            \
+        kw = tap - kh * g.KW;                                                                       \
+        ci = (kbase & (g.C - 1)) + cL * E;                                                          \
+      } else if (row_uniform) {                                                                     \
+        kh = (KT);                                                                                  \
+        kw = kw_row;                                                                                \
+        ci = ci_row;                                                                                \
+      } else {                                                                                      \
+        const int k = kbase + cL * E;                                                               \
+        const int tap = k >> g.logC;                                                                \
+        kh = tap / g.KW;                                                                            \
+        kw = tap - kh * g.KW;                                                                       \
+        ci = k & (g.C - 1);                                                                         \
+        kvalid = k < g.K;                                                                           \
+      }                                                                                             \
+      _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                              \
+        const int hi = hb[i] + kh, wi = wb[i] + kw;                                                 \
+        const bool ok = kvalid && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&         \
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);                     \
+        const int off = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB;                      \
+        dma16(xrs, off, As_ + i * 4096);                                                            \
+      }                                                                                             \
     }                                                                                               \
-    _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                                \
-      const int hi = hb[i] + kh, wi = wb[i] + kw;                                                   \
-      const bool ok = kvalid && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&           \
-                      static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);                       \
-      const int off = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * static_cast<int>(sizeof(T)) : OOB; \
-      const auto t = __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0);                         \
-      ra[i] = make_uint4(t[0], t[1], t[2], t[3]);                                                   \
-    }                                                                                               \
-    _Pragma("unroll") for (int i = 0; i < RB; ++i) {                                                \
-      const int nrow = n0 + (tid >> 3) + 32 * i;                                                    \
-      rb[i] = *reinterpret_cast<const uint4*>(wp + static_cast<size_t>(nrow) * g.Kpad + kbase + cA * E); \
-    }                                                                                               \
-  }
-#define POSU_STORE_TILE(BUF)                                                                        \
-  {                                                                                                 \
-    char* As_ = smem + (BUF) * STAGE;                                                               \
-    char* Bs_ = As_ + A_BYTES;                                                                      \
-    _Pragma("unroll") for (int i = 0; i < RA; ++i)                                                  \
-      *reinterpret_cast<uint4*>(As_ + swz((tid >> 3) + 32 * i, cA)) = ra[i];                        \
     _Pragma("unroll") for (int i = 0; i < RB; ++i)                                                  \
-      *reinterpret_cast<uint4*>(Bs_ + swz((tid >> 3) + 32 * i, cA)) = rb[i];                        \
+      dma16(wrs, (wbrow + 32 * i * g.Kpad + kbase) * ES, Bs_ + i * 4096);                           \
   }
   // MFMAs over one LDS K-tile
 #define POSU_COMPUTE(BUF)                                                                           \
@@ -240,53 +301,68 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  POSU_LOAD_TILE(0);
-  POSU_STORE_TILE(0);
+  // two LDS buffers: the DMA of K-tile t+1 overlaps the MFMAs of tile t; one
+  // vmcnt(0) + barrier per K-tile retires it before anyone reads it
+  POSU_DMA_TILE(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int kt = 0; kt + 1 < nk; ++kt) {
     const int cur = kt & 1;
-    POSU_LOAD_TILE(kt + 1);
+    POSU_DMA_TILE(kt + 1, cur ^ 1);
     POSU_COMPUTE(cur);
-    POSU_STORE_TILE(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
   POSU_COMPUTE((nk - 1) & 1);
-  __syncthreads();
+#undef POSU_DMA_TILE
+#undef POSU_COMPUTE
 
-  // ---- epilogue: stage the f32 tile in LDS (after the barrier above)
   constexpr int LD = BN + 4;
   float* Cs = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * WTN + j * 16 + r16;
-    const int co = n0 + col;
-    float sc = 1.f, sh = 0.f;
-    if (co < g.Cout) {
-      if (g.scale) sc = g.scale[co];
-      if (g.shift) sh = g.shift[co];
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wm * WTM + i * 16 + q * 4 + e;
-        Cs[row * LD + col] = acc[i][j][e] * sc + sh;
-      }
-  }
-  __syncthreads();
-
   if (g.mode == 0) {
-    constexpr int CPR = BN / E;  // output chunks per row
+    constexpr int CPR = BN / E;               // output chunks per tile row
+    constexpr int ITER = BM * CPR / 256;      // chunks per thread
     T* __restrict__ yp = reinterpret_cast<T*>(g.y);
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
-    for (int idx = tid; idx < BM * CPR; idx += 256) {
+    size_t off[ITER];
+    bool ok[ITER];
+    uint4 rv[ITER];
+    // decode output chunks and issue the residual loads before the LDS staging
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = tid + it * 256;
       const int row = idx / CPR, cc = idx - row * CPR;
       const int m = m0 + row, co = n0 + cc * E;
-      if (m >= g.M || co >= g.Cout) continue;
-      const int n = m / HoWo, rem = m - n * HoWo;
+      ok[it] = m < g.M && co < g.Cout;
+      const int mm = ok[it] ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
       const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-      const size_t off =
-          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout + co;
+      off[it] = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout +
+                (ok[it] ? co : 0);
+      rv[it] = make_uint4(0, 0, 0, 0);
+      if (rp && ok[it]) rv[it] = *reinterpret_cast<const uint4*>(rp + off[it]);
+    }
+    __syncthreads();  // all waves are done reading the last K-tile
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 16 + r16;
+      const int co = n0 + col;
+      float sc = 1.f, sh = 0.f;
+      if (co < g.Cout) {
+        if (g.scale) sc = g.scale[co];
+        if (g.shift) sh = g.shift[co];
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cs[(wm * WTM + i * 16 + q * 4 + e) * LD + col] = acc[i][j][e] * sc + sh;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      if (!ok[it]) continue;
+      const int idx = tid + it * 256;
+      const int row = idx / CPR, cc = idx - row * CPR;
       float v[E];
 #pragma unroll
       for (int e = 0; e < E; e += 4) {
@@ -298,7 +374,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
       }
       if (rp) {
         float r[E];
-        O::load_vals(*reinterpret_cast<const uint4*>(rp + off), r);
+        O::load_vals(rv[it], r);
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] += r[e];
       }
@@ -306,9 +382,21 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      *reinterpret_cast<uint4*>(yp + off) = O::store_vals(v);
+      *reinterpret_cast<uint4*>(yp + off[it]) = O::store_vals(v);
     }
   } else {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 16 + r16;
+      const int co = n0 + col;
+      const float sh = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Cs[(wm * WTM + i * 16 + q * 4 + e) * LD + col] = acc[i][j][e] + sh;
+    }
+    __syncthreads();
     // NCHW f32 (heatmap head): consecutive threads walk pixels of one channel
     float* __restrict__ yp = reinterpret_cast<float*>(g.y);
     const int ncol = min(BN, g.Cout - n0);
@@ -322,9 +410,6 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
       yp[(static_cast<size_t>(n) * g.Cout + n0 + col) * HoWo + pix] = v;
     }
   }
-#undef POSU_LOAD_TILE
-#undef POSU_STORE_TILE
-#undef POSU_COMPUTE
 }
 
 int ilog2(int v) {
@@ -333,30 +418,53 @@ int ilog2(int v) {
   return ((1 << l) == v) ? l : -1;
 }
 
-template <typename T>
+template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
+  // tile choice: 64-channel layers take 256 x 64 tiles (four waves stacked along M,
+  // 64 x 64 each); wider layers 128 x 128; grids that would not give every CU two
+  // blocks drop to 64-row tiles.
   const bool wide = g.CoutPad % 128 == 0;
-  constexpr int BM = 128;
-  const int BN = wide ? 128 : 64;
-  g.mtiles = (g.M + BM - 1) / BM;
+  auto blocks = [&](int bm, int bn) {
+    return static_cast<long long>((g.M + bm - 1) / bm) * (g.CoutPad / bn) * nclass;
+  };
+  int BM, BN;
+  if (!wide) {
+    BN = 64;
+    if (blocks(256, 64) >= 1024) BM = 256;
+    else if (blocks(128, 64) >= 512) BM = 128;
+    else BM = 64;
+  } else {
+    BN = 128;
+
+    BM = blocks(128, 128) >= 512 ? 128 : 64;
+  }
   g.ntiles = g.CoutPad / BN;
+  g.mtiles = (g.M + BM - 1) / BM;
   dim3 grid(g.mtiles * g.ntiles, 1, nclass);
-  if (wide)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BM, 128>), grid, dim3(256), 0, s, g);
+  if (BM == 256)
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 64, 4, DUAL>), grid, dim3(256), 0, s, g);
+  else if (BM == 128 && BN == 128)
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 2, DUAL>), grid, dim3(256), 0, s, g);
+  else if (BM == 128)
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 64, 2, DUAL>), grid, dim3(256), 0, s, g);
+  else if (BN == 128)
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 128, 2, DUAL>), grid, dim3(256), 0, s, g);
   else
-    hipLaunchKernelGGL((conv_igemm_kernel<T, BM, 64>), grid, dim3(256), 0, s, g);
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 64, 2, DUAL>), grid, dim3(256), 0, s, g);
   return check_launch(what);
 }
 
+template <bool DUAL>
 int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what) {
   hipStream_t s = as_stream(stream);
-  if (dtype == POSU_BF16) return launch<uint16_t>(g, nclass, s, what);
-  if (dtype == POSU_F32) return launch<float>(g, nclass, s, what);
+  if (dtype == POSU_BF16) return launch<uint16_t, DUAL>(g, nclass, s, what);
+  if (dtype == POSU_F32) return launch<float, DUAL>(g, nclass, s, what);
   set_error(std::string(what) + ": unsupported dtype");
   return POSU_ERR_ARG;
 }
 
 int bk_of(int dtype) { return dtype == POSU_F32 ? 32 : 64; }
+int esz_of(int dtype) { return dtype == POSU_F32 ? 4 : 2; }
 
 int common_checks(int dtype, const void* x, const void* w, const void* y, int N, int H, int W, int C,
                   int Cout, const char* what) {
@@ -364,10 +472,26 @@ int common_checks(int dtype, const void* x, const void* w, const void* y, int N,
   POSU_REQUIRE(x && w && y, std::string(what) + ": null pointer");
   POSU_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0, std::string(what) + ": empty shape");
   POSU_REQUIRE(C >= 8 && ilog2(C) >= 0, std::string(what) + ": C must be a power of two >= 8");
-  const long long esz = dtype == POSU_F32 ? 4 : 2;
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * esz < (1LL << 31) - 256,
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * esz_of(dtype) < (1LL << 31) - 256,
                std::string(what) + ": input exceeds the 2 GiB buffer-descriptor range");
   return POSU_OK;
+}
+
+ConvGeom base_geom(const void* x, int N, int H, int W, int C, const void* w, int Cout, int dtype) {
+  ConvGeom g{};
+  g.x = x;
+  g.w = w;
+  g.N = N;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.logC = ilog2(C);
+  g.Cout = Cout;
+  g.CoutPad = round_up(Cout, 64);
+  g.stride = 1;
+  g.KH = g.KW = 1;
+  (void)dtype;
+  return g;
 }
 
 }  // namespace
@@ -384,26 +508,17 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   const int E = dtype == POSU_F32 ? 4 : 8;
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
-  POSU_REQUIRE(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
-               "posu_conv2d_fwd: Ho/Wo inconsistent with the window");
+  POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
+               "posu_conv2d_fwd: Ho/Wo larger than the window allows");
   POSU_REQUIRE(static_cast<long long>(N) * Ho * Wo * Cout < (1LL << 31), "posu_conv2d_fwd: output too large");
-  ConvGeom g{};
-  g.x = x;
-  g.w = w;
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
   g.shift = shift;
   g.res = residual;
   g.y = y;
-  g.N = N;
-  g.H = H;
-  g.W = W;
-  g.C = C;
-  g.logC = ilog2(C);
   g.Ho = Ho;
   g.Wo = Wo;
   g.M = N * Ho * Wo;
-  g.Cout = Cout;
-  g.CoutPad = round_up(Cout, 64);
   g.K = KH * KW * C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.KH = KH;
@@ -412,11 +527,40 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   g.pad_h = pad;
   g.pad_w = pad;
   g.relu = relu;
-  g.deconv = 0;
   g.out_H = Ho;
   g.out_W = Wo;
-  g.mode = 0;
-  return dispatch(dtype, g, 1, stream, "posu_conv2d_fwd");
+  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd");
+}
+
+extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2, int H2,
+                                     int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
+                                     const float* shift, int relu, void* y, void* stream) {
+  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
+  if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
+  const int BK = bk_of(dtype);
+  POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
+  POSU_REQUIRE(stride2 > 0 && (H - 1) * stride2 < H2 && (W - 1) * stride2 < W2,
+               "posu_conv1x1_dual_fwd: source-2 grid too small for the output grid");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * Cout < (1LL << 31), "posu_conv1x1_dual_fwd: output too large");
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
+  g.x2 = x2;
+  g.H2 = H2;
+  g.W2 = W2;
+  g.C2 = C2;
+  g.stride2 = stride2;
+  g.K1 = C;
+  g.scale = scale;
+  g.shift = shift;
+  g.y = y;
+  g.Ho = H;
+  g.Wo = W;
+  g.M = N * H * W;
+  g.K = C + C2;
+  g.Kpad = C + C2;
+  g.relu = relu;
+  g.out_H = H;
+  g.out_W = W;
+  return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_fwd");
 }
 
 extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
@@ -427,65 +571,37 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
                "posu_deconv4x4s2_fwd: output too large");
-  ConvGeom g{};
-  g.x = x;
-  g.w = w;
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
   g.shift = shift;
-  g.res = nullptr;
   g.y = y;
-  g.N = N;
-  g.H = H;
-  g.W = W;
-  g.C = C;
-  g.logC = ilog2(C);
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.Cout = Cout;
-  g.CoutPad = round_up(Cout, 64);
   g.K = 4 * C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.KH = 2;
   g.KW = 2;
-  g.stride = 1;
   g.relu = relu;
   g.deconv = 1;
   g.out_H = 2 * H;
   g.out_W = 2 * W;
-  g.mode = 0;
-  return dispatch(dtype, g, 4, stream, "posu_deconv4x4s2_fwd");
+  return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_fwd");
 }
 
 extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
                                      int Cout, const float* bias, float* y, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_head1x1_nchw_fwd")) return st;
-  ConvGeom g{};
-  g.x = x;
-  g.w = w;
-  g.scale = nullptr;
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.shift = bias;
-  g.res = nullptr;
   g.y = y;
-  g.N = N;
-  g.H = H;
-  g.W = W;
-  g.C = C;
-  g.logC = ilog2(C);
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.Cout = Cout;
-  g.CoutPad = round_up(Cout, 64);
   g.K = C;
   g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = 1;
-  g.KW = 1;
-  g.stride = 1;
-  g.relu = 0;
-  g.deconv = 0;
   g.out_H = H;
   g.out_W = W;
   g.mode = 1;
-  return dispatch(dtype, g, 1, stream, "posu_head1x1_nchw_fwd");
+  return dispatch<false>(dtype, g, 1, stream, "posu_head1x1_nchw_fwd");
 }

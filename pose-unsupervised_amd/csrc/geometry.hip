@@ -107,108 +107,129 @@ __global__ __launch_bounds__(256) void epipolar_bwd_kernel(const float* __restri
 
 constexpr int kMaxViews = 16;
 
+// pymvg CameraModel.undistort (OpenCV fixed point, 5 iterations); returns the input
+// unchanged when every coefficient is zero, as pymvg does
+__device__ __forceinline__ void undistort_px(const double* c, double& u, double& v) {
+  const double fx = c[0], fy = c[1], cx = c[2], cy = c[3];
+  const double k1 = c[4], k2 = c[5], p1 = c[6], p2 = c[7], k3 = c[8];
+  if (fabs(k1) + fabs(k2) + fabs(p1) + fabs(p2) + fabs(k3) == 0.0) return;
+  const double xd = (u - cx) / fx, yd = (v - cy) / fy;
+  double xx = xd, yy = yd;
+#pragma unroll
+  for (int it = 0; it < 5; ++it) {
+    const double r2 = xx * xx + yy * yy;
+    const double icdist = 1.0 / (1.0 + ((k3 * r2 + k2) * r2 + k1) * r2);
+    const double dX = 2.0 * p1 * xx * yy + p2 * (r2 + 2.0 * xx * xx);
+    const double dY = p1 * (r2 + 2.0 * yy * yy) + 2.0 * p2 * xx * yy;
+    xx = (xd - dX) * icdist;
+    yy = (yd - dY) * icdist;
+  }
+  u = xx * fx + cx;
+  v = yy * fy + cy;
+}
+
+// Rows of invisible views are zero: a zero row adds nothing to A^T A, so the right
+// singular vectors of the remaining rows are unchanged.  ROWS is a compile-time
+// bound, so A lives in registers (no scratch) for the 4-view case.
+template <int VMAX>
 __global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ Mall,
                                                          const double* __restrict__ intr,
                                                          const void* __restrict__ xyv, int xy_dtype, int sg,
                                                          int sv, const unsigned char* __restrict__ vis, int G, int V,
                                                          int J, int undistort, double* __restrict__ X) {
+  constexpr int ROWS = 2 * VMAX;
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= G * J) return;
   const int g = t / J, k = t - g * J;
-  double A[2 * kMaxViews][4];
-  int rows = 0;
-  for (int v = 0; v < V; ++v) {
-    const size_t gv = static_cast<size_t>(g) * V + v;
-    if (vis && !vis[gv * J + k]) continue;
-    double u, vv;
-    const size_t xoff = static_cast<size_t>(g) * sg + static_cast<size_t>(v) * sv + 2 * k;
-    if (xy_dtype == POSU_F64) {
-      const double* p = static_cast<const double*>(xyv) + xoff;
-      u = p[0];
-      vv = p[1];
-    } else {
-      const float* p = static_cast<const float*>(xyv) + xoff;
-      u = p[0];
-      vv = p[1];
-    }
-    const double* c = intr + gv * 9;
-    if (undistort) {
-      const double fx = c[0], fy = c[1], cx = c[2], cy = c[3];
-      const double k1 = c[4], k2 = c[5], p1 = c[6], p2 = c[7], k3 = c[8];
-      // pymvg returns the input untouched when every coefficient is zero
-      if (fabs(k1) + fabs(k2) + fabs(p1) + fabs(p2) + fabs(k3) != 0.0) {
-        const double xd = (u - cx) / fx, yd = (vv - cy) / fy;
-        double xx = xd, yy = yd;
-        for (int it = 0; it < 5; ++it) {
-          const double r2 = xx * xx + yy * yy;
-          const double icdist = 1.0 / (1.0 + ((k3 * r2 + k2) * r2 + k1) * r2);
-          const double dX = 2.0 * p1 * xx * yy + p2 * (r2 + 2.0 * xx * xx);
-          const double dY = p1 * (r2 + 2.0 * yy * yy) + 2.0 * p2 * xx * yy;
-          xx = (xd - dX) * icdist;
-          yy = (yd - dY) * icdist;
-        }
-        u = xx * fx + cx;
-        vv = yy * fy + cy;
+  double A[ROWS][4];
+  int nvis = 0;
+#pragma unroll
+  for (int v = 0; v < VMAX; ++v) {
+    const size_t gv = static_cast<size_t>(g) * V + (v < V ? v : 0);
+    const bool on = v < V && (!vis || vis[gv * J + k]);
+    double u = 0.0, vv = 0.0;
+    if (on) {
+      const size_t xoff = static_cast<size_t>(g) * sg + static_cast<size_t>(v) * sv + 2 * k;
+      if (xy_dtype == POSU_F64) {
+        u = static_cast<const double*>(xyv)[xoff];
+        vv = static_cast<const double*>(xyv)[xoff + 1];
+      } else {
+        u = static_cast<const float*>(xyv)[xoff];
+        vv = static_cast<const float*>(xyv)[xoff + 1];
       }
+      if (undistort) undistort_px(intr + gv * 9, u, vv);
+      ++nvis;
     }
     const double* M = Mall + gv * 12;
 #pragma unroll
-    for (int cidx = 0; cidx < 4; ++cidx) {
-      A[rows][cidx] = u * M[8 + cidx] - M[cidx];
-      A[rows + 1][cidx] = vv * M[8 + cidx] - M[4 + cidx];
+    for (int c = 0; c < 4; ++c) {
+      A[2 * v][c] = on ? u * M[8 + c] - M[c] : 0.0;
+      A[2 * v + 1][c] = on ? vv * M[8 + c] - M[4 + c] : 0.0;
     }
-    rows += 2;
   }
   double* out = X + static_cast<size_t>(t) * 3;
-  if (rows < 4) {  // fewer than two views: the reference leaves zeros
+  if (nvis < 2) {  // fewer than two views: the reference leaves zeros (triangulate.py:95-96)
     out[0] = out[1] = out[2] = 0.0;
     return;
   }
-  // one-sided Jacobi: rotate column pairs of A until mutually orthogonal; V accumulates
+  // one-sided Jacobi: rotate column pairs of A until mutually orthogonal; Vm accumulates
   double Vm[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
   for (int sweep = 0; sweep < 30; ++sweep) {
     bool rotated = false;
+#pragma unroll
     for (int p = 0; p < 3; ++p) {
+#pragma unroll
       for (int q = p + 1; q < 4; ++q) {
         double alpha = 0, beta = 0, gamma = 0;
-        for (int r = 0; r < rows; ++r) {
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
           alpha += A[r][p] * A[r][p];
           beta += A[r][q] * A[r][q];
           gamma += A[r][p] * A[r][q];
         }
-        if (fabs(gamma) <= 1e-15 * sqrt(alpha * beta) || gamma == 0.0) continue;
-        rotated = true;
-        const double zeta = (beta - alpha) / (2.0 * gamma);
-        const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-        const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
-        for (int r = 0; r < rows; ++r) {
-          const double ap = A[r][p], aq = A[r][q];
-          A[r][p] = cs * ap - sn * aq;
-          A[r][q] = sn * ap + cs * aq;
-        }
-        for (int r = 0; r < 4; ++r) {
-          const double vp = Vm[r][p], vq = Vm[r][q];
-          Vm[r][p] = cs * vp - sn * vq;
-          Vm[r][q] = sn * vp + cs * vq;
+        if (gamma != 0.0 && fabs(gamma) > 1e-15 * sqrt(alpha * beta)) {
+          rotated = true;
+          const double zeta = (beta - alpha) / (2.0 * gamma);
+          const double tt = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+          const double cs = 1.0 / sqrt(1.0 + tt * tt), sn = cs * tt;
+#pragma unroll
+          for (int r = 0; r < ROWS; ++r) {
+            const double ap = A[r][p], aq = A[r][q];
+            A[r][p] = cs * ap - sn * aq;
+            A[r][q] = sn * ap + cs * aq;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const double vp = Vm[r][p], vq = Vm[r][q];
+            Vm[r][p] = cs * vp - sn * vq;
+            Vm[r][q] = sn * vp + cs * vq;
+          }
         }
       }
     }
     if (!rotated) break;
   }
-  int best = 0;
-  double bn = INFINITY;
-  for (int cidx = 0; cidx < 4; ++cidx) {
-    double nrm = 0;
-    for (int r = 0; r < rows; ++r) nrm += A[r][cidx] * A[r][cidx];
-    if (nrm < bn) {
-      bn = nrm;
-      best = cidx;
+  double nrm[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    nrm[c] = 0;
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) nrm[c] += A[r][c] * A[r][c];
+  }
+  double v0 = Vm[0][0], v1 = Vm[1][0], v2 = Vm[2][0], v3 = Vm[3][0], bn = nrm[0];
+#pragma unroll
+  for (int c = 1; c < 4; ++c) {
+    if (nrm[c] < bn) {
+      bn = nrm[c];
+      v0 = Vm[0][c];
+      v1 = Vm[1][c];
+      v2 = Vm[2][c];
+      v3 = Vm[3][c];
     }
   }
-  const double h = Vm[3][best];
-  out[0] = Vm[0][best] / h;
-  out[1] = Vm[1][best] / h;
-  out[2] = Vm[2][best] / h;
+  out[0] = v0 / v3;
+  out[1] = v1 / v3;
+  out[2] = v2 / v3;
 }
 
 }  // namespace
@@ -248,8 +269,12 @@ extern "C" int posu_triangulate_dlt(const double* M, const double* intr, const v
   POSU_REQUIRE(xy_stride_g >= 0 && xy_stride_v >= 0, "posu_triangulate_dlt: negative xy stride");
   if (G == 0) return POSU_OK;
   const int total = G * J;
-  hipLaunchKernelGGL(triangulate_kernel, dim3((total + 63) / 64), dim3(64), 0, as_stream(stream), M, intr, xy,
-                     xy_dtype, xy_stride_g, xy_stride_v, vis, G, V, J, undistort, X);
+  if (V <= 4)
+    hipLaunchKernelGGL(triangulate_kernel<4>, dim3((total + 63) / 64), dim3(64), 0, as_stream(stream), M, intr, xy,
+                       xy_dtype, xy_stride_g, xy_stride_v, vis, G, V, J, undistort, X);
+  else
+    hipLaunchKernelGGL(triangulate_kernel<kMaxViews>, dim3((total + 63) / 64), dim3(64), 0, as_stream(stream), M,
+                       intr, xy, xy_dtype, xy_stride_g, xy_stride_v, vis, G, V, J, undistort, X);
   return check_launch("posu_triangulate_dlt");
 }
 

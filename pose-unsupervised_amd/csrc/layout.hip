@@ -64,6 +64,35 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, 
   }
 }
 
+// space-to-depth 2x2 pack for the stem: y[n][y][x][(dy*2+dx)*C + c] = x[n][c][2y+dy][2x+dx]
+// (one thread per output pixel and 16-B chunk)
+template <typename T>
+__global__ __launch_bounds__(256) void pack_s2d_kernel(const float* __restrict__ x, int N, int C, int H, int W,
+                                                       T* __restrict__ y, int Cpad) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = Cpad / E;
+  const int Hs = H / 2, Ws = W / 2;
+  const long long total = static_cast<long long>(N) * Hs * Ws * chunks;
+  const long long HW = static_cast<long long>(H) * W;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const int xs = static_cast<int>(pix % Ws);
+    const long long t = pix / Ws;
+    const int ys = static_cast<int>(t % Hs);
+    const long long n = t / Hs;
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int cc = ch * E + e;
+      const int sub = cc / C, c = cc - sub * C;
+      v[e] = sub < 4 ? x[(n * C + c) * HW + static_cast<long long>(2 * ys + (sub >> 1)) * W + 2 * xs + (sub & 1)]
+                     : 0.f;
+    }
+    *reinterpret_cast<uint4*>(y + pix * Cpad + ch * E) = Vec<T>::pack(v);
+  }
+}
+
 // one thread per (pixel, 16-B input chunk); writes E channel planes
 template <typename T>
 __global__ __launch_bounds__(256) void unpack_kernel(const T* __restrict__ x, int N, int H, int W, int C,
@@ -146,6 +175,28 @@ extern "C" int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, i
     return POSU_ERR_ARG;
   }
   return check_launch("posu_pack_nchw_to_nhwc");
+}
+
+extern "C" int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W, void* y, int Cpad,
+                                  void* stream) {
+  POSU_REQUIRE(x && y, "posu_pack_s2d_nchw: null pointer");
+  POSU_REQUIRE(N > 0 && C > 0 && H > 1 && W > 1 && H % 2 == 0 && W % 2 == 0 && 4 * C <= Cpad,
+               "posu_pack_s2d_nchw: bad shape (H, W even, 4C <= Cpad)");
+  hipStream_t s = as_stream(stream);
+  const long long pix = static_cast<long long>(N) * (H / 2) * (W / 2);
+  if (dtype == POSU_BF16) {
+    POSU_REQUIRE(Cpad % 8 == 0, "posu_pack_s2d_nchw: Cpad % 8 != 0");
+    hipLaunchKernelGGL(pack_s2d_kernel<uint16_t>, dim3(grid_for(pix * Cpad / 8)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<uint16_t*>(y), Cpad);
+  } else if (dtype == POSU_F32) {
+    POSU_REQUIRE(Cpad % 4 == 0, "posu_pack_s2d_nchw: Cpad % 4 != 0");
+    hipLaunchKernelGGL(pack_s2d_kernel<float>, dim3(grid_for(pix * Cpad / 4)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<float*>(y), Cpad);
+  } else {
+    set_error("posu_pack_s2d_nchw: unsupported dtype");
+    return POSU_ERR_ARG;
+  }
+  return check_launch("posu_pack_s2d_nchw");
 }
 
 extern "C" int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C, float* y,

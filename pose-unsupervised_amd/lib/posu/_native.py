@@ -28,7 +28,9 @@ _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _p],
+    'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _p],
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
+    'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],
     'posu_conv_bk': [_i],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],

@@ -41,6 +41,17 @@ def pack_nchw_to_nhwc(x, code, cpad, out=None):
     return out
 
 
+def pack_s2d_nchw(x, code, cpad, out=None):
+    """[N, C, H, W] f32 -> space-to-depth [N, H/2, W/2, cpad] (channel (dy*2+dx)*C + c)."""
+    require_cuda(x)
+    x = x.contiguous().float()
+    n, c, h, w = x.shape
+    if out is None:
+        out = torch.empty((n, h // 2, w // 2, cpad), dtype=torch_dtype(code), device=x.device)
+    call('posu_pack_s2d_nchw', code, ptr(x), n, c, h, w, ptr(out), cpad, stream_of(x.device))
+    return out
+
+
 def nhwc_to_nchw_f32(x, code):
     require_cuda(x)
     n, h, w, c = x.shape
@@ -50,14 +61,27 @@ def nhwc_to_nchw_f32(x, code):
 
 
 # ------------------------------------------------------------------ conv ops
-def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None):
+def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None, out_hw=None):
     n, h, w, c = x.shape
     ho = (h + 2 * pad - kh) // stride + 1
     wo = (w + 2 * pad - kw) // stride + 1
+    if out_hw is not None:
+        ho, wo = out_hw
     if out is None:
         out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
     call('posu_conv2d_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, kh, kw, stride, pad,
          ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, stream_of(x.device))
+    return out
+
+
+def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None):
+    """act(W[:, :C] x + W[:, C:] x2[::stride2, ::stride2] + shift) (two 1x1 sources, one output)."""
+    n, h, w, c = x.shape
+    _, h2, w2, c2 = x2.shape
+    if out is None:
+        out = torch.empty((n, h, w, cout), dtype=x.dtype, device=x.device)
+    call('posu_conv1x1_dual_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
+         None, ptr(shift), int(relu), ptr(out), stream_of(x.device))
     return out
 
 

@@ -27,6 +27,40 @@ def pack_conv_weight(w, cin_pad, bk, dtype):
     return out.to(dtype).contiguous()
 
 
+def pack_stem_s2d_weight(w, cpad, bk, dtype):
+    """7x7 / stride 2 / pad 3 stem weight [Cout, Cin, 7, 7] -> the equivalent 4x4 / stride 1 /
+    top-left pad 2 weight over the 2x2 space-to-depth input (channel (dy*2+dx)*Cin + c):
+    tap (ty, tx, dy, dx) is the 7x7 tap (2ty+dy-1, 2tx+dx-1) (zero where that is -1)."""
+    cout, cin, kh, kw = w.shape
+    if (kh, kw) != (7, 7) or 4 * cin > cpad:
+        raise NotImplementedError('space-to-depth stem needs a 7x7 kernel and 4*Cin <= cpad')
+    wf = w.detach().float()
+    ws = torch.zeros((cout, 4, 4, cpad), dtype=torch.float32, device=w.device)
+    for ty in range(4):
+        for tx in range(4):
+            for dy in range(2):
+                for dx in range(2):
+                    r, c = 2 * ty + dy - 1, 2 * tx + dx - 1
+                    if 0 <= r < 7 and 0 <= c < 7:
+                        sub = dy * 2 + dx
+                        ws[:, ty, tx, sub * cin:(sub + 1) * cin] = wf[:, :, r, c]
+    k = 16 * cpad
+    out = torch.zeros((round_up(cout, COUT_ALIGN), round_up(k, bk)), dtype=torch.float32, device=w.device)
+    out[:cout, :k] = ws.reshape(cout, k)
+    return out.to(dtype).contiguous()
+
+
+def pack_dual_1x1_weight(w_a, scale_a, w_b, scale_b, dtype):
+    """Two 1x1 conv weights with their BN scales folded in, concatenated along K:
+    [CoutPad][Ca + Cb] = [W_a * s_a | W_b * s_b] (fp64 product, one rounding)."""
+    cout = w_a.shape[0]
+    a = w_a.detach().double().reshape(cout, -1) * scale_a.double().view(-1, 1)
+    b = w_b.detach().double().reshape(cout, -1) * scale_b.double().view(-1, 1)
+    out = torch.zeros((round_up(cout, COUT_ALIGN), a.shape[1] + b.shape[1]), dtype=torch.float64, device=w_a.device)
+    out[:cout] = torch.cat([a, b], dim=1)
+    return out.to(dtype).contiguous()
+
+
 def pack_deconv4x4_weight(w, bk, dtype):
     cin, cout, kh, kw = w.shape
     if (kh, kw) != (4, 4):

@@ -17,9 +17,11 @@ torch.cuda.CUDAGraph (hipGraph) by the caller.
 import torch
 
 from . import ops
-from .packing import fold_bn, pack_conv_weight, pack_deconv4x4_weight
+from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dual_1x1_weight,
+                      pack_stem_s2d_weight)
 
-STEM_CIN_PAD = 8
+STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
+STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
 
 class _Conv:
@@ -42,21 +44,49 @@ class _Conv:
                                self.shift, residual, self.relu, code)
 
 
+class _DualTail:
+    """Bottleneck conv3/bn3 + downsample conv/bn as one two-source 1x1 GEMM."""
+    __slots__ = ('w', 'shift', 'cout', 'stride2')
+
+    def __init__(self, conv3, bn3, dconv, dbn, code):
+        s3, b3 = fold_bn(bn3, conv3.bias)
+        sd, bd = fold_bn(dbn, dconv.bias)
+        self.w = pack_dual_1x1_weight(conv3.weight, s3, dconv.weight, sd, ops.torch_dtype(code))
+        self.shift = (b3.double() + bd.double()).float().contiguous()
+        self.cout = conv3.weight.shape[0]
+        self.stride2 = dconv.stride[0]
+
+    def __call__(self, mid, x, code):
+        return ops.conv1x1_dual_nhwc(mid, x, self.stride2, self.w, self.cout, self.shift, True, code)
+
+
 class _Block:
-    __slots__ = ('convs', 'down')
+    __slots__ = ('convs', 'down', 'dual')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
         self.convs = []
-        for i, nm in enumerate(names):
-            self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
         self.down = None
-        if blk.downsample is not None:
-            self.down = _Conv(blk.downsample[0], blk.downsample[1], False, code, bk)
+        self.dual = None
+        ds = blk.downsample
+        if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
+                blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
+            for nm in names[:2]:
+                self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
+            self.dual = _DualTail(blk.conv3, blk.bn3, ds[0], ds[1], code)
+            return
+        for nm in names:
+            self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
+        if ds is not None:
+            self.down = _Conv(ds[0], ds[1], False, code, bk)
 
     def __call__(self, x, code):
-        res = self.down(x, code) if self.down is not None else x
         out = x
+        if self.dual is not None:
+            for c in self.convs:
+                out = c(out, code)
+            return self.dual(out, x, code)
+        res = self.down(x, code) if self.down is not None else x
         for c in self.convs[:-1]:
             out = c(out, code)
         return self.convs[-1](out, code, residual=res)
@@ -83,6 +113,8 @@ class PoseResNetPlan:
         self.code = code
         bk = ops.conv_bk(code)
         self.stem = _Conv(net.conv1, net.bn1, True, code, bk, cin_pad=STEM_CIN_PAD)
+        # the same stem as a 4x4/s1 conv over the 2x2 space-to-depth input (even sizes)
+        self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, STEM_S2D_PAD, bk, ops.torch_dtype(code))
         self.layers = [[_Block(b, code, bk) for b in layer] for layer in
                        (net.layer1, net.layer2, net.layer3, net.layer4)]
         mods = list(net.deconv_layers)
@@ -98,18 +130,31 @@ class PoseResNetPlan:
         self.njoints = fl.weight.shape[0]
 
     def pack_input(self, views):
-        """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N)."""
+        """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N):
+        space-to-depth [N, H/2, W/2, 16] for even H, W, else [N, H, W, 8]."""
         n, _, h, w = views[0].shape
-        x = torch.empty((n * len(views), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(self.code),
-                        device=views[0].device)
+        s2d = h % 2 == 0 and w % 2 == 0
+        shape = (n * len(views), h // 2, w // 2, STEM_S2D_PAD) if s2d else (n * len(views), h, w, STEM_CIN_PAD)
+        x = torch.empty(shape, dtype=ops.torch_dtype(self.code), device=views[0].device)
         for i, v in enumerate(views):
-            ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n])
+            if s2d:
+                ops.pack_s2d_nchw(v, self.code, STEM_S2D_PAD, out=x[i * n:(i + 1) * n])
+            else:
+                ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n])
         return x
 
-    def run(self, x):
-        """NHWC packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC)."""
+    def run_stem(self, x):
         code = self.code
-        x = self.stem(x, code)
+        if x.shape[3] == STEM_S2D_PAD:
+            st = self.stem
+            return ops.conv2d_nhwc(x, self.stem_s2d_w, st.cout, 4, 4, 1, 2, st.scale, st.shift, None, True, code,
+                                   out_hw=(x.shape[1], x.shape[2]))
+        return self.stem(x, code)
+
+    def run(self, x):
+        """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC)."""
+        code = self.code
+        x = self.run_stem(x)
         x = ops.maxpool3x3s2_nhwc(x, code)
         x1 = None
         for li, layer in enumerate(self.layers):

@@ -168,3 +168,42 @@ def test_forward_refuses_cpu_tensors():
     net.train()
     with pytest.raises(NotImplementedError):
         net(torch.zeros(1, 3, 64, 64))
+
+
+def _s2d(x, cpad):
+    n, c, h, w = x.shape
+    out = torch.zeros(n, h // 2, w // 2, cpad)
+    for dy in range(2):
+        for dx in range(2):
+            sub = dy * 2 + dx
+            out[..., sub * c:(sub + 1) * c] = x[:, :, dy::2, dx::2].permute(0, 2, 3, 1)
+    return out
+
+
+def test_space_to_depth_stem_equals_7x7_stride2_conv():
+    torch.manual_seed(2)
+    x = torch.randn(2, 3, 20, 18)
+    w = torch.randn(64, 3, 7, 7)
+    ref = F.conv2d(x, w, stride=2, padding=3)
+    wp = packing.pack_stem_s2d_weight(w, 16, 64, torch.float32)
+    xs = _s2d(x, 16)
+    # 4x4 / stride 1 / top-left pad 2 (bottom/right pad 1) over the s2d grid
+    xp = F.pad(xs.permute(0, 3, 1, 2), (2, 1, 2, 1)).permute(0, 2, 3, 1)
+    A, ho, wo = _im2col_nhwc(xp, 4, 4, 1, 0)
+    assert (ho, wo) == (10, 9)
+    got = (A @ wp[:64, :256].t()).reshape(2, ho, wo, 64).permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_dual_tail_weight_folds_both_bn_branches():
+    torch.manual_seed(3)
+    mid, cin, cout = 16, 24, 32
+    w3, wd = torch.randn(cout, mid, 1, 1), torch.randn(cout, cin, 1, 1)
+    s3, sd = torch.rand(cout) + 0.5, torch.rand(cout) + 0.5
+    a, x = torch.randn(2, mid, 5, 5), torch.randn(2, cin, 10, 10)
+    ref = F.conv2d(a, w3) * s3.view(1, -1, 1, 1) + F.conv2d(x, wd, stride=2) * sd.view(1, -1, 1, 1)
+    wp = packing.pack_dual_1x1_weight(w3, s3, wd, sd, torch.float32)
+    assert wp.shape == (64, mid + cin)
+    feat = torch.cat([a.permute(0, 2, 3, 1), x[:, :, ::2, ::2].permute(0, 2, 3, 1)], dim=3)
+    got = (feat @ wp[:cout].t()).permute(0, 3, 1, 2)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)

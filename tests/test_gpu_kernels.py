@@ -222,3 +222,40 @@ def test_triangulate_one_point_api(cuda, golden):
     pts = [('camera_%d' % v, g['proj_nodist'][v, 4]) for v in (0, 2, 3)]
     X = triangulate_one_point(system, pts)
     np.testing.assert_allclose(X, g['poses3d'][0, 4], atol=1e-6)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+def test_s2d_stem_matches_torch(cuda, code, tol):
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 3, 36, 40, generator=g)
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    sc = torch.rand(64, generator=g) + 0.5
+    sh = torch.randn(64, generator=g) * 0.1
+    ref = F.relu(F.conv2d(x, w, stride=2, padding=3) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    dt = ops.torch_dtype(code)
+    xs = ops.pack_s2d_nchw(x.to(cuda), code, 16)
+    assert xs.shape == (2, 18, 20, 16)
+    wp = packing.pack_stem_s2d_weight(w.to(cuda), 16, ops.conv_bk(code), dt)
+    out = ops.conv2d_nhwc(xs, wp, 64, 4, 4, 1, 2, sc.to(cuda), sh.to(cuda), None, True, code, out_hw=(18, 20))
+    torch.testing.assert_close(out.float().cpu().permute(0, 3, 1, 2), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('stride', [1, 2])
+def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
+    g = torch.Generator().manual_seed(7)
+    mid, cin, cout, h = 64, 128, 256, 9
+    a = torch.relu(torch.randn(3, mid, h, h, generator=g))
+    x = torch.randn(3, cin, h * stride, h * stride, generator=g)
+    w3 = torch.randn(cout, mid, 1, 1, generator=g) * 0.1
+    wd = torch.randn(cout, cin, 1, 1, generator=g) * 0.1
+    s3, sd = torch.rand(cout, generator=g) + 0.5, torch.rand(cout, generator=g) + 0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    ref = F.relu(F.conv2d(a, w3) * s3.view(1, -1, 1, 1) + F.conv2d(x, wd, stride=stride) * sd.view(1, -1, 1, 1)
+                 + b.view(1, -1, 1, 1))
+    dt = ops.torch_dtype(code)
+    wp = packing.pack_dual_1x1_weight(w3.to(cuda), s3.to(cuda), wd.to(cuda), sd.to(cuda), dt)
+    out = ops.conv1x1_dual_nhwc(a.permute(0, 2, 3, 1).contiguous().to(cuda, dt),
+                                x.permute(0, 2, 3, 1).contiguous().to(cuda, dt), stride, wp, cout, b.to(cuda), True,
+                                code)
+    torch.testing.assert_close(out.float().cpu().permute(0, 3, 1, 2), ref, atol=tol, rtol=tol)
