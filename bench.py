@@ -47,6 +47,8 @@ def parse():
     ap.add_argument('--size', type=int, default=256)
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--chunks', type=int, default=1,
+                    help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     return ap.parse_args()
@@ -136,7 +138,7 @@ def main():
 
     # two stages so the network can be timed on its own with events between replays
     def stage_net():
-        return plan.run(plan.pack_input(views))[0]
+        return plan.run(plan.pack_input(views), chunks=args.chunks, keep_features=False)[0]
 
     def stage_geo(hm):
         coords = ops.softargmax2d(hm, beta=100.0, affine=meta.affines).view(4, args.groups, hm.shape[1], 2)
@@ -234,7 +236,7 @@ def main():
                                % (args.groups, args.size, args.size, args.layers),
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
-                   'hipgraph': use_graph},
+                   'hipgraph': use_graph, 'chunks': args.chunks},
         'network_ms': round(net_ms, 4), 'decode_geometry_ms': round(geo_ms, 4),
         'groups_per_s': round(value / 4, 2),
         'roofline': roof, 'cpu_baseline': cpu,

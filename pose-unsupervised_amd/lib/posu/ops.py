@@ -74,7 +74,7 @@ def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu,
     return out
 
 
-def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None):
+def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None):  # noqa: D401
     """act(W[:, :C] x + W[:, C:] x2[::stride2, ::stride2] + shift) (two 1x1 sources, one output)."""
     n, h, w, c = x.shape
     _, h2, w2, c2 = x2.shape

@@ -33,14 +33,15 @@ class MultiViewBatchMeta:
 
 
 class MultiViewPipeline:
-    def __init__(self, model, nviews=4):
+    def __init__(self, model, nviews=4, chunks=1):
         self.model = model
         self.nviews = nviews
+        self.chunks = chunks
 
     def step(self, views, meta):
         """One batch: returns (heatmaps [V*B, J, h, w], coords [V, B, J, 2], loss [], X [B, J, 3] f64)."""
         plan = self.model.plan(views[0].device)
-        hm, _, _ = plan.run(plan.pack_input(views))
+        hm, _, _ = plan.run(plan.pack_input(views), chunks=self.chunks, keep_features=False)
         nb = views[0].shape[0]
         j = hm.shape[1]
         coords = ops.softargmax2d(hm, beta=100.0, affine=meta.affines).view(self.nviews, nb, j, 2)

@@ -39,9 +39,9 @@ class _Conv:
         self.pad = conv.padding[0]
         self.relu = relu
 
-    def __call__(self, x, code, residual=None):
+    def __call__(self, x, code, residual=None, out=None):
         return ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale,
-                               self.shift, residual, self.relu, code)
+                               self.shift, residual, self.relu, code, out=out)
 
 
 class _DualTail:
@@ -56,8 +56,8 @@ class _DualTail:
         self.cout = conv3.weight.shape[0]
         self.stride2 = dconv.stride[0]
 
-    def __call__(self, mid, x, code):
-        return ops.conv1x1_dual_nhwc(mid, x, self.stride2, self.w, self.cout, self.shift, True, code)
+    def __call__(self, mid, x, code, out=None):
+        return ops.conv1x1_dual_nhwc(mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out)
 
 
 class _Block:
@@ -80,16 +80,16 @@ class _Block:
         if ds is not None:
             self.down = _Conv(ds[0], ds[1], False, code, bk)
 
-    def __call__(self, x, code):
-        out = x
+    def __call__(self, x, code, out=None):
+        y = x
         if self.dual is not None:
             for c in self.convs:
-                out = c(out, code)
-            return self.dual(out, x, code)
+                y = c(y, code)
+            return self.dual(y, x, code, out=out)
         res = self.down(x, code) if self.down is not None else x
         for c in self.convs[:-1]:
-            out = c(out, code)
-        return self.convs[-1](out, code, residual=res)
+            y = c(y, code)
+        return self.convs[-1](y, code, residual=res, out=out)
 
 
 class _Deconv:
@@ -102,8 +102,8 @@ class _Deconv:
         self.scale, self.shift = fold_bn(bn, dc.bias)
         self.cout = dc.weight.shape[1]
 
-    def __call__(self, x, code):
-        return ops.deconv4x4s2_nhwc(x, self.w, self.cout, self.scale, self.shift, True, code)
+    def __call__(self, x, code, out=None):
+        return ops.deconv4x4s2_nhwc(x, self.w, self.cout, self.scale, self.shift, True, code, out=out)
 
 
 class PoseResNetPlan:
@@ -151,18 +151,83 @@ class PoseResNetPlan:
                                    out_hw=(x.shape[1], x.shape[2]))
         return self.stem(x, code)
 
-    def run(self, x):
-        """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC)."""
+    def _stage_early(self, x, out=None, keep=None):
+        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
         code = self.code
-        x = self.run_stem(x)
-        x = ops.maxpool3x3s2_nhwc(x, code)
-        x1 = None
-        for li, layer in enumerate(self.layers):
-            for blk in layer:
-                x = blk(x, code)
+        x = ops.maxpool3x3s2_nhwc(self.run_stem(x), code)
+        for li in (0, 1):
+            layer = self.layers[li]
+            for bi, blk in enumerate(layer):
+                last = bi == len(layer) - 1
+                if li == 0 and last and keep is not None:
+                    x = blk(x, code, out=keep)
+                elif li == 1 and last and out is not None:
+                    x = blk(x, code, out=out)
+                else:
+                    x = blk(x, code)
             if li == 0:
                 x1 = x
-        for dc in self.deconvs:
-            x = dc(x, code)
-        hm = ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code)
-        return hm, x1, x
+        return x, x1
+
+    def _stage_late(self, x, hm_out=None, f_out=None):
+        """deconv2 -> deconv3 -> head."""
+        code = self.code
+        for i, dc in enumerate(self.deconvs[1:]):
+            last = i == len(self.deconvs) - 2
+            x = dc(x, code, out=f_out if last else None)
+        return ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code, out=hm_out), x
+
+    @staticmethod
+    def _block_cout(blk):
+        return blk.dual.cout if blk.dual is not None else blk.convs[-1].cout
+
+    def run(self, x, chunks=1, keep_features=True):
+        """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC).
+
+        chunks > 1 runs the HBM-bound ends of the network (stem..layer2 and
+        deconv2..head) depth-first over `chunks` slices of the batch, so their
+        activations stay resident in the 256 MiB Infinity Cache between producer and
+        consumer; layer3..deconv1 run on the whole batch.  keep_features=False skips
+        materialising the full layer1 / deconv outputs (returned as None)."""
+        code = self.code
+        n = x.shape[0]
+        if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
+            x = self.run_stem(x)
+            x = ops.maxpool3x3s2_nhwc(x, code)
+            x1 = None
+            for li, layer in enumerate(self.layers):
+                for blk in layer:
+                    x = blk(x, code)
+                if li == 0:
+                    x1 = x
+            for dc in self.deconvs:
+                x = dc(x, code)
+            hm = ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code)
+            return hm, (x1 if keep_features else None), (x if keep_features else None)
+        c = n // chunks
+        dt = ops.torch_dtype(code)
+        dev = x.device
+        if x.shape[3] == STEM_S2D_PAD:
+            hs, ws = x.shape[1], x.shape[2]
+        else:
+            hs, ws = (x.shape[1] - 1) // 2 + 1, (x.shape[2] - 1) // 2 + 1
+        hp, wp = (hs - 1) // 2 + 1, (ws - 1) // 2 + 1          # after maxpool = layer1 grid
+        h2, w2 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1          # layer2 grid
+        x2 = torch.empty((n, h2, w2, self._block_cout(self.layers[1][-1])), dtype=dt, device=dev)
+        x1 = (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1])), dtype=dt, device=dev)
+              if keep_features else None)
+        for k in range(chunks):
+            sl = slice(k * c, (k + 1) * c)
+            self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
+        y = x2
+        for layer in self.layers[2:]:
+            for blk in layer:
+                y = blk(y, code)
+        y = self.deconvs[0](y, code)
+        hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
+        hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)
+        f = (torch.empty((n, hf, wf, self.deconvs[-1].cout), dtype=dt, device=dev) if keep_features else None)
+        for k in range(chunks):
+            sl = slice(k * c, (k + 1) * c)
+            self._stage_late(y[sl], hm_out=hm[sl], f_out=None if f is None else f[sl])
+        return hm, x1, f

@@ -90,3 +90,20 @@ def test_pipeline_matches_cpu_oracle(cuda):
     p2d = coords.permute(1, 0, 2, 3).reshape(ng * 4, 16, 2).double().cpu().numpy()
     Xref = G.triangulate_poses(host['cams'], p2d.astype(np.float32).astype(np.float64))
     np.testing.assert_allclose(X.cpu().numpy(), Xref, atol=1e-2, rtol=1e-9)
+
+
+@pytest.mark.parametrize('chunks', [2, 4])
+def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks):
+    net = _model(50, 128, 0, 'fp32', cuda)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 128, seed=4)]
+    plan = net.plan(cuda)
+    x = plan.pack_input(views)
+    with torch.no_grad():
+        hm0, x10, f0 = plan.run(x)
+        hm1, x11, f1 = plan.run(x, chunks=chunks)
+        hm2, x12, f2 = plan.run(x, chunks=chunks, keep_features=False)
+    assert x12 is None and f2 is None
+    torch.testing.assert_close(hm1, hm0, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(hm2, hm0, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(x11, x10, atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(f1, f0, atol=1e-6, rtol=1e-6)
