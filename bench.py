@@ -114,16 +114,14 @@ def _cpu_meta(ng, size):
 
 def main():
     args = parse()
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
+    from posu import dist as pdist
+    rank, local, world = pdist.env_rank()
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
+        pdist.init('nccl', device=dev)
 
     from posu import synthetic as syn
     from posu.pipeline import MultiViewPipeline, synthetic_meta
@@ -206,11 +204,8 @@ def main():
         net_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
         geo_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
 
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    value = world * frames * args.steps / elapsed
+    elapsed = pdist.max_over_ranks(elapsed, device=dev)
+    value = pdist.throughput(frames, args.steps, world, elapsed)
     gf = GFLOP_PER_FRAME.get((args.layers, args.size))
     peak = PEAK_BF16_TFLOPS if args.precision == 'bf16' else PEAK_F32_TFLOPS
     roof = None

@@ -107,6 +107,18 @@ int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
                          const void* w, int Cout, const float* scale,
                          const float* shift, int relu, void* y, void* stream);
 
+/* The last deconv stage fused with the final 1x1 head: deconv + BN + ReLU as
+ * posu_deconv4x4s2_fwd, then per output pixel hm[n][j][pix] = bias[j] +
+ * sum_c hw[j][c] f[c] (lib/models/pose_resnet.py:202-203) from the tile still in LDS,
+ * so the 256-channel deconv output need not round-trip through HBM.
+ *   y: NULL (do not store f) or [N, 2H, 2W, Cout] dtype; Cout == 256;
+ *   hw: packed head weight [>= 16][round_up(Cout, posu_conv_bk)] dtype (rows >= J zero);
+ *   hbias: [J] f32; hm: [N, J, 2H, 2W] f32; J <= 16. */
+int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                              const void* w, int Cout, const float* scale, const float* shift,
+                              void* y, const void* hw, int J, const float* hbias, float* hm,
+                              void* stream);
+
 /* 1x1 convolution (+bias) writing NCHW fp32 heatmaps: PoseResNet.final_layer
  * (lib/models/pose_resnet.py:126-132, 203).
  *   x: [N, H, W, C] dtype; w: packed [CoutPad][Kpad]; bias: [Cout] f32;

@@ -56,6 +56,11 @@ struct ConvGeom {
   int deconv;        // blockIdx.z = parity class
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out
+  // fused 1x1 head (mode 0, BN == Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
+  const void* hw;    // packed head weight [>= 16 rows][hkp] (dtype)
+  const float* hbias;
+  float* hm;
+  int J, hkp;
   int mtiles, ntiles;
 };
 
@@ -170,13 +175,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
   const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int nt = wg % g.ntiles, mt = wg / g.ntiles;
+  // tile id -> (m-tile, [deconv parity class,] n-tile), n fastest; the 4 parity
+  // classes of one m-tile are adjacent so their overlapping input windows are read
+  // from the same XCD's L2 instead of once per class from HBM
+  const int nt = wg % g.ntiles;
+  const int rest = wg / g.ntiles;
+  const int mt = g.deconv ? rest >> 2 : rest;
   const int m0 = mt * BM, n0 = nt * BN;
 
   int pad_h = g.pad_h, pad_w = g.pad_w, oy_off = 0, ox_off = 0, osc = 1;
   const T* __restrict__ wp = reinterpret_cast<const T*>(g.w);
   if (g.deconv) {
-    const int cls = blockIdx.z, py = cls >> 1, px = cls & 1;
+    const int cls = rest & 3, py = cls >> 1, px = cls & 1;
     pad_h = 1 - py;
     pad_w = 1 - px;
     oy_off = py;
@@ -382,7 +392,59 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
         for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
       }
-      *reinterpret_cast<uint4*>(yp + off[it]) = O::store_vals(v);
+      const uint4 packed = O::store_vals(v);
+      if (yp) *reinterpret_cast<uint4*>(yp + off[it]) = packed;
+      if constexpr (BN == 256) {
+        if (g.hm) {  // keep the rounded activation for the fused head
+          float vr[E];
+          O::load_vals(packed, vr);
+#pragma unroll
+          for (int e = 0; e < E; e += 4)
+            *reinterpret_cast<float4*>(Cs + row * LD + cc * E + e) =
+                make_float4(vr[e], vr[e + 1], vr[e + 2], vr[e + 3]);
+        }
+      }
+    }
+    if constexpr (BN == 256) {
+      if (g.hm) {
+        // final_layer (pose_resnet.py:126-132, 203) on the tile in LDS: wave w takes
+        // pixel rows 16w..16w+15, one 16x16 MFMA tile = 16 joints, K = Cout
+        __syncthreads();
+        static_assert(BM == 64, "fused head assumes 64-row tiles (4 waves x 16 rows)");
+        f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+        const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
+        const int hrow = wid * 16 + r16;
+        for (int kc = 0; kc < g.Cout / (4 * E); ++kc) {
+          const int c = 4 * kc + q;
+          float av[E];
+#pragma unroll
+          for (int e = 0; e < E; e += 4) {
+            const float4 t4 = *reinterpret_cast<const float4*>(Cs + hrow * LD + c * E + e);
+            av[e] = t4.x;
+            av[e + 1] = t4.y;
+            av[e + 2] = t4.z;
+            av[e + 3] = t4.w;
+          }
+          const uint4 a = O::store_vals(av);
+          const uint4 b = *reinterpret_cast<const uint4*>(hwp + static_cast<size_t>(r16) * g.hkp + c * E);
+          O::mma(hacc, a, b);
+        }
+        const int joint = r16;
+        if (joint < g.J) {
+          const float bj = g.hbias ? g.hbias[joint] : 0.f;
+          const int HWo = g.out_H * g.out_W;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = m0 + wid * 16 + q * 4 + e;
+            if (m < g.M) {
+              const int n = m / HoWo, rem = m - n * HoWo;
+              const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+              const int pix = (oy * osc + oy_off) * g.out_W + ox * osc + ox_off;
+              g.hm[(static_cast<size_t>(n) * g.J + joint) * HWo + pix] = hacc[e] + bj;
+            }
+          }
+        }
+      }
     }
   } else {
     __syncthreads();
@@ -428,6 +490,12 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
     return static_cast<long long>((g.M + bm - 1) / bm) * (g.CoutPad / bn) * nclass;
   };
   int BM, BN;
+  if (g.hm) {  // fused head: one block owns all 256 output channels
+    g.ntiles = 1;
+    g.mtiles = (g.M + 63) / 64;
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 1, DUAL>), dim3(g.mtiles * nclass), dim3(256), 0, s, g);
+    return check_launch(what);
+  }
   if (!wide) {
     BN = 64;
     if (blocks(256, 64) >= 1024) BM = 256;
@@ -440,7 +508,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
   }
   g.ntiles = g.CoutPad / BN;
   g.mtiles = (g.M + BM - 1) / BM;
-  dim3 grid(g.mtiles * g.ntiles, 1, nclass);
+  dim3 grid(g.mtiles * g.ntiles * nclass);
   if (BM == 256)
     hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 64, 4, DUAL>), grid, dim3(256), 0, s, g);
   else if (BM == 128 && BN == 128)
@@ -587,6 +655,35 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   g.out_H = 2 * H;
   g.out_W = 2 * W;
   return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_fwd");
+}
+
+extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
+                                         int Cout, const float* scale, const float* shift, void* y, const void* hw,
+                                         int J, const float* hbias, float* hm, void* stream) {
+  if (int st = common_checks(dtype, x, w, hm, N, H, W, C, Cout, "posu_deconv4x4s2_head_fwd")) return st;
+  POSU_REQUIRE(hw && Cout == 256 && J > 0 && J <= 16,
+               "posu_deconv4x4s2_head_fwd: needs Cout == 256, 0 < J <= 16 and head weights");
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
+  g.scale = scale;
+  g.shift = shift;
+  g.y = y;
+  g.Ho = H;
+  g.Wo = W;
+  g.M = N * H * W;
+  g.K = 4 * C;
+  g.Kpad = round_up(g.K, bk_of(dtype));
+  g.KH = 2;
+  g.KW = 2;
+  g.relu = 1;
+  g.deconv = 1;
+  g.out_H = 2 * H;
+  g.out_W = 2 * W;
+  g.hw = hw;
+  g.hbias = hbias;
+  g.hm = hm;
+  g.J = J;
+  g.hkp = round_up(Cout, bk_of(dtype));
+  return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_head_fwd");
 }
 
 extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,

@@ -128,6 +128,8 @@ class PoseResNetPlan:
         self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None
                        else torch.zeros(fl.weight.shape[0], device=fl.weight.device))
         self.njoints = fl.weight.shape[0]
+        last = self.deconvs[-1] if self.deconvs else None
+        self.fuse_head = last is not None and last.cout == 256 and self.njoints <= 16
 
     def pack_input(self, views):
         """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N):
@@ -169,13 +171,22 @@ class PoseResNetPlan:
                 x1 = x
         return x, x1
 
-    def _stage_late(self, x, hm_out=None, f_out=None):
-        """deconv2 -> deconv3 -> head."""
+    def _last_deconv_head(self, x, keep_f, hm_out=None, f_out=None):
+        """Last deconv (+BN+ReLU) and the 1x1 head, fused into one launch when possible."""
         code = self.code
-        for i, dc in enumerate(self.deconvs[1:]):
-            last = i == len(self.deconvs) - 2
-            x = dc(x, code, out=f_out if last else None)
-        return ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code, out=hm_out), x
+        dc = self.deconvs[-1]
+        if self.fuse_head:
+            return ops.deconv4x4s2_head(x, dc.w, dc.cout, dc.scale, dc.shift, self.head_w, self.njoints, self.head_b,
+                                        code, keep_f=keep_f, hm_out=hm_out, f_out=f_out)
+        f = dc(x, code, out=f_out)
+        return ops.head1x1_nchw(f, self.head_w, self.njoints, self.head_b, code, out=hm_out), f
+
+    def _stage_late(self, x, hm_out=None, f_out=None, keep_f=True):
+        """deconv2 .. last deconv -> head."""
+        code = self.code
+        for dc in self.deconvs[1:-1]:
+            x = dc(x, code)
+        return self._last_deconv_head(x, keep_f, hm_out=hm_out, f_out=f_out)
 
     @staticmethod
     def _block_cout(blk):
@@ -200,10 +211,10 @@ class PoseResNetPlan:
                     x = blk(x, code)
                 if li == 0:
                     x1 = x
-            for dc in self.deconvs:
+            for dc in self.deconvs[:-1]:
                 x = dc(x, code)
-            hm = ops.head1x1_nchw(x, self.head_w, self.njoints, self.head_b, code)
-            return hm, (x1 if keep_features else None), (x if keep_features else None)
+            hm, f = self._last_deconv_head(x, keep_features)
+            return hm, (x1 if keep_features else None), f
         c = n // chunks
         dt = ops.torch_dtype(code)
         dev = x.device
@@ -229,5 +240,5 @@ class PoseResNetPlan:
         f = (torch.empty((n, hf, wf, self.deconvs[-1].cout), dtype=dt, device=dev) if keep_features else None)
         for k in range(chunks):
             sl = slice(k * c, (k + 1) * c)
-            self._stage_late(y[sl], hm_out=hm[sl], f_out=None if f is None else f[sl])
+            self._stage_late(y[sl], hm_out=hm[sl], f_out=None if f is None else f[sl], keep_f=f is not None)
         return hm, x1, f

@@ -259,3 +259,32 @@ def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
                                 x.permute(0, 2, 3, 1).contiguous().to(cuda, dt), stride, wp, cout, b.to(cuda), True,
                                 code)
     torch.testing.assert_close(out.float().cpu().permute(0, 3, 1, 2), ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('keep_f', [True, False])
+def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f):
+    g = torch.Generator().manual_seed(8)
+    n, cin, h, w, cout, J = 3, 64, 5, 6, 256, 16
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cin, cout, 4, 4, generator=g) * (2.0 / (cin * 4)) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    hw = torch.randn(J, cout, 1, 1, generator=g) * 0.06
+    hb = torch.randn(J, generator=g)
+    f_ref = F.relu(F.conv_transpose2d(x, wt, stride=2, padding=1) * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+    hm_ref = F.conv2d(f_ref, hw, hb)
+    dt = ops.torch_dtype(code)
+    wp = packing.pack_deconv4x4_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    hwp = packing.pack_conv_weight(hw.to(cuda), cout, ops.conv_bk(code), dt)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    hm, f = ops.deconv4x4s2_head(xd, wp, cout, sc.to(cuda), sh.to(cuda), hwp, J, hb.to(cuda), code, keep_f=keep_f)
+    torch.testing.assert_close(hm.cpu(), hm_ref, atol=tol, rtol=tol)
+    if keep_f:
+        torch.testing.assert_close(f.float().cpu().permute(0, 3, 1, 2), f_ref, atol=tol, rtol=tol)
+    else:
+        assert f is None
+    # identical to the two-launch path on the same device (same rounding of f)
+    f2 = ops.deconv4x4s2_nhwc(xd, wp, cout, sc.to(cuda), sh.to(cuda), True, code)
+    hm2 = ops.head1x1_nchw(f2, hwp, J, hb.to(cuda), code)
+    torch.testing.assert_close(hm, hm2, atol=1e-5, rtol=1e-5)
