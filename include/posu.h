@@ -78,6 +78,16 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
  *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied). */
 int posu_conv_bk(int dtype);
+/* Tuning knob: depth of the LDS-DMA ring of the convolution kernels (2 or 3
+ * K-tiles; process-wide, default 2). */
+int posu_set_conv_stages(int stages);
+/* Tuning knob: allow the eight-wave 256x256 / 256x128 tiles for layers with
+ * Cout >= 128 (1, default) or restrict to the four-wave tiles (0). */
+int posu_set_conv_tiles(int big);
+/* Test hook: force one tile configuration for every conv launch that admits it
+ * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
+ * 6: 256x128 (8 waves)); -1 restores the automatic choice. */
+int posu_force_conv_config(int cfg);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,

@@ -34,6 +34,8 @@
 // output parity class (py, px) = blockIdx.z: output (2*qy+py, 2*qx+px) reads inputs
 // qy + py - 1 + ty, qx + px - 1 + tx with the deconv tap (3-py-2ty, 3-px-2tx);
 // the Python layer packs those taps per class.
+#include <type_traits>
+
 #include "posu_common.h"
 
 namespace posu {
@@ -116,9 +118,16 @@ __device__ __forceinline__ int swz(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }
 
-template <int BM, int BN>
-constexpr int smem_bytes() {
-  return (2 * (BM + BN) * 128) > (BM * (BN + 4) * 4) ? (2 * (BM + BN) * 128) : (BM * (BN + 4) * 4);
+template <int BM, int BN, int S>
+constexpr int ring_bytes() {
+  return S * (BM + BN) * 128;
+}
+// rows per epilogue pass: the f32 [rows][BN+4] staging tile must fit in the ring
+template <int BM, int BN, int S>
+constexpr int pass_rows() {
+  return (BM * (BN + 4) * 4 <= ring_bytes<BM, BN, S>())         ? BM
+         : ((BM / 2) * (BN + 4) * 4 <= ring_bytes<BM, BN, S>()) ? BM / 2
+                                                                 : BM / 4;
 }
 
 constexpr int kOOB = 0x7ffffff0;  // buffer offset past num_records: the load returns zeros
@@ -140,8 +149,8 @@ __device__ __forceinline__ u32x4 make_srd(const void* base, int bytes) {
 // One 16-B-per-lane LDS-DMA: buffer_load_dwordx4 ... lds writes lane l's 16 bytes to
 // LDS address lds + 16*l (wave-uniform `lds` in M0); offsets past num_records load 0.
 // Issued from inline asm so hipcc neither waits for it before unrelated ds_reads of
-// the other LDS buffer nor drains it early: the kernel retires it itself with
-// s_waitcnt vmcnt(0) before the barrier that precedes the reads.
+// the other ring slots nor drains it early: the kernel retires it itself with a
+// counted s_waitcnt vmcnt(N) before the barrier that precedes the reads.
 __device__ __forceinline__ void dma16(u32x4 srd, int voff, unsigned lds) {
   unsigned keep;
   asm volatile(
@@ -152,18 +161,32 @@ __device__ __forceinline__ void dma16(u32x4 srd, int voff, unsigned lds) {
       : "memory");
 }
 
-template <typename T, int BM, int BN, int WGM, bool DUAL>
-__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
+// wait until at most N of this wave's vector-memory ops are outstanding
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL>
+__global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
+  constexpr int NT = NW * 64;
   constexpr int E = O::E;
   constexpr int ES = static_cast<int>(sizeof(T));
-  constexpr int BK = 8 * E;  // 128-byte LDS rows
-  constexpr int WGN = 4 / WGM;                // wave grid WGM x WGN
+  constexpr int BK = 8 * E;                   // 128-byte LDS rows
+  constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int RA = BM / 32, RB = BN / 32;  // 16-B chunks per thread per K-tile
+  constexpr int ROWS = NW * 8;                // LDS rows filled per DMA round (1 KiB per wave)
+  constexpr int RA = BM / ROWS, RB = BN / ROWS;
+  constexpr int ND = RA + RB;                 // DMA instructions per thread per K-tile
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<BM, BN>()];
+  constexpr int PR = pass_rows<BM, BN, S>();
+  static_assert(S >= 2 && S <= 4, "2..4 stages");
+  static_assert(ND * (S - 2) < 64, "vmcnt range");
+  static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
+  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -201,10 +224,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
   const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
 
   // ---- LDS-DMA staging.  One buffer_load_dwordx4 ... lds per wave writes 1 KiB =
-  // 8 LDS rows x 8 chunks, lane l at byte 16*l: row (tid >> 3) + 32*i, physical
+  // 8 LDS rows x 8 chunks, lane l at byte 16*l: row (tid >> 3) + ROWS*i, physical
   // chunk tid & 7.  The XOR swizzle of the fragment reads is applied on the SOURCE:
   // that lane fetches logical chunk cL = (tid & 7) ^ ((row >> 1) & 7), which is the
-  // same for every i because 32*i does not touch bits 1..3 of the row.
+  // same for every i because ROWS*i does not touch bits 1..3 of the row.
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
   const int HoWo = g.Ho * g.Wo;
   int hb[RA], wb[RA], nb[RA];   // generic window gather
@@ -213,7 +236,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
   if constexpr (DUAL) x2rs = make_srd(g.x2, g.N * g.H2 * g.W2 * g.C2 * ES);
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
+    const int m = m0 + (tid >> 3) + ROWS * i;
     if (m < g.M) {
       const int n = m / HoWo, rem = m - n * HoWo;
       const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
@@ -244,7 +267,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
   const int nk = g.Kpad / BK;
   const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;  // weight row offset (elements) for i = 0
 
-  // global -> LDS (async DMA) for K-tile KT into buffer BUF
+  // global -> LDS (async DMA) for K-tile KT into ring slot BUF: exactly ND dma16 per thread
 #define POSU_DMA_TILE(KT, BUF)                                                                      \
   {                                                                                                 \
     const int kbase = (KT) * BK;                                                                    \
@@ -255,7 +278,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
       _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                              \
         const int o = first ? o1[i] : o2[i];                                                        \
         const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;                 \
-        dma16(first ? xrs : x2rs, off, As_ + i * 4096);                                             \
+        dma16(first ? xrs : x2rs, off, As_ + i * NW * 1024);                                        \
       }                                                                                             \
     } else {                                                                                        \
       int kh, kw, ci;                                                                               \
@@ -282,13 +305,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
         const bool ok = kvalid && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&         \
                         static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);                     \
         const int off = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB;                      \
-        dma16(xrs, off, As_ + i * 4096);                                                            \
+        dma16(xrs, off, As_ + i * NW * 1024);                                                       \
       }                                                                                             \
     }                                                                                               \
     _Pragma("unroll") for (int i = 0; i < RB; ++i)                                                  \
-      dma16(wrs, (wbrow + 32 * i * g.Kpad + kbase) * ES, Bs_ + i * 4096);                           \
+      dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs_ + i * NW * 1024);                    \
   }
-  // MFMAs over one LDS K-tile
+  // MFMAs over one LDS K-tile.  Operands are swapped (A = weights, B = pixels), so a
+  // lane's accumulator holds 4 consecutive output channels of one pixel, staged into
+  // LDS with one 16-B write.
 #define POSU_COMPUTE(BUF)                                                                           \
   {                                                                                                 \
     const char* As_ = smem + (BUF) * STAGE;                                                         \
@@ -301,175 +326,204 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvGeom g) {
       _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                \
         bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));            \
       _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                \
-        _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], af[i], bfr[j]);            \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);            \
     }                                                                                               \
   }
 
+  // acc[i][j]: rows = channels of n-tile j (16 per MFMA tile), cols = pixels of m-tile i;
+  // lane holds channels 4q..4q+3 of pixel r16
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // two LDS buffers: the DMA of K-tile t+1 overlaps the MFMAs of tile t; one
-  // vmcnt(0) + barrier per K-tile retires it before anyone reads it
-  POSU_DMA_TILE(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt + 1 < nk; ++kt) {
-    const int cur = kt & 1;
-    POSU_DMA_TILE(kt + 1, cur ^ 1);
-    POSU_COMPUTE(cur);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // S-slot ring, DMA running S-1 K-tiles ahead; per K-tile one counted vmcnt (the
+  // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
+  // barrier (makes the DMA visible to every wave and retires the slot the next DMA
+  // overwrites, which every wave finished reading in the previous iteration)
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) POSU_DMA_TILE(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = min(S - 2, nk - 1 - kt);  // younger K-tiles in flight
+    if (S >= 4 && ahead >= 2) vm_wait<ND * (S >= 4 ? 2 : 0)>();
+    else if (S >= 3 && ahead >= 1) vm_wait<ND * (S >= 3 ? 1 : 0)>();
+    else vm_wait<0>();
     __syncthreads();
+    if (kt + S - 1 < nk) POSU_DMA_TILE(kt + S - 1, (kt + S - 1) % S);
+    POSU_COMPUTE(kt % S);
   }
-  POSU_COMPUTE((nk - 1) & 1);
 #undef POSU_DMA_TILE
 #undef POSU_COMPUTE
 
+  // ---- epilogue through LDS, PR rows per pass: the accumulators (BN applied) are
+  // staged as an f32 [pixel][channel] tile, then written as whole 16-B NHWC chunks
+  // with residual add + ReLU (mode 0), as NCHW f32 planes (mode 1), or fed to the
+  // fused 1x1 head (g.hm, single pass)
   constexpr int LD = BN + 4;
   float* Cs = reinterpret_cast<float*>(smem);
-  if (g.mode == 0) {
-    constexpr int CPR = BN / E;               // output chunks per tile row
-    constexpr int ITER = BM * CPR / 256;      // chunks per thread
-    T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+  constexpr int CPR = BN / E;            // output chunks per tile row
+  constexpr int ITER = PR * CPR / NT;    // chunks per thread per pass
+  static_assert(ITER * NT == PR * CPR, "epilogue chunk split");
+  const bool mode0 = g.mode == 0 && !g.hm;
+  const bool relu_at_stage = g.relu && !mode0;  // mode 0: ReLU after the residual add
+  float sc[TN][4], sh[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int co = n0 + wn * WTN + j * 16 + q * 4 + e;
+      sc[j][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
+      sh[j][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+    }
+#pragma unroll
+  for (int p = 0; p < BM / PR; ++p) {
+    // residual chunks of this pass first (their latency overlaps the staging)
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     size_t off[ITER];
     bool ok[ITER];
     uint4 rv[ITER];
-    // decode output chunks and issue the residual loads before the LDS staging
+    if (mode0) {
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      const int idx = tid + it * 256;
-      const int row = idx / CPR, cc = idx - row * CPR;
-      const int m = m0 + row, co = n0 + cc * E;
-      ok[it] = m < g.M && co < g.Cout;
-      const int mm = ok[it] ? m : 0;
-      const int n = mm / HoWo, rem = mm - n * HoWo;
-      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-      off[it] = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout +
-                (ok[it] ? co : 0);
-      rv[it] = make_uint4(0, 0, 0, 0);
-      if (rp && ok[it]) rv[it] = *reinterpret_cast<const uint4*>(rp + off[it]);
-    }
-    __syncthreads();  // all waves are done reading the last K-tile
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + j * 16 + r16;
-      const int co = n0 + col;
-      float sc = 1.f, sh = 0.f;
-      if (co < g.Cout) {
-        if (g.scale) sc = g.scale[co];
-        if (g.shift) sh = g.shift[co];
+      for (int it = 0; it < ITER; ++it) {
+        const int idx = tid + it * NT;
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = m0 + p * PR + row, co = n0 + cc * E;
+        ok[it] = m < g.M && co < g.Cout;
+        const int mm = ok[it] ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+        off[it] = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout +
+                  (ok[it] ? co : 0);
+        rv[it] = make_uint4(0, 0, 0, 0);
+        if (rp && ok[it]) rv[it] = *reinterpret_cast<const uint4*>(rp + off[it]);
       }
+    }
+    __syncthreads();  // the ring (or the previous pass) is no longer read
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + r16 - p * PR;
+      if ((wm * WTM + i * 16) / PR != p) continue;  // wave-uniform
 #pragma unroll
-        for (int e = 0; e < 4; ++e) Cs[(wm * WTM + i * 16 + q * 4 + e) * LD + col] = acc[i][j][e] * sc + sh;
+      for (int j = 0; j < TN; ++j) {
+        const int colb = wn * WTN + j * 16 + q * 4;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] * sc[j][e] + sh[j][e];
+          if (relu_at_stage) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<float4*>(Cs + row * LD + colb) = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
     __syncthreads();
+    if (mode0) {
+      T* __restrict__ yp = reinterpret_cast<T*>(g.y);
 #pragma unroll
-    for (int it = 0; it < ITER; ++it) {
-      if (!ok[it]) continue;
-      const int idx = tid + it * 256;
-      const int row = idx / CPR, cc = idx - row * CPR;
-      float v[E];
+      for (int it = 0; it < ITER; ++it) {
+        if (!ok[it]) continue;
+        const int idx = tid + it * NT;
+        const int row = idx / CPR, cc = idx - row * CPR;
+        float v[E];
 #pragma unroll
-      for (int e = 0; e < E; e += 4) {
-        const float4 t4 = *reinterpret_cast<const float4*>(Cs + row * LD + cc * E + e);
-        v[e] = t4.x;
-        v[e + 1] = t4.y;
-        v[e + 2] = t4.z;
-        v[e + 3] = t4.w;
+        for (int e = 0; e < E; e += 4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(Cs + row * LD + cc * E + e);
+          v[e] = t4.x;
+          v[e + 1] = t4.y;
+          v[e + 2] = t4.z;
+          v[e + 3] = t4.w;
+        }
+        if (rp) {
+          float r[E];
+          O::load_vals(rv[it], r);
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[e] += r[e];
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<uint4*>(yp + off[it]) = O::store_vals(v);
       }
-      if (rp) {
-        float r[E];
-        O::load_vals(rv[it], r);
-#pragma unroll
-        for (int e = 0; e < E; ++e) v[e] += r[e];
+    } else if (!g.hm) {
+      // NCHW f32 (heatmap head): consecutive threads walk pixels of one channel
+      float* __restrict__ yp = reinterpret_cast<float*>(g.y);
+      const int ncol = min(BN, g.Cout - n0);
+      for (int idx = tid; idx < PR * ncol; idx += NT) {
+        const int col = idx / PR, row = idx - col * PR;
+        const int m = m0 + p * PR + row;
+        if (m >= g.M) continue;
+        const int n = m / HoWo, pixo = m - n * HoWo;
+        yp[(static_cast<size_t>(n) * g.Cout + n0 + col) * HoWo + pixo] = Cs[row * LD + col];
       }
-      if (g.relu) {
+    } else if constexpr (BN == 256 && BM == 64 && PR == BM && NW == 4) {
+      // optional store of the deconv output f (NHWC), values rounded to T in place so
+      // the head sees exactly what a separate head launch would read
+      T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+      for (int idx = tid; idx < BM * CPR; idx += NT) {
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = m0 + row;
+        float v[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
-      }
-      const uint4 packed = O::store_vals(v);
-      if (yp) *reinterpret_cast<uint4*>(yp + off[it]) = packed;
-      if constexpr (BN == 256) {
-        if (g.hm) {  // keep the rounded activation for the fused head
-          float vr[E];
-          O::load_vals(packed, vr);
+        for (int e = 0; e < E; e += 4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(Cs + row * LD + cc * E + e);
+          v[e] = t4.x;
+          v[e + 1] = t4.y;
+          v[e + 2] = t4.z;
+          v[e + 3] = t4.w;
+        }
+        const uint4 packed = O::store_vals(v);
+        float vr[E];
+        O::load_vals(packed, vr);
 #pragma unroll
-          for (int e = 0; e < E; e += 4)
-            *reinterpret_cast<float4*>(Cs + row * LD + cc * E + e) =
-                make_float4(vr[e], vr[e + 1], vr[e + 2], vr[e + 3]);
+        for (int e = 0; e < E; e += 4)
+          *reinterpret_cast<float4*>(Cs + row * LD + cc * E + e) = make_float4(vr[e], vr[e + 1], vr[e + 2], vr[e + 3]);
+        if (yp && m < g.M) {
+          const int n = m / HoWo, rem = m - n * HoWo;
+          const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+          const size_t off2 =
+              (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout +
+              cc * E;
+          *reinterpret_cast<uint4*>(yp + off2) = packed;
         }
       }
-    }
-    if constexpr (BN == 256) {
-      if (g.hm) {
-        // final_layer (pose_resnet.py:126-132, 203) on the tile in LDS: wave w takes
-        // pixel rows 16w..16w+15, one 16x16 MFMA tile = 16 joints, K = Cout
-        __syncthreads();
-        static_assert(BM == 64, "fused head assumes 64-row tiles (4 waves x 16 rows)");
-        f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
-        const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
-        const int hrow = wid * 16 + r16;
-        for (int kc = 0; kc < g.Cout / (4 * E); ++kc) {
-          const int c = 4 * kc + q;
-          float av[E];
+      __syncthreads();
+      // final_layer (pose_resnet.py:126-132, 203) on the tile in LDS: wave w takes
+      // pixel rows 16w..16w+15, one 16x16 MFMA tile = 16 joints, K = Cout
+      f32x4 hacc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
+      const int hrow = wid * 16 + r16;
+      for (int kc = 0; kc < g.Cout / (4 * E); ++kc) {
+        const int c = 4 * kc + q;
+        float av[E];
 #pragma unroll
-          for (int e = 0; e < E; e += 4) {
-            const float4 t4 = *reinterpret_cast<const float4*>(Cs + hrow * LD + c * E + e);
-            av[e] = t4.x;
-            av[e + 1] = t4.y;
-            av[e + 2] = t4.z;
-            av[e + 3] = t4.w;
+        for (int e = 0; e < E; e += 4) {
+          const float4 t4 = *reinterpret_cast<const float4*>(Cs + hrow * LD + c * E + e);
+          av[e] = t4.x;
+          av[e + 1] = t4.y;
+          av[e + 2] = t4.z;
+          av[e + 3] = t4.w;
+        }
+        const uint4 a = O::store_vals(av);
+        const uint4 b = *reinterpret_cast<const uint4*>(hwp + static_cast<size_t>(r16) * g.hkp + c * E);
+        O::mma(hacc, a, b);  // rows = pixels, cols = joints
+      }
+      const int joint = r16;
+      if (joint < g.J) {
+        const float bj = g.hbias ? g.hbias[joint] : 0.f;
+        const int HWo = g.out_H * g.out_W;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = m0 + wid * 16 + q * 4 + e;
+          if (m < g.M) {
+            const int n = m / HoWo, rem = m - n * HoWo;
+            const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+            const int pixo = (oy * osc + oy_off) * g.out_W + ox * osc + ox_off;
+            g.hm[(static_cast<size_t>(n) * g.J + joint) * HWo + pixo] = hacc[e] + bj;
           }
-          const uint4 a = O::store_vals(av);
-          const uint4 b = *reinterpret_cast<const uint4*>(hwp + static_cast<size_t>(r16) * g.hkp + c * E);
-          O::mma(hacc, a, b);
-        }
-        const int joint = r16;
-        if (joint < g.J) {
-          const float bj = g.hbias ? g.hbias[joint] : 0.f;
-          const int HWo = g.out_H * g.out_W;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = m0 + wid * 16 + q * 4 + e;
-            if (m < g.M) {
-              const int n = m / HoWo, rem = m - n * HoWo;
-              const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-              const int pix = (oy * osc + oy_off) * g.out_W + ox * osc + ox_off;
-              g.hm[(static_cast<size_t>(n) * g.J + joint) * HWo + pix] = hacc[e] + bj;
-            }
-          }
         }
       }
-    }
-  } else {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + j * 16 + r16;
-      const int co = n0 + col;
-      const float sh = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) Cs[(wm * WTM + i * 16 + q * 4 + e) * LD + col] = acc[i][j][e] + sh;
-    }
-    __syncthreads();
-    // NCHW f32 (heatmap head): consecutive threads walk pixels of one channel
-    float* __restrict__ yp = reinterpret_cast<float*>(g.y);
-    const int ncol = min(BN, g.Cout - n0);
-    for (int idx = tid; idx < BM * ncol; idx += 256) {
-      const int col = idx / BM, row = idx - col * BM;
-      const int m = m0 + row;
-      if (m >= g.M) continue;
-      const int n = m / HoWo, pix = m - n * HoWo;
-      float v = Cs[row * LD + col];
-      if (g.relu) v = fmaxf(v, 0.f);
-      yp[(static_cast<size_t>(n) * g.Cout + n0 + col) * HoWo + pix] = v;
     }
   }
 }
@@ -480,45 +534,67 @@ int ilog2(int v) {
   return ((1 << l) == v) ? l : -1;
 }
 
+template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
+void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
+  if constexpr (ring_bytes<BM, BN, 3>() <= 160 * 1024) {
+    if (stages >= 3) {
+      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 3, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 2, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
+}
+
+int g_stages = 2;   // ring depth (posu_set_conv_stages)
+int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (posu_set_conv_tiles)
+int g_force = -1;   // forced tile configuration (tests), -1 = automatic
+
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
-  // tile choice: 64-channel layers take 256 x 64 tiles (four waves stacked along M,
-  // 64 x 64 each); wider layers 128 x 128; grids that would not give every CU two
-  // blocks drop to 64-row tiles.
-  const bool wide = g.CoutPad % 128 == 0;
-  auto blocks = [&](int bm, int bn) {
-    return static_cast<long long>((g.M + bm - 1) / bm) * (g.CoutPad / bn) * nclass;
-  };
-  int BM, BN;
   if (g.hm) {  // fused head: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 1, DUAL>), dim3(g.mtiles * nclass), dim3(256), 0, s, g);
+    if constexpr (!DUAL)
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 4, 1, 2, false>), dim3(g.mtiles * nclass), dim3(256), 0, s,
+                         g);
     return check_launch(what);
   }
-  if (!wide) {
-    BN = 64;
-    if (blocks(256, 64) >= 1024) BM = 256;
-    else if (blocks(128, 64) >= 512) BM = 128;
-    else BM = 64;
+  // tile choice: 64-channel layers take 256 x 64 tiles (four waves stacked along M,
+  // 64 x 64 each); wider layers 256 x 256 / 256 x 128 with eight 128 x 64 waves when
+  // the grid still gives every CU a block, else 128 x 128; grids that would not give
+  // every CU two blocks drop to 64-row tiles.
+  auto blocks = [&](int bm, int bn) {
+    return static_cast<long long>((g.M + bm - 1) / bm) * (g.CoutPad / bn) * nclass;
+  };
+  int cfg;
+  if (g.CoutPad % 128 != 0) {
+    cfg = blocks(256, 64) >= 1024 ? 0 : (blocks(128, 64) >= 512 ? 1 : 2);
+  } else if (g_big && g.CoutPad % 256 == 0 && blocks(256, 256) >= 256) {
+    cfg = 5;
+  } else if (g_big && blocks(256, 128) >= 256) {
+    cfg = 6;
   } else {
-    BN = 128;
-
-    BM = blocks(128, 128) >= 512 ? 128 : 64;
+    cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
-  g.ntiles = g.CoutPad / BN;
-  g.mtiles = (g.M + BM - 1) / BM;
-  dim3 grid(g.mtiles * g.ntiles * nclass);
-  if (BM == 256)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 64, 4, DUAL>), grid, dim3(256), 0, s, g);
-  else if (BM == 128 && BN == 128)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 2, DUAL>), grid, dim3(256), 0, s, g);
-  else if (BM == 128)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 64, 2, DUAL>), grid, dim3(256), 0, s, g);
-  else if (BN == 128)
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 128, 2, DUAL>), grid, dim3(256), 0, s, g);
-  else
-    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 64, 2, DUAL>), grid, dim3(256), 0, s, g);
+  if (g_force >= 0) {
+    const bool wide_ok = g.CoutPad % 128 == 0 && (g_force != 5 || g.CoutPad % 256 == 0);
+    if (g_force <= 2 || wide_ok) cfg = g_force;
+  }
+  static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
+  static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
+  g.ntiles = g.CoutPad / kBN[cfg];
+  g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
+  const int nb = g.mtiles * g.ntiles * nclass;
+  const int st = g_stages;
+  switch (cfg) {
+    case 0: launch_cfg<T, 256, 64, 4, 4, DUAL>(g, nb, st, s); break;
+    case 1: launch_cfg<T, 128, 64, 4, 2, DUAL>(g, nb, st, s); break;
+    case 2: launch_cfg<T, 64, 64, 4, 2, DUAL>(g, nb, st, s); break;
+    case 3: launch_cfg<T, 128, 128, 4, 2, DUAL>(g, nb, st, s); break;
+    case 4: launch_cfg<T, 64, 128, 4, 2, DUAL>(g, nb, st, s); break;
+    case 5: launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s); break;
+    default: launch_cfg<T, 256, 128, 8, 4, DUAL>(g, nb, 2, s); break;
+  }
   return check_launch(what);
 }
 
@@ -568,6 +644,23 @@ ConvGeom base_geom(const void* x, int N, int H, int W, int C, const void* w, int
 using namespace posu;
 
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
+
+extern "C" int posu_force_conv_config(int cfg) {
+  POSU_REQUIRE(cfg >= -1 && cfg <= 6, "posu_force_conv_config: -1 (auto) or 0..6");
+  g_force = cfg;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_tiles(int big) {
+  g_big = big ? 1 : 0;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_stages(int stages) {
+  POSU_REQUIRE(stages == 2 || stages == 3, "posu_set_conv_stages: 2 or 3");
+  g_stages = stages;
+  return POSU_OK;
+}
 
 extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,

@@ -29,6 +29,21 @@ def conv_bk(code):
     return nat.load().posu_conv_bk(code)
 
 
+def force_conv_config(cfg):
+    """Test hook: force a conv tile configuration (see include/posu.h), -1 = automatic."""
+    call('posu_force_conv_config', int(cfg))
+
+
+def set_conv_tiles(big):
+    """Enable (True) / disable the eight-wave 256-row tiles for wide layers."""
+    call('posu_set_conv_tiles', int(bool(big)))
+
+
+def set_conv_stages(stages):
+    """Depth of the conv kernels' LDS-DMA ring (2 or 3 K-tiles in flight)."""
+    call('posu_set_conv_stages', int(stages))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C)."""

@@ -288,3 +288,43 @@ def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f):
     f2 = ops.deconv4x4s2_nhwc(xd, wp, cout, sc.to(cuda), sh.to(cuda), True, code)
     hm2 = ops.head1x1_nchw(f2, hwp, J, hb.to(cuda), code)
     torch.testing.assert_close(hm, hm2, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('case', CONV_CASES[1:5])
+def test_conv2d_three_stage_ring_matches_torch(cuda, case):
+    ops.set_conv_stages(3)
+    try:
+        got, ref = _conv_case(cuda, F32, *case)
+    finally:
+        ops.set_conv_stages(2)
+    torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_every_tile_configuration_matches_torch(cuda, cfg, code):
+    """Each tile shape (incl. LDS rings above 64 KiB and eight-wave blocks) on ragged shapes:
+    3x3 with residual, 1x1 strided, and the dual-source tail."""
+    cout = 256 if cfg in (3, 4, 5, 6) else 64
+    ops.force_conv_config(cfg)
+    try:
+        for case in [(2, 64, 17, 15, cout, 3, 1, 1, True, True), (3, 128, 12, 12, cout, 1, 2, 0, False, False)]:
+            got, ref = _conv_case(cuda, code, *case)
+            if code == F32:
+                torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+            else:
+                assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
+    finally:
+        ops.force_conv_config(-1)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, None)])
+@pytest.mark.parametrize('cout', [256, 384])
+def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
+    """Large grids take the eight-wave 256 x 256 / 256 x 128 tiles (residual epilogue in passes)."""
+    case = (64, 64, 32, 32, cout, 3, 1, 1, True, True)  # M = 65536: >= 256 big tiles
+    got, ref = _conv_case(cuda, code, *case)
+    if tol is None:
+        assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
+    else:
+        torch.testing.assert_close(got, ref, atol=tol, rtol=tol)

@@ -36,11 +36,15 @@ def main():
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--precision', default='bf16')
     ap.add_argument('--reps', type=int, default=20)
+    ap.add_argument('--stages', type=int, default=2)
+    ap.add_argument('--big', type=int, default=1)
     args = ap.parse_args()
     import bench
     dev = torch.device('cuda', 0)
     net = bench.build_model(args.layers, args.size, args.precision, dev)
     plan = net.plan(dev)
+    ops.set_conv_stages(args.stages)
+    ops.set_conv_tiles(args.big)
     code = plan.code
     esz = 2 if code == ops.BF16 else 4
     x_in = [torch.randn(args.batch, 3, args.size, args.size, device=dev)]
@@ -89,10 +93,18 @@ def main():
                 out = o
             x = out
     for i, dc in enumerate(plan.deconvs):
+        xs_last = x
         o = dc(x, code)
         rec('deconv%d' % (i + 1), lambda dc=dc, x=x: dc(x, code),
             2 * o.numel() * x.shape[3] * 4, (x.numel() + o.numel()) * esz)
         x = o
+    if plan.fuse_head:
+        dc = plan.deconvs[-1]
+        xin = xs_last
+        rec('deconv3+head(fused)', lambda: ops.deconv4x4s2_head(xin, dc.w, dc.cout, dc.scale, dc.shift, plan.head_w,
+                                                                  plan.njoints, plan.head_b, code, keep_f=False),
+            2 * x.numel() * xin.shape[3] * 4 + 2 * x.shape[0] * x.shape[1] * x.shape[2] * 16 * 256,
+            xin.numel() * esz + x.shape[0] * 16 * x.shape[1] * x.shape[2] * 4)
     hm = ops.head1x1_nchw(x, plan.head_w, plan.njoints, plan.head_b, code)
     rec('head', lambda: ops.head1x1_nchw(x, plan.head_w, plan.njoints, plan.head_b, code),
         2 * hm.numel() * x.shape[3], x.numel() * esz + hm.numel() * 4)
