@@ -45,7 +45,7 @@ def parse():
     ap.add_argument('--groups', type=int, default=32, help='4-view groups per GPU per step')
     ap.add_argument('--layers', type=int, default=50)
     ap.add_argument('--size', type=int, default=256)
-    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--chunks', type=int, default=1,
                     help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
@@ -124,13 +124,12 @@ def main():
         pdist.init('nccl', device=dev)
 
     from posu import synthetic as syn
-    from posu.pipeline import MultiViewPipeline, synthetic_meta
+    from posu.pipeline import synthetic_meta
     from posu import ops
 
     net = build_model(args.layers, args.size, args.precision, dev)
     meta, _ = synthetic_meta(args.groups, dev, image_size=args.size)
     views = [v.to(dev) for v in syn.synthetic_views(4, args.groups, args.size, seed=100 + rank)]
-    pipe = MultiViewPipeline(net)
     plan = net.plan(dev)
     frames = 4 * args.groups
 
@@ -207,7 +206,7 @@ def main():
     elapsed = pdist.max_over_ranks(elapsed, device=dev)
     value = pdist.throughput(frames, args.steps, world, elapsed)
     gf = GFLOP_PER_FRAME.get((args.layers, args.size))
-    peak = PEAK_BF16_TFLOPS if args.precision == 'bf16' else PEAK_F32_TFLOPS
+    peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS  # fp16 dense peak == bf16
     roof = None
     if gf is not None:
         achieved = gf * frames / (net_ms * 1e-3) / 1e3  # TFLOP/s

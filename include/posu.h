@@ -21,7 +21,9 @@
  *   - Return value: 0 (POSU_OK) or a POSU_ERR_* code; posu_last_error() then
  *     returns a thread-local message.
  *   - dtype codes: POSU_F32 (fp32 operands, exact-f32 MFMA, the parity mode)
- *                  POSU_BF16 (bf16 operands, f32 accumulate, the fast mode).
+ *                  POSU_BF16 (bf16 operands, f32 accumulate, the fast mode),
+ *                  POSU_F16  (IEEE fp16 operands, f32 accumulate: BASELINE configs[4]'s
+ *                             fp16 backbone; same kernels and speed as bf16).
  */
 #ifndef POSU_H_
 #define POSU_H_
@@ -37,6 +39,7 @@ extern "C" {
 #define POSU_F32 0
 #define POSU_BF16 1
 #define POSU_F64 2
+#define POSU_F16 3
 
 /* ---------------------------------------------------------------- runtime */
 const char* posu_last_error(void);

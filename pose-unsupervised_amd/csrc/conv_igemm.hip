@@ -94,6 +94,26 @@ struct Op<uint16_t> {  // bf16
 };
 
 template <>
+struct Op<f16_t> {  // IEEE fp16
+  static constexpr int E = 8;
+  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc,
+                                                 0, 0, 0);
+  }
+  static __device__ __forceinline__ void load_vals(const uint4& u, float* v) {
+    const f16x8 h = __builtin_bit_cast(f16x8, u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(h[i]);
+  }
+  static __device__ __forceinline__ uint4 store_vals(const float* v) {
+    f16x8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = static_cast<_Float16>(v[i]);
+    return __builtin_bit_cast(uint4, h);
+  }
+};
+
+template <>
 struct Op<float> {
   static constexpr int E = 4;
   static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
@@ -571,9 +591,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
     cfg = blocks(256, 64) >= 1024 ? 0 : (blocks(128, 64) >= 512 ? 1 : 2);
   } else if (g_big && g.CoutPad % 256 == 0 && blocks(256, 256) >= 256) {
     cfg = 5;
-  } else if (g_big && blocks(256, 128) >= 256) {
-    cfg = 6;
-  } else {
+  } else {  // 128-channel layers: 256 x 128 measured slower than 128 x 128 (layer2 c1/c2, R50@256)
     cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
   if (g_force >= 0) {
@@ -603,6 +621,7 @@ int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what)
   hipStream_t s = as_stream(stream);
   if (dtype == POSU_BF16) return launch<uint16_t, DUAL>(g, nclass, s, what);
   if (dtype == POSU_F32) return launch<float, DUAL>(g, nclass, s, what);
+  if (dtype == POSU_F16) return launch<f16_t, DUAL>(g, nclass, s, what);
   set_error(std::string(what) + ": unsupported dtype");
   return POSU_ERR_ARG;
 }
@@ -612,7 +631,8 @@ int esz_of(int dtype) { return dtype == POSU_F32 ? 4 : 2; }
 
 int common_checks(int dtype, const void* x, const void* w, const void* y, int N, int H, int W, int C,
                   int Cout, const char* what) {
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F32, std::string(what) + ": dtype must be F32 or BF16");
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F32 || dtype == POSU_F16,
+               std::string(what) + ": dtype must be F32, BF16 or F16");
   POSU_REQUIRE(x && w && y, std::string(what) + ": null pointer");
   POSU_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0, std::string(what) + ": empty shape");
   POSU_REQUIRE(C >= 8 && ilog2(C) >= 0, std::string(what) + ": C must be a power of two >= 8");
@@ -666,7 +686,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  const int E = dtype == POSU_F32 ? 4 : 8;
+  const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
   POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
@@ -728,7 +748,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  const int E = dtype == POSU_F32 ? 4 : 8;
+  const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
                "posu_deconv4x4s2_fwd: output too large");

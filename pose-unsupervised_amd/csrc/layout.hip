@@ -28,6 +28,21 @@ struct Vec<uint16_t> {
   }
 };
 template <>
+struct Vec<f16_t> {
+  static constexpr int E = 8;
+  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
+    const f16x8 h = __builtin_bit_cast(f16x8, u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(h[i]);
+  }
+  static __device__ __forceinline__ uint4 pack(const float* v) {
+    f16x8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = static_cast<_Float16>(v[i]);
+    return __builtin_bit_cast(uint4, h);
+  }
+};
+template <>
 struct Vec<float> {
   static constexpr int E = 4;
   static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
@@ -151,6 +166,19 @@ inline int grid_for(long long total) {
   return static_cast<int>(g < 8192 ? (g > 0 ? g : 1) : 8192);
 }
 
+// storage-type dispatch: fn(T{}) for the dtype code, false if unsupported
+template <typename Fn>
+bool with_storage(int dtype, Fn&& fn) {
+  switch (dtype) {
+    case POSU_BF16: fn(uint16_t{}); return true;
+    case POSU_F16: fn(f16_t{}); return true;
+    case POSU_F32: fn(float{}); return true;
+    default: return false;
+  }
+}
+
+int chunk_elems(int dtype) { return dtype == POSU_F32 ? 4 : 8; }
+
 }  // namespace
 }  // namespace posu
 
@@ -160,20 +188,15 @@ extern "C" int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, i
                                       void* stream) {
   POSU_REQUIRE(x && y, "posu_pack_nchw_to_nhwc: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && Cpad >= C, "posu_pack_nchw_to_nhwc: bad shape");
+  POSU_REQUIRE(Cpad % chunk_elems(dtype) == 0, "posu_pack_nchw_to_nhwc: Cpad is not a whole number of 16-B chunks");
   hipStream_t s = as_stream(stream);
   const long long pix = static_cast<long long>(N) * H * W;
-  if (dtype == POSU_BF16) {
-    POSU_REQUIRE(Cpad % 8 == 0, "posu_pack_nchw_to_nhwc: Cpad % 8 != 0");
-    hipLaunchKernelGGL(pack_kernel<uint16_t>, dim3(grid_for(pix * Cpad / 8)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<uint16_t*>(y), Cpad);
-  } else if (dtype == POSU_F32) {
-    POSU_REQUIRE(Cpad % 4 == 0, "posu_pack_nchw_to_nhwc: Cpad % 4 != 0");
-    hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(pix * Cpad / 4)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<float*>(y), Cpad);
-  } else {
-    set_error("posu_pack_nchw_to_nhwc: unsupported dtype");
-    return POSU_ERR_ARG;
-  }
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(pack_kernel<T>, dim3(grid_for(pix * Cpad / Vec<T>::E)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<T*>(y), Cpad);
+  });
+  POSU_REQUIRE(ok, "posu_pack_nchw_to_nhwc: unsupported dtype");
   return check_launch("posu_pack_nchw_to_nhwc");
 }
 
@@ -182,20 +205,15 @@ extern "C" int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H
   POSU_REQUIRE(x && y, "posu_pack_s2d_nchw: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 1 && W > 1 && H % 2 == 0 && W % 2 == 0 && 4 * C <= Cpad,
                "posu_pack_s2d_nchw: bad shape (H, W even, 4C <= Cpad)");
+  POSU_REQUIRE(Cpad % chunk_elems(dtype) == 0, "posu_pack_s2d_nchw: Cpad is not a whole number of 16-B chunks");
   hipStream_t s = as_stream(stream);
   const long long pix = static_cast<long long>(N) * (H / 2) * (W / 2);
-  if (dtype == POSU_BF16) {
-    POSU_REQUIRE(Cpad % 8 == 0, "posu_pack_s2d_nchw: Cpad % 8 != 0");
-    hipLaunchKernelGGL(pack_s2d_kernel<uint16_t>, dim3(grid_for(pix * Cpad / 8)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<uint16_t*>(y), Cpad);
-  } else if (dtype == POSU_F32) {
-    POSU_REQUIRE(Cpad % 4 == 0, "posu_pack_s2d_nchw: Cpad % 4 != 0");
-    hipLaunchKernelGGL(pack_s2d_kernel<float>, dim3(grid_for(pix * Cpad / 4)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<float*>(y), Cpad);
-  } else {
-    set_error("posu_pack_s2d_nchw: unsupported dtype");
-    return POSU_ERR_ARG;
-  }
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(pack_s2d_kernel<T>, dim3(grid_for(pix * Cpad / Vec<T>::E)), dim3(256), 0, s, x, N, C, H, W,
+                       static_cast<T*>(y), Cpad);
+  });
+  POSU_REQUIRE(ok, "posu_pack_s2d_nchw: unsupported dtype");
   return check_launch("posu_pack_s2d_nchw");
 }
 
@@ -203,20 +221,15 @@ extern "C" int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int
                                      void* stream) {
   POSU_REQUIRE(x && y, "posu_nhwc_to_nchw_f32: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, "posu_nhwc_to_nchw_f32: bad shape");
+  POSU_REQUIRE(C % chunk_elems(dtype) == 0, "posu_nhwc_to_nchw_f32: C is not a whole number of 16-B chunks");
   hipStream_t s = as_stream(stream);
   const long long el = static_cast<long long>(N) * H * W * C;
-  if (dtype == POSU_BF16) {
-    POSU_REQUIRE(C % 8 == 0, "posu_nhwc_to_nchw_f32: C % 8 != 0");
-    hipLaunchKernelGGL(unpack_kernel<uint16_t>, dim3(grid_for(el / 8)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), N, H, W, C, y);
-  } else if (dtype == POSU_F32) {
-    POSU_REQUIRE(C % 4 == 0, "posu_nhwc_to_nchw_f32: C % 4 != 0");
-    hipLaunchKernelGGL(unpack_kernel<float>, dim3(grid_for(el / 4)), dim3(256), 0, s,
-                       static_cast<const float*>(x), N, H, W, C, y);
-  } else {
-    set_error("posu_nhwc_to_nchw_f32: unsupported dtype");
-    return POSU_ERR_ARG;
-  }
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(unpack_kernel<T>, dim3(grid_for(el / Vec<T>::E)), dim3(256), 0, s, static_cast<const T*>(x),
+                       N, H, W, C, y);
+  });
+  POSU_REQUIRE(ok, "posu_nhwc_to_nchw_f32: unsupported dtype");
   return check_launch("posu_nhwc_to_nchw_f32");
 }
 
@@ -224,20 +237,15 @@ extern "C" int posu_maxpool3x3s2_fwd(int dtype, const void* x, int N, int H, int
                                      void* stream) {
   POSU_REQUIRE(x && y, "posu_maxpool3x3s2_fwd: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0, "posu_maxpool3x3s2_fwd: bad shape");
+  POSU_REQUIRE(C % chunk_elems(dtype) == 0, "posu_maxpool3x3s2_fwd: C is not a whole number of 16-B chunks");
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipStream_t s = as_stream(stream);
   const long long el = static_cast<long long>(N) * Ho * Wo * C;
-  if (dtype == POSU_BF16) {
-    POSU_REQUIRE(C % 8 == 0, "posu_maxpool3x3s2_fwd: C % 8 != 0");
-    hipLaunchKernelGGL(maxpool_kernel<uint16_t>, dim3(grid_for(el / 8)), dim3(256), 0, s,
-                       static_cast<const uint16_t*>(x), N, H, W, C, static_cast<uint16_t*>(y), Ho, Wo);
-  } else if (dtype == POSU_F32) {
-    POSU_REQUIRE(C % 4 == 0, "posu_maxpool3x3s2_fwd: C % 4 != 0");
-    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_for(el / 4)), dim3(256), 0, s,
-                       static_cast<const float*>(x), N, H, W, C, static_cast<float*>(y), Ho, Wo);
-  } else {
-    set_error("posu_maxpool3x3s2_fwd: unsupported dtype");
-    return POSU_ERR_ARG;
-  }
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(maxpool_kernel<T>, dim3(grid_for(el / Vec<T>::E)), dim3(256), 0, s, static_cast<const T*>(x),
+                       N, H, W, C, static_cast<T*>(y), Ho, Wo);
+  });
+  POSU_REQUIRE(ok, "posu_maxpool3x3s2_fwd: unsupported dtype");
   return check_launch("posu_maxpool3x3s2_fwd");
 }

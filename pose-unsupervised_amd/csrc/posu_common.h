@@ -26,6 +26,13 @@ int check_launch(const char* what);
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+// IEEE binary16 storage type (POSU_F16); distinct from the bf16 storage type uint16_t
+// so the kernels' per-dtype traits can tell them apart.
+struct f16_t {
+  uint16_t bits;
+};
 
 __device__ __forceinline__ float bf2f(uint16_t b) {
   return __uint_as_float(static_cast<uint32_t>(b) << 16);

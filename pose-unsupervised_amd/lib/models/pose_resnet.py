@@ -10,8 +10,9 @@ The modules hold the parameters in the reference's NCHW fp32 layout; forward run
 :class:`posu.plan.PoseResNetPlan` (NHWC, MFMA implicit-GEMM kernels, BN folded into
 the conv epilogues) that is re-packed whenever a parameter or buffer changes.
 
-Compute dtype: ``precision='bf16'`` (default, bf16 operands / f32 accumulate) or
-``'fp32'`` (exact-f32 MFMA; the parity mode).  Heatmaps are always returned as NCHW
+Compute dtype: ``precision='bf16'`` (default, bf16 operands / f32 accumulate),
+``'fp16'`` (IEEE fp16 operands / f32 accumulate, the fp16 setting of BASELINE
+configs[4]) or ``'fp32'`` (exact-f32 MFMA; the parity mode).  Heatmaps are always returned as NCHW
 float32; ``layer1_out`` / ``deconv_out`` are returned as NCHW-shaped channels-last
 views of the NHWC activations in the compute dtype (zero-copy).
 
@@ -185,7 +186,7 @@ resnet_spec = {18: (BasicBlock, [2, 2, 2, 2]),
 
 
 def get_pose_net(cfg, is_train, **kwargs):
-    """Reference factory (pose_resnet.py:257-267); extra kwarg ``precision`` = 'bf16' | 'fp32'."""
+    """Reference factory (pose_resnet.py:257-267); extra kwarg ``precision`` = 'bf16' | 'fp16' | 'fp32'."""
     block_class, layers = resnet_spec[cfg.POSE_RESNET.NUM_LAYERS]
     model = PoseResNet(block_class, layers, cfg, **kwargs)
     if is_train:

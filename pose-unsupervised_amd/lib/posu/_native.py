@@ -14,6 +14,7 @@ import torch  # noqa: F401  -- loads PyTorch's HIP runtime before libposeu.so bi
 F32 = 0
 BF16 = 1
 F64 = 2
+F16 = 3
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()

@@ -8,9 +8,9 @@ through (soft-argmax, crop affine, epipolar loss, heatmap MSE).
 import torch
 
 from . import _native as nat
-from ._native import F32, BF16, F64, ptr, call, stream_of, require_cuda
+from ._native import F32, BF16, F64, F16, ptr, call, stream_of, require_cuda
 
-_TORCH_OF = {F32: torch.float32, BF16: torch.bfloat16}
+_TORCH_OF = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
 
 
 def dtype_code(dtype):
@@ -18,7 +18,9 @@ def dtype_code(dtype):
         return BF16
     if dtype in ('fp32', 'f32', torch.float32, F32):
         return F32
-    raise ValueError('unsupported compute dtype %r (bf16 | fp32)' % (dtype,))
+    if dtype in ('fp16', 'f16', torch.float16, F16):
+        return F16
+    raise ValueError('unsupported compute dtype %r (bf16 | fp16 | fp32)' % (dtype,))
 
 
 def torch_dtype(code):

@@ -7,7 +7,7 @@ import torch.nn.functional as F
 
 from oracle import geometry_ref as G
 from posu import ops, packing, synthetic as syn
-from posu._native import BF16, F32
+from posu._native import BF16, F16, F32
 
 pytestmark = pytest.mark.gpu
 
@@ -63,7 +63,15 @@ def test_conv2d_bf16_close_to_torch(cuda, case):
     assert err <= 0.03 * scale + 0.02, (err, scale)
 
 
-@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('case', CONV_CASES)
+def test_conv2d_fp16_close_to_torch(cuda, case):
+    got, ref = _conv_case(cuda, F16, *case)
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= 0.004 * scale + 0.004, (err, scale)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 def test_deconv4x4s2_matches_conv_transpose(cuda, code, tol):
     g = torch.Generator().manual_seed(3)
     n, cin, h, w, cout = 2, 64, 6, 5, 64
@@ -80,7 +88,7 @@ def test_deconv4x4s2_matches_conv_transpose(cuda, code, tol):
     torch.testing.assert_close(got, ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 def test_head1x1_writes_nchw_heatmaps(cuda, code, tol):
     g = torch.Generator().manual_seed(4)
     x = torch.randn(3, 256, 16, 16, generator=g)
@@ -93,7 +101,7 @@ def test_head1x1_writes_nchw_heatmaps(cuda, code, tol):
     torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize('code', [F32, BF16])
+@pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_maxpool_pack_unpack(cuda, code):
     g = torch.Generator().manual_seed(5)
     x = torch.randn(2, 3, 33, 30, generator=g)
@@ -224,7 +232,7 @@ def test_triangulate_one_point_api(cuda, golden):
     np.testing.assert_allclose(X, g['poses3d'][0, 4], atol=1e-6)
 
 
-@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 def test_s2d_stem_matches_torch(cuda, code, tol):
     g = torch.Generator().manual_seed(6)
     x = torch.randn(2, 3, 36, 40, generator=g)
@@ -240,7 +248,7 @@ def test_s2d_stem_matches_torch(cuda, code, tol):
     torch.testing.assert_close(out.float().cpu().permute(0, 3, 1, 2), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 @pytest.mark.parametrize('stride', [1, 2])
 def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
     g = torch.Generator().manual_seed(7)
@@ -261,7 +269,7 @@ def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
     torch.testing.assert_close(out.float().cpu().permute(0, 3, 1, 2), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05)])
+@pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 @pytest.mark.parametrize('keep_f', [True, False])
 def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f):
     g = torch.Generator().manual_seed(8)
@@ -301,7 +309,7 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
 
 
 @pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
-@pytest.mark.parametrize('code', [F32, BF16])
+@pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB and eight-wave blocks) on ragged shapes:
     3x3 with residual, 1x1 strided, and the dual-source tail."""
@@ -321,7 +329,8 @@ def test_every_tile_configuration_matches_torch(cuda, cfg, code):
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, None)])
 @pytest.mark.parametrize('cout', [256, 384])
 def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
-    """Large grids take the eight-wave 256 x 256 / 256 x 128 tiles (residual epilogue in passes)."""
+    """Large grids take the eight-wave 256 x 256 tiles (residual epilogue in passes) when
+    Cout % 256 == 0; 384 channels take the automatic fallback (128 x 128)."""
     case = (64, 64, 32, 32, cout, 3, 1, 1, True, True)  # M = 65536: >= 256 big tiles
     got, ref = _conv_case(cuda, code, *case)
     if tol is None:
