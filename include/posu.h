@@ -233,6 +233,64 @@ int posu_triangulate_dlt(const double* M, const double* intr, const void* xy, in
                          int xy_stride_g, int xy_stride_v, const unsigned char* vis, int G,
                          int V, int J, int undistort, double* X, void* stream);
 
+/* ----------------------------------------------------------- training path */
+/* BASELINE configs[3]: the data-parallel training step (run/pose2d/train.py +
+ * core/function.py:91-366: per-view backbone forward in train mode, JointsMSELoss,
+ * FundamentalLoss, loss.backward(), optimizer step).  Replaces the autograd of
+ * torch.nn.Conv2d / ConvTranspose2d / BatchNorm2d / ReLU / MaxPool2d for the
+ * PoseResNet modules (lib/models/pose_resnet.py:21-205). */
+
+/* Data gradient of conv2d x[N,H,W,Cin] -> y[N,Ho,Wo,Cout] (KHxKW, stride 1|2, pad):
+ *   dy: [N,Ho,Wo,Cout] dtype; wt: weights flipped + transposed, packed
+ *   [round_up(Cin,64)][round_up(KH*KW*Cout, BK)] (K order (kh, kw, co)), i.e. the
+ *   forward packing of W[:, :, ::-1, ::-1].transpose(0, 1);
+ *   residual: NULL or [N,H,W,Cin] added to dx; dx: [N,H,W,Cin] dtype.
+ *   Cout must be a power of two >= 8 (it is the GEMM's reduction channel count). */
+int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
+                      int Cin, int KH, int KW, int stride, int pad, const void* residual,
+                      void* dx, int H, int W, void* stream);
+
+/* Weight gradient dW[Cout][Creal][KH][KW] (f32, the nn.Conv2d weight layout) of a
+ * conv over x[N,H,W,C] (C >= Creal, padded channels ignored) with output gradient
+ * dy[N,Ho,Wo,Cout].  Also ConvTranspose2d(4, s2, p1): pass x = the transposed
+ * conv's output gradient (as a [N,2H,2W,Cout_t] input), dy = its input
+ * [N,H,W,Cin_t], KH=KW=4, stride 2, pad 1 -> dW[Cin_t][Cout_t][4][4].
+ * workspace >= posu_conv2d_wgrad_workspace(...) bytes (split-K partials). */
+long long posu_conv2d_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int KH,
+                                      int KW, int stride, int pad);
+int posu_conv2d_wgrad(int dtype, const void* dy, const void* x, int N, int H, int W, int C,
+                      int Creal, int Cout, int KH, int KW, int stride, int pad, float* dw,
+                      void* workspace, long long workspace_bytes, void* stream);
+
+/* Training-mode BatchNorm2d over z[nseg*Pseg, C] (NHWC, nseg batch segments = camera
+ * views with separate statistics, torch.nn.functional.batch_norm(training=True)
+ * per segment): mean/rstd/scale/shift [nseg, C] f32 out; running_mean/var
+ * (optional) updated once per segment in order, unbiased variance. */
+long long posu_bn_workspace(int nseg, int C);
+int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const float* gamma,
+                      const float* beta, float eps, float momentum, float* running_mean,
+                      float* running_var, float* mean, float* rstd, float* scale, float* shift,
+                      void* workspace, long long workspace_bytes, void* stream);
+/* y = act(z * scale[seg] + shift[seg] (+ residual)) */
+int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                  const float* shift, const void* residual, int relu, void* y, void* stream);
+/* Backward of y = relu?(bn(z) (+ r)):  g' = gy * [y > 0] (y NULL: no ReLU);
+ * dz = gamma*rstd*(g' - mean(g') - xhat*mean(g'*xhat)) per segment; dgamma/dbeta
+ * [C] f32 written (summed over segments); gres (optional) = g'. */
+int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const void* z, int nseg, int Pseg,
+                      int C, const float* mean, const float* rstd, const float* gamma,
+                      float* dgamma, float* dbeta, void* dz, void* gres, void* workspace,
+                      long long workspace_bytes, void* stream);
+/* out[c] = sum_p x[p][c] (f32), e.g. the final layer's bias gradient;
+ * workspace >= posu_bn_workspace(1, C). */
+int posu_channel_sum(int dtype, const void* x, int P, int C, float* out, void* workspace,
+                     long long workspace_bytes, void* stream);
+/* MaxPool2d(3, 2, 1) backward (PyTorch's first-maximum tie rule), x the forward
+ * input [N,H,W,C], gy [N,Ho,Wo,C] -> gx [N,H,W,C]; workspace: argmax taps. */
+long long posu_maxpool3x3s2_bwd_workspace(int N, int H, int W, int C);
+int posu_maxpool3x3s2_bwd(int dtype, const void* x, int N, int H, int W, int C, const void* gy,
+                          void* gx, void* workspace, long long workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,473 @@
+// Training-mode BatchNorm2d on NHWC activations (BASELINE configs[3] training step):
+// batch statistics per segment (the reference runs the backbone once per camera view,
+// multiview_pose_resnet.py:74-78, so every view has its own statistics; here the views
+// are stacked along the batch as `nseg` segments of `Pseg` pixels and one launch
+// serves all of them), the normalise + residual + ReLU epilogue, the matching
+// backward, the bias-gradient channel sum and the stem max-pool backward.
+//
+// Reductions are deterministic: per-block partial sums in f64 written to a workspace,
+// then one thread per channel sums the blocks in a fixed order.  Running statistics
+// follow torch.nn.BatchNorm2d: biased variance for normalisation, unbiased variance in
+// running_var, running = (1 - momentum) * running + momentum * batch, updated once per
+// segment in segment (= view) order like the reference's four backbone calls.
+#include "posu_common.h"
+
+namespace posu {
+namespace {
+
+constexpr int kMaxNB = 256;  // partial-sum blocks per segment
+
+struct RedShape {
+  int CPR, CB, PL, CG, NB, PPB;
+};
+
+RedShape red_shape(int Pseg, int C, int E, int nseg) {
+  RedShape r;
+  r.CPR = C / E;
+  r.CB = std::min(r.CPR, 256);
+  r.PL = 256 / r.CB;
+  r.CG = (r.CPR + r.CB - 1) / r.CB;
+  int nb = std::max(1, 1024 / (r.CG * nseg));
+  nb = std::min(nb, kMaxNB);
+  nb = std::min(nb, std::max(1, Pseg / r.PL));
+  r.NB = nb;
+  r.PPB = (Pseg + nb - 1) / nb;
+  return r;
+}
+
+// MODE 0: (sum z, sum z^2)            -- forward statistics / channel sums
+// MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0] (y optional)
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z, const T* __restrict__ gy,
+                                                         const T* __restrict__ y, const float* __restrict__ mean,
+                                                         const float* __restrict__ rstd, int Pseg, int C,
+                                                         RedShape rs, double* __restrict__ part) {
+  constexpr int E = Vec<T>::E;
+  __shared__ double red[2][256][E];
+  const int tid = threadIdx.x;
+  const int pl = tid / rs.CB, cb = tid - pl * rs.CB;
+  const int ch = blockIdx.y * rs.CB + cb;
+  const int seg = blockIdx.z, blk = blockIdx.x;
+  const bool active = ch < rs.CPR;
+  float a[E], b[E], mu[E], rd[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    a[e] = 0.f;
+    b[e] = 0.f;
+    mu[e] = 0.f;
+    rd[e] = 0.f;
+  }
+  if (MODE == 1 && active) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      mu[e] = mean[seg * C + ch * E + e];
+      rd[e] = rstd[seg * C + ch * E + e];
+    }
+  }
+  if (active) {
+    const int pbeg = blk * rs.PPB, pend = min(Pseg, pbeg + rs.PPB);
+    for (int p = pbeg + pl; p < pend; p += rs.PL) {
+      const size_t off = (static_cast<size_t>(seg) * Pseg + p) * C + ch * E;
+      float v[E];
+      if constexpr (MODE == 0) {
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          a[e] += v[e];
+          b[e] += v[e] * v[e];
+        }
+      } else {
+        float gv[E];
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + off), gv);
+        if (y) {
+          float yv[E];
+          Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+          for (int e = 0; e < E; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+        }
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          a[e] += gv[e];
+          b[e] += gv[e] * ((v[e] - mu[e]) * rd[e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    red[0][tid][e] = a[e];
+    red[1][tid][e] = b[e];
+  }
+  __syncthreads();
+  for (int s = rs.PL / 2; s > 0; s >>= 1) {
+    if (pl < s) {
+      const int o = tid + s * rs.CB;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        red[0][tid][e] += red[0][o][e];
+        red[1][tid][e] += red[1][o][e];
+      }
+    }
+    __syncthreads();
+  }
+  if (pl == 0 && active) {
+    double* dst = part + (static_cast<size_t>(seg) * rs.NB + blk) * 2 * C;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      dst[ch * E + e] = red[0][tid][e];
+      dst[C + ch * E + e] = red[1][tid][e];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                                int Pseg, int C, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float momentum, float* running_mean,
+                                                                float* running_var, float* __restrict__ mean,
+                                                                float* __restrict__ rstd, float* __restrict__ scale,
+                                                                float* __restrict__ shift) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double n = static_cast<double>(Pseg);
+  for (int seg = 0; seg < nseg; ++seg) {
+    double s = 0.0, q = 0.0;
+    for (int b = 0; b < NB; ++b) {
+      const double* src = part + (static_cast<size_t>(seg) * NB + b) * 2 * C;
+      s += src[c];
+      q += src[C + c];
+    }
+    const double mu = s / n;
+    const double var = fmax(q / n - mu * mu, 0.0);
+    const double r = 1.0 / sqrt(var + static_cast<double>(eps));
+    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+    mean[seg * C + c] = static_cast<float>(mu);
+    rstd[seg * C + c] = static_cast<float>(r);
+    scale[seg * C + c] = static_cast<float>(gm * r);
+    shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
+    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mu);
+    if (running_var)
+      running_var[c] = (1.f - momentum) * running_var[c] +
+                       momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+  }
+}
+
+// y = act(z * scale[seg] + shift[seg] (+ res)), one thread per 16-B chunk
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ z, int Pseg, int C,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, const T* __restrict__ res,
+                                                       int relu, T* __restrict__ y, long long total) {
+  constexpr int E = Vec<T>::E;
+  const int CPR = C / E;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const long long pix = i / CPR;
+    const int c0 = static_cast<int>(i - pix * CPR) * E;
+    const int seg = static_cast<int>(pix / Pseg);
+    float v[E];
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + i * E), v);
+    float r[E];
+    if (res) Vec<T>::unpack(*reinterpret_cast<const uint4*>(res + i * E), r);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float t = v[e] * scale[seg * C + c0 + e] + shift[seg * C + c0 + e];
+      if (res) t += r[e];
+      v[e] = relu ? fmaxf(t, 0.f) : t;
+    }
+    *reinterpret_cast<uint4*>(y + i * E) = Vec<T>::pack(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                              int Pseg, int C, const float* __restrict__ gamma,
+                                                              const float* __restrict__ rstd,
+                                                              float* __restrict__ coef, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const double n = static_cast<double>(Pseg);
+  double tg = 0.0, tgx = 0.0;
+  for (int seg = 0; seg < nseg; ++seg) {
+    double sg = 0.0, sgx = 0.0;
+    for (int b = 0; b < NB; ++b) {
+      const double* src = part + (static_cast<size_t>(seg) * NB + b) * 2 * C;
+      sg += src[c];
+      sgx += src[C + c];
+    }
+    tg += sg;
+    tgx += sgx;
+    const float gm = gamma ? gamma[c] : 1.f;
+    coef[(seg * 3 + 0) * C + c] = gm * rstd[seg * C + c];
+    coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
+    coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
+  }
+  if (dgamma) dgamma[c] = static_cast<float>(tgx);
+  if (dbeta) dbeta[c] = static_cast<float>(tg);
+}
+
+// dz = gamma*rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = gy * [y > 0];
+// gres (optional) = g', the gradient of the residual branch
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ y,
+                                                           const T* __restrict__ z, int Pseg, int C,
+                                                           const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd,
+                                                           const float* __restrict__ coef, T* __restrict__ dz,
+                                                           T* __restrict__ gres, long long total) {
+  constexpr int E = Vec<T>::E;
+  const int CPR = C / E;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const long long pix = i / CPR;
+    const int c0 = static_cast<int>(i - pix * CPR) * E;
+    const int seg = static_cast<int>(pix / Pseg);
+    float g[E], v[E];
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + i * E), g);
+    if (y) {
+      float yv[E];
+      Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + i * E), yv);
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+    }
+    if (gres) *reinterpret_cast<uint4*>(gres + i * E) = Vec<T>::pack(g);
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + i * E), v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int c = c0 + e;
+      const float xh = (v[e] - mean[seg * C + c]) * rstd[seg * C + c];
+      const float k1 = coef[(seg * 3 + 0) * C + c], mg = coef[(seg * 3 + 1) * C + c],
+                  mgx = coef[(seg * 3 + 2) * C + c];
+      v[e] = k1 * (g[e] - mg - xh * mgx);
+    }
+    *reinterpret_cast<uint4*>(dz + i * E) = Vec<T>::pack(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                                   int C, float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  double s = 0.0;
+  for (int seg = 0; seg < nseg; ++seg)
+    for (int b = 0; b < NB; ++b) s += part[(static_cast<size_t>(seg) * NB + b) * 2 * C + c];
+  out[c] = static_cast<float>(s);
+}
+
+// ---- max-pool 3x3 / s2 / p1 backward (PyTorch's tie rule: the first maximum in
+// window scan order, pool.h max_pool2d `val > maxval || isnan(val)`).
+// pass 1: argmax tap (0..8) per output element; pass 2: every input element gathers
+// the gradients of the (at most 2 x 2) windows whose argmax it is -- no atomics.
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_argmax_kernel(const T* __restrict__ x, int N, int H, int W, int C,
+                                                             int Ho, int Wo, uint8_t* __restrict__ idx) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = C / E;
+  const long long total = static_cast<long long>(N) * Ho * Wo * chunks;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const int ox = static_cast<int>(pix % Wo);
+    const long long t = pix / Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const long long n = t / Ho;
+    float m[E];
+    int am[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      m[e] = 0.f;
+      am[e] = -1;
+    }
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap - 3 * dy;
+      const int iy = oy * 2 - 1 + dy, ix = ox * 2 - 1 + dx;
+      if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+      float v[E];
+      Vec<T>::unpack(*reinterpret_cast<const uint4*>(x + ((n * H + iy) * W + ix) * C + ch * E), v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const bool take = am[e] < 0 || v[e] > m[e] || v[e] != v[e];
+        m[e] = take ? v[e] : m[e];
+        am[e] = take ? tap : am[e];
+      }
+    }
+    uint8_t* dst = idx + pix * C + ch * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) dst[e] = static_cast<uint8_t>(am[e]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint8_t* __restrict__ idx, const T* __restrict__ gy,
+                                                          int N, int H, int W, int C, int Ho, int Wo,
+                                                          T* __restrict__ gx) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = C / E;
+  const long long total = static_cast<long long>(N) * H * W * chunks;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const int ix = static_cast<int>(pix % W);
+    const long long t = pix / W;
+    const int iy = static_cast<int>(t % H);
+    const long long n = t / H;
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+    // windows oy with 2*oy - 1 <= iy <= 2*oy + 1, in increasing (oy, ox) order
+    const int oy0 = max(0, (iy - 1) / 2), oy1 = min(Ho - 1, (iy + 1) / 2);
+    const int ox0 = max(0, (ix - 1) / 2), ox1 = min(Wo - 1, (ix + 1) / 2);
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      const int dy = iy - (oy * 2 - 1);
+      if (dy < 0 || dy > 2) continue;
+      for (int ox = ox0; ox <= ox1; ++ox) {
+        const int dx = ix - (ox * 2 - 1);
+        if (dx < 0 || dx > 2) continue;
+        const long long o = ((n * Ho + oy) * Wo + ox) * C + ch * E;
+        float g[E];
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + o), g);
+        const int tap = dy * 3 + dx;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+          if (idx[o + e] == tap) acc[e] += g[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(gx + pix * C + ch * E) = Vec<T>::pack(acc);
+  }
+}
+
+inline int grid_for(long long total) {
+  long long g = (total + 255) / 256;
+  return static_cast<int>(g < 8192 ? (g > 0 ? g : 1) : 8192);
+}
+
+int chunk_elems(int dtype) { return dtype == POSU_F32 ? 4 : 8; }
+
+// the block reduction pairs pixel lanes in powers of two
+bool reducible(int C, int dtype) {
+  const int cpr = C / chunk_elems(dtype);
+  return cpr >= 256 ? cpr % 256 == 0 : ilog2(cpr) >= 0;
+}
+
+long long partial_bytes(int nseg, int C) { return static_cast<long long>(nseg) * kMaxNB * 2 * C * 8; }
+
+}  // namespace
+}  // namespace posu
+
+using namespace posu;
+
+extern "C" long long posu_bn_workspace(int nseg, int C) {
+  return partial_bytes(nseg, C) + static_cast<long long>(nseg) * 3 * C * 4;
+}
+
+extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const float* gamma,
+                                 const float* beta, float eps, float momentum, float* running_mean,
+                                 float* running_var, float* mean, float* rstd, float* scale, float* shift,
+                                 void* workspace, long long workspace_bytes, void* stream) {
+  POSU_REQUIRE(z && mean && rstd && scale && shift && workspace, "posu_bn_train_fwd: null pointer");
+  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0 && reducible(C, dtype),
+               "posu_bn_train_fwd: bad shape (C / chunk must be a power of two or a multiple of 256)");
+  POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_fwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
+                       static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part);
+  });
+  POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+                     gamma, beta, eps, momentum, running_mean, running_var, mean, rstd, scale, shift);
+  return check_launch("posu_bn_train_fwd");
+}
+
+extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                             const float* shift, const void* residual, int relu, void* y, void* stream) {
+  POSU_REQUIRE(z && scale && shift && y, "posu_bn_apply: null pointer");
+  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_bn_apply: bad shape");
+  hipStream_t s = as_stream(stream);
+  const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(z), Pseg,
+                       C, scale, shift, static_cast<const T*>(residual), relu, static_cast<T*>(y), total);
+  });
+  POSU_REQUIRE(ok, "posu_bn_apply: unsupported dtype");
+  return check_launch("posu_bn_apply");
+}
+
+extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const void* z, int nseg, int Pseg, int C,
+                                 const float* mean, const float* rstd, const float* gamma, float* dgamma,
+                                 float* dbeta, void* dz, void* gres, void* workspace, long long workspace_bytes,
+                                 void* stream) {
+  POSU_REQUIRE(gy && z && mean && rstd && dz && workspace, "posu_bn_train_bwd: null pointer");
+  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0 && reducible(C, dtype),
+               "posu_bn_train_bwd: bad shape (C / chunk must be a power of two or a multiple of 256)");
+  POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_bwd: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  float* coef = reinterpret_cast<float*>(static_cast<char*>(workspace) + partial_bytes(nseg, C));
+  const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
+  const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
+  bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
+                       static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), mean, rstd, Pseg,
+                       C, rs, part);
+  });
+  POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
+                     rstd, coef, dgamma, dbeta);
+  with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(gy),
+                       static_cast<const T*>(y), static_cast<const T*>(z), Pseg, C, mean, rstd, coef,
+                       static_cast<T*>(dz), static_cast<T*>(gres), total);
+  });
+  return check_launch("posu_bn_train_bwd");
+}
+
+extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* out, void* workspace,
+                                long long workspace_bytes, void* stream) {
+  POSU_REQUIRE(x && out && workspace, "posu_channel_sum: null pointer");
+  POSU_REQUIRE(P > 0 && C > 0 && C % chunk_elems(dtype) == 0 && reducible(C, dtype),
+               "posu_channel_sum: bad shape (C / chunk must be a power of two or a multiple of 256)");
+  POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(1, C), "posu_channel_sum: workspace too small");
+  hipStream_t s = as_stream(stream);
+  double* part = static_cast<double*>(workspace);
+  const RedShape rs = red_shape(P, C, chunk_elems(dtype), 1);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, 1), dim3(256), 0, s, static_cast<const T*>(x),
+                       nullptr, nullptr, nullptr, nullptr, P, C, rs, part);
+  });
+  POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
+  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, 1, rs.NB, C, out);
+  return check_launch("posu_channel_sum");
+}
+
+extern "C" long long posu_maxpool3x3s2_bwd_workspace(int N, int H, int W, int C) {
+  const long long Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  return N * Ho * Wo * C;
+}
+
+extern "C" int posu_maxpool3x3s2_bwd(int dtype, const void* x, int N, int H, int W, int C, const void* gy, void* gx,
+                                     void* workspace, long long workspace_bytes, void* stream) {
+  POSU_REQUIRE(x && gy && gx && workspace, "posu_maxpool3x3s2_bwd: null pointer");
+  POSU_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_maxpool3x3s2_bwd: bad shape");
+  POSU_REQUIRE(workspace_bytes >= posu_maxpool3x3s2_bwd_workspace(N, H, W, C),
+               "posu_maxpool3x3s2_bwd: workspace too small");
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipStream_t s = as_stream(stream);
+  uint8_t* idx = static_cast<uint8_t*>(workspace);
+  const int E = chunk_elems(dtype);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(maxpool_argmax_kernel<T>, dim3(grid_for(static_cast<long long>(N) * Ho * Wo * C / E)),
+                       dim3(256), 0, s, static_cast<const T*>(x), N, H, W, C, Ho, Wo, idx);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(static_cast<long long>(N) * H * W * C / E)), dim3(256),
+                       0, s, idx, static_cast<const T*>(gy), N, H, W, C, Ho, Wo, static_cast<T*>(gx));
+  });
+  POSU_REQUIRE(ok, "posu_maxpool3x3s2_bwd: unsupported dtype");
+  return check_launch("posu_maxpool3x3s2_bwd");
+}

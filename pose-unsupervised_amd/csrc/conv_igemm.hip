@@ -55,6 +55,8 @@ struct ConvGeom {
   int Cout, CoutPad, K, Kpad;
   int KH, KW, stride, pad_h, pad_w;
   int relu;
+  int up;            // 1: the input is read as its zero-upsampled image u[2i] = x[i], u[odd] = 0
+                     //    (data gradient of a stride-2 convolution as a stride-1 one)
   int deconv;        // blockIdx.z = parity class
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out
@@ -321,8 +323,10 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         kvalid = k < g.K;                                                                           \
       }                                                                                             \
       _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                              \
-        const int hi = hb[i] + kh, wi = wb[i] + kw;                                                 \
-        const bool ok = kvalid && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&         \
+        const int hl = hb[i] + kh, wl = wb[i] + kw;                                                 \
+        const int hi = hl >> g.up, wi = wl >> g.up;                                                 \
+        const bool ok = kvalid && ((hl | wl) & g.up) == 0 &&                                        \
+                        static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&                   \
                         static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);                     \
         const int off = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB;                      \
         dma16(xrs, off, As_ + i * NW * 1024);                                                       \
@@ -546,12 +550,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       }
     }
   }
-}
-
-int ilog2(int v) {
-  int l = 0;
-  while ((1 << l) < v) ++l;
-  return ((1 << l) == v) ? l : -1;
 }
 
 template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
@@ -814,4 +812,38 @@ extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int
   g.out_W = W;
   g.mode = 1;
   return dispatch<false>(dtype, g, 1, stream, "posu_head1x1_nchw_fwd");
+}
+
+// Data gradient of a KHxKW / stride / pad convolution x[N,H,W,Cin] -> y[N,Ho,Wo,Cout]:
+// dx = conv(dy, W flipped and transposed, pad K-1-pad) over dy, read as its
+// zero-upsampled image when stride == 2 (g.up), so strided layers run through the same
+// MFMA kernel as the forward.  `residual` (optional, [N,H,W,Cin]) is added in the
+// epilogue: the identity-branch gradient of a residual block.
+extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
+                                 int Cin, int KH, int KW, int stride, int pad, const void* residual, void* dx, int H,
+                                 int W, void* stream) {
+  if (int st = common_checks(dtype, dy, wt, dx, N, Ho, Wo, Cout, Cin, "posu_conv2d_dgrad")) return st;
+  POSU_REQUIRE(Cin % (16 / esz_of(dtype)) == 0, "posu_conv2d_dgrad: Cin must be a multiple of 16 bytes");
+  POSU_REQUIRE(stride == 1 || stride == 2, "posu_conv2d_dgrad: stride 1 or 2");
+  POSU_REQUIRE(KH > 0 && KW > 0 && pad >= 0 && pad < KH && pad < KW, "posu_conv2d_dgrad: bad window");
+  POSU_REQUIRE(H > 0 && W > 0 && Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1,
+               "posu_conv2d_dgrad: H/W do not produce Ho/Wo under this window");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * Cin < (1LL << 31), "posu_conv2d_dgrad: output too large");
+  ConvGeom g = base_geom(dy, N, Ho, Wo, Cout, wt, Cin, dtype);
+  g.res = residual;
+  g.y = dx;
+  g.Ho = H;
+  g.Wo = W;
+  g.M = N * H * W;
+  g.K = KH * KW * Cout;
+  g.Kpad = round_up(g.K, bk_of(dtype));
+  g.KH = KH;
+  g.KW = KW;
+  g.stride = 1;
+  g.pad_h = KH - 1 - pad;
+  g.pad_w = KW - 1 - pad;
+  g.up = stride == 2 ? 1 : 0;
+  g.out_H = H;
+  g.out_W = W;
+  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
 }

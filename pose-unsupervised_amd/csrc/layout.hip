@@ -6,57 +6,6 @@
 namespace posu {
 namespace {
 
-template <typename T>
-struct Vec;
-template <>
-struct Vec<uint16_t> {
-  static constexpr int E = 8;
-  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
-    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-    }
-  }
-  static __device__ __forceinline__ uint4 pack(const float* v) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<uint32_t>(f2bf(v[2 * i])) | (static_cast<uint32_t>(f2bf(v[2 * i + 1])) << 16);
-    return make_uint4(w[0], w[1], w[2], w[3]);
-  }
-};
-template <>
-struct Vec<f16_t> {
-  static constexpr int E = 8;
-  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
-    const f16x8 h = __builtin_bit_cast(f16x8, u);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(h[i]);
-  }
-  static __device__ __forceinline__ uint4 pack(const float* v) {
-    f16x8 h;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) h[i] = static_cast<_Float16>(v[i]);
-    return __builtin_bit_cast(uint4, h);
-  }
-};
-template <>
-struct Vec<float> {
-  static constexpr int E = 4;
-  static __device__ __forceinline__ void unpack(const uint4& u, float* v) {
-    v[0] = __uint_as_float(u.x);
-    v[1] = __uint_as_float(u.y);
-    v[2] = __uint_as_float(u.z);
-    v[3] = __uint_as_float(u.w);
-  }
-  static __device__ __forceinline__ uint4 pack(const float* v) {
-    return make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                      __float_as_uint(v[3]));
-  }
-};
-
 // one thread per (pixel, 16-B output chunk)
 template <typename T>
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, int N, int C, int H, int W,
@@ -164,17 +113,6 @@ __global__ __launch_bounds__(256) void maxpool_kernel(const T* __restrict__ x, i
 inline int grid_for(long long total) {
   long long g = (total + 255) / 256;
   return static_cast<int>(g < 8192 ? (g > 0 ? g : 1) : 8192);
-}
-
-// storage-type dispatch: fn(T{}) for the dtype code, false if unsupported
-template <typename Fn>
-bool with_storage(int dtype, Fn&& fn) {
-  switch (dtype) {
-    case POSU_BF16: fn(uint16_t{}); return true;
-    case POSU_F16: fn(f16_t{}); return true;
-    case POSU_F32: fn(float{}); return true;
-    default: return false;
-  }
 }
 
 int chunk_elems(int dtype) { return dtype == POSU_F32 ? 4 : 8; }

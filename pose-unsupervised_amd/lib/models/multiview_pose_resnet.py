@@ -2,9 +2,11 @@
 
 ``MultiViewPose.forward(list of V [N, 3, H, W])`` returns
 ``(single_views, multi_views, low_features, high_features)`` like the reference
-(multiview_pose_resnet.py:69-84).  In eval mode the V views run as ONE backbone pass
-over a V*N batch (BN is a per-channel affine there, so this equals V separate passes)
-and the outputs are split back per view; a single tensor input behaves like
+(multiview_pose_resnet.py:69-84).  The V views run as ONE backbone pass over a V*N
+batch and the outputs are split back per view: in eval mode BN is a per-channel affine,
+so this equals V separate passes; in train mode every view is a separate BatchNorm
+segment (own batch statistics, own running-stat update in view order), which equals
+the reference's V backbone calls.  A single tensor input behaves like
 ``PoseResNet.forward``.
 
 The cross-view ``Aggregation`` fusion (AGGRE: true, 12 dense HW x HW maps) is not on

@@ -16,8 +16,9 @@ configs[4]) or ``'fp32'`` (exact-f32 MFMA; the parity mode).  Heatmaps are alway
 float32; ``layer1_out`` / ``deconv_out`` are returned as NCHW-shaped channels-last
 views of the NHWC activations in the compute dtype (zero-copy).
 
-Eval-mode forward only in this round: a training-mode forward (batch-statistics BN)
-raises instead of silently running something else.
+Training mode (``model.train()``) runs posu.train_plan: batch-statistics BN per view,
+differentiable through one autograd Function whose backward is the HIP kernel chain;
+parameter gradients land in ``.grad`` as usual (optimizers / DDP unchanged).
 """
 import logging
 import os
@@ -27,6 +28,7 @@ import torch.nn as nn
 
 from posu import ops
 from posu.plan import PoseResNetPlan
+from posu.train_plan import TrainPlan, train_forward
 
 BN_MOMENTUM = 0.1
 logger = logging.getLogger(__name__)
@@ -94,6 +96,7 @@ class PoseResNet(nn.Module):
         self.precision = precision
         self._plan = None
         self._plan_key = None
+        self._train_plan = None
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -136,11 +139,16 @@ class PoseResNet(nn.Module):
             self._plan_key = key
         return self._plan
 
+    def train_plan(self):
+        """The training-mode launch sequence (posu.train_plan.TrainPlan); packs per step."""
+        code = ops.dtype_code(self.precision)
+        if code == ops.F16:
+            raise NotImplementedError('training in fp16 needs loss scaling; use precision bf16 or fp32')
+        if self._train_plan is None or self._train_plan.code != code:
+            self._train_plan = TrainPlan(self, code)
+        return self._train_plan
+
     def _run_views(self, views):
-        if self.training:
-            raise NotImplementedError(
-                'pose-unsupervised_amd: training-mode forward (batch-statistics BatchNorm + backward) is not '
-                'available yet; call .eval() (eval-mode BN is folded into the MFMA conv epilogues)')
         for v in views:
             if not v.is_cuda:
                 raise RuntimeError('PoseResNet runs on the MI355X HIP path only: input must be a cuda tensor')
@@ -149,6 +157,10 @@ class PoseResNet(nn.Module):
         if self.conv1.weight.device != views[0].device:
             raise RuntimeError('model parameters are on %s but input is on %s'
                                % (self.conv1.weight.device, views[0].device))
+        if self.training:
+            # batch-statistics BN per view (one segment per view), differentiable
+            x = views[0] if len(views) == 1 else torch.cat(views, 0)
+            return train_forward(self, self.train_plan(), x, len(views))
         plan = self.plan(views[0].device)
         hm, x1, f = plan.run(plan.pack_input(views))
         # NHWC -> NCHW-shaped channels-last views (no copy)

@@ -23,6 +23,7 @@ _lib = None
 _p = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
+_ll = ctypes.c_longlong
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 _SIGNATURES = {
@@ -50,8 +51,20 @@ _SIGNATURES = {
     'posu_triangulate_dlt': [_p, _p, _p, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p],
     'posu_joints_mse_fwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
     'posu_joints_mse_bwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
+    # training path
+    'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
+    'posu_conv2d_wgrad_workspace': [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i],
+    'posu_conv2d_wgrad': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _ll, _p],
+    'posu_bn_workspace': [_i, _i],
+    'posu_bn_train_fwd': [_i, _p, _i, _i, _i, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
+    'posu_bn_apply': [_i, _p, _i, _i, _i, _p, _p, _p, _i, _p, _p],
+    'posu_bn_train_bwd': [_i, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
+    'posu_channel_sum': [_i, _p, _i, _i, _p, _p, _ll, _p],
+    'posu_maxpool3x3s2_bwd_workspace': [_i, _i, _i, _i],
+    'posu_maxpool3x3s2_bwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _ll, _p],
 }
-_RESTYPES = {'posu_last_error': ctypes.c_char_p}
+_RESTYPES = {'posu_last_error': ctypes.c_char_p, 'posu_conv2d_wgrad_workspace': ctypes.c_longlong,
+             'posu_bn_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong}
 
 
 def library_path():
@@ -112,3 +125,11 @@ def require_cuda(*tensors):
             raise RuntimeError(
                 'pose-unsupervised_amd ops run only on the MI355X HIP path; '
                 'got a CPU tensor (move inputs to a cuda device)')
+
+
+def dtype_code_of(t):
+    """Storage dtype code of an activation tensor."""
+    codes = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+    if t.dtype not in codes:
+        raise TypeError('unsupported activation dtype %s' % t.dtype)
+    return codes[t.dtype]

@@ -89,3 +89,11 @@ def fold_bn(bn, conv_bias=None):
     if conv_bias is not None:
         shift = shift + conv_bias.detach().double() * scale
     return scale.float().contiguous(), shift.float().contiguous()
+
+
+def pack_conv_dgrad_weight(w, bk, dtype):
+    """Data-gradient weight of a Conv2d [Cout, Cin, KH, KW]: the forward packing of
+    W[:, :, ::-1, ::-1].transpose(0, 1), i.e. [CinPad][Kpad] with k = (kh*KW + kw)*Cout + co
+    (see posu_conv2d_dgrad)."""
+    wt = w.detach().float().flip(2, 3).transpose(0, 1)
+    return pack_conv_weight(wt, wt.shape[1], bk, dtype)

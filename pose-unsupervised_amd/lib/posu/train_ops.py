@@ -1,0 +1,126 @@
+"""Tensor-level wrappers over the training-path entry points of libposeu.so
+(include/posu.h, "training path"): conv data / weight gradients, training-mode
+BatchNorm (per-view statistics), its backward, channel sums and the max-pool
+backward.  NHWC activations in the compute dtype, f32 statistics and gradients of
+parameters.  cuda tensors only; no fallback.
+"""
+import torch
+
+from . import _native as nat
+from ._native import call, ptr, stream_of, require_cuda
+
+_WS = {}
+
+
+def workspace(device, nbytes, slot='default'):
+    """Grow-only scratch buffer per (device, slot), reused by consecutive launches on one stream."""
+    key = (str(device), slot)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=None, out=None):
+    """dx [N, H, W, cin] of a conv x -> dy; `hw` = (H, W) of x; optional residual added."""
+    require_cuda(dy)
+    n, ho, wo, cout = dy.shape
+    h, w = hw
+    if out is None:
+        out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)
+    call('posu_conv2d_dgrad', code, ptr(dy), n, ho, wo, cout, ptr(wt_packed), cin, kh, kw, stride, pad,
+         ptr(residual), ptr(out), h, w, stream_of(dy.device))
+    return out
+
+
+def conv2d_wgrad(dy, x, creal, kh, kw, stride, pad, code, out=None):
+    """dW [Cout, creal, kh, kw] f32 of a conv over x [N, H, W, C >= creal] with output grad dy."""
+    require_cuda(dy, x)
+    n, h, w, c = x.shape
+    cout = dy.shape[3]
+    need = nat.load().posu_conv2d_wgrad_workspace(code, n, h, w, c, cout, kh, kw, stride, pad)
+    if need <= 0:
+        raise RuntimeError('posu_conv2d_wgrad: partial buffer too large for this shape')
+    ws = workspace(dy.device, need, 'wgrad')
+    if out is None:
+        out = torch.empty((cout, creal, kh, kw), dtype=torch.float32, device=dy.device)
+    call('posu_conv2d_wgrad', code, ptr(dy), ptr(x), n, h, w, c, creal, cout, kh, kw, stride, pad, ptr(out),
+         ptr(ws), ws.numel(), stream_of(dy.device))
+    return out
+
+
+def deconv4x4s2_wgrad(x, dy, code, out=None):
+    """dW [Cin, Cout, 4, 4] f32 of ConvTranspose2d(4, s2, p1) with input x [N,H,W,Cin], output grad dy."""
+    return conv2d_wgrad(x, dy, dy.shape[3], 4, 4, 2, 1, code, out=out)
+
+
+def _bn_ws(device, nseg, c):
+    return workspace(device, nat.load().posu_bn_workspace(nseg, c), 'bn')
+
+
+def bn_train_fwd(z, nseg, gamma, beta, eps, momentum, running_mean=None, running_var=None):
+    """Per-segment batch statistics of z [nseg*B, H, W, C]: (mean, rstd, scale, shift) each [nseg, C] f32."""
+    require_cuda(z)
+    c = z.shape[-1]
+    pix = z.numel() // c
+    if pix % nseg:
+        raise ValueError('batch does not split into %d equal segments' % nseg)
+    st = torch.empty((4, nseg, c), dtype=torch.float32, device=z.device)
+    ws = _bn_ws(z.device, nseg, c)
+    call('posu_bn_train_fwd', nat.dtype_code_of(z), ptr(z), nseg, pix // nseg, c, ptr(gamma), ptr(beta),
+         float(eps), float(momentum), ptr(running_mean), ptr(running_var), ptr(st[0]), ptr(st[1]), ptr(st[2]),
+         ptr(st[3]), ptr(ws), ws.numel(), stream_of(z.device))
+    return st[0], st[1], st[2], st[3]
+
+
+def bn_apply(z, nseg, scale, shift, residual=None, relu=True, out=None):
+    require_cuda(z)
+    c = z.shape[-1]
+    pix = z.numel() // c
+    if out is None:
+        out = torch.empty_like(z)
+    call('posu_bn_apply', nat.dtype_code_of(z), ptr(z), nseg, pix // nseg, c, ptr(scale), ptr(shift),
+         ptr(residual), int(relu), ptr(out), stream_of(z.device))
+    return out
+
+
+def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None, dbeta=None):
+    """Backward of y = relu?(bn(z) (+ r)); y=None means no ReLU.
+    Returns (dz, gres or None, dgamma [C] f32, dbeta [C] f32)."""
+    require_cuda(gy, z)
+    c = z.shape[-1]
+    pix = z.numel() // c
+    dz = torch.empty_like(z)
+    gres = torch.empty_like(z) if want_gres else None
+    if dgamma is None:
+        dgamma = torch.empty((c,), dtype=torch.float32, device=z.device)
+    if dbeta is None:
+        dbeta = torch.empty((c,), dtype=torch.float32, device=z.device)
+    ws = _bn_ws(z.device, nseg, c)
+    call('posu_bn_train_bwd', nat.dtype_code_of(z), ptr(gy), ptr(y), ptr(z), nseg, pix // nseg, c, ptr(mean),
+         ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dz), ptr(gres), ptr(ws), ws.numel(),
+         stream_of(z.device))
+    return dz, gres, dgamma, dbeta
+
+
+def channel_sum(x, out=None):
+    """sum over pixels of an NHWC tensor -> [C] f32."""
+    require_cuda(x)
+    c = x.shape[-1]
+    if out is None:
+        out = torch.empty((c,), dtype=torch.float32, device=x.device)
+    ws = _bn_ws(x.device, 1, c)
+    call('posu_channel_sum', nat.dtype_code_of(x), ptr(x), x.numel() // c, c, ptr(out), ptr(ws), ws.numel(),
+         stream_of(x.device))
+    return out
+
+
+def maxpool3x3s2_bwd(x, gy):
+    require_cuda(x, gy)
+    n, h, w, c = x.shape
+    ws = workspace(x.device, nat.load().posu_maxpool3x3s2_bwd_workspace(n, h, w, c), 'maxpool')
+    gx = torch.empty_like(x)
+    call('posu_maxpool3x3s2_bwd', nat.dtype_code_of(x), ptr(x), n, h, w, c, ptr(gy), ptr(gx), ptr(ws), ws.numel(),
+         stream_of(x.device))
+    return gx

@@ -1,0 +1,270 @@
+"""Training step of PoseResNet on the HIP kernels (BASELINE configs[3]).
+
+The reference trains with torch autograd over nn.Conv2d / BatchNorm2d / ReLU /
+MaxPool2d / ConvTranspose2d (lib/models/pose_resnet.py:21-205, train mode, called once
+per camera view by multiview_pose_resnet.py:74-78) and Adam
+(core/function.py:364-366, utils/utils.py:79-83).  Here one autograd Function runs the
+whole network forward and backward as explicit kernel launches on NHWC activations:
+
+  forward   conv (raw, MFMA implicit GEMM) -> per-view batch statistics -> normalise
+            (+ residual) + ReLU, for every conv / deconv; max-pool; 1x1 head
+  backward  BN/ReLU backward (residual-branch gradient split off), conv weight
+            gradient (split-K MFMA, transposed LDS reads), conv data gradient (the
+            forward kernel on flipped weights, zero-upsampled input for stride 2, the
+            identity-branch gradient added in its epilogue), max-pool backward.
+
+Views are stacked on the batch axis as `nseg` segments: one launch per layer serves
+all views while every view keeps its own BatchNorm statistics and its own running-stat
+update (in view order), as in the reference's four backbone calls.
+
+Parameters stay NCHW f32 in the nn.Modules (so optimizers, DDP and checkpoints are
+unchanged); they are packed into the kernels' layouts in the compute dtype once per
+step, and their gradients come back f32 in the modules' layouts.
+"""
+import torch
+
+from . import ops, train_ops as T
+from .packing import pack_conv_dgrad_weight, pack_conv_weight, pack_deconv4x4_weight
+
+STEM_CIN_PAD = 8
+HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
+
+
+class _ConvBN:
+    """conv (no bias) -> BatchNorm2d (train) -> [+ residual] -> [ReLU]."""
+
+    def __init__(self, conv, bn, relu, cin_pad=None):
+        self.conv, self.bn, self.relu = conv, bn, relu
+        self.k = conv.kernel_size[0]
+        self.stride = conv.stride[0]
+        self.pad = conv.padding[0]
+        self.cout, self.cin = conv.weight.shape[:2]
+        self.cin_pad = cin_pad or self.cin
+        if conv.bias is not None:
+            raise NotImplementedError('conv + BN with a conv bias')
+
+    def params(self):
+        return [self.conv.weight, self.bn.weight, self.bn.bias]
+
+    def pack(self, code, bk, dt, need_dgrad=True):
+        self.w = pack_conv_weight(self.conv.weight, self.cin_pad, bk, dt)
+        self.wt = pack_conv_dgrad_weight(self.conv.weight, bk, dt) if need_dgrad else None
+
+    def forward(self, x, nseg, code, residual=None):
+        z = ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, None, None, None, False,
+                            code)
+        bn = self.bn
+        mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                            bn.running_var)
+        y = T.bn_apply(z, nseg, sc, sh, residual, self.relu)
+        return y, (x, z, y, mean, rstd)
+
+    def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None):
+        x, z, y, mean, rstd = saved
+        dz, gres, dgam, dbet = T.bn_train_bwd(gy, y if self.relu else None, z, nseg, mean, rstd, self.bn.weight,
+                                              want_gres=want_gres)
+        grads[self.conv.weight] = T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad, code)
+        grads[self.bn.weight] = dgam
+        grads[self.bn.bias] = dbet
+        dx = None
+        if need_dx:
+            dx = T.conv2d_dgrad(dz, self.wt, self.cin, self.k, self.k, self.stride, self.pad, x.shape[1:3], code,
+                                residual=dx_residual)
+        return dx, gres
+
+
+class _Block:
+    def __init__(self, blk):
+        self.bottleneck = hasattr(blk, 'conv3')
+        names = ['1', '2', '3'] if self.bottleneck else ['1', '2']
+        self.units = [_ConvBN(getattr(blk, 'conv' + s), getattr(blk, 'bn' + s), s != names[-1]) for s in names]
+        self.units[-1].relu = True   # relu(bn(conv) + residual)
+        self.down = None
+        if blk.downsample is not None:
+            self.down = _ConvBN(blk.downsample[0], blk.downsample[1], False)
+
+    def all_units(self):
+        return self.units + ([self.down] if self.down is not None else [])
+
+    def forward(self, x, nseg, code):
+        saved = []
+        res, sd = x, None
+        if self.down is not None:
+            res, sd = self.down.forward(x, nseg, code)
+        y = x
+        for u in self.units[:-1]:
+            y, s = u.forward(y, nseg, code)
+            saved.append(s)
+        y, s = self.units[-1].forward(y, nseg, code, residual=res)
+        saved.append(s)
+        return y, (saved, sd)
+
+    def backward(self, gy, saved, nseg, code, grads):
+        su, sd = saved
+        g, gres = self.units[-1].backward(gy, su[-1], nseg, code, grads, want_gres=True)
+        for u, s in zip(reversed(self.units[:-1]), reversed(su[:-1])):
+            if u is self.units[0]:
+                break
+            g, _ = u.backward(g, s, nseg, code, grads)
+        if self.down is None:
+            # identity residual: its gradient joins the first conv's data gradient
+            dx, _ = self.units[0].backward(g, su[0], nseg, code, grads, dx_residual=gres)
+            return dx
+        dx_main, _ = self.units[0].backward(g, su[0], nseg, code, grads)
+        dx, _ = self.down.backward(gres, sd, nseg, code, grads, dx_residual=dx_main)
+        return dx
+
+
+class _DeconvBN:
+    def __init__(self, dc, bn):
+        if dc.stride != (2, 2) or dc.padding != (1, 1) or dc.output_padding != (0, 0) or dc.kernel_size != (4, 4):
+            raise NotImplementedError('deconv supported for kernel 4, stride 2, padding 1')
+        if dc.bias is not None:
+            raise NotImplementedError('deconv with bias')
+        self.dc, self.bn = dc, bn
+        self.cin, self.cout = dc.weight.shape[:2]
+
+    def params(self):
+        return [self.dc.weight, self.bn.weight, self.bn.bias]
+
+    def pack(self, code, bk, dt):
+        self.w = pack_deconv4x4_weight(self.dc.weight, bk, dt)
+        # data gradient = conv 4x4 / s2 / p1 with the [Cin][Cout] weight read as conv weights
+        self.wd = pack_conv_weight(self.dc.weight, self.cout, bk, dt)
+
+    def forward(self, x, nseg, code):
+        z = ops.deconv4x4s2_nhwc(x, self.w, self.cout, None, None, False, code)
+        bn = self.bn
+        mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                            bn.running_var)
+        y = T.bn_apply(z, nseg, sc, sh, None, True)
+        return y, (x, z, y, mean, rstd)
+
+    def backward(self, gy, saved, nseg, code, grads):
+        x, z, y, mean, rstd = saved
+        dz, _, dgam, dbet = T.bn_train_bwd(gy, y, z, nseg, mean, rstd, self.bn.weight)
+        grads[self.dc.weight] = T.deconv4x4s2_wgrad(x, dz, code)
+        grads[self.bn.weight] = dgam
+        grads[self.bn.bias] = dbet
+        return ops.conv2d_nhwc(dz, self.wd, self.cin, 4, 4, 2, 1, None, None, None, False, code)
+
+
+class TrainPlan:
+    """Forward/backward launch sequence of one PoseResNet in training mode."""
+
+    def __init__(self, net, code):
+        self.net = net
+        self.code = code
+        self.stem = _ConvBN(net.conv1, net.bn1, True, cin_pad=STEM_CIN_PAD)
+        self.layers = [[_Block(b) for b in layer] for layer in (net.layer1, net.layer2, net.layer3, net.layer4)]
+        mods = list(net.deconv_layers)
+        self.deconvs = [_DeconvBN(mods[i], mods[i + 1]) for i in range(0, len(mods), 3)]
+        fl = net.final_layer
+        if fl.kernel_size != (1, 1):
+            raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
+        self.head = fl
+        self.njoints = fl.weight.shape[0]
+        if self.njoints > HEAD_CPAD:
+            raise NotImplementedError('more than %d joints' % HEAD_CPAD)
+
+    def units(self):
+        out = [self.stem]
+        for layer in self.layers:
+            for b in layer:
+                out += b.all_units()
+        return out
+
+    def pack(self):
+        code = self.code
+        bk, dt = ops.conv_bk(code), ops.torch_dtype(code)
+        self.stem.pack(code, bk, dt, need_dgrad=False)
+        for layer in self.layers:
+            for b in layer:
+                for u in b.all_units():
+                    u.pack(code, bk, dt)
+        for d in self.deconvs:
+            d.pack(code, bk, dt)
+        fl = self.head
+        self.head_w = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, dt)
+        wpad = torch.zeros((HEAD_CPAD,) + tuple(fl.weight.shape[1:]), dtype=torch.float32, device=fl.weight.device)
+        wpad[:self.njoints] = fl.weight.detach()
+        self.head_wt = pack_conv_dgrad_weight(wpad, bk, dt)
+        self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None else
+                       torch.zeros(self.njoints, device=fl.weight.device))
+
+    def forward(self, x_nchw, nseg):
+        """x [nseg*B, 3, H, W] f32 -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC, saved)."""
+        code = self.code
+        self.pack()
+        x = ops.pack_nchw_to_nhwc(x_nchw, code, STEM_CIN_PAD)
+        a0, s0 = self.stem.forward(x, nseg, code)
+        p0 = ops.maxpool3x3s2_nhwc(a0, code)
+        saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
+        y = p0
+        x1 = None
+        for li, layer in enumerate(self.layers):
+            for b in layer:
+                y, sb = b.forward(y, nseg, code)
+                saved['blocks'].append(sb)
+            if li == 0:
+                x1 = y
+        saved['deconvs'] = []
+        for d in self.deconvs:
+            y, sd = d.forward(y, nseg, code)
+            saved['deconvs'].append(sd)
+        saved['head_in'] = y
+        hm = ops.head1x1_nchw(y, self.head_w, self.njoints, self.head_b, code)
+        for bn in self._bns():
+            if bn.num_batches_tracked is not None:
+                bn.num_batches_tracked.add_(nseg)
+        return hm, x1, y, saved
+
+    def _bns(self):
+        out = [u.bn for u in self.units()] + [d.bn for d in self.deconvs]
+        return out
+
+    def backward(self, dhm, saved, nseg):
+        """dL/dheatmaps (NCHW f32) -> {parameter: gradient (f32, parameter layout)}."""
+        code = self.code
+        grads = {}
+        f = saved['head_in']
+        gh = ops.pack_nchw_to_nhwc(dhm, code, HEAD_CPAD)
+        fl = self.head
+        dwh = T.conv2d_wgrad(gh, f, f.shape[3], 1, 1, 1, 0, code)
+        grads[fl.weight] = dwh[:self.njoints].contiguous()
+        if fl.bias is not None:
+            grads[fl.bias] = T.channel_sum(gh)[:self.njoints].contiguous()
+        g = T.conv2d_dgrad(gh, self.head_wt, f.shape[3], 1, 1, 1, 0, f.shape[1:3], code)
+        for d, sd in zip(reversed(self.deconvs), reversed(saved['deconvs'])):
+            g = d.backward(g, sd, nseg, code, grads)
+        blocks = [b for layer in self.layers for b in layer]
+        for b, sb in zip(reversed(blocks), reversed(saved['blocks'])):
+            g = b.backward(g, sb, nseg, code, grads)
+        g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
+        self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
+        return grads
+
+
+class _PoseResNetTrainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, plan, nseg, *params):
+        hm, x1, f, saved = plan.forward(x, nseg)
+        ctx.plan, ctx.saved, ctx.nseg, ctx.params = plan, saved, nseg, params
+        ctx.mark_non_differentiable(x1, f)
+        return hm, x1, f
+
+    @staticmethod
+    def backward(ctx, dhm, dx1, df):
+        if dhm is None:
+            return (None, None, None) + (None,) * len(ctx.params)
+        grads = ctx.plan.backward(dhm.contiguous().float(), ctx.saved, ctx.nseg)
+        ctx.saved = None
+        return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
+
+
+def train_forward(net, plan, x, nseg):
+    """Differentiable training-mode forward: (heatmaps NCHW f32, layer1 out, deconv out);
+    the features are NCHW-shaped channels-last views, not differentiable."""
+    params = tuple(net.parameters())
+    hm, x1, f = _PoseResNetTrainFn.apply(x, plan, nseg, *params)
+    return hm, x1.permute(0, 3, 1, 2), f.permute(0, 3, 1, 2)

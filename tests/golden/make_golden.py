@@ -13,6 +13,9 @@ What it imports and how (all in-process, nothing is copied into the repo):
     which is -1 on CPU tensors: it is patched to return 'cpu' while generating.
     FundamentalLoss.__init__ needs torch.distributed + CUDA: the object is built with
     __new__ and given its fundamental-matrix dict directly;
+  * one training step of the reference model (train mode, per-view calls, the reference's
+    JointsMSELoss / soft-argmax / transform_back / FundamentalLoss, loss.backward()):
+    tests/golden/train_step_r50_128.npz (gradients, losses, BN buffers after the step);
   * multiviews.cameras (imports as-is) -- projection of known 3-D points, used as the
     exact known-answer input of the triangulation tests (pymvg is not importable).
 """
@@ -213,6 +216,67 @@ def camera_golden(ref_cam):
     print('cameras: proj range', proj.min(), proj.max())
 
 
+TRAIN_FUND_WEIGHT = 10.0
+TRAIN_PARAMS_FULL = ['conv1.weight', 'bn1.weight', 'bn1.bias', 'layer1.0.conv1.weight', 'layer1.0.bn3.weight',
+                     'layer4.2.bn3.bias', 'deconv_layers.4.weight', 'final_layer.weight', 'final_layer.bias']
+TRAIN_BUFFERS = ['bn1.running_mean', 'bn1.running_var', 'bn1.num_batches_tracked', 'layer4.2.bn3.running_mean',
+                 'layer4.2.bn3.running_var', 'deconv_layers.7.running_mean', 'deconv_layers.7.running_var']
+
+
+def train_step_golden(ref_pr, ref_tf, ref_loss, num_layers=50, image_size=128, nviews=4, batch=2, seed=3):
+    """One reference training step (core/function.py:154-366 without the optimizer):
+    per-view train-mode backbone calls, JointsMSELoss(use_target_weight) per view, and
+    FundamentalLoss on soft-argmax -> transform_back coordinates; loss.backward()."""
+    cfg = syn.make_cfg(num_layers=num_layers, image_size=image_size)
+    block, layers = ref_pr.resnet_spec[num_layers]
+    net = ref_pr.PoseResNet(block, layers, cfg)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=seed))
+    net.train()
+    views = syn.synthetic_views(nviews, batch, image_size, seed=seed + 1)
+    hms = image_size // 4
+    targets = peaked_heatmaps(nviews * batch, 16, hms, hms, seed=seed + 2).reshape(nviews, batch, 16, hms, hms)
+    r = np.random.default_rng(seed + 3)
+    tw = (r.uniform(size=(nviews, batch, 16, 1)) > 0.15).astype(np.float32)
+    centers = r.uniform(400, 600, size=(nviews, batch, 2))
+    scales = np.full((nviews, batch, 2), 5.0)
+    subjects = np.array([9, 11][:batch] + [9] * max(0, batch - 2))
+    meta = [{'center': torch.from_numpy(centers[v]), 'scale': torch.from_numpy(scales[v]),
+             'subject': torch.from_numpy(subjects)} for v in range(nviews)]
+    outs = [net(v)[0] for v in views]
+    crit = ref_loss.JointsMSELoss(use_target_weight=True)
+    mse = 0
+    for v in range(nviews):
+        mse = mse + crit(outs[v], torch.from_numpy(targets[v]), torch.from_numpy(tw[v]))
+    orig, gd = _patched_get_device()
+    torch.Tensor.get_device = gd
+    try:
+        joints = ref_tf.transform_back_th(cfg, [ref_tf.generate_integral_preds_2d_th(o) for o in outs], meta)
+    finally:
+        torch.Tensor.get_device = orig
+    fl = ref_loss.FundamentalLoss.__new__(ref_loss.FundamentalLoss)
+    fl.use_target_weight = True
+    fl.fundamental_matrix_dict = {k: torch.from_numpy(np.asarray(v, np.float32))
+                                  for k, v in syn.fundamental_dict().items()}
+    fund = fl(joints, [torch.from_numpy(w) for w in tw], meta) * TRAIN_FUND_WEIGHT
+    loss = mse + fund
+    loss.backward()
+    named = dict(net.named_parameters())
+    sd = net.state_dict()
+    out = dict(num_layers=num_layers, image_size=image_size, nviews=nviews, batch=batch, seed=seed,
+               fund_weight=TRAIN_FUND_WEIGHT, targets=targets, target_weight=tw, centers=centers, scales=scales,
+               subjects=subjects, loss_mse=mse.detach().numpy(), loss_fund=fund.detach().numpy(),
+               heatmaps=torch.stack([o.detach() for o in outs]).numpy(),
+               joints=torch.stack([j.detach() for j in joints]).numpy(),
+               grad_names=np.array(list(named)),
+               grad_norms=np.array([named[k].grad.norm().item() for k in named]))
+    for k in TRAIN_PARAMS_FULL:
+        out['grad__' + k] = named[k].grad.numpy()
+    for k in TRAIN_BUFFERS:
+        out['buf__' + k] = sd[k].numpy()
+    np.savez_compressed(os.path.join(HERE, 'train_step_r%d_%d.npz' % (num_layers, image_size)), **out)
+    print('train step r%d@%d: mse %.6g fund %.6g' % (num_layers, image_size, mse.item(), fund.item()))
+
+
 def main():
     torch.manual_seed(0)
     torch.set_num_threads(8)
@@ -223,6 +287,7 @@ def main():
     decode_golden(ref_tf, ref_inf)
     loss_golden(ref_loss)
     camera_golden(ref_cam)
+    train_step_golden(ref_pr, ref_tf, ref_loss)
 
 
 if __name__ == '__main__':

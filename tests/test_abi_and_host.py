@@ -165,9 +165,12 @@ def test_forward_refuses_cpu_tensors():
     net = get_pose_net(syn.make_cfg(num_layers=18, image_size=64), is_train=False).eval()
     with pytest.raises(RuntimeError, match='cuda'):
         net(torch.zeros(1, 3, 64, 64))
-    net.train()
-    with pytest.raises(NotImplementedError):
+    net.train()  # the training path refuses CPU tensors the same way
+    with pytest.raises(RuntimeError, match='cuda'):
         net(torch.zeros(1, 3, 64, 64))
+    net.precision = 'fp16'  # fp16 training would need loss scaling: refused
+    with pytest.raises(NotImplementedError):
+        net.train_plan()
 
 
 def _s2d(x, cpad):

@@ -1,0 +1,134 @@
+"""The training step (BASELINE configs[3]) on the MI355X against one step of the
+reference model, written the way the reference's core/function.py:154-366 writes it:
+per-view train-mode backbone outputs, JointsMSELoss(use_target_weight) per view,
+soft-argmax -> transform_back -> FundamentalLoss, loss.backward().  The golden step
+(tests/golden/train_step_r50_128.npz) is the reference's own modules run on CPU."""
+import numpy as np
+import pytest
+import torch
+
+from posu import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(cuda, g, precision):
+    from core.loss import FundamentalLoss, JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    from utils.transforms import generate_integral_preds_2d_th, transform_back_th
+    nl, size, nv, b, seed = (int(g[k]) for k in ('num_layers', 'image_size', 'nviews', 'batch', 'seed'))
+    cfg = syn.make_cfg(num_layers=nl, image_size=size)
+    net = get_pose_net(cfg, is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=seed))
+    net = net.to(cuda).train()
+    model = get_multiview_pose_net(net, cfg)
+    views = [v.to(cuda) for v in syn.synthetic_views(nv, b, size, seed=seed + 1)]
+    meta = [{'center': torch.from_numpy(g['centers'][v]), 'scale': torch.from_numpy(g['scales'][v]),
+             'subject': torch.from_numpy(g['subjects'])} for v in range(nv)]
+    target = [torch.from_numpy(g['targets'][v]).to(cuda) for v in range(nv)]
+    weight = [torch.from_numpy(g['target_weight'][v]).to(cuda) for v in range(nv)]
+
+    raw_features, _, _, _ = model(views)
+    crit = JointsMSELoss(use_target_weight=True)
+    mse = 0
+    for t, w, r in zip(target, weight, raw_features):
+        mse = mse + crit(r, t, w)
+    joints2d = transform_back_th(cfg, [generate_integral_preds_2d_th(o) for o in raw_features], meta)
+    fl = FundamentalLoss(cfg, fundamental_matrix_dict=syn.fundamental_dict(), device=cuda)
+    fl.use_target_weight = True
+    fund = fl(joints2d, weight, meta) * float(g['fund_weight'])
+    loss = mse + fund
+    loss.backward()
+    torch.cuda.synchronize()
+    return net, raw_features, joints2d, mse, fund
+
+
+def test_train_step_fp32_matches_reference_gradients(cuda, golden):
+    g = golden('train_step_r50_128.npz')
+    net, hm, joints, mse, fund = _step(cuda, g, 'fp32')
+    np.testing.assert_allclose(torch.stack(hm).detach().cpu().numpy(), g['heatmaps'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(torch.stack(joints).detach().cpu().numpy(), g['joints'], atol=0.25, rtol=0)  # image px; soft-argmax beta=100
+    np.testing.assert_allclose(mse.item(), g['loss_mse'], rtol=1e-4)
+    np.testing.assert_allclose(fund.item(), g['loss_fund'], rtol=1e-3)
+    named = dict(net.named_parameters())
+    assert [n for n in named] == list(g['grad_names'])
+    norms = np.array([named[n].grad.norm().item() for n in g['grad_names']])
+    worst = np.argmax(np.abs(norms / g['grad_norms'] - 1))
+    print('worst grad-norm ratio %s: %.6f' % (g['grad_names'][worst], norms[worst] / g['grad_norms'][worst]))
+    np.testing.assert_allclose(norms, g['grad_norms'], rtol=2e-3)
+    for k in g:
+        if k.startswith('grad__'):
+            ref = g[k]
+            got = named[k[6:]].grad.cpu().numpy()
+            np.testing.assert_allclose(got, ref, atol=2e-3 * np.abs(ref).max(), rtol=2e-3, err_msg=k)
+    sd = net.state_dict()
+    for k in g:
+        if k.startswith('buf__'):
+            np.testing.assert_allclose(sd[k[5:]].cpu().numpy(), g[k], atol=1e-4, rtol=1e-4, err_msg=k)
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_step_along_negative_gradient_reduces_the_loss(cuda, precision):
+    """First-order check of the whole backward in each compute dtype: a small step
+    against the gradient lowers the (batch-statistics) loss by about eta * |g|^2."""
+    from core.loss import JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    cfg = syn.make_cfg(num_layers=50, image_size=128)
+    net = get_pose_net(cfg, is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=5))
+    net = net.to(cuda).train()
+    model = get_multiview_pose_net(net, cfg)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 128, seed=51)]
+    ys, xs = torch.meshgrid(torch.arange(32.), torch.arange(32.), indexing='ij')
+    c = torch.rand(8, 16, 2, generator=torch.Generator().manual_seed(52)) * 24 + 4
+    tgt = torch.exp(-((ys - c[..., 1, None, None]) ** 2 + (xs - c[..., 0, None, None]) ** 2) / 8.0)
+    tgt = tgt.to(cuda).view(4, 2, 16, 32, 32)
+    w = torch.ones(2, 16, 1, device=cuda)
+    crit = JointsMSELoss(use_target_weight=True)
+
+    def loss_fn():
+        out, _, _, _ = model(views)
+        return sum(crit(o, tgt[v], w) for v, o in enumerate(out))
+
+    loss0 = loss_fn()
+    loss0.backward()
+    params = [p for p in net.parameters()]
+    g2 = sum(float((p.grad.double() ** 2).sum()) for p in params)
+    eta = 0.02 * loss0.item() / g2
+    with torch.no_grad():
+        for p in params:
+            p -= eta * p.grad
+        loss1 = loss_fn().item()
+    predicted = eta * g2
+    print('%s: loss %.6f -> %.6f, predicted decrease %.6f' % (precision, loss0.item(), loss1, predicted))
+    assert loss0.item() - loss1 > 0.5 * predicted
+
+
+def test_adam_steps_run(cuda):
+    """The reference's optimizer (Adam, lr 1e-3) over a few steps of the HIP training path."""
+    from core.loss import JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    cfg = syn.make_cfg(num_layers=18, image_size=128)
+    net = get_pose_net(cfg, is_train=True, precision='bf16').to(cuda).train()
+    model = get_multiview_pose_net(net, cfg)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 128, seed=41)]
+    ys, xs = torch.meshgrid(torch.arange(32.), torch.arange(32.), indexing='ij')
+    c = torch.rand(8, 16, 2, generator=torch.Generator().manual_seed(42)) * 24 + 4
+    tgt = torch.exp(-((ys - c[..., 1, None, None]) ** 2 + (xs - c[..., 0, None, None]) ** 2) / 8.0)
+    tgt = tgt.to(cuda).view(4, 2, 16, 32, 32)
+    w = torch.ones(2, 16, 1, device=cuda)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    crit = JointsMSELoss(use_target_weight=True)
+    losses = []
+    for _ in range(6):
+        out, _, _, _ = model(views)
+        loss = sum(crit(o, tgt[v], w) for v, o in enumerate(out))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    print('losses', losses)
+    assert all(np.isfinite(losses)) and min(losses[1:]) < losses[0]

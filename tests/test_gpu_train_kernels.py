@@ -1,0 +1,194 @@
+"""Training-path kernels on the MI355X against torch autograd (CPU, fp32) of the same
+ops: conv data / weight gradients (incl. strided, padded-channel stem and the
+ConvTranspose2d weight gradient), training-mode BatchNorm with per-view segments and
+running statistics, its backward through ReLU / residual, channel sums and the max-pool
+backward with ties."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from posu import ops, packing, train_ops as T
+from posu._native import BF16, F16, F32
+
+pytestmark = pytest.mark.gpu
+
+FP32_TOL = dict(atol=2e-4, rtol=2e-4)
+
+
+def _nhwc(t, cuda, dt, cpad=None):
+    t = t.permute(0, 2, 3, 1)
+    if cpad is not None and cpad > t.shape[-1]:
+        t = F.pad(t, (0, cpad - t.shape[-1]))
+    return t.contiguous().to(cuda, dt)
+
+
+def _nchw(t):
+    return t.float().cpu().permute(0, 3, 1, 2)
+
+
+def _close_lowp(got, ref, frac=0.02):
+    err = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert err <= frac * scale + 1e-3, (err, scale)
+
+
+DGRAD_CASES = [
+    # n, cin, h, w, cout, k, stride, pad
+    (2, 64, 16, 16, 64, 3, 1, 1),
+    (2, 64, 17, 15, 128, 3, 2, 1),    # strided 3x3, odd input
+    (2, 128, 16, 16, 256, 1, 2, 0),   # downsample 1x1 / s2
+    (3, 256, 8, 8, 64, 1, 1, 0),
+    (2, 128, 8, 8, 64, 4, 2, 1),      # the deconv's data gradient is this forward conv's shape
+]
+
+
+@pytest.mark.parametrize('case', DGRAD_CASES)
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_conv_dgrad_matches_autograd(cuda, case, code):
+    n, cin, h, w, cout, k, s, p = case
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, cin, h, w, generator=g, requires_grad=True)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    y = F.conv2d(x, wt, stride=s, padding=p)
+    dy = torch.randn_like(y)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    res = torch.randn_like(dx_ref)
+    dt = ops.torch_dtype(code)
+    wpk = packing.pack_conv_dgrad_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    dx = T.conv2d_dgrad(_nhwc(dy, cuda, dt), wpk, cin, k, k, s, p, (h, w), code)
+    dx_r = T.conv2d_dgrad(_nhwc(dy, cuda, dt), wpk, cin, k, k, s, p, (h, w), code, residual=_nhwc(res, cuda, dt))
+    torch.cuda.synchronize()
+    if code == F32:
+        torch.testing.assert_close(_nchw(dx), dx_ref, **FP32_TOL)
+        torch.testing.assert_close(_nchw(dx_r), dx_ref + res, **FP32_TOL)
+    else:
+        _close_lowp(_nchw(dx), dx_ref)
+
+
+WGRAD_CASES = [
+    # n, cin, cin_pad, h, w, cout, k, stride, pad
+    (2, 3, 8, 32, 30, 64, 7, 2, 3),      # direct stem (channels padded to 8)
+    (2, 64, 64, 16, 16, 64, 3, 1, 1),    # 64-row tiles, K = 576 (ragged n-tile)
+    (2, 64, 64, 17, 15, 128, 3, 2, 1),   # strided, odd
+    (3, 256, 256, 8, 8, 512, 1, 1, 0),
+    (2, 128, 128, 16, 16, 256, 1, 2, 0),
+    (1, 16, 16, 40, 40, 64, 3, 1, 1),    # P = 1600: several splits
+]
+
+
+@pytest.mark.parametrize('case', WGRAD_CASES)
+@pytest.mark.parametrize('code', [F32, BF16, F16])
+def test_conv_wgrad_matches_autograd(cuda, case, code):
+    n, cin, cpad, h, w, cout, k, s, p = case
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = (torch.randn(cout, cin, k, k, generator=g) * 0.1).requires_grad_(True)
+    y = F.conv2d(x, wt, stride=s, padding=p)
+    dy = torch.randn_like(y)
+    (dw_ref,) = torch.autograd.grad(y, wt, dy)
+    dt = ops.torch_dtype(code)
+    dw = T.conv2d_wgrad(_nhwc(dy, cuda, dt), _nhwc(x, cuda, dt, cpad), cin, k, k, s, p, code)
+    torch.cuda.synchronize()
+    assert dw.shape == dw_ref.shape
+    if code == F32:
+        torch.testing.assert_close(dw.cpu(), dw_ref, atol=1e-3, rtol=1e-4)
+    else:
+        _close_lowp(dw.cpu(), dw_ref)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_deconv_weight_and_data_gradients(cuda, code):
+    g = torch.Generator().manual_seed(13)
+    n, cin, h, w, cout = 2, 128, 6, 5, 64
+    x = torch.randn(n, cin, h, w, generator=g, requires_grad=True)
+    wt = (torch.randn(cin, cout, 4, 4, generator=g) * 0.05).requires_grad_(True)
+    y = F.conv_transpose2d(x, wt, stride=2, padding=1)
+    dy = torch.randn_like(y)
+    dx_ref, dw_ref = torch.autograd.grad(y, (x, wt), dy)
+    dt = ops.torch_dtype(code)
+    dyd = _nhwc(dy, cuda, dt)
+    dw = T.deconv4x4s2_wgrad(_nhwc(x.detach(), cuda, dt), dyd, code)
+    # data gradient = forward conv 4x4 / s2 / p1 of dy with W read as [Cin][Cout] conv weights
+    wpk = packing.pack_conv_weight(wt.detach().to(cuda), cout, ops.conv_bk(code), dt)
+    dx = ops.conv2d_nhwc(dyd, wpk, cin, 4, 4, 2, 1, None, None, None, False, code)
+    torch.cuda.synchronize()
+    if code == F32:
+        torch.testing.assert_close(dw.cpu(), dw_ref, atol=1e-3, rtol=1e-4)
+        torch.testing.assert_close(_nchw(dx), dx_ref, **FP32_TOL)
+    else:
+        _close_lowp(dw.cpu(), dw_ref)
+        _close_lowp(_nchw(dx), dx_ref)
+
+
+def _bn_ref(z, nseg, gamma, beta, rm, rv, res, relu):
+    outs = []
+    for zs, rs in zip(z.chunk(nseg), (res.chunk(nseg) if res is not None else [None] * nseg)):
+        o = F.batch_norm(zs, rm, rv, gamma, beta, training=True, momentum=0.1, eps=1e-5)
+        if rs is not None:
+            o = o + rs
+        outs.append(F.relu(o) if relu else o)
+    return torch.cat(outs)
+
+
+@pytest.mark.parametrize('c,nseg,residual,relu', [(64, 4, False, True), (256, 2, True, True),
+                                                  (2048, 1, False, False), (128, 4, True, True)])
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, relu, code):
+    g = torch.Generator().manual_seed(14)
+    b, h, w = 2, 9, 7
+    dt = ops.torch_dtype(code)
+    # activations representable in the compute dtype, so the reference sees the same
+    # inputs (and the same ReLU mask) as the kernels
+    z = (torch.randn(nseg * b, c, h, w, generator=g) * 2 + 0.5).to(dt).float().requires_grad_(True)
+    gamma = (torch.rand(c, generator=g) + 0.5).requires_grad_(True)
+    beta = (torch.randn(c, generator=g) * 0.1).requires_grad_(True)
+    res = torch.randn(nseg * b, c, h, w, generator=g).to(dt).float().requires_grad_(True) if residual else None
+    rm0, rv0 = torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5
+    rm, rv = rm0.clone(), rv0.clone()
+    y = _bn_ref(z, nseg, gamma, beta, rm, rv, res, relu)
+    gy = torch.randn(y.shape, generator=g).to(dt).float()
+    grads = torch.autograd.grad(y, [z, gamma, beta] + ([res] if residual else []), gy)
+    zd = _nhwc(z.detach(), cuda, dt)
+    rmd, rvd = rm0.clone().to(cuda), rv0.clone().to(cuda)
+    mean, rstd, sc, sh = T.bn_train_fwd(zd, nseg, gamma.detach().to(cuda), beta.detach().to(cuda), 1e-5, 0.1,
+                                        rmd, rvd)
+    rd = _nhwc(res.detach(), cuda, dt) if residual else None
+    yd = T.bn_apply(zd, nseg, sc, sh, rd, relu)
+    dz, gres, dgam, dbet = T.bn_train_bwd(_nhwc(gy, cuda, dt), yd if relu else None, zd, nseg, mean, rstd,
+                                          gamma.detach().to(cuda), want_gres=residual)
+    torch.cuda.synchronize()
+    if code == F32:
+        tol = dict(atol=1e-4, rtol=1e-4)
+        torch.testing.assert_close(rmd.cpu(), rm, **tol)
+        torch.testing.assert_close(rvd.cpu(), rv, **tol)
+        torch.testing.assert_close(_nchw(yd), y.detach(), **tol)
+        torch.testing.assert_close(_nchw(dz), grads[0], atol=1e-4, rtol=1e-3)
+        torch.testing.assert_close(dgam.cpu(), grads[1], atol=1e-3, rtol=1e-4)
+        torch.testing.assert_close(dbet.cpu(), grads[2], atol=1e-3, rtol=1e-4)
+        if residual:
+            torch.testing.assert_close(_nchw(gres), grads[3], **tol)
+    else:
+        torch.testing.assert_close(rmd.cpu(), rm, atol=1e-2, rtol=1e-2)
+        _close_lowp(_nchw(yd), y.detach())
+        _close_lowp(_nchw(dz), grads[0], 0.03)
+        _close_lowp(dgam.cpu(), grads[1], 0.03)
+        _close_lowp(dbet.cpu(), grads[2], 0.03)
+
+
+def test_channel_sum(cuda):
+    g = torch.Generator().manual_seed(15)
+    x = torch.randn(3, 17, 11, 64, generator=g)
+    out = T.channel_sum(x.to(cuda))
+    torch.testing.assert_close(out.cpu(), x.double().sum(dim=(0, 1, 2)).float(), atol=1e-4, rtol=1e-5)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_maxpool_backward_with_ties_matches_autograd(cuda, code):
+    g = torch.Generator().manual_seed(16)
+    x = torch.randint(-2, 3, (2, 64, 17, 16), generator=g).float().requires_grad_(True)  # many ties
+    y = F.max_pool2d(x, 3, stride=2, padding=1)
+    gy = torch.randint(-4, 5, y.shape, generator=g).float()  # exact in bf16
+    (gx_ref,) = torch.autograd.grad(y, x, gy)
+    dt = ops.torch_dtype(code)
+    gx = T.maxpool3x3s2_bwd(_nhwc(x.detach(), cuda, dt), _nhwc(gy, cuda, dt))
+    torch.testing.assert_close(_nchw(gx), gx_ref, atol=0, rtol=0)
