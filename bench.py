@@ -32,14 +32,19 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 GFLOP_PER_FRAME = {(50, 256): 14.47, (152, 384): 76.19, (18, 128): None}
+# training step: 3x forward minus the stem's data gradient
+TRAIN_GFLOP_PER_FRAME = {(50, 256): 43.1}
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_F32_TFLOPS = 157.3
 METRIC = '4-view 256x256 frames/sec (fwd+triangulate)'
+TRAIN_METRIC = '4-view 256x256 training frames/sec (fwd+bwd+Adam, per-view BN)'
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--mode', default='infer', choices=['infer', 'train'],
+                    help='infer: BASELINE metric (fwd + triangulate); train: configs[3] training step')
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--groups', type=int, default=32, help='4-view groups per GPU per step')
@@ -112,8 +117,105 @@ def _cpu_meta(ng, size):
             'subjects': syn.group_subjects(ng), 'F_dict': syn.fundamental_dict()}
 
 
+def train_main(args):
+    """configs[3]: one training step = 4-view batch (groups x 4 frames per GPU) through the
+    reference's step (core/function.py:154-366): train-mode forward with per-view BN,
+    JointsMSELoss per view + FundamentalLoss on soft-argmax coords, backward, Adam.
+    N > 1: DistributedDataParallel over RCCL (gradient all-reduce), weak scaling."""
+    from posu import dist as pdist
+    from posu import synthetic as syn
+    from posu.pipeline import synthetic_meta
+    from core.loss import JointsMSELoss, FundamentalLoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from utils.transforms import integral_preds_image_th
+    rank, local, world = pdist.env_rank()
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        pdist.init('nccl', device=dev)
+    cfg = syn.make_cfg(num_layers=args.layers, image_size=args.size)
+    net = build_model(args.layers, args.size, args.precision, dev).train()
+    model = get_multiview_pose_net(net, cfg)
+    if dist is not None:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local,
+                                                          bucket_cap_mb=64)
+    nb, nv, hs = args.groups, 4, args.size // 4
+    views = [v.to(dev) for v in syn.synthetic_views(nv, nb, args.size, seed=100 + rank)]
+    meta, _ = synthetic_meta(nb, dev, image_size=args.size)
+    g = torch.Generator().manual_seed(7 + rank)
+    ys, xs = torch.meshgrid(torch.arange(hs, dtype=torch.float32), torch.arange(hs, dtype=torch.float32),
+                            indexing='ij')
+    c = torch.rand(nv * nb, 16, 2, generator=g) * (hs - 8) + 4
+    target = torch.exp(-((ys - c[..., 1, None, None]) ** 2 + (xs - c[..., 0, None, None]) ** 2) / 8.0).to(dev)
+    target = target.view(nv, nb, 16, hs, hs)
+    weight = torch.ones(nb, 16, 1, device=dev)
+    mse = JointsMSELoss(use_target_weight=True)
+    fund = FundamentalLoss(cfg, fundamental_matrix_dict=syn.fundamental_dict(), device=dev)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    subj = meta.subj
+
+    def step():
+        raw, _, _, _ = model(views)
+        loss = 0
+        for v in range(nv):
+            loss = loss + mse(raw[v], target[v], weight)
+        coords = integral_preds_image_th(torch.cat(raw, 0), meta.affines).view(nv, nb, 16, 2)
+        from posu import ops
+        loss = loss + 1e-3 * ops.epipolar_loss(coords, None, fund.F, subj)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.max_over_ranks(elapsed, device=dev)
+    frames = nv * nb
+    value = pdist.throughput(frames, args.steps, world, elapsed)
+    gf = TRAIN_GFLOP_PER_FRAME.get((args.layers, args.size))
+    roof = None
+    if gf is not None:
+        achieved = gf * value / world / 1e3
+        peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS
+        roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': round(achieved / peak, 4), 'traffic': None,
+                'kernel': 'whole training step per GPU (fwd + bwd convs, BN, Adam)',
+                'flop_per_launch': '%.1f GFLOP/frame x %d frames' % (gf, frames)}
+    if rank == 0:
+        line = {
+            'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision,
+            'data': 'synthetic',
+            'config': {'workload': '4-view batch %dx4 at %dx%d: PoseResNet-%d train step (per-view BN, '
+                                   'JointsMSE + FundamentalLoss, Adam) (BASELINE configs[3])'
+                                   % (nb, args.size, args.size, args.layers),
+                       'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
+                       'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce)' % world},
+            'loss': round(float(loss), 5), 'roofline': roof, 'cpu_baseline': None,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.mode == 'train':
+        return train_main(args)
     from posu import dist as pdist
     rank, local, world = pdist.env_rank()
     dev = torch.device('cuda', local)

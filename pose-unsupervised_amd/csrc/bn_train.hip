@@ -121,6 +121,34 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
   }
 }
 
+// ---- finalize: one block per FCH channels, FLN lanes sum the partial blocks of a
+// segment (16 strided loads per lane in flight), fixed-order LDS combine.
+constexpr int FCH = 16, FLN = 16;
+
+__device__ __forceinline__ void reduce_seg(const double* __restrict__ part, int seg, int NB, int C, int c, bool valid,
+                                           int cl, int ln, double (*red)[FLN][FCH], double& s, double& q) {
+  double a = 0.0, b = 0.0;
+  if (valid) {
+    const double* base = part + static_cast<size_t>(seg) * NB * 2 * C;
+#pragma unroll 4
+    for (int blk = ln; blk < NB; blk += FLN) {
+      a += base[static_cast<size_t>(blk) * 2 * C + c];
+      b += base[static_cast<size_t>(blk) * 2 * C + C + c];
+    }
+  }
+  red[0][ln][cl] = a;
+  red[1][ln][cl] = b;
+  __syncthreads();
+  s = 0.0;
+  q = 0.0;
+  if (ln == 0)
+    for (int l = 0; l < FLN; ++l) {
+      s += red[0][l][cl];
+      q += red[1][l][cl];
+    }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
                                                                 int Pseg, int C, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
@@ -128,18 +156,17 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
                                                                 float* running_var, float* __restrict__ mean,
                                                                 float* __restrict__ rstd, float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ double red[2][FLN][FCH];
+  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int c = blockIdx.x * FCH + cl;
+  const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
-  for (int seg = 0; seg < nseg; ++seg) {
-    double s = 0.0, q = 0.0;
-    for (int b = 0; b < NB; ++b) {
-      const double* src = part + (static_cast<size_t>(seg) * NB + b) * 2 * C;
-      s += src[c];
-      q += src[C + c];
-    }
-    const double mu = s / n;
-    const double var = fmax(q / n - mu * mu, 0.0);
+  for (int seg = 0; seg < nseg; ++seg) {  // in segment order: running stats compose like V calls
+    double sum, sq;
+    reduce_seg(part, seg, NB, C, c, valid, cl, ln, red, sum, sq);
+    if (ln != 0 || !valid) continue;
+    const double mu = sum / n;
+    const double var = fmax(sq / n - mu * mu, 0.0);
     const double r = 1.0 / sqrt(var + static_cast<double>(eps));
     const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
     mean[seg * C + c] = static_cast<float>(mu);
@@ -184,17 +211,16 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
                                                               const float* __restrict__ rstd,
                                                               float* __restrict__ coef, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ double red[2][FLN][FCH];
+  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int c = blockIdx.x * FCH + cl;
+  const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
   double tg = 0.0, tgx = 0.0;
   for (int seg = 0; seg < nseg; ++seg) {
-    double sg = 0.0, sgx = 0.0;
-    for (int b = 0; b < NB; ++b) {
-      const double* src = part + (static_cast<size_t>(seg) * NB + b) * 2 * C;
-      sg += src[c];
-      sgx += src[C + c];
-    }
+    double sg, sgx;
+    reduce_seg(part, seg, NB, C, c, valid, cl, ln, red, sg, sgx);
+    if (ln != 0 || !valid) continue;
     tg += sg;
     tgx += sgx;
     const float gm = gamma ? gamma[c] : 1.f;
@@ -202,8 +228,10 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
     coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
     coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
   }
-  if (dgamma) dgamma[c] = static_cast<float>(tgx);
-  if (dbeta) dbeta[c] = static_cast<float>(tg);
+  if (ln == 0 && valid) {
+    if (dgamma) dgamma[c] = static_cast<float>(tgx);
+    if (dbeta) dbeta[c] = static_cast<float>(tg);
+  }
 }
 
 // dz = gamma*rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = gy * [y > 0];
@@ -243,14 +271,14 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
 }
 
-__global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
-                                                                   int C, float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0;
-  for (int seg = 0; seg < nseg; ++seg)
-    for (int b = 0; b < NB; ++b) s += part[(static_cast<size_t>(seg) * NB + b) * 2 * C + c];
-  out[c] = static_cast<float>(s);
+__global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double* __restrict__ part, int NB, int C,
+                                                                   float* __restrict__ out) {
+  __shared__ double red[2][FLN][FCH];
+  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int c = blockIdx.x * FCH + cl;
+  double s, q;
+  reduce_seg(part, 0, NB, C, c, c < C, cl, ln, red, s, q);
+  if (ln == 0 && c < C) out[c] = static_cast<float>(s);
 }
 
 // ---- max-pool 3x3 / s2 / p1 backward (PyTorch's tie rule: the first maximum in
@@ -376,7 +404,7 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
                        static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
                      gamma, beta, eps, momentum, running_mean, running_var, mean, rstd, scale, shift);
   return check_launch("posu_bn_train_fwd");
 }
@@ -416,7 +444,7 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
                        C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
                      rstd, coef, dgamma, dbeta);
   with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
@@ -442,7 +470,7 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
                        nullptr, nullptr, nullptr, nullptr, P, C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
-  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + 255) / 256), dim3(256), 0, s, part, 1, rs.NB, C, out);
+  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);
   return check_launch("posu_channel_sum");
 }
 

@@ -301,7 +301,10 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     const int tap = k / C, ci = k - tap * C;
     if (ci >= Creal) continue;
     float s = 0.f;
-    for (int sp = 0; sp < splits; ++sp) s += part[(static_cast<size_t>(sp) * Mpad + m) * Npad + k];
+    const float* src = part + static_cast<size_t>(m) * Npad + k;
+    const size_t stride = static_cast<size_t>(Mpad) * Npad;
+#pragma unroll 8
+    for (int sp = 0; sp < splits; ++sp) s += src[sp * stride];
     const int kh = tap / KW, kw = tap - kh * KW;
     out[((static_cast<size_t>(m) * Creal + ci) * KH + kh) * KW + kw] = s;
   }
