@@ -49,16 +49,19 @@ int posu_abi_version(void);
 /* NCHW fp32 image batch -> NHWC activations with Cpad (>= C) channels,
  * zero-filled above C.  Replaces the implicit layout of the first
  * nn.Conv2d call in PoseResNet.forward (lib/models/pose_resnet.py:192).
- * x: [N, C, H, W] f32.  y: [N, H, W, Cpad] of `dtype`. */
+ * x: [N, C, H, W] f32.  y: [N, H, W, Cpad] of `dtype`.  hflip != 0 reads the
+ * image mirrored along W (the flip test's torch.flip(view, dims=[3]),
+ * lib/core/function.py:569). */
 int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W,
-                           void* y, int Cpad, void* stream);
+                           void* y, int Cpad, int hflip, void* stream);
 
 /* NCHW fp32 -> space-to-depth NHWC for the stem: y[n][i][j][(dy*2+dx)*C + c] =
  * x[n][c][2i+dy][2j+dx], zero above 4C.  The 7x7/s2/p3 stem conv then runs as a
  * 4x4/s1 conv with top/left padding 2 over this grid (K = 16 * Cpad instead of
- * 49 * Cpad taps of a Cin-padded 7x7 window).  H, W even; y: [N, H/2, W/2, Cpad]. */
+ * 49 * Cpad taps of a Cin-padded 7x7 window).  H, W even; y: [N, H/2, W/2, Cpad];
+ * hflip as above. */
 int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W,
-                       void* y, int Cpad, void* stream);
+                       void* y, int Cpad, int hflip, void* stream);
 
 /* NHWC activations -> NCHW fp32 (for returning x1 / f in the reference
  * layout: lib/models/pose_resnet.py:205). */
@@ -194,6 +197,16 @@ int posu_joints_mse_fwd(const float* pred, const float* gt, const float* w, int 
  *   gpred = gloss * 2 w^2 (pred - gt) / (N*HW).  gpred: [N, J, HW] f32. */
 int posu_joints_mse_bwd(const float* pred, const float* gt, const float* w, int N, int J, int HW,
                         const float* gloss, float* gpred, void* stream);
+
+/* Flip test (lib/core/function.py:566-583): heatmaps of the mirrored input brought
+ * back -- W mirrored, joint channels permuted by the dataset's flip pairs
+ * (flip_back_th, lib/utils/transforms.py:33-47), optionally shifted right by one
+ * column (SHIFT_HEATMAP, function.py:579-582) -- and, when hm is non-NULL, averaged
+ * with the plain heatmaps: out = 0.5 * (hm + flip_back(hm_flipped)).
+ *   hm_flipped, hm, out: [N, J, H, W] f32 (out may alias hm); perm: NULL or [J] int32
+ *   device array, perm[j] = the joint whose flipped map becomes joint j. */
+int posu_flip_back(const float* hm_flipped, const int* perm, const float* hm, int N, int J,
+                   int H, int W, int shift, float* out, void* stream);
 
 /* ------------------------------------------------------------- geometry */
 /* Epipolar consistency loss (FundamentalLoss.__call__, lib/core/loss.py:101-133):

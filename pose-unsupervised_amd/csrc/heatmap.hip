@@ -275,3 +275,45 @@ extern "C" int posu_joints_mse_bwd(const float* pred, const float* gt, const flo
                      N * J, HW, gloss, static_cast<float>(static_cast<long long>(N) * HW), gpred);
   return check_launch("posu_joints_mse_bwd");
 }
+
+// ---------------------------------------------------------------- flip test
+namespace posu {
+namespace {
+
+// out[n][j][y][x] = (avg ? 0.5 * (hm[n][j][y][x] + F) : F),
+// F = hf[n][perm[j]][y][W-1-xs], xs = shift ? max(x-1, 0) : x
+// (flip_back_th transforms.py:33-47 + SHIFT_HEATMAP function.py:579-582 + the average
+// of function.py:583), one thread per heatmap element.
+__global__ __launch_bounds__(256) void flip_back_kernel(const float* __restrict__ hf, const int* __restrict__ perm,
+                                                        const float* __restrict__ hm, int N, int J, int H, int W,
+                                                        int shift, float* __restrict__ out) {
+  const long long total = static_cast<long long>(N) * J * H * W;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int x = static_cast<int>(i % W);
+    const long long r = i / W;
+    const int y = static_cast<int>(r % H);
+    const long long nj = r / H;
+    const int j = static_cast<int>(nj % J);
+    const long long n = nj / J;
+    const int xs = shift ? (x > 0 ? x - 1 : 0) : x;
+    const int js = perm ? perm[j] : j;
+    const float f = hf[((n * J + js) * H + y) * W + (W - 1 - xs)];
+    out[i] = hm ? 0.5f * (hm[i] + f) : f;
+  }
+}
+
+}  // namespace
+}  // namespace posu
+
+extern "C" int posu_flip_back(const float* hm_flipped, const int* perm, const float* hm, int N, int J, int H, int W,
+                              int shift, float* out, void* stream) {
+  POSU_REQUIRE(hm_flipped && out, "posu_flip_back: null pointer");
+  POSU_REQUIRE(N >= 0 && J > 0 && H > 0 && W > 0, "posu_flip_back: bad shape");
+  POSU_REQUIRE(out != hm_flipped, "posu_flip_back: out must not alias the flipped heatmaps");
+  if (N == 0) return POSU_OK;
+  const long long total = static_cast<long long>(N) * J * H * W;
+  const long long blocks = std::min<long long>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL(flip_back_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, as_stream(stream),
+                     hm_flipped, perm, hm, N, J, H, W, shift, out);
+  return check_launch("posu_flip_back");
+}

@@ -9,7 +9,7 @@ namespace {
 // one thread per (pixel, 16-B output chunk)
 template <typename T>
 __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, int N, int C, int H, int W,
-                                                   T* __restrict__ y, int Cpad) {
+                                                   T* __restrict__ y, int Cpad, int hflip) {
   constexpr int E = Vec<T>::E;
   const int chunks = Cpad / E;
   const long long total = static_cast<long long>(N) * H * W * chunks;
@@ -17,7 +17,12 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, 
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
     const int ch = static_cast<int>(i % chunks);
     const long long pix = i / chunks;
-    const long long n = pix / HW, p = pix - n * HW;
+    const long long n = pix / HW;
+    long long p = pix - n * HW;
+    if (hflip) {  // torch.flip(x, dims=[3]) (function.py:569) folded into the pack
+      const long long row = p / W;
+      p = row * W + (W - 1 - (p - row * W));
+    }
     float v[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -32,7 +37,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ x, 
 // (one thread per output pixel and 16-B chunk)
 template <typename T>
 __global__ __launch_bounds__(256) void pack_s2d_kernel(const float* __restrict__ x, int N, int C, int H, int W,
-                                                       T* __restrict__ y, int Cpad) {
+                                                       T* __restrict__ y, int Cpad, int hflip) {
   constexpr int E = Vec<T>::E;
   const int chunks = Cpad / E;
   const int Hs = H / 2, Ws = W / 2;
@@ -50,7 +55,8 @@ __global__ __launch_bounds__(256) void pack_s2d_kernel(const float* __restrict__
     for (int e = 0; e < E; ++e) {
       const int cc = ch * E + e;
       const int sub = cc / C, c = cc - sub * C;
-      v[e] = sub < 4 ? x[(n * C + c) * HW + static_cast<long long>(2 * ys + (sub >> 1)) * W + 2 * xs + (sub & 1)]
+      const int col = 2 * xs + (sub & 1);
+      v[e] = sub < 4 ? x[(n * C + c) * HW + static_cast<long long>(2 * ys + (sub >> 1)) * W + (hflip ? W - 1 - col : col)]
                      : 0.f;
     }
     *reinterpret_cast<uint4*>(y + pix * Cpad + ch * E) = Vec<T>::pack(v);
@@ -123,7 +129,7 @@ int chunk_elems(int dtype) { return dtype == POSU_F32 ? 4 : 8; }
 using namespace posu;
 
 extern "C" int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W, void* y, int Cpad,
-                                      void* stream) {
+                                      int hflip, void* stream) {
   POSU_REQUIRE(x && y, "posu_pack_nchw_to_nhwc: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && Cpad >= C, "posu_pack_nchw_to_nhwc: bad shape");
   POSU_REQUIRE(Cpad % chunk_elems(dtype) == 0, "posu_pack_nchw_to_nhwc: Cpad is not a whole number of 16-B chunks");
@@ -132,14 +138,14 @@ extern "C" int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, i
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL(pack_kernel<T>, dim3(grid_for(pix * Cpad / Vec<T>::E)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<T*>(y), Cpad);
+                       static_cast<T*>(y), Cpad, hflip);
   });
   POSU_REQUIRE(ok, "posu_pack_nchw_to_nhwc: unsupported dtype");
   return check_launch("posu_pack_nchw_to_nhwc");
 }
 
 extern "C" int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W, void* y, int Cpad,
-                                  void* stream) {
+                                  int hflip, void* stream) {
   POSU_REQUIRE(x && y, "posu_pack_s2d_nchw: null pointer");
   POSU_REQUIRE(N > 0 && C > 0 && H > 1 && W > 1 && H % 2 == 0 && W % 2 == 0 && 4 * C <= Cpad,
                "posu_pack_s2d_nchw: bad shape (H, W even, 4C <= Cpad)");
@@ -149,7 +155,7 @@ extern "C" int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL(pack_s2d_kernel<T>, dim3(grid_for(pix * Cpad / Vec<T>::E)), dim3(256), 0, s, x, N, C, H, W,
-                       static_cast<T*>(y), Cpad);
+                       static_cast<T*>(y), Cpad, hflip);
   });
   POSU_REQUIRE(ok, "posu_pack_s2d_nchw: unsupported dtype");
   return check_launch("posu_pack_s2d_nchw");

@@ -29,8 +29,8 @@ _ll = ctypes.c_longlong
 _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
-    'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _p],
-    'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _p],
+    'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
+    'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
     'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],
     'posu_conv_bk': [_i],
@@ -51,6 +51,7 @@ _SIGNATURES = {
     'posu_triangulate_dlt': [_p, _p, _p, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p],
     'posu_joints_mse_fwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
     'posu_joints_mse_bwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
+    'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
     'posu_conv2d_wgrad_workspace': [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i],

@@ -47,25 +47,25 @@ def set_conv_stages(stages):
 
 
 # ---------------------------------------------------------------- layout ops
-def pack_nchw_to_nhwc(x, code, cpad, out=None):
-    """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C)."""
+def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
+    """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""
     require_cuda(x)
     x = x.contiguous().float()
     n, c, h, w = x.shape
     if out is None:
         out = torch.empty((n, h, w, cpad), dtype=torch_dtype(code), device=x.device)
-    call('posu_pack_nchw_to_nhwc', code, ptr(x), n, c, h, w, ptr(out), cpad, stream_of(x.device))
+    call('posu_pack_nchw_to_nhwc', code, ptr(x), n, c, h, w, ptr(out), cpad, int(hflip), stream_of(x.device))
     return out
 
 
-def pack_s2d_nchw(x, code, cpad, out=None):
-    """[N, C, H, W] f32 -> space-to-depth [N, H/2, W/2, cpad] (channel (dy*2+dx)*C + c)."""
+def pack_s2d_nchw(x, code, cpad, out=None, hflip=False):
+    """[N, C, H, W] f32 -> space-to-depth [N, H/2, W/2, cpad] (channel (dy*2+dx)*C + c); hflip mirrors W."""
     require_cuda(x)
     x = x.contiguous().float()
     n, c, h, w = x.shape
     if out is None:
         out = torch.empty((n, h // 2, w // 2, cpad), dtype=torch_dtype(code), device=x.device)
-    call('posu_pack_s2d_nchw', code, ptr(x), n, c, h, w, ptr(out), cpad, stream_of(x.device))
+    call('posu_pack_s2d_nchw', code, ptr(x), n, c, h, w, ptr(out), cpad, int(hflip), stream_of(x.device))
     return out
 
 
@@ -216,6 +216,24 @@ def argmax2d(hm, post_process=True, affine64=None):
     call('posu_argmax2d_fwd', ptr(hm), n, j, h, w, int(bool(post_process)), ptr(affine64), ptr(preds), ptr(maxv),
          stream_of(hm.device))
     return preds, maxv
+
+
+def flip_back(hm_flipped, perm=None, hm=None, shift=False, out=None):
+    """Flip-test heatmaps back (mirror W, permute joints by `perm`, optional one-column
+    shift) and, with `hm`, average: 0.5 * (hm + flip_back(hm_flipped))."""
+    require_cuda(hm_flipped)
+    hf = hm_flipped.contiguous().float()
+    n, j, h, w = hf.shape
+    if perm is not None and not isinstance(perm, torch.Tensor):
+        perm = torch.tensor(list(perm), dtype=torch.int32)
+    if perm is not None:
+        perm = perm.to(device=hf.device, dtype=torch.int32).contiguous()
+    if hm is not None:
+        hm = hm.contiguous().float()
+    if out is None:
+        out = torch.empty_like(hf)
+    call('posu_flip_back', ptr(hf), ptr(perm), ptr(hm), n, j, h, w, int(bool(shift)), ptr(out), stream_of(hf.device))
+    return out
 
 
 # ----------------------------------------------------------------- losses

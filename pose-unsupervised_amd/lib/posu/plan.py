@@ -131,18 +131,19 @@ class PoseResNetPlan:
         last = self.deconvs[-1] if self.deconvs else None
         self.fuse_head = last is not None and last.cout == 256 and self.njoints <= 16
 
-    def pack_input(self, views):
+    def pack_input(self, views, hflip=False):
         """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N):
-        space-to-depth [N, H/2, W/2, 16] for even H, W, else [N, H, W, 8]."""
+        space-to-depth [N, H/2, W/2, 16] for even H, W, else [N, H, W, 8]; hflip mirrors
+        every image along W (flip test)."""
         n, _, h, w = views[0].shape
         s2d = h % 2 == 0 and w % 2 == 0
         shape = (n * len(views), h // 2, w // 2, STEM_S2D_PAD) if s2d else (n * len(views), h, w, STEM_CIN_PAD)
         x = torch.empty(shape, dtype=ops.torch_dtype(self.code), device=views[0].device)
         for i, v in enumerate(views):
             if s2d:
-                ops.pack_s2d_nchw(v, self.code, STEM_S2D_PAD, out=x[i * n:(i + 1) * n])
+                ops.pack_s2d_nchw(v, self.code, STEM_S2D_PAD, out=x[i * n:(i + 1) * n], hflip=hflip)
             else:
-                ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n])
+                ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n], hflip=hflip)
         return x
 
     def run_stem(self, x):

@@ -26,7 +26,7 @@ def _ns(**kw):
 
 
 def make_cfg(num_layers=50, image_size=256, num_joints=16, deconv_with_bias=False, use_target_weight_fund=True,
-             post_process=True, data_root=''):
+             post_process=True, data_root='', flip_test=False, shift_heatmap=False):
     """The config fields the hot path reads (reference lib/core/config.py defaults)."""
     hm = image_size // 4
     return _ns(
@@ -36,8 +36,10 @@ def make_cfg(num_layers=50, image_size=256, num_joints=16, deconv_with_bias=Fals
                     HEATMAP_SIZE=np.array([hm, hm])),
         LOSS=_ns(USE_TARGET_WEIGHT=True, USE_TARGET_WEIGHT_FUND=use_target_weight_fund, USE_FUNDAMENTAL_LOSS=True,
                  FUNDAMENTAL_LOSS_WEIGHT=5.0, MSE_LOSS_WEIGHT=1.0),
-        TEST=_ns(POST_PROCESS=post_process, FUSE_OUTPUT=False, FLIP_TEST=False, SHIFT_HEATMAP=False),
+        TEST=_ns(POST_PROCESS=post_process, FUSE_OUTPUT=False, FLIP_TEST=flip_test, SHIFT_HEATMAP=shift_heatmap),
         DATASET=_ns(ROOT=data_root, NO_DISTORTION=False),
+        DEBUG=_ns(SAVE_ALL_PREDS=False),
+        PRINT_FREQ=100,
     )
 
 

@@ -111,12 +111,20 @@ def transform_back_th(cfg, joints_2d_list, meta):
     return out
 
 
+def flip_pair_order(num_joints, matched_parts):
+    """perm[j] = joint whose flipped heatmap becomes joint j (transforms.py:40-44)."""
+    order = list(range(num_joints))
+    for a, b in matched_parts:
+        order[a] = b
+        order[b] = a
+    return order
+
+
 def flip_back_th(output_flipped, matched_parts):
-    """Reference transforms.py:33-47 (flip test): mirror columns and swap L/R joints."""
+    """Reference transforms.py:33-47 (flip test): mirror columns and swap L/R joints,
+    one posu_flip_back launch per view."""
     assert len(output_flipped) == 4
     assert output_flipped[0].dim() == 4
-    order = list(range(output_flipped[0].size(1)))
-    for a, b in matched_parts:
-        order[a], order[b] = b, a
-    idx = torch.tensor(order, device=output_flipped[0].device)
-    return [torch.index_select(torch.flip(v, dims=[3]), 1, idx) for v in output_flipped]
+    perm = torch.tensor(flip_pair_order(output_flipped[0].size(1), matched_parts), dtype=torch.int32,
+                        device=output_flipped[0].device)
+    return [ops.flip_back(v, perm) for v in output_flipped]

@@ -216,6 +216,32 @@ def camera_golden(ref_cam):
     print('cameras: proj range', proj.min(), proj.max())
 
 
+MPII_FLIP_PAIRS = [[0, 5], [1, 4], [2, 3], [10, 15], [11, 14], [12, 13]]
+
+
+def flip_golden(ref_tf):
+    """Flip test (function.py:566-583): reference flip_back (numpy form of flip_back_th,
+    transforms.py:20-31), SHIFT_HEATMAP's one-column shift and the average."""
+    r = np.random.default_rng(21)
+    hm = r.standard_normal((3, 16, 12, 10)).astype(np.float32)
+    hmf = r.standard_normal((3, 16, 12, 10)).astype(np.float32)
+    back = ref_tf.flip_back(hmf.copy(), MPII_FLIP_PAIRS)
+    shifted = back.copy()
+    shifted[:, :, :, 1:] = shifted.copy()[:, :, :, 0:-1]
+    avg = (hm + shifted) * 0.5
+    # PCK accuracy of validate() (core/evaluate.py:42-73)
+    import core.evaluate as ref_eval
+    target = peaked_heatmaps(6, 16, 32, 32, seed=23)
+    target[0, 0] = 0.0
+    target[0, 0, 1, 20] = 1.0                      # peak on row 1 -> excluded (-1 distance)
+    output = target + 0.3 * r.standard_normal(target.shape).astype(np.float32)
+    acc, avg_acc, cnt, pred = ref_eval.accuracy(output.copy(), target.copy())
+    np.savez_compressed(os.path.join(HERE, 'flip.npz'), hm=hm, hm_flipped=hmf, pairs=np.array(MPII_FLIP_PAIRS),
+                        flip_back=back, avg_shift=avg, avg_noshift=(hm + back) * 0.5,
+                        acc_output=output, acc_target=target, acc=acc, avg_acc=avg_acc, cnt=cnt, acc_pred=pred)
+    print('flip: done; accuracy', avg_acc, cnt)
+
+
 TRAIN_FUND_WEIGHT = 10.0
 TRAIN_PARAMS_FULL = ['conv1.weight', 'bn1.weight', 'bn1.bias', 'layer1.0.conv1.weight', 'layer1.0.bn3.weight',
                      'layer4.2.bn3.bias', 'deconv_layers.4.weight', 'final_layer.weight', 'final_layer.bias']
@@ -288,6 +314,7 @@ def main():
     loss_golden(ref_loss)
     camera_golden(ref_cam)
     train_step_golden(ref_pr, ref_tf, ref_loss)
+    flip_golden(ref_tf)
 
 
 if __name__ == '__main__':

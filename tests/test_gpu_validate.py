@@ -1,0 +1,103 @@
+"""The evaluation slice: flip test, PCK accuracy and the
+validate() batch body (core/function.py:555-644) on the MI355X, against
+reference-generated goldens (tests/golden/flip.npz) and the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import geometry_ref as G
+from oracle import pose_resnet_ref as PR
+from posu import ops, synthetic as syn
+from posu._native import BF16, F32
+
+pytestmark = pytest.mark.gpu
+
+
+def _perm(pairs, j=16):
+    from utils.transforms import flip_pair_order
+    return flip_pair_order(j, [list(p) for p in pairs])
+
+
+def test_flip_back_matches_reference_golden(cuda, golden):
+    g = golden('flip.npz')
+    hm, hmf = torch.from_numpy(g['hm']).to(cuda), torch.from_numpy(g['hm_flipped']).to(cuda)
+    perm = _perm(g['pairs'])
+    np.testing.assert_array_equal(ops.flip_back(hmf, perm).cpu().numpy(), g['flip_back'])
+    np.testing.assert_array_equal(ops.flip_back(hmf, perm, hm=hm, shift=True).cpu().numpy(), g['avg_shift'])
+    np.testing.assert_array_equal(ops.flip_back(hmf, perm, hm=hm, shift=False).cpu().numpy(), g['avg_noshift'])
+    # in place over the plain heatmaps (the validate loop's output buffer)
+    out = hm.clone()
+    ops.flip_back(hmf, perm, hm=out, shift=True, out=out)
+    np.testing.assert_array_equal(out.cpu().numpy(), g['avg_shift'])
+
+
+def test_flip_back_th_drop_in(cuda, golden):
+    from utils.transforms import flip_back_th
+    g = golden('flip.npz')
+    views = [torch.from_numpy(g['hm_flipped']).to(cuda) for _ in range(4)]
+    for v in flip_back_th(views, g['pairs'].tolist()):
+        np.testing.assert_array_equal(v.cpu().numpy(), g['flip_back'])
+
+
+def test_accuracy_matches_reference_golden(cuda, golden):
+    from core.evaluate import accuracy
+    g = golden('flip.npz')
+    acc, avg, cnt, pred = accuracy(g['acc_output'].copy(), g['acc_target'].copy())
+    np.testing.assert_allclose(acc, g['acc'], rtol=0, atol=1e-12)
+    assert cnt == int(g['cnt'])
+    np.testing.assert_allclose(avg, g['avg_acc'], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(pred, g['acc_pred'])
+    # cuda tensors in: same answer
+    acc2, _, _, _ = accuracy(torch.from_numpy(g['acc_output']).to(cuda), torch.from_numpy(g['acc_target']).to(cuda))
+    np.testing.assert_allclose(acc2, g['acc'], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_hflip_input_pack_equals_packing_the_flipped_image(cuda, code):
+    x = torch.randn(2, 3, 16, 12, generator=torch.Generator().manual_seed(3)).to(cuda)
+    xf = torch.flip(x, dims=[3])
+    torch.testing.assert_close(ops.pack_s2d_nchw(x, code, 16, hflip=True), ops.pack_s2d_nchw(xf, code, 16),
+                               atol=0, rtol=0)
+    torch.testing.assert_close(ops.pack_nchw_to_nhwc(x, code, 8, hflip=True), ops.pack_nchw_to_nhwc(xf, code, 8),
+                               atol=0, rtol=0)
+
+
+def test_validate_batch_with_flip_test_matches_oracle(cuda, golden):
+    from core.function import validate_batch
+    from core.loss import JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    pairs = golden('flip.npz')['pairs'].tolist()
+    size, n = 128, 2
+    cfg = syn.make_cfg(num_layers=18, image_size=size, flip_test=True, shift_heatmap=True)
+    net = get_pose_net(cfg, is_train=False, precision='fp32')
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=1, bn_stats=syn.load_bn_stats(18, 128)))
+    net = net.to(cuda).eval()
+    model = get_multiview_pose_net(net, cfg)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, n, size, seed=33)]
+    r = np.random.default_rng(34)
+    centers = r.uniform(400, 600, size=(4, n, 2))
+    scales = np.full((4, n, 2), 5.0)
+    meta = [{'center': torch.from_numpy(centers[v]), 'scale': torch.from_numpy(scales[v])} for v in range(4)]
+    target = [torch.rand(n, 16, 32, 32) for _ in range(4)]
+    weight = [torch.ones(n, 16, 1) for _ in range(4)]
+    res = validate_batch(cfg, model, views, target, weight, meta, flip_pairs=pairs,
+                         criterion=JointsMSELoss(use_target_weight=True))
+    # oracle: plain + mirrored forward, reference flip-back / shift / average, per view
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    perm = _perm(pairs)
+    for k in range(4):
+        x = views[k].cpu()
+        hm, _, _ = PR.pose_resnet_forward(x, sd, 18)
+        hmf, _, _ = PR.pose_resnet_forward(torch.flip(x, dims=[3]), sd, 18)
+        back = torch.flip(hmf, dims=[3])[:, perm]
+        back[:, :, :, 1:] = back.clone()[:, :, :, :-1]
+        ref = ((hm + back) * 0.5).numpy()
+        got = res['heatmaps'][k::4]
+        np.testing.assert_allclose(got, ref, atol=1e-3, rtol=0)
+        # decode of the device heatmaps vs the oracle decode (isolates the argmax stage)
+        p, mv = G.get_final_preds(got, centers[k], scales[k], post_process=True)
+        np.testing.assert_allclose(res['preds'][k::4, :, :2], p, atol=1e-4, rtol=0)
+        np.testing.assert_allclose(res['preds'][k::4, :, 2:], mv, atol=1e-6, rtol=0)
+    assert res['loss'] is not None and np.isfinite(res['loss'])
+    assert 0.0 <= res['acc'] <= 1.0
