@@ -52,6 +52,7 @@ def parse():
     ap.add_argument('--size', type=int, default=256)
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
     ap.add_argument('--chunks', type=int, default=1,
                     help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
@@ -250,6 +251,9 @@ def main():
             hm = stage_net()
             stage_geo(hm)
         torch.cuda.synchronize()
+        if not args.no_autotune:  # per-layer conv tile choice, timed on the real operands
+            plan.autotune(plan.pack_input(views), chunks=args.chunks, keep_features=False)
+            torch.cuda.synchronize()
         use_graph = not args.no_graph
         if use_graph:
             try:
@@ -332,7 +336,7 @@ def main():
                                % (args.groups, args.size, args.size, args.layers),
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
-                   'hipgraph': use_graph, 'chunks': args.chunks},
+                   'hipgraph': use_graph, 'chunks': args.chunks, 'autotuned_tiles': not args.no_autotune},
         'network_ms': round(net_ms, 4), 'decode_geometry_ms': round(geo_ms, 4),
         'groups_per_s': round(value / 4, 2),
         'roofline': roof, 'cpu_baseline': cpu,

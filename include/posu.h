@@ -82,7 +82,11 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *   scale/shift: [Cout] f32 (may be NULL: scale 1, shift 0).
  *   residual: NULL or [N, Ho, Wo, Cout] dtype.
  *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
- *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied). */
+ *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied).
+ *   tile (here and in posu_conv1x1_dual_fwd / posu_deconv4x4s2_fwd): -1 = the
+ *   built-in heuristic, 0..6 = a fixed tile configuration (numbering of
+ *   posu_force_conv_config); the Python plan picks it per layer by timing every
+ *   admissible configuration once (PoseResNetPlan.autotune). */
 int posu_conv_bk(int dtype);
 /* Tuning knob: depth of the LDS-DMA ring of the convolution kernels (2 or 3
  * K-tiles; process-wide, default 2). */
@@ -97,7 +101,7 @@ int posu_force_conv_config(int cfg);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,
-                    int relu, void* y, int Ho, int Wo, void* stream);
+                    int relu, void* y, int Ho, int Wo, int tile, void* stream);
 
 /* Two 1x1 convolutions summed into one output (Bottleneck conv3/bn3 + the
  * downsample conv/bn residual branch, lib/models/pose_resnet.py:90-99, 136-141):
@@ -109,7 +113,7 @@ int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
 int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C,
                           const void* x2, int H2, int W2, int C2, int stride2,
                           const void* w, int Cout, const float* scale, const float* shift,
-                          int relu, void* y, void* stream);
+                          int relu, void* y, int tile, void* stream);
 
 /* ConvTranspose2d(kernel 4, stride 2, padding 1, output_padding 0) as four
  * stride-1 2x2 sub-pixel convolutions (one per output parity class) in one
@@ -121,7 +125,7 @@ int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C,
  *   y: [N, 2H, 2W, Cout] dtype. */
 int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
                          const void* w, int Cout, const float* scale,
-                         const float* shift, int relu, void* y, void* stream);
+                         const float* shift, int relu, void* y, int tile, void* stream);
 
 /* The last deconv stage fused with the final 1x1 head: deconv + BN + ReLU as
  * posu_deconv4x4s2_fwd, then per output pixel hm[n][j][pix] = bias[j] +

@@ -568,7 +568,7 @@ int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (p
 int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 
 template <typename T, bool DUAL>
-int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
+int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   if (g.hm) {  // fused head: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
@@ -592,9 +592,10 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
   } else {  // 128-channel layers: 256 x 128 measured slower than 128 x 128 (layer2 c1/c2, R50@256)
     cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
-  if (g_force >= 0) {
-    const bool wide_ok = g.CoutPad % 128 == 0 && (g_force != 5 || g.CoutPad % 256 == 0);
-    if (g_force <= 2 || wide_ok) cfg = g_force;
+  const int want = tile >= 0 ? tile : g_force;  // per-call tile (autotuned plans) > test hook > heuristic
+  if (want >= 0) {
+    const bool wide_ok = g.CoutPad % 128 == 0 && (want != 5 || g.CoutPad % 256 == 0);
+    if (want <= 2 || wide_ok) cfg = want;
   }
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
@@ -615,11 +616,11 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what) {
 }
 
 template <bool DUAL>
-int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what) {
+int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what, int tile = -1) {
   hipStream_t s = as_stream(stream);
-  if (dtype == POSU_BF16) return launch<uint16_t, DUAL>(g, nclass, s, what);
-  if (dtype == POSU_F32) return launch<float, DUAL>(g, nclass, s, what);
-  if (dtype == POSU_F16) return launch<f16_t, DUAL>(g, nclass, s, what);
+  if (dtype == POSU_BF16) return launch<uint16_t, DUAL>(g, nclass, s, what, tile);
+  if (dtype == POSU_F32) return launch<float, DUAL>(g, nclass, s, what, tile);
+  if (dtype == POSU_F16) return launch<f16_t, DUAL>(g, nclass, s, what, tile);
   set_error(std::string(what) + ": unsupported dtype");
   return POSU_ERR_ARG;
 }
@@ -682,8 +683,9 @@ extern "C" int posu_set_conv_stages(int stages) {
 
 extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
-                               const void* residual, int relu, void* y, int Ho, int Wo, void* stream) {
+                               const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
+  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_conv2d_fwd: tile must be -1 (auto) or 0..6");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -708,13 +710,14 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   g.relu = relu;
   g.out_H = Ho;
   g.out_W = Wo;
-  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd");
+  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd", tile);
 }
 
 extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2, int H2,
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
-                                     const float* shift, int relu, void* y, void* stream) {
+                                     const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
+  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_conv1x1_dual_fwd: tile must be -1 (auto) or 0..6");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -739,13 +742,14 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
   g.relu = relu;
   g.out_H = H;
   g.out_W = W;
-  return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_fwd");
+  return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_fwd", tile);
 }
 
 extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
-                                    int Cout, const float* scale, const float* shift, int relu, void* y,
+                                    int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
+  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_deconv4x4s2_fwd: tile must be -1 (auto) or 0..6");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
@@ -765,7 +769,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   g.deconv = 1;
   g.out_H = 2 * H;
   g.out_W = 2 * W;
-  return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_fwd");
+  return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_fwd", tile);
 }
 
 extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,

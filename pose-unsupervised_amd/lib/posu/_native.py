@@ -32,13 +32,13 @@ _SIGNATURES = {
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
-    'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],
+    'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_conv_bk': [_i],
     'posu_set_conv_stages': [_i],
     'posu_set_conv_tiles': [_i],
     'posu_force_conv_config': [_i],
-    'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _p],
-    'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _p],
+    'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
+    'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p],
     'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],
     'posu_maxpool3x3s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _p],

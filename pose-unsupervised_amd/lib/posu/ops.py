@@ -78,7 +78,8 @@ def nhwc_to_nchw_f32(x, code):
 
 
 # ------------------------------------------------------------------ conv ops
-def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None, out_hw=None):
+def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None, out_hw=None,
+                tile=-1):
     n, h, w, c = x.shape
     ho = (h + 2 * pad - kh) // stride + 1
     wo = (w + 2 * pad - kw) // stride + 1
@@ -87,27 +88,27 @@ def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu,
     if out is None:
         out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
     call('posu_conv2d_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, kh, kw, stride, pad,
-         ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, stream_of(x.device))
+         ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, int(tile), stream_of(x.device))
     return out
 
 
-def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None):  # noqa: D401
+def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, tile=-1):  # noqa: D401
     """act(W[:, :C] x + W[:, C:] x2[::stride2, ::stride2] + shift) (two 1x1 sources, one output)."""
     n, h, w, c = x.shape
     _, h2, w2, c2 = x2.shape
     if out is None:
         out = torch.empty((n, h, w, cout), dtype=x.dtype, device=x.device)
     call('posu_conv1x1_dual_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
-         None, ptr(shift), int(relu), ptr(out), stream_of(x.device))
+         None, ptr(shift), int(relu), ptr(out), int(tile), stream_of(x.device))
     return out
 
 
-def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None):
+def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
     call('posu_deconv4x4s2_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(scale), ptr(shift),
-         int(relu), ptr(out), stream_of(x.device))
+         int(relu), ptr(out), int(tile), stream_of(x.device))
     return out
 
 

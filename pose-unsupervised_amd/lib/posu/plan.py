@@ -23,6 +23,50 @@ from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dua
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
+# ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
+# shared by every plan, so a re-packed plan does not re-tune)
+_TUNE_CACHE = {}
+
+
+class _Tuner:
+    active = False
+    reps = 3
+
+
+def _tile_candidates(cout):
+    cpad = (cout + 63) // 64 * 64
+    c = [0, 1, 2]
+    if cpad % 128 == 0:
+        c += [3, 4, 6]
+    if cpad % 256 == 0:
+        c.append(5)
+    return c
+
+
+def _tuned(key, cout, launch):
+    """launch(tile) -> output.  While tuning, time every admissible tile once on the real
+    operands (HIP events) and keep the fastest for this geometry."""
+    if _Tuner.active and key not in _TUNE_CACHE:
+        best = None
+        for t in _tile_candidates(cout):
+            launch(t)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(_Tuner.reps):
+                launch(t)
+            b.record()
+            b.synchronize()
+            ms = a.elapsed_time(b)
+            if best is None or ms < best[0]:
+                best = (ms, t)
+        _TUNE_CACHE[key] = best[1]
+    return launch(_TUNE_CACHE.get(key, -1))
+
+
+def tuned_tiles():
+    """The autotuned table (geometry key -> tile), e.g. for logging."""
+    return dict(_TUNE_CACHE)
+
 
 class _Conv:
     __slots__ = ('w', 'scale', 'shift', 'cout', 'k', 'stride', 'pad', 'relu')
@@ -40,8 +84,14 @@ class _Conv:
         self.relu = relu
 
     def __call__(self, x, code, residual=None, out=None):
-        return ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale,
-                               self.shift, residual, self.relu, code, out=out)
+        if out is None:
+            ho = (x.shape[1] + 2 * self.pad - self.k) // self.stride + 1
+            wo = (x.shape[2] + 2 * self.pad - self.k) // self.stride + 1
+            out = torch.empty((x.shape[0], ho, wo, self.cout), dtype=x.dtype, device=x.device)
+        key = ('conv', code, tuple(x.shape), self.cout, self.k, self.stride, self.pad, residual is not None)
+        return _tuned(key, self.cout, lambda t: ops.conv2d_nhwc(
+            x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale, self.shift, residual, self.relu,
+            code, out=out, tile=t))
 
 
 class _DualTail:
@@ -57,7 +107,11 @@ class _DualTail:
         self.stride2 = dconv.stride[0]
 
     def __call__(self, mid, x, code, out=None):
-        return ops.conv1x1_dual_nhwc(mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out)
+        if out is None:
+            out = torch.empty(tuple(mid.shape[:3]) + (self.cout,), dtype=mid.dtype, device=mid.device)
+        key = ('dual', code, tuple(mid.shape), tuple(x.shape), self.cout)
+        return _tuned(key, self.cout, lambda t: ops.conv1x1_dual_nhwc(
+            mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out, tile=t))
 
 
 class _Block:
@@ -103,7 +157,11 @@ class _Deconv:
         self.cout = dc.weight.shape[1]
 
     def __call__(self, x, code, out=None):
-        return ops.deconv4x4s2_nhwc(x, self.w, self.cout, self.scale, self.shift, True, code, out=out)
+        if out is None:
+            out = torch.empty((x.shape[0], 2 * x.shape[1], 2 * x.shape[2], self.cout), dtype=x.dtype, device=x.device)
+        key = ('deconv', code, tuple(x.shape), self.cout)
+        return _tuned(key, self.cout, lambda t: ops.deconv4x4s2_nhwc(
+            x, self.w, self.cout, self.scale, self.shift, True, code, out=out, tile=t))
 
 
 class PoseResNetPlan:
@@ -150,8 +208,11 @@ class PoseResNetPlan:
         code = self.code
         if x.shape[3] == STEM_S2D_PAD:
             st = self.stem
-            return ops.conv2d_nhwc(x, self.stem_s2d_w, st.cout, 4, 4, 1, 2, st.scale, st.shift, None, True, code,
-                                   out_hw=(x.shape[1], x.shape[2]))
+            out = torch.empty(tuple(x.shape[:3]) + (st.cout,), dtype=x.dtype, device=x.device)
+            key = ('stem_s2d', code, tuple(x.shape), st.cout)
+            return _tuned(key, st.cout, lambda t: ops.conv2d_nhwc(
+                x, self.stem_s2d_w, st.cout, 4, 4, 1, 2, st.scale, st.shift, None, True, code,
+                out=out, out_hw=(x.shape[1], x.shape[2]), tile=t))
         return self.stem(x, code)
 
     def _stage_early(self, x, out=None, keep=None):
@@ -192,6 +253,18 @@ class PoseResNetPlan:
     @staticmethod
     def _block_cout(blk):
         return blk.dual.cout if blk.dual is not None else blk.convs[-1].cout
+
+    def autotune(self, x, chunks=1, keep_features=True, reps=3):
+        """Time every admissible tile configuration of every conv launch of this forward
+        (on the packed input x) and keep the fastest per layer geometry; later runs (and
+        hipGraph captures) use the tuned tiles."""
+        _Tuner.active, _Tuner.reps = True, reps
+        try:
+            with torch.no_grad():
+                out = self.run(x, chunks=chunks, keep_features=keep_features)
+        finally:
+            _Tuner.active = False
+        return out
 
     def run(self, x, chunks=1, keep_features=True):
         """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC).

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _native.exported_symbols()
-    assert lib.posu_abi_version() == 2
+    assert lib.posu_abi_version() == 3
     assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
 
 
@@ -35,7 +35,7 @@ def test_argument_errors_are_reported_without_a_gpu():
     # shape validation happens on the host before any launch
     lib = _native.load()
     st = lib.posu_conv2d_fwd(_native.BF16, None, 1, 8, 8, 8, None, 64, 3, 3, 1, 1, None, None, None, 1, None, 8, 8,
-                             None)
+                             -1, None)
     assert st == 1 and 'null pointer' in _native.last_error()
     st = lib.posu_triangulate_dlt(None, None, None, _native.F32, 128, 32, None, 1, 4, 16, 1, None, None)
     assert st == 1

@@ -38,6 +38,7 @@ def main():
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--stages', type=int, default=2)
     ap.add_argument('--big', type=int, default=1)
+    ap.add_argument('--autotune', action='store_true', help='per-layer tile autotuning first')
     args = ap.parse_args()
     import bench
     dev = torch.device('cuda', 0)
@@ -56,6 +57,11 @@ def main():
         print('%-22s %9.1f us %8.1f TF %8.0f GB/s' % (name, us, flops / us / 1e6, nbytes / us / 1e3), flush=True)
 
     xp = plan.pack_input(x_in)
+    if args.autotune:
+        from posu.plan import tuned_tiles
+        plan.autotune(xp, keep_features=False)
+        for k, v in tuned_tiles().items():
+            print('tile', v, k)
     rec('pack', lambda: plan.pack_input(x_in), 0, x_in[0].numel() * 4 + xp.numel() * esz)
     y = plan.run_stem(xp)
     n, ho, wo, co = y.shape
