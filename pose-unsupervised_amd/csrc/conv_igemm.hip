@@ -205,8 +205,9 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int ND = RA + RB;                 // DMA instructions per thread per K-tile
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int PR = pass_rows<BM, BN, S>();
-  static_assert(S >= 2 && S <= 4, "2..4 stages");
+  static_assert(S >= 1 && S <= 4, "1..4 stages");
   static_assert(ND * (S - 2) < 64, "vmcnt range");
+  static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
   static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
   __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
 
@@ -366,17 +367,29 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
   // overwrites, which every wave finished reading in the previous iteration)
+  if constexpr (S == 1) {
+    // single slot (short-K layers): a quarter of the LDS of a 2-slot ring, so more
+    // blocks share a CU and one block's epilogue overlaps another's operand fetch
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt > 0) __syncthreads();  // every wave is done reading the slot
+      POSU_DMA_TILE(kt, 0);
+      vm_wait<0>();
+      __syncthreads();
+      POSU_COMPUTE(0);
+    }
+  } else {
 #pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) POSU_DMA_TILE(s, s);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int ahead = min(S - 2, nk - 1 - kt);  // younger K-tiles in flight
-    if (S >= 4 && ahead >= 2) vm_wait<ND * (S >= 4 ? 2 : 0)>();
-    else if (S >= 3 && ahead >= 1) vm_wait<ND * (S >= 3 ? 1 : 0)>();
-    else vm_wait<0>();
-    __syncthreads();
-    if (kt + S - 1 < nk) POSU_DMA_TILE(kt + S - 1, (kt + S - 1) % S);
-    POSU_COMPUTE(kt % S);
+    for (int s = 0; s < S - 1; ++s)
+      if (s < nk) POSU_DMA_TILE(s, s);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = min(S - 2, nk - 1 - kt);  // younger K-tiles in flight
+      if (S >= 4 && ahead >= 2) vm_wait<ND * (S >= 4 ? 2 : 0)>();
+      else if (S >= 3 && ahead >= 1) vm_wait<ND * (S >= 3 ? 1 : 0)>();
+      else vm_wait<0>();
+      __syncthreads();
+      if (kt + S - 1 < nk) POSU_DMA_TILE(kt + S - 1, (kt + S - 1) % S);
+      POSU_COMPUTE(kt % S);
+    }
   }
 #undef POSU_DMA_TILE
 #undef POSU_COMPUTE
@@ -554,6 +567,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 
 template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
 void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
+  if constexpr (NW == 4) {
+    if (stages == 1) {
+      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 1, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
+      return;
+    }
+  }
   if constexpr (ring_bytes<BM, BN, 3>() <= 160 * 1024) {
     if (stages >= 3) {
       hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 3, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
@@ -592,17 +611,23 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   } else {  // 128-channel layers: 256 x 128 measured slower than 128 x 128 (layer2 c1/c2, R50@256)
     cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
-  const int want = tile >= 0 ? tile : g_force;  // per-call tile (autotuned plans) > test hook > heuristic
+  // per-call tile (autotuned plans) > test hook > heuristic; tile = cfg + 8 * variant,
+  // variant 1 = single-slot ring (four-wave tiles only)
+  const int want = tile >= 0 ? tile : g_force;
+  int st = g_stages;
   if (want >= 0) {
-    const bool wide_ok = g.CoutPad % 128 == 0 && (want != 5 || g.CoutPad % 256 == 0);
-    if (want <= 2 || wide_ok) cfg = want;
+    const int c = want & 7;
+    const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
+    if (c <= 2 || wide_ok) {
+      cfg = c;
+      if ((want >> 3) == 1 && c <= 4) st = 1;
+    }
   }
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
-  const int st = g_stages;
   switch (cfg) {
     case 0: launch_cfg<T, 256, 64, 4, 4, DUAL>(g, nb, st, s); break;
     case 1: launch_cfg<T, 128, 64, 4, 2, DUAL>(g, nb, st, s); break;
@@ -665,7 +690,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg >= -1 && cfg <= 6, "posu_force_conv_config: -1 (auto) or 0..6");
+  POSU_REQUIRE(cfg >= -1 && cfg <= 12 && cfg != 7, "posu_force_conv_config: -1 (auto), 0..6 or 8..12");
   g_force = cfg;
   return POSU_OK;
 }
@@ -685,7 +710,8 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_conv2d_fwd: tile must be -1 (auto) or 0..6");
+  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
+               "posu_conv2d_fwd: tile must be -1 (auto), 0..6 or 8..12");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -717,7 +743,8 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_conv1x1_dual_fwd: tile must be -1 (auto) or 0..6");
+  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
+               "posu_conv1x1_dual_fwd: tile must be -1 (auto), 0..6 or 8..12");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -749,7 +776,8 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 6, "posu_deconv4x4s2_fwd: tile must be -1 (auto) or 0..6");
+  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
+               "posu_deconv4x4s2_fwd: tile must be -1 (auto), 0..6 or 8..12");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

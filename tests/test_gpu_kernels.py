@@ -308,12 +308,12 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
-    """Each tile shape (incl. LDS rings above 64 KiB and eight-wave blocks) on ragged shapes:
-    3x3 with residual, 1x1 strided, and the dual-source tail."""
-    cout = 256 if cfg in (3, 4, 5, 6) else 64
+    """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks and the
+    single-slot variants 8..12) on ragged shapes: 3x3 with residual, 1x1 strided."""
+    cout = 256 if (cfg & 7) in (3, 4, 5, 6) else 64
     ops.force_conv_config(cfg)
     try:
         for case in [(2, 64, 17, 15, cout, 3, 1, 1, True, True), (3, 128, 12, 12, cout, 1, 2, 0, False, False)]:
