@@ -68,6 +68,21 @@ def build_model(layers, size, precision, device):
     return net.to(device).eval()
 
 
+def pmc_traffic(layers, size, precision, groups):
+    """HBM bytes of one network forward from the newest committed PMC reduction
+    (profiles/<round>/pmc_traffic_network.txt, tools/profile_round.sh), for the default
+    workload it was measured on; None otherwise."""
+    if (layers, size, precision, groups) != (50, 256, 'bf16', 32):
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*', 'pmc_traffic_network.txt')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.loads(f.readline())
+    return d['traffic_bytes'], os.path.relpath(files[-1], REPO)
+
+
 def cpu_baseline(layers, size, seconds):
     """Oracle chain on the host cores for a bounded sample of the same workload."""
     from oracle import geometry_ref as G
@@ -316,10 +331,14 @@ def main():
     roof = None
     if gf is not None:
         achieved = gf * frames / (net_ms * 1e-3) / 1e3  # TFLOP/s
+        traffic, src = pmc_traffic(args.layers, args.size, args.precision, args.groups)
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
-                'frac': round(achieved / peak, 4), 'traffic': None,
+                'frac': round(achieved / peak, 4), 'traffic': traffic,
                 'kernel': 'conv stack (conv_igemm_kernel launches + pack + maxpool) per network replay',
                 'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (gf, frames)}
+        if traffic:
+            roof['traffic_source'] = src + ' (PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward)'
+            roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()

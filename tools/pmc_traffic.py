@@ -7,7 +7,8 @@
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced streaming reads, so it
 is doubled; WRITE_SIZE is exact for 16-B stores.  Infinity-Cache hits are counted too.
-Takes the LAST forward's network launches (pack + conv stack + maxpool).
+Takes the LAST forward's network launches (pack + conv stack + maxpool), found from the
+last run of input-pack launches unless a launch count is given.
 """
 import csv
 import json
@@ -28,7 +29,16 @@ def load(path, counter):
 def main():
     fetch = load(sys.argv[1], 'FETCH_SIZE')
     write = load(sys.argv[2], 'WRITE_SIZE')
-    per_fwd = int(sys.argv[3]) if len(sys.argv) > 3 else 58
+    if len(sys.argv) > 3:
+        per_fwd = int(sys.argv[3])
+    else:  # the last forward starts at the first input-pack launch of the final run of packs
+        names = [x[1] for x in fetch]
+        i = len(names) - 1
+        while i >= 0 and 'pack' not in names[i]:
+            i -= 1
+        while i > 0 and 'pack' in names[i - 1]:
+            i -= 1
+        per_fwd = len(names) - i
     f = fetch[-per_fwd:]
     w = write[-per_fwd:]
     fb = sum(x[2] for x in f) * 2 * 1024

@@ -1,0 +1,43 @@
+"""Cross-check bench.py's roofline against a rocprofv3 kernel trace of the same command.
+
+    python tools/roofline_check.py <dir>/infer/run_kernel_trace.csv <bench log> [launches_per_forward]
+
+Groups the trace into network forwards (input pack .. fused deconv+head, 57 launches for
+R50), sums kernel durations per forward for the last timed forwards, and prints them next
+to bench.py's HIP-event network time and the implied TFLOP/s.
+"""
+import csv
+import json
+import sys
+
+NET = ('conv_igemm_kernel', 'maxpool_kernel', 'pack_s2d_kernel', 'pack_kernel')
+
+
+def forwards(trace, per_fwd):
+    tr = sorted(csv.DictReader(open(trace)), key=lambda r: int(r['Start_Timestamp']))
+    net = [r for r in tr if any(k in r['Kernel_Name'] for k in NET)]
+    starts = [i for i, r in enumerate(net) if 'pack' in r['Kernel_Name'] and (i == 0 or 'pack' not in net[i - 1]['Kernel_Name'])]
+    out = []
+    for a in starts:
+        seq = net[a:a + per_fwd]
+        if len(seq) == per_fwd:
+            out.append((sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in seq) / 1e6,
+                        (int(seq[-1]['End_Timestamp']) - int(seq[0]['Start_Timestamp'])) / 1e6))
+    return out
+
+
+def main():
+    per_fwd = int(sys.argv[3]) if len(sys.argv) > 3 else 57
+    fw = forwards(sys.argv[1], per_fwd)[-10:]
+    line = next(json.loads(l) for l in open(sys.argv[2]) if l.startswith('{"metric"'))
+    gf = 14.47 * line['config']['frames_per_gpu_step']
+    busy = sum(f[0] for f in fw) / len(fw)
+    print('bench: network_ms %.4f  achieved %.1f TFLOP/s  (value %.1f frames/s)'
+          % (line['network_ms'], line['roofline']['achieved'], line['value']))
+    print('trace: %d forwards, kernel-busy %.4f ms/forward (span %.4f ms) -> %.1f TFLOP/s'
+          % (len(fw), busy, sum(f[1] for f in fw) / len(fw), gf / busy))
+    print('agreement: trace / events = %.3f' % (busy / line['network_ms']))
+
+
+if __name__ == '__main__':
+    main()
