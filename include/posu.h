@@ -84,7 +84,7 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
  *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied).
  *   tile (here and in posu_conv1x1_dual_fwd / posu_deconv4x4s2_fwd): -1 = the
- *   built-in heuristic, 0..6 / 8..12 = a fixed tile configuration (numbering of
+ *   built-in heuristic, cfg + 8 * variant = a fixed tile configuration (numbering of
  *   posu_force_conv_config); the Python plan picks it per layer by timing every
  *   admissible configuration once (PoseResNetPlan.autotune). */
 int posu_conv_bk(int dtype);
@@ -96,8 +96,9 @@ int posu_set_conv_stages(int stages);
 int posu_set_conv_tiles(int big);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
- * 6: 256x128 (8 waves); 8..12: configurations 0..4 with a single-slot LDS ring,
- * for short-K layers); -1 restores the automatic choice. */
+ * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K
+ * layers); + 16: a three-slot ring (two K-tiles in flight; not 5)); -1 restores the
+ * automatic choice. */
 int posu_force_conv_config(int cfg);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,

@@ -612,7 +612,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
   // per-call tile (autotuned plans) > test hook > heuristic; tile = cfg + 8 * variant,
-  // variant 1 = single-slot ring (four-wave tiles only)
+  // variant 1 = single-slot ring (four-wave tiles), 2 = three-slot ring (where it fits)
   const int want = tile >= 0 ? tile : g_force;
   int st = g_stages;
   if (want >= 0) {
@@ -620,7 +620,8 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
     if (c <= 2 || wide_ok) {
       cfg = c;
-      if ((want >> 3) == 1 && c <= 4) st = 1;
+      const int v = want >> 3;
+      st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
     }
   }
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
@@ -635,7 +636,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     case 3: launch_cfg<T, 128, 128, 4, 2, DUAL>(g, nb, st, s); break;
     case 4: launch_cfg<T, 64, 128, 4, 2, DUAL>(g, nb, st, s); break;
     case 5: launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s); break;
-    default: launch_cfg<T, 256, 128, 8, 4, DUAL>(g, nb, 2, s); break;
+    default: launch_cfg<T, 256, 128, 8, 4, DUAL>(g, nb, st == 3 ? 3 : 2, s); break;
   }
   return check_launch(what);
 }
@@ -690,7 +691,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg >= -1 && cfg <= 12 && cfg != 7, "posu_force_conv_config: -1 (auto), 0..6 or 8..12");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 24 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -710,8 +711,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
-               "posu_conv2d_fwd: tile must be -1 (auto), 0..6 or 8..12");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -743,8 +743,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
-               "posu_conv1x1_dual_fwd: tile must be -1 (auto), 0..6 or 8..12");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -776,8 +775,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile >= -1 && tile <= 14 && (tile < 7 || (tile >= 8 && tile <= 12)),
-               "posu_deconv4x4s2_fwd: tile must be -1 (auto), 0..6 or 8..12");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

@@ -34,15 +34,15 @@ class _Tuner:
 
 
 def _tile_candidates(cout):
-    """Tile ids (include/posu.h): cfg 0..6, plus cfg + 8 = the single-slot-ring variant
-    of the four-wave tiles (short-K layers: more blocks per CU)."""
+    """Tile ids (include/posu.h): cfg 0..6, cfg + 8 = single-slot ring (four-wave tiles;
+    short-K layers: more blocks per CU), cfg + 16 = three-slot ring (two K-tiles in flight)."""
     cpad = (cout + 63) // 64 * 64
     c = [0, 1, 2]
     if cpad % 128 == 0:
         c += [3, 4, 6]
     if cpad % 256 == 0:
         c.append(5)
-    return c + [t + 8 for t in c if t <= 4]
+    return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5]
 
 
 def _tuned(key, cout, launch):

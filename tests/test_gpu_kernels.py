@@ -308,11 +308,11 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 22])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks and the
-    single-slot variants 8..12) on ragged shapes: 3x3 with residual, 1x1 strided."""
+    single- / three-slot variants) on ragged shapes: 3x3 with residual, 1x1 strided."""
     cout = 256 if (cfg & 7) in (3, 4, 5, 6) else 64
     ops.force_conv_config(cfg)
     try:
