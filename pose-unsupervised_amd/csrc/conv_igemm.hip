@@ -285,6 +285,25 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   //  row_uniform: KW*C == BK, one kernel row per K-tile (space-to-depth stem);
   //  generic    : per-chunk tap decode (C = 8 direct stem, f32 stem).
   const bool tap_uniform = (g.C % BK) == 0;
+  const bool fast_gather = tap_uniform && g.up == 0;
+  const bool row_fast = !tap_uniform && g.KW * g.C == BK && g.up == 0;
+  int rbase[RA];   // row_fast: window row origin + this lane's (kw, ci) column
+  bool wok[RA];
+  {
+    const int kwl = (cL * E) >> g.logC, cil = (cL * E) & (g.C - 1);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      wok[i] = static_cast<unsigned>(wb[i] + kwl) < static_cast<unsigned>(g.W);
+      rbase[i] = static_cast<int>(static_cast<unsigned>(nb[i]) +
+                                  (static_cast<unsigned>(hb[i]) * g.W + static_cast<unsigned>(wb[i] + kwl)) * g.C +
+                                  cil);
+    }
+  }
+  int pbase[RA];  // element offset of row i's window origin + this lane's channel chunk
+#pragma unroll
+  for (int i = 0; i < RA; ++i)  // unsigned: rows past M carry a huge negative hb (never dereferenced)
+    pbase[i] = static_cast<int>(static_cast<unsigned>(nb[i]) +
+                                (static_cast<unsigned>(hb[i]) * g.W + static_cast<unsigned>(wb[i])) * g.C + cL * E);
   const bool row_uniform = !tap_uniform && g.KW * g.C == BK;
   const int kw_row = (cL * E) >> g.logC, ci_row = (cL * E) & (g.C - 1);
   const int nk = g.Kpad / BK;
@@ -306,6 +325,26 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     } else {                                                                                        \
       int kh, kw, ci;                                                                               \
       bool kvalid = true;                                                                           \
+      if (fast_gather) {                                                                            \
+        /* one tap per K-tile, no zero-upsampling: row base + a wave-uniform tap offset */          \
+        const int tap = kbase >> g.logC;                                                            \
+        const int th = tap / g.KW, tw = tap - th * g.KW;                                            \
+        const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));                               \
+        _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                            \
+          const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&         \
+                          static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);           \
+          const int off = ok ? (pbase[i] + toff) * ES : kOOB;                                       \
+          dma16(xrs, off, As_ + i * NW * 1024);                                                     \
+        }                                                                                           \
+      } else if (row_fast) {                                                                        \
+        /* one kernel row per K-tile (space-to-depth stem): lane column fixed per row */            \
+        const int roff = (KT) * g.W * g.C;                                                          \
+        _Pragma("unroll") for (int i = 0; i < RA; ++i) {                                            \
+          const bool ok = wok[i] && static_cast<unsigned>(hb[i] + (KT)) < static_cast<unsigned>(g.H); \
+          const int off = ok ? (rbase[i] + roff) * ES : kOOB;                                       \
+          dma16(xrs, off, As_ + i * NW * 1024);                                                     \
+        }                                                                                           \
+      } else {                                                                                      \
       if (tap_uniform) {                                                                            \
         const int tap = kbase >> g.logC;                                                            \
         kh = tap / g.KW;                                                                            \
@@ -331,6 +370,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
                         static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);                     \
         const int off = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB;                      \
         dma16(xrs, off, As_ + i * NW * 1024);                                                       \
+      }                                                                                             \
       }                                                                                             \
     }                                                                                               \
     _Pragma("unroll") for (int i = 0; i < RB; ++i)                                                  \
