@@ -205,6 +205,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int ND = RA + RB;                 // DMA instructions per thread per K-tile
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int PR = pass_rows<BM, BN, S>();
+  constexpr bool PRELOAD = TM + TN <= 8;  // both k-steps' fragments fit the VGPR budget
   static_assert(S >= 1 && S <= 4, "1..4 stages");
   static_assert(ND * (S - 2) < 64, "vmcnt range");
   static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
@@ -383,15 +384,31 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   {                                                                                                 \
     const char* As_ = smem + (BUF) * STAGE;                                                         \
     const char* Bs_ = As_ + A_BYTES;                                                                \
-    _Pragma("unroll") for (int cb = 0; cb < 2; ++cb) {                                              \
-      const int c = 4 * cb + q;                                                                     \
-      uint4 af[TM], bfr[TN];                                                                        \
-      _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                \
-        af[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));             \
-      _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                \
-        bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));            \
-      _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                \
-        _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);            \
+    if constexpr (PRELOAD) {                                                                        \
+      /* both k-steps' fragments first: the MFMAs then run back to back while the */                \
+      /* second half's reads land, instead of stalling on them mid-tile */                          \
+      uint4 af[2][TM], bfr[2][TN];                                                                  \
+      _Pragma("unroll") for (int cb = 0; cb < 2; ++cb) {                                            \
+        const int c = 4 * cb + q;                                                                   \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                              \
+          bfr[cb][j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));      \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          af[cb][i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));       \
+      }                                                                                             \
+      _Pragma("unroll") for (int cb = 0; cb < 2; ++cb)                                              \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[cb][j], af[cb][i]);  \
+    } else {                                                                                        \
+      _Pragma("unroll") for (int cb = 0; cb < 2; ++cb) {                                            \
+        const int c = 4 * cb + q;                                                                   \
+        uint4 af[TM], bfr[TN];                                                                      \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          af[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));           \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                              \
+          bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));          \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);          \
+      }                                                                                             \
     }                                                                                               \
   }
 
