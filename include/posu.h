@@ -129,6 +129,24 @@ int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
                          const void* w, int Cout, const float* scale,
                          const float* shift, int relu, void* y, int tile, void* stream);
 
+/* A Bottleneck's last conv (Cout == 256, + residual + ReLU; or the two-source
+ * conv3|downsample tail) chained with the NEXT block's conv1 (1x1, stride 1, folded BN
+ * cscale/cshift, ReLU; Cout2 <= 128, multiple of 16) on the same output tile: y is
+ * written as by posu_conv2d_fwd / posu_conv1x1_dual_fwd and cy = relu(conv1x1(y) *
+ * cscale + cshift) [N, Ho, Wo, Cout2] is computed from the rounded y in LDS, so the next
+ * block never re-reads y for its conv1 (pose_resnet.py:79-99 -> the next block's
+ * conv1).  cw: packed [round_up(Cout2, 64)][256] dtype. */
+int posu_conv2d_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
+                          int Cout, int KH, int KW, int stride, int pad, const float* scale,
+                          const float* shift, const void* residual, int relu, void* y,
+                          const void* cw, int Cout2, const float* cscale, const float* cshift,
+                          void* cy, void* stream);
+int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int H, int W, int C,
+                                const void* x2, int H2, int W2, int C2, int stride2,
+                                const void* w, int Cout, const float* shift, int relu, void* y,
+                                const void* cw, int Cout2, const float* cscale,
+                                const float* cshift, void* cy, void* stream);
+
 /* The last deconv stage fused with the final 1x1 head: deconv + BN + ReLU as
  * posu_deconv4x4s2_fwd, then per output pixel hm[n][j][pix] = bias[j] +
  * sum_c hw[j][c] f[c] (lib/models/pose_resnet.py:202-203) from the tile still in LDS,

@@ -61,6 +61,13 @@ struct ConvGeom {
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out
   // fused 1x1 head (mode 0, BN == Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
+  // chained 1x1 conv (mode 0, BN == Cout == 256): cy[m][co] = relu(cscale[co] *
+  // sum_c cw[co][c] y[m][c] + cshift[co]) -- the next Bottleneck's conv1 on this tile
+  const void* cw;    // packed [>= Cout2 rows][ckp] (dtype)
+  const float* cscale;
+  const float* cshift;
+  void* cy;
+  int Cout2, ckp;
   const void* hw;    // packed head weight [>= 16 rows][hkp] (dtype)
   const float* hbias;
   float* hm;
@@ -206,6 +213,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int PR = pass_rows<BM, BN, S>();
   constexpr bool PRELOAD = TM + TN <= 8;  // both k-steps' fragments fit the VGPR budget
+  constexpr bool CHAINABLE = BN == 256 && BM == 64 && NW == 4 && PR == BM;
   static_assert(S >= 1 && S <= 4, "1..4 stages");
   static_assert(ND * (S - 2) < 64, "vmcnt range");
   static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
@@ -538,7 +546,72 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
           for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        *reinterpret_cast<uint4*>(yp + off[it]) = O::store_vals(v);
+        const uint4 packed = O::store_vals(v);
+        *reinterpret_cast<uint4*>(yp + off[it]) = packed;
+        if constexpr (CHAINABLE) {
+          if (g.cy) {  // the chained conv reads exactly the stored (rounded) values
+            float vr[E];
+            O::load_vals(packed, vr);
+#pragma unroll
+            for (int e = 0; e < E; e += 4)
+              *reinterpret_cast<float4*>(Cs + row * LD + cc * E + e) = make_float4(vr[e], vr[e + 1], vr[e + 2],
+                                                                                   vr[e + 3]);
+          }
+        }
+      }
+      if constexpr (CHAINABLE) {
+        if (g.cy) {
+          __syncthreads();
+          // next block's conv1 (1x1) on the tile in LDS: wave w takes pixel rows
+          // 16w..16w+15 (the MFMA B operand), all Cout2 channels (A = weights), K = 256
+          constexpr int MAXT = 8;
+          f32x4 cacc[MAXT];
+#pragma unroll
+          for (int j = 0; j < MAXT; ++j) cacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          const T* __restrict__ cwp = reinterpret_cast<const T*>(g.cw);
+          const int ntc = g.Cout2 / 16;
+          const int prow = wid * 16 + r16;
+          for (int kc = 0; kc < BN / (4 * E); ++kc) {
+            const int c = 4 * kc + q;
+            float av[E];
+#pragma unroll
+            for (int e = 0; e < E; e += 4) {
+              const float4 t4 = *reinterpret_cast<const float4*>(Cs + prow * LD + c * E + e);
+              av[e] = t4.x;
+              av[e + 1] = t4.y;
+              av[e + 2] = t4.z;
+              av[e + 3] = t4.w;
+            }
+            const uint4 a = O::store_vals(av);
+#pragma unroll
+            for (int j = 0; j < MAXT; ++j)
+              if (j < ntc) {
+                const uint4 b = *reinterpret_cast<const uint4*>(cwp + static_cast<size_t>(j * 16 + r16) * g.ckp + c * E);
+                O::mma(cacc[j], b, a);  // rows = channels, cols = pixels
+              }
+          }
+          const int m = m0 + prow;
+          if (m < g.M) {
+            T* __restrict__ cyp = reinterpret_cast<T*>(g.cy);
+#pragma unroll
+            for (int j = 0; j < MAXT; ++j)
+              if (j < ntc) {
+                const int co = j * 16 + q * 4;
+                float v[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) v[e] = 0.f;
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  v[e] = fmaxf(cacc[j][e] * g.cscale[co + e] + g.cshift[co + e], 0.f);
+                if constexpr (E == 4) {
+                  *reinterpret_cast<uint4*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = O::store_vals(v);
+                } else {  // 4 two-byte values: the low 8 bytes of a packed chunk
+                  const uint4 pk = O::store_vals(v);
+                  *reinterpret_cast<uint2*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = make_uint2(pk.x, pk.y);
+                }
+              }
+          }
+        }
       }
     } else if (!g.hm) {
       // NCHW f32 (heatmap head): consecutive threads walk pixels of one channel
@@ -645,12 +718,10 @@ int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
-  if (g.hm) {  // fused head: one block owns all 256 output channels
+  if (g.hm || g.cy) {  // fused head / chained conv: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
-    if constexpr (!DUAL)
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 4, 1, 2, false>), dim3(g.mtiles * nclass), dim3(256), 0, s,
-                         g);
+    hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 4, 1, 2, DUAL>), dim3(g.mtiles * nclass), dim3(256), 0, s, g);
     return check_launch(what);
   }
   // tile choice: 64-channel layers take 256 x 64 tiles (four waves stacked along M,
@@ -933,4 +1004,87 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
   g.out_H = H;
   g.out_W = W;
   return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
+}
+
+// Bottleneck tail + the next block's conv1 in one launch (layer1: Cout 256): the block
+// output y is written as usual and, from the same tile in LDS, cy = relu(bn(conv1x1(y)))
+// (pose_resnet.py:79-99: out of block b feeds conv1 of block b + 1), so y is not read
+// back from HBM by the next block.
+namespace posu {
+namespace {
+int attach_chain(ConvGeom& g, int dtype, const void* cw, int Cout2, const float* cscale, const float* cshift, void* cy,
+                 const char* what) {
+  POSU_REQUIRE(cw && cscale && cshift && cy, std::string(what) + ": null chained operand");
+  POSU_REQUIRE(g.Cout == 256 && g.relu && Cout2 > 0 && Cout2 % 16 == 0 && Cout2 <= 128,
+               std::string(what) + ": needs Cout == 256, ReLU, and 16 <= Cout2 <= 128 (multiple of 16)");
+  g.cw = cw;
+  g.Cout2 = Cout2;
+  g.cscale = cscale;
+  g.cshift = cshift;
+  g.cy = cy;
+  g.ckp = round_up(g.Cout, bk_of(dtype));
+  return POSU_OK;
+}
+}  // namespace
+}  // namespace posu
+
+extern "C" int posu_conv2d_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
+                                     int KH, int KW, int stride, int pad, const float* scale, const float* shift,
+                                     const void* residual, int relu, void* y, const void* cw, int Cout2,
+                                     const float* cscale, const float* cshift, void* cy, void* stream) {
+  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_chain_fwd")) return st;
+  POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_chain_fwd: bad window");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  POSU_REQUIRE(Ho > 0 && Wo > 0, "posu_conv2d_chain_fwd: empty output");
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
+  g.scale = scale;
+  g.shift = shift;
+  g.res = residual;
+  g.y = y;
+  g.Ho = Ho;
+  g.Wo = Wo;
+  g.M = N * Ho * Wo;
+  g.K = KH * KW * C;
+  g.Kpad = round_up(g.K, bk_of(dtype));
+  g.KH = KH;
+  g.KW = KW;
+  g.stride = stride;
+  g.pad_h = pad;
+  g.pad_w = pad;
+  g.relu = relu;
+  g.out_H = Ho;
+  g.out_W = Wo;
+  if (int st = attach_chain(g, dtype, cw, Cout2, cscale, cshift, cy, "posu_conv2d_chain_fwd")) return st;
+  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_chain_fwd");
+}
+
+extern "C" int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2,
+                                           int H2, int W2, int C2, int stride2, const void* w, int Cout,
+                                           const float* shift, int relu, void* y, const void* cw, int Cout2,
+                                           const float* cscale, const float* cshift, void* cy, void* stream) {
+  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_chain_fwd")) return st;
+  if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_chain_fwd")) return st;
+  const int BK = bk_of(dtype);
+  POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_chain_fwd: C and C2 must be multiples of the K-tile");
+  POSU_REQUIRE(stride2 > 0 && (H - 1) * stride2 < H2 && (W - 1) * stride2 < W2,
+               "posu_conv1x1_dual_chain_fwd: source-2 grid too small for the output grid");
+  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
+  g.x2 = x2;
+  g.H2 = H2;
+  g.W2 = W2;
+  g.C2 = C2;
+  g.stride2 = stride2;
+  g.K1 = C;
+  g.shift = shift;
+  g.y = y;
+  g.Ho = H;
+  g.Wo = W;
+  g.M = N * H * W;
+  g.K = C + C2;
+  g.Kpad = C + C2;
+  g.relu = relu;
+  g.out_H = H;
+  g.out_W = W;
+  if (int st = attach_chain(g, dtype, cw, Cout2, cscale, cshift, cy, "posu_conv1x1_dual_chain_fwd")) return st;
+  return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_chain_fwd");
 }

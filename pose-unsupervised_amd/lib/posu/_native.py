@@ -38,6 +38,10 @@ _SIGNATURES = {
     'posu_set_conv_tiles': [_i],
     'posu_force_conv_config': [_i],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
+    'posu_conv2d_chain_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _p, _i, _p, _p, _p,
+                              _p],
+    'posu_conv1x1_dual_chain_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i, _p, _p,
+                                    _p, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p],
     'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],

@@ -103,6 +103,32 @@ def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, ti
     return out
 
 
+def conv2d_chain_nhwc(x, wpk, cout, k, stride, pad, scale, shift, residual, code, cw, cout2, cscale, cshift,
+                      out=None):
+    """Block tail conv (+residual, ReLU) and the next block's 1x1 conv1 in one launch:
+    returns (y [N, Ho, Wo, cout], cy [N, Ho, Wo, cout2])."""
+    n, h, w, c = x.shape
+    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+    if out is None:
+        out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
+    cy = torch.empty((n, ho, wo, cout2), dtype=x.dtype, device=x.device)
+    call('posu_conv2d_chain_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, k, k, stride, pad, ptr(scale), ptr(shift),
+         ptr(residual), 1, ptr(out), ptr(cw), cout2, ptr(cscale), ptr(cshift), ptr(cy), stream_of(x.device))
+    return out, cy
+
+
+def conv1x1_dual_chain_nhwc(x, x2, stride2, wpk, cout, shift, code, cw, cout2, cscale, cshift, out=None):
+    """Two-source Bottleneck tail (conv3|downsample, ReLU) chained with the next conv1."""
+    n, h, w, c = x.shape
+    _, h2, w2, c2 = x2.shape
+    if out is None:
+        out = torch.empty((n, h, w, cout), dtype=x.dtype, device=x.device)
+    cy = torch.empty((n, h, w, cout2), dtype=x.dtype, device=x.device)
+    call('posu_conv1x1_dual_chain_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
+         ptr(shift), 1, ptr(out), ptr(cw), cout2, ptr(cscale), ptr(cshift), ptr(cy), stream_of(x.device))
+    return out, cy
+
+
 def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):
     n, h, w, c = x.shape
     if out is None:

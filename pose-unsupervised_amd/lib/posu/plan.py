@@ -23,6 +23,11 @@ from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dua
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
+# Bottleneck tails that also compute the next block's conv1 (layer1 -> layer2.0).
+# Off by default: measured slower on R50@256 (the 64x256 chain tile re-reads the whole
+# 256-channel weight per 64-pixel block: 381 vs 341 us for block0 + the next conv1).
+CHAIN_BLOCKS = False
+
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
 _TUNE_CACHE = {}
@@ -117,13 +122,14 @@ class _DualTail:
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual')
+    __slots__ = ('convs', 'down', 'dual', 'chain')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
         self.convs = []
         self.down = None
         self.dual = None
+        self.chain = None   # the next block's conv1, computed in this block's tail launch
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -136,16 +142,39 @@ class _Block:
         if ds is not None:
             self.down = _Conv(ds[0], ds[1], False, code, bk)
 
-    def __call__(self, x, code, out=None):
-        y = x
+    @property
+    def cout(self):
+        return self.dual.cout if self.dual is not None else self.convs[-1].cout
+
+    def chainable_to(self, nxt):
+        """This block's tail can also compute `nxt`'s conv1 (posu_conv2d_chain_fwd): all 256
+        output channels in one tile, and a 1x1 / stride-1 next conv1 of <= 128 channels."""
+        c1 = nxt.convs[0]
+        return (self.cout == 256 and c1.k == 1 and c1.stride == 1 and c1.pad == 0 and c1.relu
+                and c1.cout <= 128 and c1.cout % 16 == 0 and c1.w.shape[1] == 256)
+
+    def __call__(self, x, code, out=None, pre=None):
+        """-> (block output, the next block's conv1 output if chained else None).
+        pre: this block's conv1 output, already computed by the previous block."""
+        y = pre if pre is not None else x
+        first = 1 if pre is not None else 0
+        ch = self.chain
         if self.dual is not None:
-            for c in self.convs:
+            for c in self.convs[first:]:
                 y = c(y, code)
-            return self.dual(y, x, code, out=out)
+            if ch is not None:
+                dl = self.dual
+                return ops.conv1x1_dual_chain_nhwc(y, x, dl.stride2, dl.w, dl.cout, dl.shift, code, ch.w, ch.cout,
+                                                   ch.scale, ch.shift, out=out)
+            return self.dual(y, x, code, out=out), None
         res = self.down(x, code) if self.down is not None else x
-        for c in self.convs[:-1]:
+        for c in self.convs[first:-1]:
             y = c(y, code)
-        return self.convs[-1](y, code, residual=res, out=out)
+        last = self.convs[-1]
+        if ch is not None:
+            return ops.conv2d_chain_nhwc(y, last.w, last.cout, last.k, last.stride, last.pad, last.scale,
+                                         last.shift, res, code, ch.w, ch.cout, ch.scale, ch.shift, out=out)
+        return last(y, code, residual=res, out=out), None
 
 
 class _Deconv:
@@ -177,6 +206,11 @@ class PoseResNetPlan:
         self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, STEM_S2D_PAD, bk, ops.torch_dtype(code))
         self.layers = [[_Block(b, code, bk) for b in layer] for layer in
                        (net.layer1, net.layer2, net.layer3, net.layer4)]
+        if CHAIN_BLOCKS:
+            blocks = [b for layer in self.layers for b in layer]
+            for b, nxt in zip(blocks, blocks[1:]):
+                if b.chainable_to(nxt):
+                    b.chain = nxt.convs[0]
         mods = list(net.deconv_layers)
         self.deconvs = []
         for i in range(0, len(mods), 3):
@@ -221,18 +255,20 @@ class PoseResNetPlan:
         """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
         code = self.code
         x = ops.maxpool3x3s2_nhwc(self.run_stem(x), code)
+        pre = None
         for li in (0, 1):
             layer = self.layers[li]
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
                 if li == 0 and last and keep is not None:
-                    x = blk(x, code, out=keep)
+                    x, pre = blk(x, code, out=keep, pre=pre)
                 elif li == 1 and last and out is not None:
-                    x = blk(x, code, out=out)
+                    x, pre = blk(x, code, out=out, pre=pre)
                 else:
-                    x = blk(x, code)
+                    x, pre = blk(x, code, pre=pre)
             if li == 0:
                 x1 = x
+        assert pre is None
         return x, x1
 
     def _last_deconv_head(self, x, keep_f, hm_out=None, f_out=None):
@@ -254,7 +290,7 @@ class PoseResNetPlan:
 
     @staticmethod
     def _block_cout(blk):
-        return blk.dual.cout if blk.dual is not None else blk.convs[-1].cout
+        return blk.cout
 
     def autotune(self, x, chunks=1, keep_features=True, reps=3):
         """Time every admissible tile configuration of every conv launch of this forward
@@ -282,9 +318,10 @@ class PoseResNetPlan:
             x = self.run_stem(x)
             x = ops.maxpool3x3s2_nhwc(x, code)
             x1 = None
+            pre = None
             for li, layer in enumerate(self.layers):
                 for blk in layer:
-                    x = blk(x, code)
+                    x, pre = blk(x, code, pre=pre)
                 if li == 0:
                     x1 = x
             for dc in self.deconvs[:-1]:
@@ -307,9 +344,10 @@ class PoseResNetPlan:
             sl = slice(k * c, (k + 1) * c)
             self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
         y = x2
+        pre = None
         for layer in self.layers[2:]:
             for blk in layer:
-                y = blk(y, code)
+                y, pre = blk(y, code, pre=pre)
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)

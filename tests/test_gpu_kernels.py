@@ -337,3 +337,36 @@ def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
         assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
     else:
         torch.testing.assert_close(got, ref, atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('code,tol', [(F32, 1e-5), (BF16, 0.02), (F16, 0.005)])
+@pytest.mark.parametrize('dual,cout2', [(False, 64), (True, 64), (False, 128)])
+def test_chained_next_conv1_matches_two_launches(cuda, code, tol, dual, cout2):
+    """Block tail (+residual / downsample source) with the next block's 1x1 conv1 in the
+    same launch == the tail launch followed by a separate conv1 launch on its output."""
+    g = torch.Generator().manual_seed(9)
+    dt = ops.torch_dtype(code)
+    bk = ops.conv_bk(code)
+    n, h, w, mid, cin = 3, 9, 7, 64, 128
+    a = torch.relu(torch.randn(n, h, w, mid, generator=g)).to(cuda, dt)
+    x = torch.randn(n, h, w, cin if dual else 256, generator=g).to(cuda, dt)
+    w3 = torch.randn(256, mid, 1, 1, generator=g) * 0.1
+    sc = (torch.rand(256, generator=g) + 0.5).to(cuda)
+    sh = (torch.randn(256, generator=g) * 0.1).to(cuda)
+    w1 = torch.randn(cout2, 256, 1, 1, generator=g) * 0.06
+    s1 = (torch.rand(cout2, generator=g) + 0.5).to(cuda)
+    b1 = (torch.randn(cout2, generator=g) * 0.1).to(cuda)
+    cw = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
+    if dual:
+        wd = torch.randn(256, cin, 1, 1, generator=g) * 0.1
+        sd = (torch.rand(256, generator=g) + 0.5).to(cuda)
+        wp = packing.pack_dual_1x1_weight(w3.to(cuda), sc, wd.to(cuda), sd, dt)
+        y, cy = ops.conv1x1_dual_chain_nhwc(a, x, 1, wp, 256, sh, code, cw, cout2, s1, b1)
+        y_ref = ops.conv1x1_dual_nhwc(a, x, 1, wp, 256, sh, True, code)
+    else:
+        wp = packing.pack_conv_weight(w3.to(cuda), mid, bk, dt)
+        y, cy = ops.conv2d_chain_nhwc(a, wp, 256, 1, 1, 0, sc, sh, x, code, cw, cout2, s1, b1)
+        y_ref = ops.conv2d_nhwc(a, wp, 256, 1, 1, 1, 0, sc, sh, x, True, code)
+    cy_ref = ops.conv2d_nhwc(y_ref, cw, cout2, 1, 1, 1, 0, s1, b1, None, True, code)
+    torch.testing.assert_close(y, y_ref, atol=0, rtol=0)        # same kernel math for the tail
+    torch.testing.assert_close(cy.float(), cy_ref.float(), atol=tol, rtol=tol)
