@@ -311,10 +311,14 @@ int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const
 /* y = act(z * scale[seg] + shift[seg] (+ residual)) */
 int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
                   const float* shift, const void* residual, int relu, void* y, void* stream);
-/* Backward of y = relu?(bn(z) (+ r)):  g' = gy * [y > 0] (y NULL: no ReLU);
+/* Backward of y = relu?(bn(z) (+ r)):  g' = gy * [y > 0]; without a residual the mask
+ * can instead be recomputed from z with the forward's per-segment relu_scale/relu_shift
+ * ([nseg, C], posu_bn_train_fwd's scale/shift: y > 0 <=> z*scale + shift > 0), which
+ * saves reading y; y = relu_scale = NULL: no ReLU.
  * dz = gamma*rstd*(g' - mean(g') - xhat*mean(g'*xhat)) per segment; dgamma/dbeta
  * [C] f32 written (summed over segments); gres (optional) = g'. */
-int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const void* z, int nseg, int Pseg,
+int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const float* relu_scale,
+                      const float* relu_shift, const void* z, int nseg, int Pseg,
                       int C, const float* mean, const float* rstd, const float* gamma,
                       float* dgamma, float* dbeta, void* dz, void* gres, void* workspace,
                       long long workspace_bytes, void* stream);

@@ -39,7 +39,9 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
 // MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0] (y optional)
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z, const T* __restrict__ gy,
-                                                         const T* __restrict__ y, const float* __restrict__ mean,
+                                                         const T* __restrict__ y, const float* __restrict__ msc,
+                                                         const float* __restrict__ msh,
+                                                         const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, int Pseg, int C,
                                                          RedShape rs, double* __restrict__ part) {
   constexpr int E = Vec<T>::E;
@@ -49,19 +51,25 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
   const int ch = blockIdx.y * rs.CB + cb;
   const int seg = blockIdx.z, blk = blockIdx.x;
   const bool active = ch < rs.CPR;
-  float a[E], b[E], mu[E], rd[E];
+  float a[E], b[E], mu[E], rd[E], ks[E], kh[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     a[e] = 0.f;
     b[e] = 0.f;
     mu[e] = 0.f;
     rd[e] = 0.f;
+    ks[e] = 0.f;
+    kh[e] = 0.f;
   }
   if (MODE == 1 && active) {
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       mu[e] = mean[seg * C + ch * E + e];
       rd[e] = rstd[seg * C + ch * E + e];
+      if (msc) {
+        ks[e] = msc[seg * C + ch * E + e];
+        kh[e] = msh[seg * C + ch * E + e];
+      }
     }
   }
   if (active) {
@@ -79,13 +87,16 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       } else {
         float gv[E];
         Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + off), gv);
+        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
         if (y) {
           float yv[E];
           Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + off), yv);
 #pragma unroll
           for (int e = 0; e < E; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
+        } else if (msc) {  // ReLU mask recomputed from z (no residual): y > 0 <=> z*scale+shift > 0
+#pragma unroll
+          for (int e = 0; e < E; ++e) gv[e] = v[e] * ks[e] + kh[e] > 0.f ? gv[e] : 0.f;
         }
-        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           a[e] += gv[e];
@@ -238,6 +249,8 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
 // gres (optional) = g', the gradient of the residual branch
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ y,
+                                                           const float* __restrict__ msc,
+                                                           const float* __restrict__ msh,
                                                            const T* __restrict__ z, int Pseg, int C,
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
@@ -251,14 +264,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     const int seg = static_cast<int>(pix / Pseg);
     float g[E], v[E];
     Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + i * E), g);
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + i * E), v);
     if (y) {
       float yv[E];
       Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + i * E), yv);
 #pragma unroll
       for (int e = 0; e < E; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+    } else if (msc) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = v[e] * msc[seg * C + c0 + e] + msh[seg * C + c0 + e] > 0.f ? g[e] : 0.f;
     }
     if (gres) *reinterpret_cast<uint4*>(gres + i * E) = Vec<T>::pack(g);
-    Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + i * E), v);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       const int c = c0 + e;
@@ -401,7 +417,7 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
-                       static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part);
+                       static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
   hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
@@ -424,7 +440,8 @@ extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C
   return check_launch("posu_bn_apply");
 }
 
-extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const void* z, int nseg, int Pseg, int C,
+extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const float* relu_scale,
+                                 const float* relu_shift, const void* z, int nseg, int Pseg, int C,
                                  const float* mean, const float* rstd, const float* gamma, float* dgamma,
                                  float* dbeta, void* dz, void* gres, void* workspace, long long workspace_bytes,
                                  void* stream) {
@@ -440,8 +457,8 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
   bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
-                       static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), mean, rstd, Pseg,
-                       C, rs, part);
+                       static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale,
+                       relu_shift, mean, rstd, Pseg, C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
@@ -449,7 +466,7 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
   with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(gy),
-                       static_cast<const T*>(y), static_cast<const T*>(z), Pseg, C, mean, rstd, coef,
+                       static_cast<const T*>(y), relu_scale, relu_shift, static_cast<const T*>(z), Pseg, C, mean, rstd, coef,
                        static_cast<T*>(dz), static_cast<T*>(gres), total);
   });
   return check_launch("posu_bn_train_bwd");
@@ -467,7 +484,7 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, 1), dim3(256), 0, s, static_cast<const T*>(x),
-                       nullptr, nullptr, nullptr, nullptr, P, C, rs, part);
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
   hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);

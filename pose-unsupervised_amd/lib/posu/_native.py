@@ -63,7 +63,7 @@ _SIGNATURES = {
     'posu_bn_workspace': [_i, _i],
     'posu_bn_train_fwd': [_i, _p, _i, _i, _i, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_bn_apply': [_i, _p, _i, _i, _i, _p, _p, _p, _i, _p, _p],
-    'posu_bn_train_bwd': [_i, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
+    'posu_bn_train_bwd': [_i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_channel_sum': [_i, _p, _i, _i, _p, _p, _ll, _p],
     'posu_maxpool3x3s2_bwd_workspace': [_i, _i, _i, _i],
     'posu_maxpool3x3s2_bwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _ll, _p],

@@ -85,8 +85,9 @@ def bn_apply(z, nseg, scale, shift, residual=None, relu=True, out=None):
     return out
 
 
-def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None, dbeta=None):
-    """Backward of y = relu?(bn(z) (+ r)); y=None means no ReLU.
+def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None, dbeta=None, relu_from=None):
+    """Backward of y = relu?(bn(z) (+ r)); y=None and relu_from=None means no ReLU;
+    relu_from=(scale, shift) recomputes the ReLU mask from z (no residual) instead of reading y.
     Returns (dz, gres or None, dgamma [C] f32, dbeta [C] f32)."""
     require_cuda(gy, z)
     c = z.shape[-1]
@@ -98,7 +99,9 @@ def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None
     if dbeta is None:
         dbeta = torch.empty((c,), dtype=torch.float32, device=z.device)
     ws = _bn_ws(z.device, nseg, c)
-    call('posu_bn_train_bwd', nat.dtype_code_of(z), ptr(gy), ptr(y), ptr(z), nseg, pix // nseg, c, ptr(mean),
+    msc, msh = relu_from if relu_from is not None else (None, None)
+    call('posu_bn_train_bwd', nat.dtype_code_of(z), ptr(gy), ptr(y), ptr(msc), ptr(msh), ptr(z), nseg, pix // nseg, c,
+         ptr(mean),
          ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dz), ptr(gres), ptr(ws), ws.numel(),
          stream_of(z.device))
     return dz, gres, dgamma, dbeta

@@ -57,12 +57,15 @@ class _ConvBN:
         mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
                                             bn.running_var)
         y = T.bn_apply(z, nseg, sc, sh, residual, self.relu)
-        return y, (x, z, y, mean, rstd)
+        return y, (x, z, y, mean, rstd, sc, sh, residual is not None)
 
     def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None):
-        x, z, y, mean, rstd = saved
-        dz, gres, dgam, dbet = T.bn_train_bwd(gy, y if self.relu else None, z, nseg, mean, rstd, self.bn.weight,
-                                              want_gres=want_gres)
+        x, z, y, mean, rstd, sc, sh, has_res = saved
+        # ReLU mask: from y after a residual add, else recomputed from z (one tensor read less)
+        mask_y = y if (self.relu and has_res) else None
+        relu_from = (sc, sh) if (self.relu and not has_res) else None
+        dz, gres, dgam, dbet = T.bn_train_bwd(gy, mask_y, z, nseg, mean, rstd, self.bn.weight, want_gres=want_gres,
+                                              relu_from=relu_from)
         grads[self.conv.weight] = T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad, code)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
@@ -138,11 +141,11 @@ class _DeconvBN:
         mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
                                             bn.running_var)
         y = T.bn_apply(z, nseg, sc, sh, None, True)
-        return y, (x, z, y, mean, rstd)
+        return y, (x, z, mean, rstd, sc, sh)
 
     def backward(self, gy, saved, nseg, code, grads):
-        x, z, y, mean, rstd = saved
-        dz, _, dgam, dbet = T.bn_train_bwd(gy, y, z, nseg, mean, rstd, self.bn.weight)
+        x, z, mean, rstd, sc, sh = saved
+        dz, _, dgam, dbet = T.bn_train_bwd(gy, None, z, nseg, mean, rstd, self.bn.weight, relu_from=(sc, sh))
         grads[self.dc.weight] = T.deconv4x4s2_wgrad(x, dz, code)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet

@@ -156,6 +156,12 @@ def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, r
     yd = T.bn_apply(zd, nseg, sc, sh, rd, relu)
     dz, gres, dgam, dbet = T.bn_train_bwd(_nhwc(gy, cuda, dt), yd if relu else None, zd, nseg, mean, rstd,
                                           gamma.detach().to(cuda), want_gres=residual)
+    if relu and not residual:  # mask recomputed from z instead of read from y: same result
+        dz2, _, dg2, db2 = T.bn_train_bwd(_nhwc(gy, cuda, dt), None, zd, nseg, mean, rstd, gamma.detach().to(cuda),
+                                          relu_from=(sc, sh))
+        torch.testing.assert_close(dz2, dz, atol=0, rtol=0)
+        torch.testing.assert_close(dg2, dgam, atol=0, rtol=0)
+        torch.testing.assert_close(db2, dbet, atol=0, rtol=0)
     torch.cuda.synchronize()
     if code == F32:
         tol = dict(atol=1e-4, rtol=1e-4)
