@@ -270,6 +270,25 @@ int posu_triangulate_dlt(const double* M, const double* intr, const void* xy, in
                          int xy_stride_g, int xy_stride_v, const unsigned char* vis, int G,
                          int V, int J, int undistort, double* X, void* stream);
 
+/* Pseudo-label RANSAC (multiviews/triangulate.py:102-165, ransac): per (group, joint),
+ * every pair of visible views (itertools.combinations order) is triangulated (DLT on
+ * undistorted points), re-projected into all V views (pymvg find2d: [R|t] = K^-1 M,
+ * OpenCV plumb-bob distortion of intr), and views with error < reproj_thre are that
+ * pair's inliers; pairs with fewer than min_inliers (>= 1) are skipped; the best pair has
+ * the most inliers, ties broken by the smaller mean error.  res_vis[g][v][k] = 1 for the
+ * best pair's inliers, else 0.  xy: [G, V, J, 2] f64 (all views, visible or not);
+ * vis: NULL or [G, V, J] uint8; 2 <= V <= 4. */
+int posu_ransac_inliers(const double* M, const double* intr, const double* xy,
+                        const unsigned char* vis, int G, int V, int J, int undistort,
+                        double reproj_thre, int min_inliers, unsigned char* res_vis, void* stream);
+/* reproject_poses (triangulate.py:168-213): triangulate each joint from its visible
+ * views and project into every view: proj [G, V, J, 2] f64 and res_vis = 1 where the
+ * joint has >= 2 visible views (zeros otherwise). */
+int posu_reproject(const double* M, const double* intr, const double* xy, const unsigned char* vis,
+                   int G, int V, int J, int undistort, double* proj, unsigned char* res_vis,
+                   void* stream);
+
+
 /* ----------------------------------------------------------- training path */
 /* BASELINE configs[3]: the data-parallel training step (run/pose2d/train.py +
  * core/function.py:91-366: per-view backbone forward in train mode, JointsMSELoss,

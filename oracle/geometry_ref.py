@@ -213,3 +213,69 @@ def triangulate_poses(cameras, poses2d, joints_vis=None, no_distortion=False):
             out[i, k] = find3d([cams[v][0] for v in sel], [cams[v][1] for v in sel], [cams[v][2] for v in sel],
                                [poses2d[i * nviews + v, k] for v in sel])
     return out
+
+
+# ---------------------------------------------- pseudo-label RANSAC / reprojection
+def find2d(M, K, D, X):
+    """pymvg CameraModel.project_3d_to_pixel restated: [R|t] = K^-1 M, OpenCV plumb-bob
+    distortion (k1, k2, p1, p2, k3) in normalised coordinates, back through K."""
+    P = M.dot(np.append(np.asarray(X, np.float64)[:3], 1.0))
+    Rt = np.linalg.solve(K, P)
+    x, y = Rt[0] / Rt[2], Rt[1] / Rt[2]
+    k1, k2, p1, p2, k3 = D
+    r2 = x * x + y * y
+    radial = 1 + k1 * r2 + k2 * r2 ** 2 + k3 * r2 ** 3
+    xd = x * radial + 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+    yd = y * radial + p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+    return np.array([K[0, 0] * xd + K[0, 2], K[1, 1] * yd + K[1, 2]])
+
+
+def ransac(poses2d, cameras, joints_vis, reproj_thre, num_inliers, no_distortion=False):
+    """multiviews/triangulate.py:102-165 (ransac) with the pymvg calls restated."""
+    import itertools
+    nviews = 4
+    nj = poses2d.shape[1]
+    res_vis = np.zeros_like(joints_vis)
+    for i in range(len(cameras) // nviews):
+        cams = [_camera(cameras[i * nviews + v], no_distortion) for v in range(nviews)]
+        for k in range(nj):
+            pts = [(v, poses2d[i * nviews + v, k, :]) for v in range(nviews) if joints_vis[i * nviews + v, k]]
+            if len(pts) < 2:
+                continue
+            best_inliers, best_error = [], 10000
+            for pair in itertools.combinations(pts, 2):
+                X = find3d([cams[v][0] for v, _ in pair], [cams[v][1] for v, _ in pair],
+                           [cams[v][2] for v, _ in pair], [p for _, p in pair])
+                in_thre, mean_error = [], 0
+                for j in range(nviews):
+                    err = np.linalg.norm(find2d(*cams[j], X) - poses2d[i * nviews + j, k, :])
+                    if err < reproj_thre:
+                        in_thre.append(j)
+                        mean_error += err
+                if len(in_thre) < num_inliers:
+                    continue
+                mean_error /= len(in_thre)
+                if len(in_thre) > len(best_inliers) or (len(in_thre) == len(best_inliers) and mean_error < best_error):
+                    best_inliers, best_error = in_thre, mean_error
+            for v in best_inliers:
+                res_vis[i * nviews + v, k] = 1
+    return res_vis
+
+
+def reproject_poses(poses2d, cameras, joints_vis, no_distortion=False):
+    """multiviews/triangulate.py:168-213 with the pymvg calls restated."""
+    nviews = 4
+    proj = np.zeros_like(poses2d, dtype=np.float64)
+    res_vis = np.zeros_like(joints_vis)
+    for i in range(len(cameras) // nviews):
+        cams = [_camera(cameras[i * nviews + v], no_distortion) for v in range(nviews)]
+        for k in range(poses2d.shape[1]):
+            sel = [v for v in range(nviews) if joints_vis[i * nviews + v, k]]
+            if len(sel) < 2:
+                continue
+            X = find3d([cams[v][0] for v in sel], [cams[v][1] for v in sel], [cams[v][2] for v in sel],
+                       [poses2d[i * nviews + v, k] for v in sel])
+            for j in range(nviews):
+                proj[i * nviews + j, k] = find2d(*cams[j], X)
+                res_vis[i * nviews + j, k] = 1
+    return proj, res_vis

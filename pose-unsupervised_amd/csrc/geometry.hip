@@ -128,51 +128,11 @@ __device__ __forceinline__ void undistort_px(const double* c, double& u, double&
   v = yy * fy + cy;
 }
 
-// Rows of invisible views are zero: a zero row adds nothing to A^T A, so the right
-// singular vectors of the remaining rows are unchanged.  ROWS is a compile-time
-// bound, so A lives in registers (no scratch) for the 4-view case.
-template <int VMAX>
-__global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ Mall,
-                                                         const double* __restrict__ intr,
-                                                         const void* __restrict__ xyv, int xy_dtype, int sg,
-                                                         int sv, const unsigned char* __restrict__ vis, int G, int V,
-                                                         int J, int undistort, double* __restrict__ X) {
-  constexpr int ROWS = 2 * VMAX;
-  const int t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= G * J) return;
-  const int g = t / J, k = t - g * J;
-  double A[ROWS][4];
-  int nvis = 0;
-#pragma unroll
-  for (int v = 0; v < VMAX; ++v) {
-    const size_t gv = static_cast<size_t>(g) * V + (v < V ? v : 0);
-    const bool on = v < V && (!vis || vis[gv * J + k]);
-    double u = 0.0, vv = 0.0;
-    if (on) {
-      const size_t xoff = static_cast<size_t>(g) * sg + static_cast<size_t>(v) * sv + 2 * k;
-      if (xy_dtype == POSU_F64) {
-        u = static_cast<const double*>(xyv)[xoff];
-        vv = static_cast<const double*>(xyv)[xoff + 1];
-      } else {
-        u = static_cast<const float*>(xyv)[xoff];
-        vv = static_cast<const float*>(xyv)[xoff + 1];
-      }
-      if (undistort) undistort_px(intr + gv * 9, u, vv);
-      ++nvis;
-    }
-    const double* M = Mall + gv * 12;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      A[2 * v][c] = on ? u * M[8 + c] - M[c] : 0.0;
-      A[2 * v + 1][c] = on ? vv * M[8 + c] - M[4 + c] : 0.0;
-    }
-  }
-  double* out = X + static_cast<size_t>(t) * 3;
-  if (nvis < 2) {  // fewer than two views: the reference leaves zeros (triangulate.py:95-96)
-    out[0] = out[1] = out[2] = 0.0;
-    return;
-  }
-  // one-sided Jacobi: rotate column pairs of A until mutually orthogonal; Vm accumulates
+// Smallest right singular vector of A (one-sided Jacobi), dehomogenised: the DLT
+// point of pymvg MultiCameraSystem.find3d (svd -> vt[-1, :3] / vt[-1, 3]).
+template <int ROWS>
+__device__ __forceinline__ void dlt_point(double (&A)[ROWS][4], double* out) {
+  // rotate column pairs of A until mutually orthogonal; Vm accumulates the rotations
   double Vm[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
   for (int sweep = 0; sweep < 30; ++sweep) {
     bool rotated = false;
@@ -230,6 +190,53 @@ __global__ __launch_bounds__(64) void triangulate_kernel(const double* __restric
   out[0] = v0 / v3;
   out[1] = v1 / v3;
   out[2] = v2 / v3;
+}
+
+// Rows of invisible views are zero: a zero row adds nothing to A^T A, so the right
+// singular vectors of the remaining rows are unchanged.  ROWS is a compile-time
+// bound, so A lives in registers (no scratch) for the 4-view case.
+template <int VMAX>
+__global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ Mall,
+                                                         const double* __restrict__ intr,
+                                                         const void* __restrict__ xyv, int xy_dtype, int sg,
+                                                         int sv, const unsigned char* __restrict__ vis, int G, int V,
+                                                         int J, int undistort, double* __restrict__ X) {
+  constexpr int ROWS = 2 * VMAX;
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= G * J) return;
+  const int g = t / J, k = t - g * J;
+  double A[ROWS][4];
+  int nvis = 0;
+#pragma unroll
+  for (int v = 0; v < VMAX; ++v) {
+    const size_t gv = static_cast<size_t>(g) * V + (v < V ? v : 0);
+    const bool on = v < V && (!vis || vis[gv * J + k]);
+    double u = 0.0, vv = 0.0;
+    if (on) {
+      const size_t xoff = static_cast<size_t>(g) * sg + static_cast<size_t>(v) * sv + 2 * k;
+      if (xy_dtype == POSU_F64) {
+        u = static_cast<const double*>(xyv)[xoff];
+        vv = static_cast<const double*>(xyv)[xoff + 1];
+      } else {
+        u = static_cast<const float*>(xyv)[xoff];
+        vv = static_cast<const float*>(xyv)[xoff + 1];
+      }
+      if (undistort) undistort_px(intr + gv * 9, u, vv);
+      ++nvis;
+    }
+    const double* M = Mall + gv * 12;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      A[2 * v][c] = on ? u * M[8 + c] - M[c] : 0.0;
+      A[2 * v + 1][c] = on ? vv * M[8 + c] - M[4 + c] : 0.0;
+    }
+  }
+  double* out = X + static_cast<size_t>(t) * 3;
+  if (nvis < 2) {  // fewer than two views: the reference leaves zeros (triangulate.py:95-96)
+    out[0] = out[1] = out[2] = 0.0;
+    return;
+  }
+  dlt_point<ROWS>(A, out);
 }
 
 }  // namespace
@@ -308,4 +315,176 @@ extern "C" int posu_affine2d_apply(const float* pts, const float* T, int N, int 
   hipLaunchKernelGGL(affine_kernel, dim3((N * J + 255) / 256), dim3(256), 0, as_stream(stream), pts, T, N, J,
                      transpose, out);
   return check_launch("posu_affine2d_apply");
+}
+
+// ------------------------------------------- pseudo-label RANSAC / reprojection
+// multiviews/triangulate.py:102-213 (ransac, reproject_poses) for V <= 4 views: one
+// thread per (group, joint).  The per-view camera is (M = K[R|t], intr) as for
+// posu_triangulate_dlt; find2d is pymvg's CameraModel.project_3d_to_pixel with the
+// OpenCV plumb-bob distortion of intr (zero coefficients = pinhole).
+namespace posu {
+namespace {
+
+constexpr int kPairViews = 4;
+
+__device__ __forceinline__ void project_px(const double* M, const double* c, const double* X, double& u, double& v) {
+  const double fx = c[0], fy = c[1], cx = c[2], cy = c[3];
+  const double k1 = c[4], k2 = c[5], p1 = c[6], p2 = c[7], k3 = c[8];
+  // [R|t] = K^-1 M (zero-skew K)
+  double P[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) P[r] = M[4 * r] * X[0] + M[4 * r + 1] * X[1] + M[4 * r + 2] * X[2] + M[4 * r + 3];
+  const double zc = P[2];
+  const double yc = (P[1] - cy * P[2]) / fy;
+  const double xc = (P[0] - cx * P[2]) / fx;
+  const double x = xc / zc, y = yc / zc;
+  const double r2 = x * x + y * y;
+  const double radial = 1.0 + ((k3 * r2 + k2) * r2 + k1) * r2;
+  const double xd = x * radial + 2.0 * p1 * x * y + p2 * (r2 + 2.0 * x * x);
+  const double yd = y * radial + p1 * (r2 + 2.0 * y * y) + 2.0 * p2 * x * y;
+  u = fx * xd + cx;
+  v = fy * yd + cy;
+}
+
+struct ViewPts {
+  double raw[kPairViews][2];  // predictions as given (reprojection errors are measured on these)
+  double und[kPairViews][2];  // undistorted (the DLT rows)
+  bool on[kPairViews];
+  int nvis;
+};
+
+__device__ __forceinline__ void load_views(const double* Mall, const double* intr, const double* xy,
+                                           const unsigned char* vis, int g, int k, int V, int J, int undistort,
+                                           ViewPts& p) {
+  p.nvis = 0;
+#pragma unroll
+  for (int v = 0; v < kPairViews; ++v) {
+    const size_t gv = static_cast<size_t>(g) * V + (v < V ? v : 0);
+    p.on[v] = v < V && (!vis || vis[gv * J + k]);
+    const double* q = xy + (gv * J + k) * 2;
+    p.raw[v][0] = v < V ? q[0] : 0.0;
+    p.raw[v][1] = v < V ? q[1] : 0.0;
+    double u = p.raw[v][0], w = p.raw[v][1];
+    if (p.on[v] && undistort) undistort_px(intr + gv * 9, u, w);
+    p.und[v][0] = u;
+    p.und[v][1] = w;
+    if (p.on[v]) ++p.nvis;
+  }
+}
+
+__global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ Mall, const double* __restrict__ intr,
+                                                    const double* __restrict__ xy, const unsigned char* __restrict__ vis,
+                                                    int G, int V, int J, int undistort, double thre, int min_inliers,
+                                                    unsigned char* __restrict__ res_vis) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= G * J) return;
+  const int g = t / J, k = t - g * J;
+  ViewPts p;
+  load_views(Mall, intr, xy, vis, g, k, V, J, undistort, p);
+  int best_mask = 0, best_n = 0;
+  double best_err = 10000.0;
+  if (p.nvis >= 2) {
+    // itertools.combinations over the visible views, in view order
+    for (int a = 0; a < kPairViews; ++a) {
+      if (!p.on[a]) continue;
+      for (int b = a + 1; b < kPairViews; ++b) {
+        if (!p.on[b]) continue;
+        double A[4][4];
+        const int pv[2] = {a, b};
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const double* M = Mall + (static_cast<size_t>(g) * V + pv[r]) * 12;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            A[2 * r][c] = p.und[pv[r]][0] * M[8 + c] - M[c];
+            A[2 * r + 1][c] = p.und[pv[r]][1] * M[8 + c] - M[4 + c];
+          }
+        }
+        double X[3];
+        dlt_point<4>(A, X);
+        int mask = 0, n = 0;
+        double err = 0.0;
+        for (int v = 0; v < V; ++v) {
+          const size_t gv = static_cast<size_t>(g) * V + v;
+          double u, w;
+          project_px(Mall + gv * 12, intr + gv * 9, X, u, w);
+          const double du = u - p.raw[v][0], dv = w - p.raw[v][1];
+          const double e = sqrt(du * du + dv * dv);
+          if (e < thre) {
+            mask |= 1 << v;
+            ++n;
+            err += e;
+          }
+        }
+        if (n < min_inliers) continue;
+        err /= n;
+        if (n > best_n || (n == best_n && err < best_err)) {
+          best_n = n;
+          best_mask = mask;
+          best_err = err;
+        }
+      }
+    }
+  }
+  for (int v = 0; v < V; ++v) res_vis[(static_cast<size_t>(g) * V + v) * J + k] = (best_mask >> v) & 1;
+}
+
+__global__ __launch_bounds__(64) void reproject_kernel(const double* __restrict__ Mall, const double* __restrict__ intr,
+                                                       const double* __restrict__ xy,
+                                                       const unsigned char* __restrict__ vis, int G, int V, int J,
+                                                       int undistort, double* __restrict__ proj,
+                                                       unsigned char* __restrict__ res_vis) {
+  const int t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= G * J) return;
+  const int g = t / J, k = t - g * J;
+  ViewPts p;
+  load_views(Mall, intr, xy, vis, g, k, V, J, undistort, p);
+  const bool ok = p.nvis >= 2;
+  double X[3] = {0.0, 0.0, 0.0};
+  if (ok) {
+    double A[2 * kPairViews][4];
+#pragma unroll
+    for (int v = 0; v < kPairViews; ++v) {
+      const double* M = Mall + (static_cast<size_t>(g) * V + (v < V ? v : 0)) * 12;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        A[2 * v][c] = p.on[v] ? p.und[v][0] * M[8 + c] - M[c] : 0.0;
+        A[2 * v + 1][c] = p.on[v] ? p.und[v][1] * M[8 + c] - M[4 + c] : 0.0;
+      }
+    }
+    dlt_point<2 * kPairViews>(A, X);
+  }
+  for (int v = 0; v < V; ++v) {
+    const size_t gv = static_cast<size_t>(g) * V + v;
+    double u = 0.0, w = 0.0;
+    if (ok) project_px(Mall + gv * 12, intr + gv * 9, X, u, w);
+    proj[(gv * J + k) * 2] = u;
+    proj[(gv * J + k) * 2 + 1] = w;
+    res_vis[gv * J + k] = ok ? 1 : 0;
+  }
+}
+
+}  // namespace
+}  // namespace posu
+
+extern "C" int posu_ransac_inliers(const double* M, const double* intr, const double* xy, const unsigned char* vis,
+                                   int G, int V, int J, int undistort, double reproj_thre, int min_inliers,
+                                   unsigned char* res_vis, void* stream) {
+  POSU_REQUIRE(M && intr && xy && res_vis, "posu_ransac_inliers: null pointer");
+  POSU_REQUIRE(G >= 0 && V >= 2 && V <= kPairViews && J > 0, "posu_ransac_inliers: bad shape (2 <= V <= 4)");
+  POSU_REQUIRE(min_inliers >= 1, "posu_ransac_inliers: min_inliers >= 1 (the reference divides by the inlier count)");
+  if (G == 0) return POSU_OK;
+  hipLaunchKernelGGL(ransac_kernel, dim3((G * J + 63) / 64), dim3(64), 0, as_stream(stream), M, intr, xy, vis, G, V,
+                     J, undistort, reproj_thre, min_inliers, res_vis);
+  return check_launch("posu_ransac_inliers");
+}
+
+extern "C" int posu_reproject(const double* M, const double* intr, const double* xy, const unsigned char* vis, int G,
+                              int V, int J, int undistort, double* proj, unsigned char* res_vis, void* stream) {
+  POSU_REQUIRE(M && intr && xy && proj && res_vis, "posu_reproject: null pointer");
+  POSU_REQUIRE(G >= 0 && V >= 2 && V <= kPairViews && J > 0, "posu_reproject: bad shape (2 <= V <= 4)");
+  if (G == 0) return POSU_OK;
+  hipLaunchKernelGGL(reproject_kernel, dim3((G * J + 63) / 64), dim3(64), 0, as_stream(stream), M, intr, xy, vis, G,
+                     V, J, undistort, proj, res_vis);
+  return check_launch("posu_reproject");
 }

@@ -24,6 +24,7 @@ _p = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
 _ll = ctypes.c_longlong
+_d = ctypes.c_double
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 _SIGNATURES = {
@@ -55,6 +56,8 @@ _SIGNATURES = {
     'posu_triangulate_dlt': [_p, _p, _p, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p],
     'posu_joints_mse_fwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
     'posu_joints_mse_bwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
+    'posu_ransac_inliers': [_p, _p, _p, _p, _i, _i, _i, _i, _d, _i, _p, _p],
+    'posu_reproject': [_p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p],
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],

@@ -366,3 +366,31 @@ def triangulate_dlt(M, intr, xy, vis=None, undistort=True, view_major=False):
     call('posu_triangulate_dlt', ptr(M), ptr(intr), ptr(xy), code, sg, sv, ptr(vis), g, v, j, int(bool(undistort)),
          ptr(X), stream_of(xy.device))
     return X
+
+
+def ransac_inliers(M, intr, xy, vis=None, reproj_thre=20.0, min_inliers=2, undistort=True):
+    """multiviews.triangulate.ransac on device: M [G, V, 3, 4] f64, intr [G, V, 9] f64,
+    xy [G, V, J, 2], vis [G, V, J] -> res_vis [G, V, J] uint8."""
+    require_cuda(M, intr, xy)
+    g, v, j, _ = xy.shape
+    xy = xy.to(torch.float64).contiguous()
+    if vis is not None:
+        vis = vis.to(device=xy.device, dtype=torch.uint8).contiguous()
+    out = torch.empty((g, v, j), dtype=torch.uint8, device=xy.device)
+    call('posu_ransac_inliers', ptr(M.contiguous()), ptr(intr.contiguous()), ptr(xy), ptr(vis), g, v, j,
+         int(bool(undistort)), float(reproj_thre), int(min_inliers), ptr(out), stream_of(xy.device))
+    return out
+
+
+def reproject(M, intr, xy, vis=None, undistort=True):
+    """multiviews.triangulate.reproject_poses on device -> (proj [G, V, J, 2] f64, res_vis [G, V, J] uint8)."""
+    require_cuda(M, intr, xy)
+    g, v, j, _ = xy.shape
+    xy = xy.to(torch.float64).contiguous()
+    if vis is not None:
+        vis = vis.to(device=xy.device, dtype=torch.uint8).contiguous()
+    proj = torch.empty((g, v, j, 2), dtype=torch.float64, device=xy.device)
+    res = torch.empty((g, v, j), dtype=torch.uint8, device=xy.device)
+    call('posu_reproject', ptr(M.contiguous()), ptr(intr.contiguous()), ptr(xy), ptr(vis), g, v, j,
+         int(bool(undistort)), ptr(proj), ptr(res), stream_of(xy.device))
+    return proj, res

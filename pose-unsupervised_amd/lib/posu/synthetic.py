@@ -39,6 +39,7 @@ def make_cfg(num_layers=50, image_size=256, num_joints=16, deconv_with_bias=Fals
         TEST=_ns(POST_PROCESS=post_process, FUSE_OUTPUT=False, FLIP_TEST=flip_test, SHIFT_HEATMAP=shift_heatmap),
         DATASET=_ns(ROOT=data_root, NO_DISTORTION=False),
         DEBUG=_ns(SAVE_ALL_PREDS=False),
+        PSEUDO_LABEL=_ns(NUM_INLIERS=4, REPROJ_THRE=10, IF_RANSAC=True, USE_REPROJ=False),
         PRINT_FREQ=100,
     )
 

@@ -370,3 +370,43 @@ def test_chained_next_conv1_matches_two_launches(cuda, code, tol, dual, cout2):
     cy_ref = ops.conv2d_nhwc(y_ref, cw, cout2, 1, 1, 1, 0, s1, b1, None, True, code)
     torch.testing.assert_close(y, y_ref, atol=0, rtol=0)        # same kernel math for the tail
     torch.testing.assert_close(cy.float(), cy_ref.float(), atol=tol, rtol=tol)
+
+
+@pytest.mark.parametrize('distortion', [False, True])
+def test_ransac_and_reprojection_match_oracle(cuda, distortion):
+    """Pseudo-label geometry (triangulate.py:102-213): inlier masks bit-exact and
+    re-projections to 1e-4 px against the numpy restatement, on noisy views with gross
+    outliers and partial visibility."""
+    from multiviews.triangulate import camera_tables
+    ng = 8
+    cams = syn.group_cameras(ng, distortion=distortion)
+    poses = syn.synthetic_poses3d(ng)
+    r = np.random.default_rng(17)
+    p2d = np.zeros((ng * 4, 16, 2))
+    for gi in range(ng):
+        for v in range(4):
+            M, K, D = G._camera(cams[gi * 4 + v], no_distortion=not distortion)
+            p2d[gi * 4 + v] = [G.find2d(M, K, D, X) for X in poses[gi]]
+    p2d += r.normal(0, 1.5, size=p2d.shape)
+    bad = r.uniform(size=p2d.shape[:2]) < 0.15
+    p2d[bad] += r.choice([-1, 1], size=(bad.sum(), 2)) * r.uniform(60, 120, size=(bad.sum(), 2))
+    vis = (r.uniform(size=p2d.shape[:2]) > 0.1).astype(np.int64)
+    ref_vis = G.ransac(p2d, cams, vis, reproj_thre=10, num_inliers=2, no_distortion=not distortion)
+    ref_proj, ref_rv = G.reproject_poses(p2d, cams, vis, no_distortion=not distortion)
+    M, intr = camera_tables(cams, 4, no_distortion=not distortion)
+    Md, Id = torch.from_numpy(M).to(cuda), torch.from_numpy(intr).to(cuda)
+    xy = torch.from_numpy(p2d.reshape(ng, 4, 16, 2)).to(cuda)
+    vd = torch.from_numpy(vis.reshape(ng, 4, 16)).to(cuda)
+    got = ops.ransac_inliers(Md, Id, xy, vd, 10.0, 2).cpu().numpy().reshape(ng * 4, 16)
+    np.testing.assert_array_equal(got, ref_vis)
+    proj, rv = ops.reproject(Md, Id, xy, vd)
+    np.testing.assert_array_equal(rv.cpu().numpy().reshape(ng * 4, 16), ref_rv)
+    np.testing.assert_allclose(proj.cpu().numpy().reshape(ng * 4, 16, 2), ref_proj, atol=1e-4, rtol=0)
+    # the drop-in functions (reference signatures) give the same answers
+    from multiviews.triangulate import ransac, reproject_poses
+    cfg = syn.make_cfg()
+    cfg.DATASET.NO_DISTORTION = not distortion
+    cfg.PSEUDO_LABEL.NUM_INLIERS, cfg.PSEUDO_LABEL.REPROJ_THRE = 2, 10
+    np.testing.assert_array_equal(ransac(p2d, cams, vis, cfg), ref_vis)
+    pr, rvis = reproject_poses(p2d, cams, vis, no_distortion=not distortion)
+    np.testing.assert_allclose(pr, ref_proj, atol=1e-4, rtol=0)

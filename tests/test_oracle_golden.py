@@ -121,3 +121,39 @@ def test_oracle_undistort_inverts_opencv_model():
         u = np.array([xd * K[0, 0] + K[0, 2], yd * K[1, 1] + K[1, 2]])
         und = G.undistort_point(u, K, D)
         np.testing.assert_allclose(und, [x * K[0, 0] + K[0, 2], y * K[1, 1] + K[1, 2]], atol=0.05)
+
+
+def test_find2d_restatement_is_the_pinhole_projection_of_the_reference(golden):
+    """No distortion: pymvg find2d (restated) == the reference's cameras.project_pose
+    (fx == fy, so its average-focal model coincides) -- the known-answer pin; the
+    distorted branch follows pymvg's OpenCV model (parity unpinned)."""
+    g = golden('cameras.npz')
+    cams = syn.group_cameras(g['poses3d'].shape[0], distortion=False)
+    for gi in range(g['poses3d'].shape[0]):
+        for v in range(4):
+            M, K, D = G._camera(cams[gi * 4 + v], no_distortion=True)
+            got = np.stack([G.find2d(M, K, D, X) for X in g['poses3d'][gi]])
+            np.testing.assert_allclose(got, g['proj_nodist'][gi * 4 + v], rtol=1e-10, atol=1e-8)
+
+
+def test_ransac_oracle_known_answers():
+    """Noise-free views are all inliers; a view moved by 80 px is rejected; a joint seen
+    by one view stays 0 (triangulate.py:134-136)."""
+    ng = 3
+    cams = syn.group_cameras(ng, distortion=False)
+    poses = syn.synthetic_poses3d(ng)
+    p2d = np.zeros((ng * 4, 16, 2))
+    for gi in range(ng):
+        for v in range(4):
+            M, K, D = G._camera(cams[gi * 4 + v], no_distortion=True)
+            p2d[gi * 4 + v] = [G.find2d(M, K, D, X) for X in poses[gi]]
+    vis = np.ones((ng * 4, 16), dtype=np.int64)
+    p2d[1 * 4 + 2, 5] += 80.0
+    vis[2 * 4 + 1:2 * 4 + 4, 7] = 0
+    res = G.ransac(p2d, cams, vis, reproj_thre=10, num_inliers=2, no_distortion=True)
+    assert res.sum() == ng * 4 * 16 - 1 - 4
+    assert res[1 * 4 + 2, 5] == 0 and res[1 * 4 + 0, 5] == 1
+    assert res[2 * 4:2 * 4 + 4, 7].sum() == 0
+    proj, rv = G.reproject_poses(p2d, cams, vis, no_distortion=True)
+    np.testing.assert_allclose(proj[0], p2d[0], atol=1e-6)
+    assert rv[2 * 4:2 * 4 + 4, 7].sum() == 0
