@@ -147,6 +147,17 @@ int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int H, int W, i
                                 const void* cw, int Cout2, const float* cscale,
                                 const float* cshift, void* cy, void* stream);
 
+/* Cross-view Aggregation (multiview_pose_resnet.py:16-58, ChannelWiseFC / Aggregation,
+ * NETWORK.AGGRE): the V(V-1) per-pair [HW x HW] matrices form one block matrix with
+ * zero diagonal blocks (scaled by 1/(V-1)), so all V aggregated views are ONE GEMM:
+ *   posu_pack_view_rows: x[m][o*HW + q] = src[o][m][q]   (src f32 [V][M][HW], M = N*J)
+ *   posu_gemm_rows_f32:  out[blk][m][j] = sum_k x[m][k] * wt[blk*vblk + j][k]  (f32,
+ *                        view-major output, vblk = HW; wt packed [round_up(Ncol,64)][K])
+ * K must be a power of two and a multiple of the K-tile. */
+int posu_pack_view_rows(int dtype, const float* src, int V, int M, int HW, void* dst, void* stream);
+int posu_gemm_rows_f32(int dtype, const void* x, int M, int K, const void* wt, int Ncol, int vblk,
+                       float* out, void* stream);
+
 /* The last deconv stage fused with the final 1x1 head: deconv + BN + ReLU as
  * posu_deconv4x4s2_fwd, then per output pixel hm[n][j][pix] = bias[j] +
  * sum_c hw[j][c] f[c] (lib/models/pose_resnet.py:202-203) from the tile still in LDS,

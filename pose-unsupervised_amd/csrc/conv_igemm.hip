@@ -59,7 +59,8 @@ struct ConvGeom {
                      //    (data gradient of a stride-2 convolution as a stride-1 one)
   int deconv;        // blockIdx.z = parity class
   int out_H, out_W;  // output tensor spatial dims
-  int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out
+  int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out, 2: f32 rows blocked by vblk columns
+  int vblk;          // mode 2: out[(co / vblk)][m][co % vblk] (view-major heatmaps of a GEMM)
   // fused 1x1 head (mode 0, BN == Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
   // chained 1x1 conv (mode 0, BN == Cout == 256): cy[m][co] = relu(cscale[co] *
   // sum_c cw[co][c] y[m][c] + cshift[co]) -- the next Bottleneck's conv1 on this tile
@@ -613,6 +614,19 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           }
         }
       }
+    } else if (g.mode == 2) {
+      // f32 GEMM rows, column blocks of vblk stored as separate [M][vblk] planes
+      float* __restrict__ yp = reinterpret_cast<float*>(g.y);
+      for (int idx = tid; idx < PR * CPR; idx += NT) {
+        const int row = idx / CPR, cc = idx - row * CPR;
+        const int m = m0 + p * PR + row, co = n0 + cc * E;
+        if (m >= g.M || co >= g.Cout) continue;
+        const int blk = co / g.vblk, cin = co - blk * g.vblk;
+        float* dst = yp + (static_cast<size_t>(blk) * g.M + m) * g.vblk + cin;
+#pragma unroll
+        for (int e = 0; e < E; e += 4)
+          *reinterpret_cast<float4*>(dst + e) = *reinterpret_cast<const float4*>(Cs + row * LD + cc * E + e);
+      }
     } else if (!g.hm) {
       // NCHW f32 (heatmap head): consecutive threads walk pixels of one channel
       float* __restrict__ yp = reinterpret_cast<float*>(g.y);
@@ -1087,4 +1101,29 @@ extern "C" int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int 
   g.out_W = W;
   if (int st = attach_chain(g, dtype, cw, Cout2, cscale, cshift, cy, "posu_conv1x1_dual_chain_fwd")) return st;
   return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_chain_fwd");
+}
+
+// Plain GEMM on the conv kernel (1x1 window over M "pixels" of K channels):
+//   out[blk][m][j] = sum_k x[m][k] * wt[blk * vblk + j][k]   (f32, blk = column / vblk)
+// x: [M][K] dtype, K % 64 == 0 and a power of two; wt: packed [round_up(Ncol, 64)][K]
+// dtype.  Used by the cross-view Aggregation (ChannelWiseFC, multiview_pose_resnet.py
+// :16-58): the V(V-1) per-pair [HW x HW] matrices are one block matrix, so all target
+// views come out of one launch, view-major.
+extern "C" int posu_gemm_rows_f32(int dtype, const void* x, int M, int K, const void* wt, int Ncol, int vblk,
+                                  float* out, void* stream) {
+  if (int st = common_checks(dtype, x, wt, out, M, 1, 1, K, Ncol, "posu_gemm_rows_f32")) return st;
+  POSU_REQUIRE(K % bk_of(dtype) == 0, "posu_gemm_rows_f32: K must be a multiple of the K-tile");
+  POSU_REQUIRE(vblk > 0 && vblk % 8 == 0 && Ncol % vblk == 0, "posu_gemm_rows_f32: vblk must divide Ncol (x8)");
+  ConvGeom g = base_geom(x, M, 1, 1, K, wt, Ncol, dtype);
+  g.y = out;
+  g.Ho = 1;
+  g.Wo = 1;
+  g.M = M;
+  g.K = K;
+  g.Kpad = K;
+  g.out_H = 1;
+  g.out_W = 1;
+  g.mode = 2;
+  g.vblk = vblk;
+  return dispatch<false>(dtype, g, 1, stream, "posu_gemm_rows_f32");
 }

@@ -63,6 +63,33 @@ __global__ __launch_bounds__(256) void pack_s2d_kernel(const float* __restrict__
   }
 }
 
+// rows of the cross-view aggregation GEMM: dst[m][o*HW + q] = src[o][m][q]
+// (src f32 view-major [V][M][HW], e.g. V views of [N, J, H, W] heatmaps with M = N*J)
+template <typename T>
+__global__ __launch_bounds__(256) void pack_view_rows_kernel(const float* __restrict__ src, int V, int M, int HW,
+                                                             T* __restrict__ dst) {
+  constexpr int E = Vec<T>::E;
+  const int cpv = HW / E;  // chunks per view
+  const long long total = static_cast<long long>(M) * V * cpv;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % cpv);
+    const long long r = i / cpv;
+    const int o = static_cast<int>(r % V);
+    const long long m = r / V;
+    const float* s = src + (static_cast<long long>(o) * M + m) * HW + ch * E;
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; e += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(s + e);
+      v[e] = t.x;
+      v[e + 1] = t.y;
+      v[e + 2] = t.z;
+      v[e + 3] = t.w;
+    }
+    *reinterpret_cast<uint4*>(dst + i * E) = Vec<T>::pack(v);
+  }
+}
+
 // one thread per (pixel, 16-B input chunk); writes E channel planes
 template <typename T>
 __global__ __launch_bounds__(256) void unpack_kernel(const T* __restrict__ x, int N, int H, int W, int C,
@@ -192,4 +219,19 @@ extern "C" int posu_maxpool3x3s2_fwd(int dtype, const void* x, int N, int H, int
   });
   POSU_REQUIRE(ok, "posu_maxpool3x3s2_fwd: unsupported dtype");
   return check_launch("posu_maxpool3x3s2_fwd");
+}
+
+extern "C" int posu_pack_view_rows(int dtype, const float* src, int V, int M, int HW, void* dst, void* stream) {
+  POSU_REQUIRE(src && dst, "posu_pack_view_rows: null pointer");
+  POSU_REQUIRE(V > 0 && M > 0 && HW > 0 && HW % chunk_elems(dtype) == 0 && HW % 4 == 0,
+               "posu_pack_view_rows: bad shape (HW a multiple of the 16-B chunk)");
+  hipStream_t s = as_stream(stream);
+  const long long total = static_cast<long long>(M) * V * (HW / chunk_elems(dtype));
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(pack_view_rows_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, src, V, M, HW,
+                       static_cast<T*>(dst));
+  });
+  POSU_REQUIRE(ok, "posu_pack_view_rows: unsupported dtype");
+  return check_launch("posu_pack_view_rows");
 }

@@ -29,19 +29,33 @@ from utils.transforms import flip_pair_order
 logger = logging.getLogger(__name__)
 
 
+def fuse_routing(raw_features, aggre_features, is_aggre, meta):
+    """function.py:33-45: per sample, 3/5 aggregated + 2/5 raw for H36M samples, raw
+    otherwise (one masked blend per view on the device)."""
+    if not is_aggre:
+        return raw_features
+    output = []
+    for r, a, m in zip(raw_features, aggre_features, meta):
+        h36m = torch.tensor([s == 'h36m' for s in m['source']], device=a.device).view(-1, 1, 1, 1)
+        output.append(torch.where(h36m, 3 / 5 * a + 2 / 5 * r, r))
+    return output
+
+
 def _run_model(model, views, hflip):
-    """model(views) -> per-view heatmap list; the flip test's mirrored input is packed
-    by the HIP input-pack kernel when the model is this build's (no extra copy)."""
+    """model(views) -> (per-view heatmaps, aggregated heatmaps or []); the flip test's
+    mirrored input is packed by the HIP input-pack kernel when the model is this build's."""
     base = getattr(model, 'module', model)          # DDP-wrapped or not
     resnet = getattr(base, 'resnet', None)
     if hflip and resnet is not None and hasattr(resnet, 'plan') and not resnet.training:
         plan = resnet.plan(views[0].device)
         hm, _, _ = plan.run(plan.pack_input(views, hflip=True), keep_features=False)
-        return list(torch.split(hm, views[0].shape[0], dim=0))
+        raw = list(torch.split(hm, views[0].shape[0], dim=0))
+        agg = base.aggre_layer(raw) if getattr(base, 'aggre_layer', None) is not None else []
+        return raw, agg
     if hflip:
         views = [torch.flip(v, dims=[3]) for v in views]
-    raw, _, _, _ = model(views)
-    return raw
+    raw, agg, _, _ = model(views)
+    return raw, agg
 
 
 def validate_batch(config, model, input, target=None, weight=None, meta=None, flip_pairs=None,
@@ -54,10 +68,13 @@ def validate_batch(config, model, input, target=None, weight=None, meta=None, fl
     ([V*N, J, h, w] numpy, same order), loss (float or None), acc / cnt (or None)."""
     device = input[0].device
     nviews = len(input)
+    fuse = bool(config.NETWORK.AGGRE) and bool(getattr(config.TEST, 'FUSE_OUTPUT', False))
     with torch.no_grad():
-        output = raw = _run_model(model, input, False)
+        raw, agg = _run_model(model, input, False)
+        output = fuse_routing(raw, agg, fuse, meta) if fuse else raw
         if config.TEST.FLIP_TEST:
-            flipped = _run_model(model, input, True)
+            raw_f, agg_f = _run_model(model, input, True)
+            flipped = fuse_routing(raw_f, agg_f, fuse, meta) if fuse else raw_f
             perm = torch.tensor(flip_pair_order(output[0].shape[1], flip_pairs or []), dtype=torch.int32,
                                 device=device)
             output = [ops.flip_back(f, perm, hm=o, shift=bool(config.TEST.SHIFT_HEATMAP))

@@ -9,11 +9,50 @@ segment (own batch statistics, own running-stat update in view order), which equ
 the reference's V backbone calls.  A single tensor input behaves like
 ``PoseResNet.forward``.
 
-The cross-view ``Aggregation`` fusion (AGGRE: true, 12 dense HW x HW maps) is not on
-this round's path: constructing it raises, rather than running a non-HIP fallback.
+``Aggregation`` (AGGRE: true) keeps the reference's parameters -- V(V-1) = 12
+``ChannelWiseFC`` [HW, HW] matrices in ``aggre`` (state_dict keys ``aggre.<i>.weight``)
+-- and runs all of them as ONE block-matrix MFMA GEMM (posu.aggregate), differentiable.
 """
 import torch
 import torch.nn as nn
+
+from posu import ops
+from posu.aggregate import aggregate
+
+
+class ChannelWiseFC(nn.Module):
+    """multiview_pose_resnet.py:16-29: out[n, c] = in[n, c].flatten() @ weight."""
+
+    def __init__(self, size):
+        super(ChannelWiseFC, self).__init__()
+        self.weight = nn.Parameter(torch.Tensor(size, size))
+        self.weight.data.uniform_(0, 0.1)
+
+    def forward(self, input):
+        raise NotImplementedError('ChannelWiseFC runs inside Aggregation (one fused GEMM for all view pairs)')
+
+
+class Aggregation(nn.Module):
+    """multiview_pose_resnet.py:32-58: warped_i = sum_{o != i} fc_(i,o)(x_o) / (V - 1)."""
+
+    def __init__(self, cfg, weights=[0.4, 0.2, 0.2, 0.2], precision='bf16'):
+        super(Aggregation, self).__init__()
+        NUM_NETS = 12
+        size = int(cfg.NETWORK.HEATMAP_SIZE[0])
+        self.weights = weights
+        self.precision = precision
+        self.aggre = nn.ModuleList()
+        for i in range(NUM_NETS):
+            self.aggre.append(ChannelWiseFC(size * size))
+
+    def forward(self, inputs):
+        for t in inputs:
+            if not t.is_cuda:
+                raise RuntimeError('Aggregation runs on the MI355X HIP path only: inputs must be cuda tensors')
+        nviews = len(inputs)
+        if nviews * (nviews - 1) != len(self.aggre):
+            raise ValueError('Aggregation built for %d view pairs, got %d views' % (len(self.aggre), nviews))
+        return aggregate(inputs, [fc.weight for fc in self.aggre], ops.dtype_code(self.precision))
 
 
 class MultiViewPose(nn.Module):
@@ -42,7 +81,5 @@ class MultiViewPose(nn.Module):
 
 
 def get_multiview_pose_net(PoseResNet, CFG):
-    if CFG.NETWORK.AGGRE:
-        raise NotImplementedError(
-            'pose-unsupervised_amd: NETWORK.AGGRE (ChannelWiseFC aggregation) is not on this build\'s HIP path yet')
-    return MultiViewPose(PoseResNet, None, CFG)
+    Aggre = Aggregation(CFG, precision=getattr(PoseResNet, 'precision', 'bf16')) if CFG.NETWORK.AGGRE else None
+    return MultiViewPose(PoseResNet, Aggre, CFG)

@@ -58,6 +58,8 @@ _SIGNATURES = {
     'posu_joints_mse_bwd': [_p, _p, _p, _i, _i, _i, _p, _p, _p],
     'posu_ransac_inliers': [_p, _p, _p, _p, _i, _i, _i, _i, _d, _i, _p, _p],
     'posu_reproject': [_p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p],
+    'posu_pack_view_rows': [_i, _p, _i, _i, _i, _p, _p],
+    'posu_gemm_rows_f32': [_i, _p, _i, _i, _p, _i, _i, _p, _p],
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
