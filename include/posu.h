@@ -243,6 +243,19 @@ int posu_joints_mse_bwd(const float* pred, const float* gt, const float* w, int 
 int posu_flip_back(const float* hm_flipped, const int* perm, const float* hm, int N, int J,
                    int H, int W, int shift, float* out, void* stream);
 
+/* ------------------------------------------------------------ data path */
+/* Gaussian target heatmaps of a batch (JointsDatasetCompatible.generate_heatmap,
+ * lib/dataset/joints_dataset_compatible.py:215-253): joints [N, J, 2] f32 in crop px,
+ * vis [N, J] f32 (joints_vis[:, 0]); target [N, J, hm_h, hm_w] f32, weight [N, J] f32;
+ * zero_weight: NULL or [N] uint8 (1 = weights zeroed: H36M samples without pseudo labels). */
+int posu_gaussian_targets(const float* joints, const float* vis, int N, int J, int image_w,
+                          int image_h, int hm_w, int hm_h, double sigma,
+                          const unsigned char* zero_weight, float* target, float* weight,
+                          void* stream);
+/* Sum-normalised integral coordinates (run/test/test_integral.py:63-70):
+ * out[n][j] = (sum x h, sum y h) / sum h  over hm [N, J, H, W] f32 -> [N, J, 2] f32. */
+int posu_integral2d_fwd(const float* hm, int N, int J, int H, int W, float* out, void* stream);
+
 /* ------------------------------------------------------------- geometry */
 /* Epipolar consistency loss (FundamentalLoss.__call__, lib/core/loss.py:101-133):
  *   loss = sum_{b, (i,j) in permutations(V,2), k} |x~_j^T F_{s(b),i,j} x~_i| * w_i w_j

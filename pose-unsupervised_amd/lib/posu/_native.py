@@ -60,6 +60,8 @@ _SIGNATURES = {
     'posu_reproject': [_p, _p, _p, _p, _i, _i, _i, _i, _p, _p, _p],
     'posu_pack_view_rows': [_i, _p, _i, _i, _i, _p, _p],
     'posu_gemm_rows_f32': [_i, _p, _i, _i, _p, _i, _i, _p, _p],
+    'posu_gaussian_targets': [_p, _p, _i, _i, _i, _i, _i, _i, _d, _p, _p, _p, _p],
+    'posu_integral2d_fwd': [_p, _i, _i, _i, _i, _p, _p],
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
