@@ -94,6 +94,13 @@ int posu_set_conv_stages(int stages);
 /* Tuning knob: allow the eight-wave 256x256 / 256x128 tiles for layers with
  * Cout >= 128 (1, default) or restrict to the four-wave tiles (0). */
 int posu_set_conv_tiles(int big);
+/* Diagnostics: when buf (device, int64[4 * blocks]) is non-null, every conv launch's
+ * blocks record s_memtime at start, at the end of the main loop and at exit, and their
+ * HW_ID register; null (default) turns the stamps off. */
+int posu_debug_conv_stamps(void* buf);
+/* Tuning knob: NHWC conv outputs (no chained conv / fused head) are stored straight from
+ * the MFMA accumulators (1, default) or staged through LDS as 16-B rows (0). */
+int posu_set_conv_epilogue(int direct);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K

@@ -74,6 +74,8 @@ struct ConvGeom {
   float* hm;
   int J, hkp;
   int mtiles, ntiles;
+  int direct;        // mode 0 without chain/head: store straight from the accumulators
+  long long* stamps;  // diagnostics: per block s_memtime at start / main-loop end / exit (or null)
 };
 
 template <typename T>
@@ -198,7 +200,7 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL>
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int NT = NW * 64;
@@ -225,6 +227,11 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid % WGN;
   const int r16 = lane & 15, q = lane >> 4;
+  // tile row of the wave's m-tile i / tile column of its n-tile j.  Phased loop (PH):
+  // m-tiles 0-3 of every wave lie in tile rows 0-127 and 4-7 in 128-255 (n-tiles 0-1 in
+  // columns 0-127, 2-3 in 128-255), so each LDS half-tile feeds one quadrant phase.
+  auto rowA = [&](int i) { return PH ? (i >> 2) * 128 + wm * 64 + (i & 3) * 16 : wm * WTM + i * 16; };
+  auto colB = [&](int j) { return PH ? (j >> 1) * 128 + wn * 32 + (j & 1) * 16 : wn * WTN + j * 16; };
 
   // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a
   // contiguous run of tiles so neighbouring tiles (same A rows) share its L2.
@@ -428,12 +435,122 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const long long t_start = g.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
   // S-slot ring, DMA running S-1 K-tiles ahead; per K-tile one counted vmcnt (the
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
   // overwrites, which every wave finished reading in the previous iteration)
-  if constexpr (S == 1) {
+  if constexpr (PH) {
+    // Phased 256x256 loop: each K-tile is four phases, one output quadrant
+    // (64 rows x 32 columns of the wave's tile, 16 MFMAs) per phase, each phase staging
+    // one half-tile of the NEXT K-tile (2 LDS-DMAs per thread) beside its fragment reads
+    // and MFMAs; counted vmcnt(4) keeps two half-tiles in flight across the barriers.
+    //   phase  quadrant  reads (LDS->VGPR)     stages (K-tile t+1)   waits for
+    //   1      (0,0)     A rows 0-127, B 0-127  A rows 0-127          B 128-255 (t)
+    //   2      (0,1)     B 128-255              B 0-127               A 128-255 (t)
+    //   3      (1,1)     A rows 128-255         B 128-255             -
+    //   4      (1,0)     -                      A rows 128-255        A, B 0-127 (t+1)
+    // A slot is restaged four phases after its last read (WAR-safe with one barrier
+    // per phase); a DMA is read only after its issuing waves' vmcnt and a barrier.
+    static_assert(BM == 256 && BN == 256 && NW == 8 && WGM == 2 && S == 2 && RA == 4 && RB == 4,
+                  "phased loop: 256x256 tile, 8 waves, 2 slots");
+    auto stage_a = [&](int kt, int buf, auto i0c) {
+      constexpr int I0 = decltype(i0c)::value;
+      const int kbase = kt * BK;
+      const unsigned As_ = lds0 + buf * STAGE + wid_u * 1024;
+      if constexpr (DUAL) {
+        const bool first = kbase < g.K1;
+#pragma unroll
+        for (int i = I0; i < I0 + 2; ++i) {
+          const int o = first ? o1[i] : o2[i];
+          const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
+          dma16(first ? xrs : x2rs, off, As_ + i * NW * 1024);
+        }
+      } else {  // fast gather only (one tap per K-tile)
+        const int tap = kbase >> g.logC;
+        const int th = tap / g.KW, tw = tap - th * g.KW;
+        const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));
+#pragma unroll
+        for (int i = I0; i < I0 + 2; ++i) {
+          const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
+                          static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
+          dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * NW * 1024);
+        }
+      }
+    };
+    auto stage_b = [&](int kt, int buf, auto i0c) {
+      constexpr int I0 = decltype(i0c)::value;
+      const unsigned Bs_ = lds0 + buf * STAGE + A_BYTES + wid_u * 1024;
+#pragma unroll
+      for (int i = I0; i < I0 + 2; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kt * BK) * ES, Bs_ + i * NW * 1024);
+    };
+    using I0_ = std::integral_constant<int, 0>;
+    using I2_ = std::integral_constant<int, 2>;
+    uint4 af[4][2], bq0[2][2], bq1[2][2];
+    auto read_a = [&](const char* As_, int mi) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+          af[ii][cb] = *reinterpret_cast<const uint4*>(As_ + swz(rowA(mi * 4 + ii) + r16, 4 * cb + q));
+    };
+    auto read_b = [&](const char* Bs_, int ni, uint4 (&bq)[2][2]) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+          bq[jj][cb] = *reinterpret_cast<const uint4*>(Bs_ + swz(colB(ni * 2 + jj) + r16, 4 * cb + q));
+    };
+    auto mma_q = [&](int mi, int ni, uint4 (&bq)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj) O::mma(acc[mi * 4 + ii][ni * 2 + jj], bq[jj][cb], af[ii][cb]);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    auto barrier = [] {
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    stage_a(0, 0, I0_{});
+    stage_b(0, 0, I0_{});
+    stage_b(0, 0, I2_{});
+    stage_a(0, 0, I2_{});
+    vm_wait<4>();
+    barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1, nxt = cur ^ 1;
+      const bool more = kt + 1 < nk;
+      const char* As_ = smem + cur * STAGE;
+      const char* Bs_ = As_ + A_BYTES;
+      read_a(As_, 0);
+      read_b(Bs_, 0, bq0);
+      if (more) stage_a(kt + 1, nxt, I0_{});
+      mma_q(0, 0, bq0);
+      if (more) vm_wait<4>();
+      else vm_wait<2>();
+      barrier();
+      read_b(Bs_, 1, bq1);
+      if (more) stage_b(kt + 1, nxt, I0_{});
+      mma_q(0, 1, bq1);
+      if (more) vm_wait<4>();
+      else vm_wait<0>();
+      barrier();
+      read_a(As_, 1);
+      if (more) stage_b(kt + 1, nxt, I2_{});
+      mma_q(1, 1, bq1);
+      barrier();
+      if (more) stage_a(kt + 1, nxt, I2_{});
+      mma_q(1, 0, bq0);
+      if (more) vm_wait<4>();
+      barrier();
+    }
+  } else if constexpr (S == 1) {
     // single slot (short-K layers): a quarter of the LDS of a 2-slot ring, so more
     // blocks share a CU and one block's epilogue overlaps another's operand fetch
     for (int kt = 0; kt < nk; ++kt) {
@@ -459,7 +576,120 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   }
 #undef POSU_DMA_TILE
 #undef POSU_COMPUTE
+  const long long t_loop = g.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
+  // ---- direct epilogue (NHWC outputs without a chained conv): each lane stores its 4
+  // consecutive channels of one pixel straight from the accumulators (BN, residual,
+  // ReLU applied in registers) -- no LDS round trip, no barriers
+  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && !g.hm && !g.cy) {
+    // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
+    // holds 8 consecutive channels (16-B stores, half the store instructions):
+    // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
+    T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+    const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+    constexpr int TP = TN / 2;
+    int cop[TP];
+    float sc[TP][8], sh[TP][8];
+#pragma unroll
+    for (int jp = 0; jp < TP; ++jp) {
+      cop[jp] = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = cop[jp] + e;
+        sc[jp][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
+        sh[jp][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + rowA(i) + r16;
+      const bool mok = m < g.M;
+      const int mm = mok ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
+      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      const size_t pix =
+          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      uint4 rv[TP];
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        rv[jp] = make_uint4(0, 0, 0, 0);
+        if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
+      }
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        float v[8], r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        O::load_vals(rv[jp], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = v[e] * sc[jp][e] + sh[jp][e];
+          if (rp) v[e] += r[e];
+          if (g.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
+      }
+    }
+  } else if (g.direct && g.mode == 0 && !g.hm && !g.cy) {
+    T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+    const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+    float sc[TN][4], sh[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = n0 + colB(j) + q * 4 + e;
+        sc[j][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
+        sh[j][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+      }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + rowA(i) + r16;
+      const bool mok = m < g.M;
+      const int mm = mok ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
+      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      const size_t pix =
+          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      uint4 rv[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = n0 + colB(j) + q * 4;
+        rv[j] = make_uint4(0, 0, 0, 0);
+        if (rp && mok && co < g.Cout) {
+          if constexpr (E == 4) {
+            rv[j] = *reinterpret_cast<const uint4*>(rp + pix + co);
+          } else {
+            const uint2 r2 = *reinterpret_cast<const uint2*>(rp + pix + co);
+            rv[j] = make_uint4(r2.x, r2.y, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int co = n0 + colB(j) + q * 4;
+        if (!mok || co >= g.Cout) continue;
+        float r[E], v[E];
+        O::load_vals(rv[j], r);
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = acc[i][j][e] * sc[j][e] + sh[j][e];
+          if (rp) v[e] += r[e];
+          if (g.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        const uint4 pk = O::store_vals(v);
+        if constexpr (E == 4) *reinterpret_cast<uint4*>(yp + pix + co) = pk;
+        else *reinterpret_cast<uint2*>(yp + pix + co) = make_uint2(pk.x, pk.y);
+      }
+    }
+  } else {
   // ---- epilogue through LDS, PR rows per pass: the accumulators (BN applied) are
   // staged as an f32 [pixel][channel] tile, then written as whole 16-B NHWC chunks
   // with residual add + ReLU (mode 0), as NCHW f32 planes (mode 1), or fed to the
@@ -476,7 +706,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int co = n0 + wn * WTN + j * 16 + q * 4 + e;
+      const int co = n0 + colB(j) + q * 4 + e;
       sc[j][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
       sh[j][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
     }
@@ -506,11 +736,11 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     __syncthreads();  // the ring (or the previous pass) is no longer read
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const int row = wm * WTM + i * 16 + r16 - p * PR;
-      if ((wm * WTM + i * 16) / PR != p) continue;  // wave-uniform
+      const int row = rowA(i) + r16 - p * PR;
+      if (rowA(i) / PR != p) continue;  // wave-uniform
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
-        const int colb = wn * WTN + j * 16 + q * 4;
+        const int colb = colB(j) + q * 4;
         float v[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -707,6 +937,14 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       }
     }
   }
+  }  // LDS epilogue
+  if (g.stamps && tid == 0) {
+    long long* st = g.stamps + 4 * static_cast<size_t>(blockIdx.x);
+    st[0] = t_start;
+    st[1] = t_loop;
+    st[2] = __builtin_amdgcn_s_memtime();
+    st[3] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID (wave, SIMD, CU, SE)
+  }
 }
 
 template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
@@ -726,12 +964,21 @@ void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
   hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 2, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
 }
 
+template <typename T>
+constexpr int bk_of_t() {
+  return 128 / static_cast<int>(sizeof(T));
+}
+
 int g_stages = 2;   // ring depth (posu_set_conv_stages)
 int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (posu_set_conv_tiles)
 int g_force = -1;   // forced tile configuration (tests), -1 = automatic
+long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
+int g_direct = 1;               // register-direct epilogue where admissible (posu_set_conv_epilogue)
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
+  g.stamps = g_stamps;
+  g.direct = g_direct;
   if (g.hm || g.cy) {  // fused head / chained conv: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
@@ -757,6 +1004,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   // variant 1 = single-slot ring (four-wave tiles), 2 = three-slot ring (where it fits)
   const int want = tile >= 0 ? tile : g_force;
   int st = g_stages;
+  bool ph = false;
   if (want >= 0) {
     const int c = want & 7;
     const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
@@ -764,6 +1012,8 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       cfg = c;
       const int v = want >> 3;
       st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
+      // variant 3: phased 256x256 loop (one-tap-per-K-tile gathers and two-source tails)
+      ph = v == 3 && c == 5 && (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0));
     }
   }
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
@@ -777,7 +1027,10 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     case 2: launch_cfg<T, 64, 64, 4, 2, DUAL>(g, nb, st, s); break;
     case 3: launch_cfg<T, 128, 128, 4, 2, DUAL>(g, nb, st, s); break;
     case 4: launch_cfg<T, 64, 128, 4, 2, DUAL>(g, nb, st, s); break;
-    case 5: launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s); break;
+    case 5:
+      if (ph) hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
+      else launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s);
+      break;
     default: launch_cfg<T, 256, 128, 8, 4, DUAL>(g, nb, st == 3 ? 3 : 2, s); break;
   }
   return check_launch(what);
@@ -833,8 +1086,18 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 24 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 32 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_epilogue(int direct) {
+  g_direct = direct ? 1 : 0;
+  return POSU_OK;
+}
+
+extern "C" int posu_debug_conv_stamps(void* buf) {
+  g_stamps = static_cast<long long*>(buf);
   return POSU_OK;
 }
 
@@ -853,7 +1116,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -885,7 +1148,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -917,7 +1180,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 24 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

@@ -46,6 +46,11 @@ def set_conv_stages(stages):
     call('posu_set_conv_stages', int(stages))
 
 
+def set_conv_epilogue(direct):
+    """NHWC conv epilogue: 1 = straight from the accumulators (default), 0 = through LDS."""
+    call('posu_set_conv_epilogue', int(bool(direct)))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""

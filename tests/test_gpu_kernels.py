@@ -308,7 +308,7 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 22])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 22, 29])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks and the
@@ -324,6 +324,71 @@ def test_every_tile_configuration_matches_torch(cuda, cfg, code):
                 assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
     finally:
         ops.force_conv_config(-1)
+
+
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 16, 29])
+@pytest.mark.parametrize('code', [F32, BF16, F16])
+def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
+    """The register-direct epilogue applies the same f32 arithmetic (BN, residual, ReLU,
+    one rounding) as the LDS-staged one: outputs equal bit for bit, for every tile shape,
+    ragged M and the deconv parity scatter."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    cout = 256
+    sc = torch.rand(cout, device=cuda, generator=g) + 0.5
+    sh = torch.randn(cout, device=cuda, generator=g) * 0.1
+    x = torch.randn(5, 19, 23, 128, device=cuda, generator=g).to(dt)
+    res = torch.randn(5, 19, 23, cout, device=cuda, generator=g).to(dt)
+    w3 = (torch.randn(cout, 9 * 128, device=cuda, generator=g) * 0.03).to(dt)
+    wdc = (torch.randn(4, cout, 4 * 128, device=cuda, generator=g) * 0.03).to(dt)
+    outs = {}
+    ops.force_conv_config(cfg)
+    try:
+        for direct in (0, 1):
+            ops.set_conv_epilogue(direct)
+            outs[direct] = [ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, res, True, code),
+                            ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, None, False, code),
+                            ops.deconv4x4s2_nhwc(x, wdc, cout, sc, sh, True, code)]
+        torch.cuda.synchronize()
+    finally:
+        ops.set_conv_epilogue(1)
+        ops.force_conv_config(-1)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize('code', [F32, BF16, F16])
+def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
+    """The phased 256x256 main loop (tile 29) keeps each accumulator's K order, so its
+    outputs equal the two-slot 256x256 loop (tile 5) bit for bit: 3x3 + residual (ragged
+    M), strided 1x1, ConvTranspose(4, s2) and the two-source Bottleneck tail."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    sc = torch.rand(256, device=cuda, generator=g) + 0.5
+    sh = torch.randn(256, device=cuda, generator=g) * 0.1
+    bk = ops.conv_bk(code)
+
+    def rnd(*shape):
+        return torch.randn(*shape, device=cuda, generator=g).to(dt)
+
+    x = rnd(9, 33, 31, 128)
+    res = rnd(9, 33, 31, 256)
+    w3 = (rnd(256, 9 * 128).float() * 0.03).to(dt)
+    x2 = rnd(9, 66, 62, 64)
+    wd = (rnd(256, 128 + 64).float() * 0.05).to(dt)
+    wdc = (rnd(4, 256, 4 * 128).float() * 0.03).to(dt)
+    assert (9 * 128) % bk == 0
+    outs = {}
+    for t in (5, 29):
+        outs[t] = [
+            ops.conv2d_nhwc(x, w3, 256, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
+            ops.conv2d_nhwc(x, w3[:, :128].contiguous(), 256, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
+            ops.deconv4x4s2_nhwc(x, wdc, 256, sc, sh, True, code, tile=t),
+            ops.conv1x1_dual_nhwc(x, x2, 2, wd, 256, sh, True, code, tile=t),
+        ]
+    torch.cuda.synchronize()
+    for a, b in zip(outs[5], outs[29]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, None)])
