@@ -99,8 +99,13 @@ int posu_set_conv_tiles(int big);
  * HW_ID register; null (default) turns the stamps off. */
 int posu_debug_conv_stamps(void* buf);
 /* Tuning knob: NHWC conv outputs (no chained conv / fused head) are stored straight from
- * the MFMA accumulators (1, default) or staged through LDS as 16-B rows (0). */
+ * the MFMA accumulators (1, default), the same with non-temporal stores (2: faster for the
+ * layer alone, slower end to end because the next layer then reads from beyond L2), or
+ * staged through LDS as 16-B rows (0). */
 int posu_set_conv_epilogue(int direct);
+/* Tuning knob: with epilogue mode 2, outputs smaller than `bytes` keep plain stores (they
+ * can stay in L2 for the next layer). Default 0. */
+int posu_set_conv_nt_threshold(long long bytes);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K

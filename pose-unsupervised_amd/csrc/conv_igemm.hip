@@ -632,7 +632,15 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (rp) v[e] += r[e];
           if (g.relu) v[e] = fmaxf(v[e], 0.f);
         }
-        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
+        if (mok && cop[jp] < g.Cout) {
+          const uint4 pk = O::store_vals(v);
+          if (g.direct == 2) {  // streaming store: do not keep the output lines in L2
+            const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
+            __builtin_nontemporal_store(pv, reinterpret_cast<u32x4*>(yp + pix + cop[jp]));
+          } else {
+            *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
+          }
+        }
       }
     }
   } else if (g.direct && g.mode == 0 && !g.hm && !g.cy) {
@@ -685,8 +693,16 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (g.relu) v[e] = fmaxf(v[e], 0.f);
         }
         const uint4 pk = O::store_vals(v);
-        if constexpr (E == 4) *reinterpret_cast<uint4*>(yp + pix + co) = pk;
-        else *reinterpret_cast<uint2*>(yp + pix + co) = make_uint2(pk.x, pk.y);
+        if constexpr (E == 4) {
+          if (g.direct == 2) {
+            const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
+            __builtin_nontemporal_store(pv, reinterpret_cast<u32x4*>(yp + pix + co));
+          } else {
+            *reinterpret_cast<uint4*>(yp + pix + co) = pk;
+          }
+        } else {
+          *reinterpret_cast<uint2*>(yp + pix + co) = make_uint2(pk.x, pk.y);
+        }
       }
     }
   } else {
@@ -973,12 +989,16 @@ int g_stages = 2;   // ring depth (posu_set_conv_stages)
 int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (posu_set_conv_tiles)
 int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
-int g_direct = 1;               // register-direct epilogue where admissible (posu_set_conv_epilogue)
+int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
+long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.stamps = g_stamps;
   g.direct = g_direct;
+  if (g.direct == 2 &&  // streaming stores only for outputs that would not stay in L2 anyway
+      static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * static_cast<int>(sizeof(T)) < g_nt_min_bytes)
+    g.direct = 1;
   if (g.hm || g.cy) {  // fused head / chained conv: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
@@ -1092,7 +1112,12 @@ extern "C" int posu_force_conv_config(int cfg) {
 }
 
 extern "C" int posu_set_conv_epilogue(int direct) {
-  g_direct = direct ? 1 : 0;
+  g_direct = direct < 0 ? 0 : direct > 2 ? 2 : direct;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_nt_threshold(long long bytes) {
+  g_nt_min_bytes = bytes;
   return POSU_OK;
 }
 

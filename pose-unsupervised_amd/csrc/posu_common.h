@@ -58,6 +58,14 @@ __device__ __forceinline__ float wave_max(float v) {
 
 inline int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
+// 16-byte streaming (non-temporal) store: activations written once and read by the
+// next layer from beyond L2 anyway, so their lines should not evict operands from L2
+__device__ __forceinline__ void st16_nt(void* p, const uint4& v) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  const u4 w = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(w, reinterpret_cast<u4*>(p));
+}
+
 // log2 of a power of two, -1 otherwise
 inline int ilog2(int v) {
   int l = 0;

@@ -47,8 +47,14 @@ def set_conv_stages(stages):
 
 
 def set_conv_epilogue(direct):
-    """NHWC conv epilogue: 1 = straight from the accumulators (default), 0 = through LDS."""
-    call('posu_set_conv_epilogue', int(bool(direct)))
+    """NHWC conv epilogue: 1 = straight from the accumulators (default), 2 = the same with
+    non-temporal (streaming) stores, 0 = through LDS."""
+    call('posu_set_conv_epilogue', int(direct))
+
+
+def set_conv_nt_threshold(nbytes):
+    """Outputs below nbytes keep plain (L2-allocating) stores under epilogue mode 2."""
+    call('posu_set_conv_nt_threshold', int(nbytes))
 
 
 # ---------------------------------------------------------------- layout ops

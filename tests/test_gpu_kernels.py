@@ -344,7 +344,7 @@ def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
     outs = {}
     ops.force_conv_config(cfg)
     try:
-        for direct in (0, 1):
+        for direct in (0, 1, 2):
             ops.set_conv_epilogue(direct)
             outs[direct] = [ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, res, True, code),
                             ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, None, False, code),
@@ -353,8 +353,8 @@ def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
     finally:
         ops.set_conv_epilogue(1)
         ops.force_conv_config(-1)
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for a, b, c in zip(outs[0], outs[1], outs[2]):
+        assert torch.equal(a, b) and torch.equal(a, c)
 
 
 @pytest.mark.parametrize('code', [F32, BF16, F16])
