@@ -106,6 +106,9 @@ int posu_set_conv_epilogue(int direct);
 /* Tuning knob: with epilogue mode 2, outputs smaller than `bytes` keep plain stores (they
  * can stay in L2 for the next layer). Default 0. */
 int posu_set_conv_nt_threshold(long long bytes);
+/* Tuning knob: residual-add launches with at most `max_ktiles` K-tiles load their residual
+ * before the operand fetch (small tiles, direct epilogue); 0 disables. Default 8. */
+int posu_set_conv_early_residual(int max_ktiles);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K

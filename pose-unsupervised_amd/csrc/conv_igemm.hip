@@ -74,6 +74,7 @@ struct ConvGeom {
   float* hm;
   int J, hkp;
   int mtiles, ntiles;
+  int early_nk;      // early residual prefetch for launches of at most this many K-tiles
   int direct;        // mode 0 without chain/head: store straight from the accumulators
   long long* stamps;  // diagnostics: per block s_memtime at start / main-loop end / exit (or null)
 };
@@ -437,6 +438,38 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const long long t_start = g.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
+  // Early residual prefetch (short-K Bottleneck tails): the residual chunks, in the direct
+  // epilogue's lane layout, are loaded before the first operand DMA, so their HBM latency
+  // overlaps the operand fetch instead of following the main loop.
+  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16 && !PH;
+  constexpr int ETM = EARLY ? TM : 1, ETP = EARLY ? TN / 2 : 1;
+  const bool early = EARLY && g.res && g.direct && g.mode == 0 && !g.hm && !g.cy && nk <= g.early_nk;
+  uint4 rve[ETM][ETP];
+  auto out_pix = [&](int i, bool& mok) -> size_t {  // element offset of the pixel of row i
+    const int m = m0 + rowA(i) + r16;
+    mok = m < g.M;
+    const int mm = mok ? m : 0;
+    const int n = mm / HoWo, rem = mm - n * HoWo;
+    const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+    return (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+  };
+  if constexpr (EARLY) {
+    if (early) {
+      const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+#pragma unroll
+      for (int i = 0; i < ETM; ++i) {
+        bool mok;
+        const size_t pix = out_pix(i, mok);
+#pragma unroll
+        for (int jp = 0; jp < ETP; ++jp) {
+          const int co = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
+          rve[i][jp] = make_uint4(0, 0, 0, 0);
+          if (mok && co < g.Cout) rve[i][jp] = *reinterpret_cast<const uint4*>(rp + pix + co);
+        }
+      }
+    }
+  }
+
   // S-slot ring, DMA running S-1 K-tiles ahead; per K-tile one counted vmcnt (the
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
@@ -613,6 +646,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
       for (int jp = 0; jp < TP; ++jp) {
         rv[jp] = make_uint4(0, 0, 0, 0);
+        if constexpr (EARLY) {
+          if (early) {
+            rv[jp] = rve[i][jp];
+            continue;
+          }
+        }
         if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
       }
 #pragma unroll
@@ -990,11 +1029,13 @@ int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (p
 int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
 int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
+int g_early_nk = 8;             // posu_set_conv_early_residual
 long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.stamps = g_stamps;
+  g.early_nk = g_early_nk;
   g.direct = g_direct;
   if (g.direct == 2 &&  // streaming stores only for outputs that would not stay in L2 anyway
       static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * static_cast<int>(sizeof(T)) < g_nt_min_bytes)
@@ -1118,6 +1159,11 @@ extern "C" int posu_set_conv_epilogue(int direct) {
 
 extern "C" int posu_set_conv_nt_threshold(long long bytes) {
   g_nt_min_bytes = bytes;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_early_residual(int max_ktiles) {
+  g_early_nk = max_ktiles;
   return POSU_OK;
 }
 

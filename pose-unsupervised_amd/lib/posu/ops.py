@@ -57,6 +57,11 @@ def set_conv_nt_threshold(nbytes):
     call('posu_set_conv_nt_threshold', int(nbytes))
 
 
+def set_conv_early_residual(max_ktiles):
+    """Residual prefetch before the operand fetch for launches of <= max_ktiles K-tiles."""
+    call('posu_set_conv_early_residual', int(max_ktiles))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""

@@ -344,17 +344,19 @@ def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
     outs = {}
     ops.force_conv_config(cfg)
     try:
-        for direct in (0, 1, 2):
-            ops.set_conv_epilogue(direct)
+        for direct in (0, 1, 2, 3):
+            ops.set_conv_epilogue(min(direct, 2))
+            ops.set_conv_early_residual(0 if direct < 3 else 64)
             outs[direct] = [ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, res, True, code),
                             ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, None, False, code),
                             ops.deconv4x4s2_nhwc(x, wdc, cout, sc, sh, True, code)]
         torch.cuda.synchronize()
     finally:
         ops.set_conv_epilogue(1)
+        ops.set_conv_early_residual(8)
         ops.force_conv_config(-1)
-    for a, b, c in zip(outs[0], outs[1], outs[2]):
-        assert torch.equal(a, b) and torch.equal(a, c)
+    for a, b, c, d in zip(outs[0], outs[1], outs[2], outs[3]):
+        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
 
 
 @pytest.mark.parametrize('code', [F32, BF16, F16])

@@ -26,6 +26,7 @@ def apply(setting):
     ops.set_conv_nt_threshold(int(float(kv.get('nt', 0)) * 2 ** 20))
     ops.set_conv_stages(int(kv.get('stages', 2)))
     ops.set_conv_tiles(int(kv.get('big', 1)))
+    ops.set_conv_early_residual(int(kv.get('early', 8)))
 
 
 def main():
