@@ -109,10 +109,14 @@ int posu_set_conv_nt_threshold(long long bytes);
 /* Tuning knob: residual-add launches with at most `max_ktiles` K-tiles load their residual
  * before the operand fetch (small tiles, direct epilogue); 0 disables. Default 8. */
 int posu_set_conv_early_residual(int max_ktiles);
+/* Tuning knob: launches without an explicit tile run the persistent K-tile-stream
+ * variant (1) or one block per tile (0, default); explicit tiles select it with +32. */
+int posu_set_conv_persistent(int on);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K
- * layers); + 16: a three-slot ring (two K-tiles in flight; not 5)); -1 restores the
+ * layers); + 16: a three-slot ring (two K-tiles in flight; not 5); 29: the phased
+ * 256x256 loop; + 32 (bf16/f16): the persistent K-tile stream); -1 restores the
  * automatic choice. */
 int posu_force_conv_config(int cfg);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,

@@ -200,6 +200,77 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
+// s_waitcnt vmcnt(n) for a runtime (wave-uniform) n in 0..63
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+  switch (n) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<1>(); break;
+    case 2: vm_wait<2>(); break;
+    case 3: vm_wait<3>(); break;
+    case 4: vm_wait<4>(); break;
+    case 5: vm_wait<5>(); break;
+    case 6: vm_wait<6>(); break;
+    case 7: vm_wait<7>(); break;
+    case 8: vm_wait<8>(); break;
+    case 9: vm_wait<9>(); break;
+    case 10: vm_wait<10>(); break;
+    case 11: vm_wait<11>(); break;
+    case 12: vm_wait<12>(); break;
+    case 13: vm_wait<13>(); break;
+    case 14: vm_wait<14>(); break;
+    case 15: vm_wait<15>(); break;
+    case 16: vm_wait<16>(); break;
+    case 17: vm_wait<17>(); break;
+    case 18: vm_wait<18>(); break;
+    case 19: vm_wait<19>(); break;
+    case 20: vm_wait<20>(); break;
+    case 21: vm_wait<21>(); break;
+    case 22: vm_wait<22>(); break;
+    case 23: vm_wait<23>(); break;
+    case 24: vm_wait<24>(); break;
+    case 25: vm_wait<25>(); break;
+    case 26: vm_wait<26>(); break;
+    case 27: vm_wait<27>(); break;
+    case 28: vm_wait<28>(); break;
+    case 29: vm_wait<29>(); break;
+    case 30: vm_wait<30>(); break;
+    case 31: vm_wait<31>(); break;
+    case 32: vm_wait<32>(); break;
+    case 33: vm_wait<33>(); break;
+    case 34: vm_wait<34>(); break;
+    case 35: vm_wait<35>(); break;
+    case 36: vm_wait<36>(); break;
+    case 37: vm_wait<37>(); break;
+    case 38: vm_wait<38>(); break;
+    case 39: vm_wait<39>(); break;
+    case 40: vm_wait<40>(); break;
+    case 41: vm_wait<41>(); break;
+    case 42: vm_wait<42>(); break;
+    case 43: vm_wait<43>(); break;
+    case 44: vm_wait<44>(); break;
+    case 45: vm_wait<45>(); break;
+    case 46: vm_wait<46>(); break;
+    case 47: vm_wait<47>(); break;
+    case 48: vm_wait<48>(); break;
+    case 49: vm_wait<49>(); break;
+    case 50: vm_wait<50>(); break;
+    case 51: vm_wait<51>(); break;
+    case 52: vm_wait<52>(); break;
+    case 53: vm_wait<53>(); break;
+    case 54: vm_wait<54>(); break;
+    case 55: vm_wait<55>(); break;
+    case 56: vm_wait<56>(); break;
+    case 57: vm_wait<57>(); break;
+    case 58: vm_wait<58>(); break;
+    case 59: vm_wait<59>(); break;
+    case 60: vm_wait<60>(); break;
+    case 61: vm_wait<61>(); break;
+    case 62: vm_wait<62>(); break;
+    case 63: vm_wait<63>(); break;
+    default: vm_wait<0>(); break;
+  }
+}
+
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
 template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
@@ -1002,6 +1073,395 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   }
 }
 
+// ---------------------------------------------------------------------------------
+// Persistent variant (2-byte dtypes, direct NHWC epilogue).  The grid is the resident
+// block count; each block walks a run of tiles (every XCD owns a contiguous slice of the
+// tile order, so its concurrently running tiles still share operand rows in its L2) as ONE
+// flattened stream of K-tiles through an S-slot LDS-DMA ring: the DMA of the next tile's
+// first K-tiles is already in flight while the current tile's epilogue stores drain, and
+// the stores never block the stream -- every epilogue issues exactly NST buffer stores per
+// thread (out-of-range rows go to an offset past num_records), so each wait is a counted
+// vmcnt that retires the K-tile being consumed and nothing younger.
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL>
+__global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
+  using O = Op<T>;
+
+  constexpr int E = O::E;
+  constexpr int ES = static_cast<int>(sizeof(T));
+  constexpr int BK = 8 * E;
+  constexpr int WGN = NW / WGM;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int ROWS = NW * 8;
+  constexpr int RA = BM / ROWS, RB = BN / ROWS;
+  constexpr int ND = RA + RB;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int TP = TN / 2;
+  constexpr int NST = TM * TP;  // 16-B stores per thread per tile
+  constexpr bool PRELOAD = TM + TN <= 8;
+  static_assert(E == 8 && TN % 2 == 0, "persistent variant: 2-byte dtypes, paired n-tiles");
+  static_assert(S == 2 || S == 3, "2 or 3 ring slots");
+  static_assert(ND * (S - 2) + 2 * NST < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int HoWo = g.Ho * g.Wo;
+
+  // ---- this block's tiles: XCD xcd = blockIdx & 7 owns tiles [cstart, cstart + clen);
+  // its nslot blocks take them round robin
+  const int ntile = g.mtiles * g.ntiles * (g.deconv ? 4 : 1);
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, nslot = gridDim.x >> 3;
+  const int qq = ntile >> 3, rr = ntile & 7;
+  const int cstart = xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq;
+  const int clen = qq + (xcd < rr ? 1 : 0);
+  const int ntl = slot < clen ? (clen - slot + nslot - 1) / nslot : 0;
+  const int nk = g.Kpad / BK;
+  const int total = ntl * nk;
+  if (total == 0) return;
+
+  auto decode = [&](int k, int& mt, int& cls, int& nt) {
+    const int w = cstart + slot + k * nslot;
+    nt = w % g.ntiles;
+    const int rest = w / g.ntiles;
+    mt = g.deconv ? rest >> 2 : rest;
+    cls = g.deconv ? rest & 3 : 0;
+  };
+
+  const u32x4 xrs = make_srd(g.x, g.N * g.H * g.W * g.C * ES);
+  u32x4 x2rs = xrs;
+  if constexpr (DUAL) x2rs = make_srd(g.x2, g.N * g.H2 * g.W2 * g.C2 * ES);
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
+  const int cL = (tid & 7) ^ ((tid >> 4) & 7);
+  const bool tap_uniform = (g.C % BK) == 0;
+  const bool fast_gather = tap_uniform && g.up == 0;
+  const bool row_fast = !tap_uniform && g.KW * g.C == BK && g.up == 0;
+  const int kwl = (cL * E) >> g.logC, cil = (cL * E) & (g.C - 1);
+
+  // ---- load side: geometry of the tile whose K-tiles the DMA is fetching
+  int l_tile = -1;
+  u32x4 wrs = make_srd(g.w, 16);
+  int wbrow = 0;
+  int hb[RA], wb[RA], nb[RA], pbase[RA], rbase[RA], o1[RA], o2[RA];
+  bool wok[RA];
+  auto setup_load = [&](int k) {
+    int mt, cls, nt;
+    decode(k, mt, cls, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
+    int pad_h = g.pad_h, pad_w = g.pad_w;
+    const T* wp = reinterpret_cast<const T*>(g.w);
+    if (g.deconv) {
+      pad_h = 1 - (cls >> 1);
+      pad_w = 1 - (cls & 1);
+      wp += static_cast<size_t>(cls) * g.CoutPad * g.Kpad;
+    }
+    wrs = make_srd(wp, g.CoutPad * g.Kpad * ES);
+    wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;
+#pragma unroll
+    for (int i = 0; i < RA; ++i) {
+      const int m = m0 + (tid >> 3) + ROWS * i;
+      if (m < g.M) {
+        const int n = m / HoWo, rem = m - n * HoWo;
+        const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+        hb[i] = oy * g.stride - pad_h;
+        wb[i] = ox * g.stride - pad_w;
+        nb[i] = n * g.H * g.W * g.C;
+        if constexpr (DUAL) {
+          o1[i] = (m * g.C + cL * E) * ES;
+          o2[i] = (((n * g.H2 + oy * g.stride2) * g.W2 + ox * g.stride2) * g.C2 + cL * E) * ES;
+        }
+      } else {
+        hb[i] = -(1 << 28);
+        wb[i] = 0;
+        nb[i] = 0;
+        if constexpr (DUAL) {
+          o1[i] = kOOB;
+          o2[i] = kOOB;
+        }
+      }
+      wok[i] = static_cast<unsigned>(wb[i] + kwl) < static_cast<unsigned>(g.W);
+      rbase[i] = static_cast<int>(static_cast<unsigned>(nb[i]) +
+                                  (static_cast<unsigned>(hb[i]) * g.W + static_cast<unsigned>(wb[i] + kwl)) * g.C +
+                                  cil);
+      pbase[i] = static_cast<int>(static_cast<unsigned>(nb[i]) +
+                                  (static_cast<unsigned>(hb[i]) * g.W + static_cast<unsigned>(wb[i])) * g.C + cL * E);
+    }
+  };
+  // DMA of stream K-tile sq into ring slot sq % S: exactly ND dma16 per thread
+  auto dma_ktile = [&](int sq) {
+    const int k = sq / nk, kt = sq - k * nk;
+    if (k != l_tile) {
+      setup_load(k);
+      l_tile = k;
+    }
+    const int kbase = kt * BK;
+    const unsigned As_ = lds0 + (sq % S) * STAGE + wid_u * 1024;
+    const unsigned Bs_ = As_ + A_BYTES;
+    if constexpr (DUAL) {
+      const bool first = kbase < g.K1;
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const int o = first ? o1[i] : o2[i];
+        const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
+        dma16(first ? xrs : x2rs, off, As_ + i * NW * 1024);
+      }
+    } else if (fast_gather) {
+      const int tap = kbase >> g.logC;
+      const int th = tap / g.KW, tw = tap - th * g.KW;
+      const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
+                        static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
+        dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * NW * 1024);
+      }
+    } else if (row_fast) {
+      const int roff = kt * g.W * g.C;
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const bool ok = wok[i] && static_cast<unsigned>(hb[i] + kt) < static_cast<unsigned>(g.H);
+        dma16(xrs, ok ? (rbase[i] + roff) * ES : kOOB, As_ + i * NW * 1024);
+      }
+    } else {
+      int kh, kw, ci;
+      bool kvalid = true;
+      if (tap_uniform) {
+        const int tap = kbase >> g.logC;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+        ci = (kbase & (g.C - 1)) + cL * E;
+      } else {
+        const int kk = kbase + cL * E;
+        const int tap = kk >> g.logC;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+        ci = kk & (g.C - 1);
+        kvalid = kk < g.K;
+      }
+#pragma unroll
+      for (int i = 0; i < RA; ++i) {
+        const int hl = hb[i] + kh, wl = wb[i] + kw;
+        const int hi = hl >> g.up, wi = wl >> g.up;
+        const bool ok = kvalid && ((hl | wl) & g.up) == 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&
+                        static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);
+        dma16(xrs, ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB, As_ + i * NW * 1024);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs_ + i * NW * 1024);
+  };
+
+  f32x4 acc[TM][TN];
+  auto zero_acc = [&] {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto compute = [&](int slot_) {
+    const char* As_ = smem + slot_ * STAGE;
+    const char* Bs_ = As_ + A_BYTES;
+    if constexpr (PRELOAD) {
+      uint4 af[2][TM], bfr[2][TN];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c = 4 * cb + q;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[cb][j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[cb][i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[cb][j], af[cb][i]);
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int c = 4 * cb + q;
+        uint4 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
+      }
+    }
+  };
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(
+      g.y, 0, g.N * g.out_H * g.out_W * g.Cout * ES, 0x00020000);
+  const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+  // Small tiles load the residual with counted (inline-asm) loads issued before the last
+  // K-tile's wait, so the epilogue waits only for them -- not for the DMA issued after.
+  constexpr bool ARES = TM * TP <= 8;
+  constexpr int NR = ARES ? TM * TP : 0;
+  const u32x4 rrs = make_srd(g.res ? g.res : g.y, g.N * g.out_H * g.out_W * g.Cout * ES);
+  u32x4 rres[ARES ? TM : 1][ARES ? TP : 1];
+  auto res_issue = [&](int k) {
+    int mt, cls, nt;
+    decode(k, mt, cls, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int osc = g.deconv ? 2 : 1, oy_off = g.deconv ? cls >> 1 : 0, ox_off = g.deconv ? cls & 1 : 0;
+    asm volatile("s_nop 4" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < (ARES ? TM : 1); ++i) {
+      const int m = m0 + wm * WTM + i * 16 + r16;
+      const bool mok = m < g.M;
+      const int mm = mok ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
+      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      const int pix = ((n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+#pragma unroll
+      for (int jp = 0; jp < (ARES ? TP : 1); ++jp) {
+        const int co = n0 + wn * WTN + (2 * jp + (q & 1)) * 16 + 8 * (q >> 1);
+        const int off = (mok && co < g.Cout) ? (pix + co) * ES : kOOB;
+        asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(rres[i][jp]) : "v"(off), "s"(rrs) : "memory");
+      }
+    }
+  };
+  const bool ares = ARES && g.res != nullptr;
+  // epilogue of stream tile k: BN, residual, ReLU in registers; NST 16-B buffer stores
+  auto epilogue = [&](int k) {
+    int mt, cls, nt;
+    decode(k, mt, cls, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
+    const int osc = g.deconv ? 2 : 1, oy_off = g.deconv ? cls >> 1 : 0, ox_off = g.deconv ? cls & 1 : 0;
+    int cop[TP];
+    float sc[TP][8], sh[TP][8];
+#pragma unroll
+    for (int jp = 0; jp < TP; ++jp) {
+      cop[jp] = n0 + wn * WTN + (2 * jp + (q & 1)) * 16 + 8 * (q >> 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = cop[jp] + e;
+        sc[jp][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
+        sh[jp][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * WTM + i * 16 + r16;
+      const bool mok = m < g.M;
+      const int mm = mok ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
+      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      const int pix = ((n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      uint4 rv[TP];
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        rv[jp] = make_uint4(0, 0, 0, 0);
+        if constexpr (ARES) {
+          if (ares) {
+            rv[jp] = make_uint4(rres[i][jp].x, rres[i][jp].y, rres[i][jp].z, rres[i][jp].w);
+            continue;
+          }
+        }
+        if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
+      }
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        float v[8], r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        O::load_vals(rv[jp], r);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = v[e] * sc[jp][e] + sh[jp][e];
+          if (rp) v[e] += r[e];
+          if (g.relu) v[e] = fmaxf(v[e], 0.f);
+        }
+        const uint4 pk = O::store_vals(v);
+        const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
+        const int voff = (mok && cop[jp] < g.Cout) ? (pix + cop[jp]) * ES : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b128(pv, yrs, voff, 0, 0);
+      }
+    }
+  };
+  auto barrier = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  zero_acc();
+#pragma unroll
+  for (int sq = 0; sq < S - 1; ++sq)
+    if (sq < total) dma_ktile(sq);
+  for (int sq = 0; sq < total; ++sq) {
+    const bool tile_end = (sq + 1) % nk == 0;
+    if (ares && tile_end) res_issue(sq / nk);
+    // retire K-tile sq: younger = the DMA groups of sq+1 .. sq+S-2, the stores of the
+    // epilogues run since sq's DMA was issued (iterations sq-S+1 .. sq-1) and the
+    // residual loads just issued
+    const int a = min(S - 2, total - 1 - sq);
+    int e = 0;
+#pragma unroll
+    for (int d = 1; d < S; ++d) e += (sq - d >= 0 && (sq - d + 1) % nk == 0) ? 1 : 0;
+    vm_wait_dyn(ND * a + NST * e + ((ares && tile_end) ? NR : 0));
+    barrier();
+    const bool more = sq + S - 1 < total;
+    if (more) dma_ktile(sq + S - 1);
+    compute(sq % S);
+    if (tile_end) {
+      if constexpr (ARES) {
+        if (ares) {  // the residual has landed once only this iteration's DMA group is younger
+          if (more) vm_wait<ND>();
+          else vm_wait<0>();
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jp = 0; jp < TP; ++jp) asm volatile("" : "+v"(rres[i][jp]));
+        }
+      }
+      epilogue(sq / nk);
+      zero_acc();
+    }
+  }
+}
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
+void launch_persist(const ConvGeom& g, int ntile, hipStream_t s) {
+  // four-wave tiles keep two slots (several blocks per CU hide each other's latencies);
+  // eight-wave tiles take a third slot where it fits
+  constexpr int S = (NW == 8 && ring_bytes<BM, BN, 3>() <= 160 * 1024) ? 3 : 2;
+  static const int occ = [] {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, conv_persist_kernel<T, BM, BN, NW, WGM, S, DUAL>, NW * 64,
+                                                     0) != hipSuccess || b < 1)
+      b = 1;
+    return b;
+  }();
+  int grid = std::min(ntile, cu_count() * occ);
+  grid = std::max(8, grid & ~7);  // whole XCD rounds (blockIdx & 7 = XCD slice)
+  hipLaunchKernelGGL((conv_persist_kernel<T, BM, BN, NW, WGM, S, DUAL>), dim3(grid), dim3(NW * 64), 0, s, g);
+}
+
 template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
 void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
   if constexpr (NW == 4) {
@@ -1030,6 +1490,7 @@ int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
 int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
 int g_early_nk = 8;             // posu_set_conv_early_residual
+int g_persist = 0;              // persistent K-tile stream by default (posu_set_conv_persistent)
 long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
 
 template <typename T, bool DUAL>
@@ -1074,14 +1535,33 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       const int v = want >> 3;
       st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
       // variant 3: phased 256x256 loop (one-tap-per-K-tile gathers and two-source tails)
-      ph = v == 3 && c == 5 && (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0));
+      ph = (v & 3) == 3 && c == 5 && (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0));
     }
   }
+  // persistent K-tile stream (tile bit 32, or the process-wide knob): 2-byte dtypes,
+  // direct NHWC epilogue, outputs addressable by a 32-bit buffer offset
+  const bool persist_ok = sizeof(T) == 2 && g.mode == 0 && !g.hm && !g.cy &&
+                          static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
+  const bool persist = persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
+  if constexpr (sizeof(T) == 2) {
+    if (persist) {
+      switch (cfg) {
+        case 0: launch_persist<T, 256, 64, 4, 4, DUAL>(g, nb, s); break;
+        case 1: launch_persist<T, 128, 64, 4, 2, DUAL>(g, nb, s); break;
+        case 2: launch_persist<T, 64, 64, 4, 2, DUAL>(g, nb, s); break;
+        case 3: launch_persist<T, 128, 128, 4, 2, DUAL>(g, nb, s); break;
+        case 4: launch_persist<T, 64, 128, 4, 2, DUAL>(g, nb, s); break;
+        case 5: launch_persist<T, 256, 256, 8, 2, DUAL>(g, nb, s); break;
+        default: launch_persist<T, 256, 128, 8, 4, DUAL>(g, nb, s); break;
+      }
+      return check_launch(what);
+    }
+  }
   switch (cfg) {
     case 0: launch_cfg<T, 256, 64, 4, 4, DUAL>(g, nb, st, s); break;
     case 1: launch_cfg<T, 128, 64, 4, 2, DUAL>(g, nb, st, s); break;
@@ -1147,7 +1627,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 32 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 64 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -1164,6 +1644,11 @@ extern "C" int posu_set_conv_nt_threshold(long long bytes) {
 
 extern "C" int posu_set_conv_early_residual(int max_ktiles) {
   g_early_nk = max_ktiles;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_persistent(int on) {
+  g_persist = on ? 1 : 0;
   return POSU_OK;
 }
 
@@ -1187,7 +1672,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -1219,7 +1704,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -1251,7 +1736,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 32 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

@@ -62,6 +62,11 @@ def set_conv_early_residual(max_ktiles):
     call('posu_set_conv_early_residual', int(max_ktiles))
 
 
+def set_conv_persistent(on):
+    """Persistent K-tile-stream conv variant for launches without an explicit tile."""
+    call('posu_set_conv_persistent', int(bool(on)))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""

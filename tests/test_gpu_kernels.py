@@ -359,6 +359,44 @@ def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
         assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
 
 
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize('code', [BF16, F16])
+def test_persistent_stream_bit_exact_vs_one_block_per_tile(cuda, cfg, code):
+    """The persistent K-tile stream (tile + 32) walks each tile's K in the same order as the
+    one-block-per-tile kernel: outputs equal bit for bit for 3x3 + residual (ragged M,
+    K-tiles >> ring), 1x1 + residual with one K-tile per tile (several epilogues inside the
+    ring window), strided 1x1, ConvTranspose(4, s2) and the two-source Bottleneck tail."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(7)
+    cout = 256
+    sc = torch.rand(cout, device=cuda, generator=g) + 0.5
+    sh = torch.randn(cout, device=cuda, generator=g) * 0.1
+
+    def rnd(*shape, scale=1.0):
+        return (torch.randn(*shape, device=cuda, generator=g) * scale).to(dt)
+
+    x = rnd(7, 21, 19, 128)
+    x64 = rnd(7, 21, 19, 64)
+    res = rnd(7, 21, 19, cout)
+    x2 = rnd(7, 42, 38, 64)
+    w3 = rnd(cout, 9 * 128, scale=0.03)
+    w1 = rnd(cout, 64, scale=0.1)
+    wd = rnd(cout, 128 + 64, scale=0.05)
+    wdc = rnd(4, cout, 4 * 128, scale=0.03)
+    outs = {}
+    for t in (cfg, cfg + 32):
+        outs[t] = [
+            ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
+            ops.conv2d_nhwc(x64, w1, cout, 1, 1, 1, 0, sc, sh, res, True, code, tile=t),
+            ops.conv2d_nhwc(x, w3[:, :128].contiguous(), cout, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
+            ops.deconv4x4s2_nhwc(x, wdc, cout, sc, sh, True, code, tile=t),
+            ops.conv1x1_dual_nhwc(x, x2, 2, wd, cout, sh, True, code, tile=t),
+        ]
+    torch.cuda.synchronize()
+    for a, b in zip(outs[cfg], outs[cfg + 32]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
     """The phased 256x256 main loop (tile 29) keeps each accumulator's K order, so its

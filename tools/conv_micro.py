@@ -25,6 +25,7 @@ CASES = {
     'l1c1': ('conv', 64, 64, 256, 64, 1, 1, 0),
     'l1c2': ('conv', 64, 64, 64, 64, 3, 1, 1),
     'l1c3': ('conv', 64, 64, 64, 256, 1, 1, 0),
+    'l1c3r': ('conv', 64, 64, 64, 256, 1, 1, 0),  # with the residual add (Bottleneck tail)
     'l2c2': ('conv', 32, 32, 128, 128, 3, 1, 1),
     'l2c3': ('conv', 32, 32, 128, 512, 1, 1, 0),
     'l3c1': ('conv', 16, 16, 1024, 256, 1, 1, 0),
@@ -67,7 +68,8 @@ def make(case, dev, code):
     if case == 'stem':
         ho, wo = 128, 128
     out = torch.empty(B, ho, wo, co, device=dev, dtype=dt)
-    return lambda t: ops.conv2d_nhwc(x, wt[0], co, k, k, s, p, scale, shift, None, True, code, out=out,
+    res = torch.randn(B, ho, wo, co, device=dev, generator=g).to(dt) if case.endswith('r') else None
+    return lambda t: ops.conv2d_nhwc(x, wt[0], co, k, k, s, p, scale, shift, res, True, code, out=out,
                                      out_hw=(ho, wo), tile=t)
 
 
@@ -92,7 +94,7 @@ def main():
 
     def wrap(f):
         def run(t):
-            if t >= 50 or len(epis) > 1:
+            if t >= 70 or len(epis) > 1:
                 ops.set_conv_epilogue((t + 50) // 100)
                 t = (t + 50) % 100 - 50
             return f(t)
