@@ -77,6 +77,10 @@ struct ConvGeom {
   int early_nk;      // early residual prefetch for launches of at most this many K-tiles
   int direct;        // mode 0 without chain/head: store straight from the accumulators
   long long* stamps;  // diagnostics: per block s_memtime at start / main-loop end / exit (or null)
+  // halo kernel: output rows per tile R = BM / Wo, segment length SL (rows of one image
+  // inside a tile), halo window KHh x KWh around each output pixel, halo pitch HWp,
+  // halo LDS rows HL, DMA rounds NHD
+  int hR, hSL, hKH, hKW, hWp, hL, hNHD, hph, hpw;
 };
 
 template <typename T>
@@ -185,6 +189,13 @@ __device__ __forceinline__ u32x4 make_srd(const void* base, int bytes) {
 // the other ring slots nor drains it early: the kernel retires it itself with a
 // counted s_waitcnt vmcnt(N) before the barrier that precedes the reads.
 __device__ __forceinline__ void dma16(u32x4 srd, int voff, unsigned lds) {
+  // the operands are wave-uniform; readfirstlane lets the compiler prove it (a no-op on
+  // values already in SGPRs)
+  srd.x = __builtin_amdgcn_readfirstlane(srd.x);
+  srd.y = __builtin_amdgcn_readfirstlane(srd.y);
+  srd.z = __builtin_amdgcn_readfirstlane(srd.z);
+  srd.w = __builtin_amdgcn_readfirstlane(srd.w);
+  lds = __builtin_amdgcn_readfirstlane(lds);
   unsigned keep;
   asm volatile(
       "s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
@@ -1191,22 +1202,27 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     }
   };
   // DMA of stream K-tile sq into ring slot sq % S: exactly ND dma16 per thread
-  auto dma_ktile = [&](int sq) {
+  // DMA of stream K-tile sq into ring slot sq % S: exactly ND dma16 per thread.  The
+  // source offsets are computed first (dma_prep), the instructions issued by dma_issue(d)
+  // -- all at once, or (eight-wave tiles) interleaved with the previous K-tile's MFMAs.
+  int doff[ND];
+  unsigned dAs = 0;
+  bool dsec = false;
+  auto dma_prep = [&](int sq) {
     const int k = sq / nk, kt = sq - k * nk;
     if (k != l_tile) {
       setup_load(k);
       l_tile = k;
     }
     const int kbase = kt * BK;
-    const unsigned As_ = lds0 + (sq % S) * STAGE + wid_u * 1024;
-    const unsigned Bs_ = As_ + A_BYTES;
+    dAs = __builtin_amdgcn_readfirstlane(lds0 + (sq % S) * STAGE + wid_u * 1024);
     if constexpr (DUAL) {
       const bool first = kbase < g.K1;
+      dsec = __builtin_amdgcn_readfirstlane(first ? 0 : 1) != 0;
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
         const int o = first ? o1[i] : o2[i];
-        const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
-        dma16(first ? xrs : x2rs, off, As_ + i * NW * 1024);
+        doff[i] = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
       }
     } else if (fast_gather) {
       const int tap = kbase >> g.logC;
@@ -1216,14 +1232,14 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
       for (int i = 0; i < RA; ++i) {
         const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
                         static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
-        dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * NW * 1024);
+        doff[i] = ok ? (pbase[i] + toff) * ES : kOOB;
       }
     } else if (row_fast) {
       const int roff = kt * g.W * g.C;
 #pragma unroll
       for (int i = 0; i < RA; ++i) {
         const bool ok = wok[i] && static_cast<unsigned>(hb[i] + kt) < static_cast<unsigned>(g.H);
-        dma16(xrs, ok ? (rbase[i] + roff) * ES : kOOB, As_ + i * NW * 1024);
+        doff[i] = ok ? (rbase[i] + roff) * ES : kOOB;
       }
     } else {
       int kh, kw, ci;
@@ -1247,11 +1263,37 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
         const int hi = hl >> g.up, wi = wl >> g.up;
         const bool ok = kvalid && ((hl | wl) & g.up) == 0 && static_cast<unsigned>(hi) < static_cast<unsigned>(g.H) &&
                         static_cast<unsigned>(wi) < static_cast<unsigned>(g.W);
-        dma16(xrs, ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB, As_ + i * NW * 1024);
+        doff[i] = ok ? (nb[i] + (hi * g.W + wi) * g.C + ci) * ES : kOOB;
       }
     }
 #pragma unroll
-    for (int i = 0; i < RB; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs_ + i * NW * 1024);
+    for (int i = 0; i < RB; ++i) doff[RA + i] = (wbrow + ROWS * i * g.Kpad + kbase) * ES;
+  };
+  auto dma_issue = [&](int d) {  // d compile-time after unrolling
+    if (d < RA) {
+      if (DUAL && dsec) dma16(x2rs, doff[d], dAs + d * NW * 1024);
+      else dma16(xrs, doff[d], dAs + d * NW * 1024);
+    } else {
+      dma16(wrs, doff[d], dAs + A_BYTES + (d - RA) * NW * 1024);
+    }
+  };
+  auto dma_ktile = [&](int sq) {
+    dma_prep(sq);
+#pragma unroll
+    for (int d = 0; d < ND; ++d) dma_issue(d);
+  };
+  constexpr bool IL = NW == 8;  // interleave the next K-tile's DMAs with the MFMAs
+  constexpr int IL_STEP = 4;    // one DMA after every IL_STEP MFMAs
+  static_assert(!IL || ND * IL_STEP <= 2 * TM * TN, "interleave slots");
+  auto mma_il = [&](int f, bool more, f32x4& a, const uint4& b, const uint4& x) {
+    O::mma(a, b, x);
+    if constexpr (IL) {
+      if (f % IL_STEP == IL_STEP - 1 && f / IL_STEP < ND && more) {
+        __builtin_amdgcn_sched_barrier(0);
+        dma_issue(f / IL_STEP);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   };
 
   f32x4 acc[TM][TN];
@@ -1261,7 +1303,7 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  auto compute = [&](int slot_) {
+  auto compute = [&](int slot_, bool more) {
     const char* As_ = smem + slot_ * STAGE;
     const char* Bs_ = As_ + A_BYTES;
     if constexpr (PRELOAD) {
@@ -1281,7 +1323,7 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[cb][j], af[cb][i]);
+          for (int j = 0; j < TN; ++j) mma_il((cb * TM + i) * TN + j, more, acc[i][j], bfr[cb][j], af[cb][i]);
     } else {
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
@@ -1294,7 +1336,7 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
+          for (int j = 0; j < TN; ++j) mma_il((cb * TM + i) * TN + j, more, acc[i][j], bfr[j], af[i]);
       }
     }
   };
@@ -1415,8 +1457,12 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     vm_wait_dyn(ND * a + NST * e + ((ares && tile_end) ? NR : 0));
     barrier();
     const bool more = sq + S - 1 < total;
-    if (more) dma_ktile(sq + S - 1);
-    compute(sq % S);
+    if (IL) {
+      if (more) dma_prep(sq + S - 1);
+    } else if (more) {
+      dma_ktile(sq + S - 1);
+    }
+    compute(sq % S, more);
     if (tile_end) {
       if constexpr (ARES) {
         if (ares) {  // the residual has landed once only this iteration's DMA group is younger
@@ -1432,6 +1478,248 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
       zero_acc();
     }
   }
+}
+
+// ---------------------------------------------------------------------------------
+// Halo variant for stride-1 KHxKW convolutions and the ConvTranspose(4, s2) parity
+// classes (2-byte dtypes, direct epilogue).  A tile is R = BM / Wo whole output rows;
+// per 64-channel K-chunk its input window -- the R rows plus the (KH-1)-row / (KW-1)-column
+// halo, one segment per image the rows belong to -- is staged ONCE in LDS and every tap
+// reads its A fragments from it at a tap-uniform row offset, instead of gathering BM rows
+// per tap (9x fewer A bytes over the L2->LDS path for 3x3, 4x for a deconv class).  The
+// K order is chunk-major (all taps of a chunk, then the next chunk); the weights stream
+// one [BN][64] K-tile per tap through a two-slot ring, the next chunk's halo is DMA'd in
+// per-tap parts into the other halo slot while the current chunk computes.
+template <int BN>
+constexpr int halo_rows_max() {  // LDS rows of one halo slot: 2 halo + 2 weight slots in 160 KiB
+  return ((160 * 1024 - 2 * BN * 128) / (2 * 128)) / 64 * 64;
+}
+
+template <typename T, int BM, int BN, int NW, int WGM>
+__global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
+  using O = Op<T>;
+  constexpr int E = O::E;
+  constexpr int ES = static_cast<int>(sizeof(T));
+  constexpr int BK = 8 * E;
+  constexpr int WGN = NW / WGM;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int ROWS = NW * 8;
+  constexpr int RB = BN / ROWS;
+  constexpr int HMAX = halo_rows_max<BN>();
+  constexpr int NHMAX = HMAX / ROWS;
+  constexpr int HALO_BYTES = HMAX * 128, B_BYTES = BN * 128;
+  constexpr int TP = TN / 2;
+  constexpr bool PRELOAD = TM + TN <= 8;
+  static_assert(E == 8 && TN % 2 == 0, "halo variant: 2-byte dtypes, paired n-tiles");
+  static_assert(2 * HALO_BYTES + 2 * B_BYTES <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) char smem[2 * HALO_BYTES + 2 * B_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
+  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+  const int nt = wg % g.ntiles;
+  const int rest = wg / g.ntiles;
+  const int mt = g.deconv ? rest >> 2 : rest;
+  const int cls = g.deconv ? rest & 3 : 0;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int dy = g.deconv ? cls >> 1 : 0, dx = g.deconv ? cls & 1 : 0;
+  const int osc = g.deconv ? 2 : 1;
+  const T* __restrict__ wp = reinterpret_cast<const T*>(g.w);
+  if (g.deconv) wp += static_cast<size_t>(cls) * g.CoutPad * g.Kpad;
+
+  const u32x4 xrs = make_srd(g.x, g.N * g.H * g.W * g.C * ES);
+  const u32x4 wrs = make_srd(wp, g.CoutPad * g.Kpad * ES);
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
+  const int cL = (tid & 7) ^ ((tid >> 4) & 7);
+
+  // ---- halo DMA sources: LDS row L = j * ROWS + (tid >> 3) of a slot <-> halo pixel
+  const int rho0 = m0 / g.Wo;                    // first output row (n * Ho + oy) of the tile
+  const int HS = g.hSL + g.hKH - 1;              // halo rows per segment
+  int goff[NHMAX];
+#pragma unroll
+  for (int j = 0; j < NHMAX; ++j) {
+    const int L = j * ROWS + (tid >> 3);
+    const int hr = L / g.hWp, hx = L - hr * g.hWp;
+    const int k = hr / HS, r = hr - k * HS;
+    const int rho = rho0 + k * g.hSL;            // first output row of segment k
+    const int n = rho / g.Ho, oys = rho - n * g.Ho;
+    const int iy = oys - g.hph + r, ix = hx - g.hpw;
+    const bool ok = L < g.hL && n < g.N && static_cast<unsigned>(iy) < static_cast<unsigned>(g.H) &&
+                    static_cast<unsigned>(ix) < static_cast<unsigned>(g.W);
+    goff[j] = ok ? ((n * g.H + iy) * g.W + ix) * g.C + cL * E : -1;
+  }
+  // ---- A fragment rows: halo LDS row of each m-tile row's pixel (tap offset added later)
+  int lbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int ml = wm * WTM + i * 16 + r16;      // row within the tile
+    const int rl = ml / g.Wo, ox = ml - rl * g.Wo;
+    const int k = rl / g.hSL, rr2 = rl - k * g.hSL;
+    lbase[i] = (k * HS + rr2) * g.hWp + ox;
+  }
+  const int nchunk = g.C / BK;
+  const int ntap = g.KH * g.KW;
+  const int nsteps = nchunk * ntap;
+  const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;
+
+  auto halo_part = [&](int c, int j0, int j1) {  // DMA rounds [j0, j1) of chunk c's halo
+    const unsigned Hs = lds0 + (c & 1) * HALO_BYTES + wid_u * 1024;
+#pragma unroll
+    for (int j = 0; j < NHMAX; ++j)
+      if (j >= j0 && j < j1) dma16(xrs, goff[j] < 0 ? kOOB : (goff[j] + c * BK) * ES, Hs + j * NW * 1024);
+  };
+  auto b_tile = [&](int st) {  // weight K-tile of step st (chunk-major: tap fastest)
+    const int c = st / ntap, t = st - c * ntap;
+    const int kbase = t * g.C + c * BK;
+    const unsigned Bs = lds0 + 2 * HALO_BYTES + (st & 1) * B_BYTES + wid_u * 1024;
+#pragma unroll
+    for (int i = 0; i < RB; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs + i * NW * 1024);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int st) {
+    const int c = st / ntap, t = st - c * ntap;
+    const int th = t / g.KW, tw = t - th * g.KW;
+    const int toff = (th + dy) * g.hWp + (tw + dx);
+    const char* Hs = smem + (c & 1) * HALO_BYTES;
+    const char* Bs = smem + 2 * HALO_BYTES + (st & 1) * B_BYTES;
+    if constexpr (PRELOAD) {
+      uint4 af[2][TM], bfr[2][TN];
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int cc = 4 * cb + q;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[cb][j] = *reinterpret_cast<const uint4*>(Bs + swz(wn * WTN + j * 16 + r16, cc));
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[cb][i] = *reinterpret_cast<const uint4*>(Hs + swz(lbase[i] + toff, cc));
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[cb][j], af[cb][i]);
+    } else {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int cc = 4 * cb + q;
+        uint4 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const uint4*>(Hs + swz(lbase[i] + toff, cc));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs + swz(wn * WTN + j * 16 + r16, cc));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
+      }
+    }
+  };
+  auto barrier = [] {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  halo_part(0, 0, g.hNHD);
+  b_tile(0);
+  vm_wait<0>();
+  barrier();
+  for (int st = 0; st < nsteps; ++st) {
+    const int c = st / ntap, t = st - c * ntap;
+    if (st + 1 < nsteps) b_tile(st + 1);
+    if (c + 1 < nchunk) {  // part t of the next chunk's halo
+      const int j0 = (t * g.hNHD) / ntap, j1 = ((t + 1) * g.hNHD) / ntap;
+      halo_part(c + 1, j0, j1);
+    }
+    compute(st);
+    vm_wait<0>();
+    barrier();
+  }
+
+  // ---- direct epilogue (as conv_igemm_kernel's): paired n-tiles, 16-B NHWC stores
+  T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+  const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+  const int HoWo = g.Ho * g.Wo;
+  int cop[TP];
+  float sc[TP][8], sh[TP][8];
+#pragma unroll
+  for (int jp = 0; jp < TP; ++jp) {
+    cop[jp] = n0 + wn * WTN + (2 * jp + (q & 1)) * 16 + 8 * (q >> 1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int co = cop[jp] + e;
+      sc[jp][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
+      sh[jp][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * WTM + i * 16 + r16;
+    const bool mok = m < g.M;
+    const int mm = mok ? m : 0;
+    const int n = mm / HoWo, rem = mm - n * HoWo;
+    const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+    const size_t pix = (static_cast<size_t>(n * g.out_H + oy * osc + dy) * g.out_W + (ox * osc + dx)) * g.Cout;
+    uint4 rv[TP];
+#pragma unroll
+    for (int jp = 0; jp < TP; ++jp) {
+      rv[jp] = make_uint4(0, 0, 0, 0);
+      if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
+    }
+#pragma unroll
+    for (int jp = 0; jp < TP; ++jp) {
+      float v[8], r[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                         __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+        v[e] = __uint_as_float(sw[0]);
+        v[4 + e] = __uint_as_float(sw[1]);
+      }
+      O::load_vals(rv[jp], r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = v[e] * sc[jp][e] + sh[jp][e];
+        if (rp) v[e] += r[e];
+        if (g.relu) v[e] = fmaxf(v[e], 0.f);
+      }
+      if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
+    }
+  }
+}
+
+// Host geometry of the halo variant for a BM-row tile; false if the launch does not fit
+// (rows per tile not whole output rows, tiles straddling images unevenly, halo > LDS slot).
+bool halo_geometry(ConvGeom& g, int BM, int BN, int NW) {
+  if (g.up || g.mode != 0 || g.hm || g.cy || g.x2 || g.Wo <= 0 || BM % g.Wo != 0) return false;
+  if (!g.deconv && g.stride != 1) return false;
+  const int R = BM / g.Wo;
+  if (!(R % g.Ho == 0 || g.Ho % R == 0)) return false;
+  g.hR = R;
+  g.hSL = std::min(R, g.Ho);
+  g.hKH = g.deconv ? 3 : g.KH;
+  g.hKW = g.deconv ? 3 : g.KW;
+  g.hph = g.deconv ? 1 : g.pad_h;
+  g.hpw = g.deconv ? 1 : g.pad_w;
+  g.hWp = g.Wo + g.hKW - 1;
+  g.hL = (R / g.hSL) * (g.hSL + g.hKH - 1) * g.hWp;
+  const int hmax = ((160 * 1024 - 2 * BN * 128) / (2 * 128)) / 64 * 64;
+  if (g.hL > hmax) return false;
+  g.hNHD = (g.hL + NW * 8 - 1) / (NW * 8);
+  return true;
 }
 
 int cu_count() {
@@ -1527,7 +1815,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   const int want = tile >= 0 ? tile : g_force;
   int st = g_stages;
   bool ph = false;
-  if (want >= 0) {
+  if (want >= 0 && want < 64) {
     const int c = want & 7;
     const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
     if (c <= 2 || wide_ok) {
@@ -1548,6 +1836,30 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
+  if constexpr (sizeof(T) == 2 && !DUAL) {
+    // halo variant (tile 64 + h): whole output rows per tile, input window staged once per
+    // K-chunk; falls through to the heuristic when the geometry does not fit
+    if (want >= 64 && want < 69 && g.C % bk_of_t<T>() == 0) {
+      static const int hBM[] = {256, 256, 256, 128, 128};
+      static const int hBN[] = {256, 128, 64, 128, 64};
+      static const int hNW[] = {8, 8, 4, 4, 4};
+      const int h = want - 64;
+      ConvGeom hg = g;
+      if (g.CoutPad % hBN[h] == 0 && halo_geometry(hg, hBM[h], hBN[h], hNW[h])) {
+        hg.ntiles = g.CoutPad / hBN[h];
+        hg.mtiles = (g.M + hBM[h] - 1) / hBM[h];
+        const int hb = hg.mtiles * hg.ntiles * nclass;
+        switch (h) {
+          case 0: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 256, 8, 2>), dim3(hb), dim3(512), 0, s, hg); break;
+          case 1: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 128, 8, 4>), dim3(hb), dim3(512), 0, s, hg); break;
+          case 2: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 64, 4, 4>), dim3(hb), dim3(256), 0, s, hg); break;
+          case 3: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 128, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
+          default: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
+        }
+        return check_launch(what);
+      }
+    }
+  }
   if constexpr (sizeof(T) == 2) {
     if (persist) {
       switch (cfg) {
@@ -1627,7 +1939,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 64 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 69 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -1672,7 +1984,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -1704,7 +2016,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -1736,7 +2048,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 64 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

@@ -397,6 +397,47 @@ def test_persistent_stream_bit_exact_vs_one_block_per_tile(cuda, cfg, code):
         assert torch.equal(a, b)
 
 
+HALO_CASES = [
+    # n, h, w, cin, cout, halo tile, deconv
+    (3, 16, 16, 256, 256, 64, False),   # one image per 256-row tile (layer3 shape)
+    (3, 32, 32, 128, 128, 65, False),   # 8 rows of a 32-wide image per tile (layer2)
+    (2, 64, 64, 64, 64, 66, False),     # 4 rows of a 64-wide image (layer1)
+    (5, 8, 8, 512, 512, 67, False),     # two 8x8 images per 128-row tile, last tile partial
+    (3, 16, 16, 256, 256, 68, False),
+    (5, 8, 8, 256, 256, 64, True),      # deconv classes, 4 images per tile, partial tile
+    (2, 32, 32, 128, 256, 64, True),    # deconv, 8 rows per tile
+    (2, 16, 16, 256, 128, 65, True),
+]
+
+
+@pytest.mark.parametrize('case', HALO_CASES)
+@pytest.mark.parametrize('code', [BF16, F16])
+def test_halo_variant_matches_gather_kernel(cuda, case, code):
+    """Halo tiles (64..68): the input window staged once per K-chunk and read at tap
+    offsets gives the gathered kernel's result up to the f32 summation order (chunk-major
+    K): 3x3 + residual on every tile shape, multi-image and partial tiles, deconv classes."""
+    n, h, w, cin, cout, tile, deconv = case
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    x = torch.randn(n, h, w, cin, device=cuda, generator=g).to(dt)
+    sc = torch.rand(cout, device=cuda, generator=g) + 0.5
+    sh = torch.randn(cout, device=cuda, generator=g) * 0.1
+    if deconv:
+        wt = (torch.randn(4, cout, 4 * cin, device=cuda, generator=g) * (1.0 / (4 * cin)) ** 0.5).to(dt)
+        got = ops.deconv4x4s2_nhwc(x, wt, cout, sc, sh, True, code, tile=tile)
+        ref = ops.deconv4x4s2_nhwc(x, wt, cout, sc, sh, True, code, tile=-1)
+    else:
+        wt = (torch.randn(cout, 9 * cin, device=cuda, generator=g) * (1.0 / (9 * cin)) ** 0.5).to(dt)
+        res = torch.randn(n, h, w, cout, device=cuda, generator=g).to(dt)
+        got = ops.conv2d_nhwc(x, wt, cout, 3, 3, 1, 1, sc, sh, res, True, code, tile=tile)
+        ref = ops.conv2d_nhwc(x, wt, cout, 3, 3, 1, 1, sc, sh, res, True, code, tile=-1)
+    torch.cuda.synchronize()
+    d = (got.float() - ref.float()).abs()
+    tol = (0.02 if code == BF16 else 0.004) * (1 + ref.float().abs())
+    assert bool((d <= tol).all()), float(d.max())
+    assert float(d.mean()) < (2e-3 if code == BF16 else 3e-4)
+
+
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
     """The phased 256x256 main loop (tile 29) keeps each accumulator's K order, so its

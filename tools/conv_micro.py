@@ -94,9 +94,9 @@ def main():
 
     def wrap(f):
         def run(t):
-            if t >= 70 or len(epis) > 1:
-                ops.set_conv_epilogue((t + 50) // 100)
-                t = (t + 50) % 100 - 50
+            if t >= 90 or len(epis) > 1:
+                ops.set_conv_epilogue((t + 10) // 100)
+                t = (t + 10) % 100 - 10
             return f(t)
         return run
 
