@@ -120,6 +120,13 @@ int posu_set_conv_persistent(int on);
  * stride-1 convs and deconvs over whole output rows): the halo variant with tiles
  * 256x256, 256x128, 256x64, 128x128, 128x64); -1 restores the automatic choice. */
 int posu_force_conv_config(int cfg);
+/* Fused stem (replaces lib/models/pose_resnet.py:192-195, conv1 -> bn1 -> relu ->
+ * maxpool, and the input pack): x NCHW f32 [N, 3, H, W] (the reference's input tensor,
+ * mirrored along W when hflip), w packed [64][224] dtype (k = kh*32 + kw*4 + c, zero for
+ * kw = 7 / c = 3; posu/packing.py:pack_stem_fused_weight), BN scale/shift [64] f32,
+ * y NHWC [N, H/4, W/4, 64] dtype.  BF16 / F16, H % 8 == 0, W in {256, 384}. */
+int posu_stem_pool_fwd(int dtype, const float* x, int N, int H, int W, int hflip, const void* w,
+                       const float* scale, const float* shift, void* y, void* stream);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,

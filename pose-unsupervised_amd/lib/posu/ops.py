@@ -181,6 +181,22 @@ def head1x1_nchw(x, wpk, cout, bias, code, out=None):
     return out
 
 
+def stem_pool(x, wpk, scale, shift, code, out=None, hflip=False):
+    """Fused input pack + 7x7/s2 stem + BN + ReLU + 3x3/s2 max-pool: NCHW f32 [N, 3, H, W]
+    -> NHWC [N, H/4, W/4, 64] (compute dtype)."""
+    if not x.is_cuda:
+        raise RuntimeError('stem_pool: HIP op needs a GPU tensor')
+    n, c, h, w = x.shape
+    if c != 3:
+        raise ValueError('stem_pool: 3 input channels expected')
+    x = x.contiguous().float()
+    if out is None:
+        out = torch.empty((n, h // 4, w // 4, 64), dtype=torch_dtype(code), device=x.device)
+    call('posu_stem_pool_fwd', code, ptr(x), n, h, w, int(bool(hflip)), ptr(wpk), ptr(scale), ptr(shift), ptr(out),
+         stream_of(x.device))
+    return out
+
+
 def maxpool3x3s2_nhwc(x, code, out=None):
     n, h, w, c = x.shape
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1

@@ -50,6 +50,17 @@ def pack_stem_s2d_weight(w, cpad, bk, dtype):
     return out.to(dtype).contiguous()
 
 
+def pack_stem_fused_weight(w, dtype):
+    """7x7 stem weight [64, 3, 7, 7] -> [64][224] for posu_stem_pool_fwd:
+    k = kh*32 + kw*4 + c (kw < 7, c < 3; the 8th tap and the 4th channel are zeros)."""
+    cout, cin, kh, kw = w.shape
+    if (cin, kh, kw) != (3, 7, 7):
+        raise NotImplementedError('fused stem needs a 3-channel 7x7 kernel')
+    out = torch.zeros((cout, 7, 8, 4), dtype=torch.float32, device=w.device)
+    out[:, :, :7, :3] = w.detach().float().permute(0, 2, 3, 1)
+    return out.reshape(cout, 224).to(dtype).contiguous()
+
+
 def pack_dual_1x1_weight(w_a, scale_a, w_b, scale_b, dtype):
     """Two 1x1 conv weights with their BN scales folded in, concatenated along K:
     [CoutPad][Ca + Cb] = [W_a * s_a | W_b * s_b] (fp64 product, one rounding)."""

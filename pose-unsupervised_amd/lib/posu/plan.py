@@ -18,7 +18,7 @@ import torch
 
 from . import ops
 from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dual_1x1_weight,
-                      pack_stem_s2d_weight)
+                      pack_stem_fused_weight, pack_stem_s2d_weight)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
@@ -27,6 +27,22 @@ STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 # Off by default: measured slower on R50@256 (the 64x256 chain tile re-reads the whole
 # 256-channel weight per 64-pixel block: 381 vs 341 us for block0 + the next conv1).
 CHAIN_BLOCKS = False
+# fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
+FUSED_STEM = True
+
+
+class RawViews:
+    """pack_input's result when the fused stem applies: the caller's NCHW f32 views
+    (stacked on N in order), consumed directly by posu_stem_pool_fwd.  .packed() gives the
+    space-to-depth pack of the two-launch path (chunked runs, tools)."""
+
+    def __init__(self, plan, views, hflip):
+        self.plan, self.views, self.hflip = plan, views, hflip
+        n, _, self.h, self.w = views[0].shape
+        self.shape = (n * len(views), self.h, self.w, 3)
+
+    def packed(self):
+        return self.plan.pack_input(self.views, hflip=self.hflip, fused=False)
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -226,12 +242,19 @@ class PoseResNetPlan:
         self.njoints = fl.weight.shape[0]
         last = self.deconvs[-1] if self.deconvs else None
         self.fuse_head = last is not None and last.cout == 256 and self.njoints <= 16
+        self.stem_fused_w = None
+        if (FUSED_STEM and code in (ops.BF16, ops.F16) and tuple(net.conv1.weight.shape) == (64, 3, 7, 7)
+                and net.conv1.stride == (2, 2) and net.conv1.padding == (3, 3)):
+            self.stem_fused_w = pack_stem_fused_weight(net.conv1.weight, ops.torch_dtype(code))
 
-    def pack_input(self, views, hflip=False):
+    def pack_input(self, views, hflip=False, fused=True):
         """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N):
         space-to-depth [N, H/2, W/2, 16] for even H, W, else [N, H, W, 8]; hflip mirrors
-        every image along W (flip test)."""
+        every image along W (flip test).  Where the fused stem applies (bf16 / fp16,
+        H % 8 == 0, W in {256, 384}) the views are handed over as they are (RawViews)."""
         n, _, h, w = views[0].shape
+        if fused and self.stem_fused_w is not None and h % 8 == 0 and w in (256, 384) and views[0].shape[1] == 3:
+            return RawViews(self, list(views), hflip)
         s2d = h % 2 == 0 and w % 2 == 0
         shape = (n * len(views), h // 2, w // 2, STEM_S2D_PAD) if s2d else (n * len(views), h, w, STEM_CIN_PAD)
         x = torch.empty(shape, dtype=ops.torch_dtype(self.code), device=views[0].device)
@@ -242,8 +265,23 @@ class PoseResNetPlan:
                 ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n], hflip=hflip)
         return x
 
+    def stem_pool(self, x):
+        """stem + max-pool: one fused launch per view for RawViews, else two launches."""
+        code = self.code
+        if isinstance(x, RawViews):
+            n = x.views[0].shape[0]
+            out = torch.empty((x.shape[0], x.h // 4, x.w // 4, self.stem.cout), dtype=ops.torch_dtype(code),
+                              device=x.views[0].device)
+            for i, v in enumerate(x.views):
+                ops.stem_pool(v, self.stem_fused_w, self.stem.scale, self.stem.shift, code,
+                              out=out[i * n:(i + 1) * n], hflip=x.hflip)
+            return out
+        return ops.maxpool3x3s2_nhwc(self.run_stem(x), code)
+
     def run_stem(self, x):
         code = self.code
+        if isinstance(x, RawViews):
+            x = x.packed()
         if x.shape[3] == STEM_S2D_PAD:
             st = self.stem
             out = torch.empty(tuple(x.shape[:3]) + (st.cout,), dtype=x.dtype, device=x.device)
@@ -256,7 +294,7 @@ class PoseResNetPlan:
     def _stage_early(self, x, out=None, keep=None):
         """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
         code = self.code
-        x = ops.maxpool3x3s2_nhwc(self.run_stem(x), code)
+        x = self.stem_pool(x)
         pre = None
         for li in (0, 1):
             layer = self.layers[li]
@@ -317,8 +355,7 @@ class PoseResNetPlan:
         code = self.code
         n = x.shape[0]
         if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
-            x = self.run_stem(x)
-            x = ops.maxpool3x3s2_nhwc(x, code)
+            x = self.stem_pool(x)
             x1 = None
             pre = None
             for li, layer in enumerate(self.layers):
@@ -330,6 +367,8 @@ class PoseResNetPlan:
                 x = dc(x, code)
             hm, f = self._last_deconv_head(x, keep_features)
             return hm, (x1 if keep_features else None), f
+        if isinstance(x, RawViews):
+            x = x.packed()
         c = n // chunks
         dt = ops.torch_dtype(code)
         dev = x.device

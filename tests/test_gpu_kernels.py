@@ -556,3 +556,31 @@ def test_ransac_and_reprojection_match_oracle(cuda, distortion):
     np.testing.assert_array_equal(ransac(p2d, cams, vis, cfg), ref_vis)
     pr, rvis = reproject_poses(p2d, cams, vis, no_distortion=not distortion)
     np.testing.assert_allclose(pr, ref_proj, atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize('size', [256, 384])
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('hflip', [False, True])
+def test_fused_stem_pool_matches_two_launch_path(cuda, size, code, hflip):
+    """posu_stem_pool_fwd (input pack + 7x7/s2 stem + BN + ReLU + 3x3/s2 max-pool in one
+    launch) against the pack -> space-to-depth stem -> max-pool launches on the same
+    inputs: equal up to the f32 summation order of the stem (one rounding step at most),
+    including the padded top row / left column, odd batch and the flip test's mirror."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(21)
+    n = 3
+    x = torch.randn(n, 3, size, size, device=cuda, generator=g)
+    wt = torch.randn(64, 3, 7, 7, device=cuda, generator=g) * (2.0 / 147) ** 0.5
+    sc = torch.rand(64, device=cuda, generator=g) + 0.5
+    sh = torch.randn(64, device=cuda, generator=g) * 0.1
+    got = ops.stem_pool(x, packing.pack_stem_fused_weight(wt, dt), sc, sh, code, hflip=hflip)
+    xp = ops.pack_s2d_nchw(x, code, 16, hflip=hflip)
+    ws = packing.pack_stem_s2d_weight(wt, 16, ops.conv_bk(code), dt)
+    stem = ops.conv2d_nhwc(xp, ws, 64, 4, 4, 1, 2, sc, sh, None, True, code, out_hw=(size // 2, size // 2))
+    ref = ops.maxpool3x3s2_nhwc(stem, code)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape == (n, size // 4, size // 4, 64)
+    d = (got.float() - ref.float()).abs()
+    ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * ref.float().abs()
+    assert bool((d <= 2 * ulp + 1e-3).all()), float(d.max())
+    assert float((d > 0).float().mean()) < 0.05

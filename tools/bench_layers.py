@@ -56,18 +56,22 @@ def main():
         rows.append((name, us, flops, nbytes))
         print('%-22s %9.1f us %8.1f TF %8.0f GB/s' % (name, us, flops / us / 1e6, nbytes / us / 1e3), flush=True)
 
-    xp = plan.pack_input(x_in)
+    xp = plan.pack_input(x_in, fused=False)
     if args.autotune:
         from posu.plan import tuned_tiles
         plan.autotune(xp, keep_features=False)
         for k, v in tuned_tiles().items():
             print('tile', v, k)
-    rec('pack', lambda: plan.pack_input(x_in), 0, x_in[0].numel() * 4 + xp.numel() * esz)
+    rec('pack', lambda: plan.pack_input(x_in, fused=False), 0, x_in[0].numel() * 4 + xp.numel() * esz)
     y = plan.run_stem(xp)
     n, ho, wo, co = y.shape
     rec('stem', lambda: plan.run_stem(xp), 2 * n * ho * wo * co * 147, xp.numel() * esz + y.numel() * esz)
     p = ops.maxpool3x3s2_nhwc(y, code)
     rec('maxpool', lambda: ops.maxpool3x3s2_nhwc(y, code), 0, (y.numel() + p.numel()) * esz)
+    raw = plan.pack_input(x_in)
+    if not isinstance(raw, torch.Tensor):
+        rec('pack+stem+pool(fused)', lambda: plan.stem_pool(raw), 2 * n * ho * wo * co * 147,
+            x_in[0].numel() * 4 + p.numel() * esz)
     x = p
     for li, layer in enumerate(plan.layers):
         for bi, blk in enumerate(layer):

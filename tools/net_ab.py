@@ -3,9 +3,10 @@
     python tools/net_ab.py --settings "epi=1" "epi=2" "epi=2,nt=16" [--rounds 5 --reps 20]
 
 Each setting is a comma list of knob=value (epi: posu_set_conv_epilogue, nt: streaming-store
-threshold in MiB, stages, big).  The plan is autotuned once (default knobs), then every
-setting gets its own captured hipGraph of the R50@256 128-frame forward; replays are timed
-with HIP events in interleaved rounds and the per-setting median / min are printed.
+threshold in MiB, stages, big, early, cand: autotune candidate set -- "all" (default), "base"
+(no persistent +32 tiles), "halo" (all + halo tiles 64..68)).  Every setting is autotuned
+under its own knobs and gets its own captured hipGraph of the R50@256 128-frame forward;
+replays are timed with HIP events in interleaved rounds, per-setting median / min printed.
 """
 import argparse
 import os
@@ -21,7 +22,18 @@ from posu import ops, synthetic as syn  # noqa: E402
 
 
 def apply(setting):
+    from posu import plan as P
     kv = dict(x.split('=') for x in setting.split(',') if x)
+    cand = kv.get('cand', 'all')
+    if not hasattr(P, '_orig_candidates'):
+        P._orig_candidates = P._tile_candidates
+    base = P._orig_candidates
+    if cand == 'base':
+        P._tile_candidates = lambda cout: [t for t in base(cout) if t < 32]
+    elif cand == 'halo':
+        P._tile_candidates = lambda cout: base(cout) + [64, 65, 66, 67, 68]
+    else:
+        P._tile_candidates = base
     ops.set_conv_epilogue(int(kv.get('epi', 1)))
     ops.set_conv_nt_threshold(int(float(kv.get('nt', 0)) * 2 ** 20))
     ops.set_conv_stages(int(kv.get('stages', 2)))
@@ -48,10 +60,12 @@ def main():
         apply('')
         for _ in range(2):
             plan.run(plan.pack_input(views), keep_features=False)
-        plan.autotune(plan.pack_input(views), keep_features=False)
-        torch.cuda.synchronize()
+        from posu import plan as P
         for st in args.settings:
             apply(st)
+            P._TUNE_CACHE.clear()
+            plan.autotune(plan.pack_input(views), keep_features=False)
+            torch.cuda.synchronize()
             s = torch.cuda.Stream(dev)
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
