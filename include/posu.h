@@ -112,6 +112,10 @@ int posu_set_conv_early_residual(int max_ktiles);
 /* Tuning knob: launches without an explicit tile run the persistent K-tile-stream
  * variant (1) or one block per tile (0, default); explicit tiles select it with +32. */
 int posu_set_conv_persistent(int on);
+/* Tuning knob: posu_deconv4x4s2_head_fwd runs on the eight-wave 256x256 tile with the head
+ * folded into the register epilogue (1, default; bf16/f16) or on 64x256 tiles with the
+ * head applied from LDS (0). */
+int posu_set_conv_head256(int on);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K

@@ -696,13 +696,32 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // ---- direct epilogue (NHWC outputs without a chained conv): each lane stores its 4
   // consecutive channels of one pixel straight from the accumulators (BN, residual,
   // ReLU applied in registers) -- no LDS round trip, no barriers
-  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && !g.hm && !g.cy) {
+  // 256x256 tiles also carry the fused 1x1 head (pose_resnet.py:126-132, 203): each
+  // wave's rounded outputs are already MFMA B fragments (8 consecutive channels of one
+  // pixel per lane), so its partial heatmaps over its 64 channels are 2 MFMAs per m-tile;
+  // the four column waves' partials are summed in LDS in a fixed order.
+  constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && !PH && E == 8;
+  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && !g.cy && (!g.hm || HEAD256)) {
     // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
     // holds 8 consecutive channels (16-B stores, half the store instructions):
     // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
     T* __restrict__ yp = reinterpret_cast<T*>(g.y);
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     constexpr int TP = TN / 2;
+    const bool head = HEAD256 && g.hm != nullptr;
+    uint4 hwf[HEAD256 ? TP : 1];
+    f32x4 hacc[HEAD256 ? TM : 1];
+    if constexpr (HEAD256) {
+      if (head) {
+        const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
+#pragma unroll
+        for (int jp = 0; jp < TP; ++jp)  // joint r16, this lane's 8 channels of pair jp
+          hwf[jp] = *reinterpret_cast<const uint4*>(hwp + static_cast<size_t>(r16) * g.hkp + n0 + colB(2 * jp) +
+                                                    16 * (q & 1) + 8 * (q >> 1));
+#pragma unroll
+        for (int i = 0; i < TM; ++i) hacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
     int cop[TP];
     float sc[TP][8], sh[TP][8];
 #pragma unroll
@@ -753,6 +772,14 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (rp) v[e] += r[e];
           if (g.relu) v[e] = fmaxf(v[e], 0.f);
         }
+        if constexpr (HEAD256) {
+          if (head) {
+            const uint4 pk = O::store_vals(v);
+            O::mma(hacc[i], hwf[jp], pk);  // rows = joints, cols = pixels
+            if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
+            continue;
+          }
+        }
         if (mok && cop[jp] < g.Cout) {
           const uint4 pk = O::store_vals(v);
           if (g.direct == 2) {  // streaming store: do not keep the output lines in L2
@@ -761,6 +788,29 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           } else {
             *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
           }
+        }
+      }
+    }
+    if constexpr (HEAD256) {
+      if (head) {
+        __syncthreads();  // the ring is no longer read: partial heatmaps [wn][joint][256 px]
+        float* Hs = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Hs[(wn * 16 + 4 * q + e) * BM + rowA(i) + r16] = hacc[i][e];
+        __syncthreads();
+        const int HWo = g.out_H * g.out_W;
+        for (int idx = tid; idx < g.J * BM; idx += NT) {
+          const int j = idx / BM, pl = idx - j * BM;
+          const int m = m0 + pl;
+          if (m >= g.M) continue;
+          float sum = g.hbias ? g.hbias[j] : 0.f;
+#pragma unroll
+          for (int w4 = 0; w4 < 4; ++w4) sum += Hs[(w4 * 16 + j) * BM + pl];
+          const int n = m / HoWo, rem = m - n * HoWo;
+          const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+          g.hm[(static_cast<size_t>(n) * g.J + j) * HWo + (oy * osc + oy_off) * g.out_W + ox * osc + ox_off] = sum;
         }
       }
     }
@@ -1778,6 +1828,7 @@ int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
 int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
 int g_early_nk = 8;             // posu_set_conv_early_residual
+int g_head256 = 1;              // fused head on the 256x256 direct-epilogue tile (posu_set_conv_head256)
 int g_persist = 0;              // persistent K-tile stream by default (posu_set_conv_persistent)
 long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
 
@@ -1789,6 +1840,14 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   if (g.direct == 2 &&  // streaming stores only for outputs that would not stay in L2 anyway
       static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * static_cast<int>(sizeof(T)) < g_nt_min_bytes)
     g.direct = 1;
+  if constexpr (sizeof(T) == 2) {  // fused head on the eight-wave 256x256 tile, direct epilogue
+    if (g.hm && !g.cy && g_head256 && g.direct && g.CoutPad == 256) {
+      g.ntiles = 1;
+      g.mtiles = (g.M + 255) / 256;
+      launch_cfg<T, 256, 256, 8, 2, DUAL>(g, g.mtiles * nclass, 2, s);
+      return check_launch(what);
+    }
+  }
   if (g.hm || g.cy) {  // fused head / chained conv: one block owns all 256 output channels
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
@@ -1956,6 +2015,11 @@ extern "C" int posu_set_conv_nt_threshold(long long bytes) {
 
 extern "C" int posu_set_conv_early_residual(int max_ktiles) {
   g_early_nk = max_ktiles;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_head256(int on) {
+  g_head256 = on ? 1 : 0;
   return POSU_OK;
 }
 

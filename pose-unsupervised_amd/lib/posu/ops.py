@@ -67,6 +67,11 @@ def set_conv_persistent(on):
     call('posu_set_conv_persistent', int(bool(on)))
 
 
+def set_conv_head256(on):
+    """Fused deconv + head on the 256x256 direct-epilogue tile (1) or the 64x256 LDS tile (0)."""
+    call('posu_set_conv_head256', int(bool(on)))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""

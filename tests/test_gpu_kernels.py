@@ -271,9 +271,22 @@ def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
 
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 @pytest.mark.parametrize('keep_f', [True, False])
-def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f):
+@pytest.mark.parametrize('head256,shape', [(1, (3, 5, 6, 16)), (0, (3, 5, 6, 16)), (1, (2, 24, 20, 13))])
+def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f, head256, shape):
+    """Last deconv + BN + ReLU + 1x1 head in one launch, on the 256x256 register-epilogue
+    tile (head256=1; partial heatmaps of the four column waves summed in LDS) and on the
+    64x256 LDS tile; ragged M, several tiles, J < 16."""
+    ops.set_conv_head256(head256)
+    try:
+        _fused_deconv_head_case(cuda, code, tol, keep_f, shape)
+    finally:
+        ops.set_conv_head256(1)
+
+
+def _fused_deconv_head_case(cuda, code, tol, keep_f, shape):
     g = torch.Generator().manual_seed(8)
-    n, cin, h, w, cout, J = 3, 64, 5, 6, 256, 16
+    n, h, w, J = shape
+    cin, cout = 64, 256
     x = torch.randn(n, cin, h, w, generator=g)
     wt = torch.randn(cin, cout, 4, 4, generator=g) * (2.0 / (cin * 4)) ** 0.5
     sc = torch.rand(cout, generator=g) + 0.5
