@@ -122,7 +122,8 @@ int posu_set_conv_head256(int on);
  * layers); + 16: a three-slot ring (two K-tiles in flight; not 5); 29: the phased
  * 256x256 loop; + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
  * stride-1 convs and deconvs over whole output rows): the halo variant with tiles
- * 256x256, 256x128, 256x64, 128x128, 128x64); -1 restores the automatic choice. */
+ * 256x256, 256x128, 256x64, 128x128, 128x64; 69, 70, 72: single-halo-slot 256x64,
+ * 128x64, 256x128 for C = one K-chunk); -1 restores the automatic choice. */
 int posu_force_conv_config(int cfg);
 /* Fused stem (replaces lib/models/pose_resnet.py:192-195, conv1 -> bn1 -> relu ->
  * maxpool, and the input pack): x NCHW f32 [N, 3, H, W] (the reference's input tensor,

@@ -1545,7 +1545,7 @@ constexpr int halo_rows_max() {  // LDS rows of one halo slot: 2 halo + 2 weight
   return ((160 * 1024 - 2 * BN * 128) / (2 * 128)) / 64 * 64;
 }
 
-template <typename T, int BM, int BN, int NW, int WGM>
+template <typename T, int BM, int BN, int NW, int WGM, int HR = halo_rows_max<BN>(), int NHS = 2>
 __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int E = O::E;
@@ -1556,14 +1556,15 @@ __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int ROWS = NW * 8;
   constexpr int RB = BN / ROWS;
-  constexpr int HMAX = halo_rows_max<BN>();
+  constexpr int HMAX = HR;  // halo LDS rows per slot; NHS = 1: one slot (a single K-chunk)
   constexpr int NHMAX = HMAX / ROWS;
   constexpr int HALO_BYTES = HMAX * 128, B_BYTES = BN * 128;
   constexpr int TP = TN / 2;
   constexpr bool PRELOAD = TM + TN <= 8;
   static_assert(E == 8 && TN % 2 == 0, "halo variant: 2-byte dtypes, paired n-tiles");
-  static_assert(2 * HALO_BYTES + 2 * B_BYTES <= 160 * 1024, "LDS budget");
-  __shared__ __attribute__((aligned(16))) char smem[2 * HALO_BYTES + 2 * B_BYTES];
+  static_assert(NHS * HALO_BYTES + 2 * B_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(HR % ROWS == 0, "halo slot = whole DMA rounds");
+  __shared__ __attribute__((aligned(16))) char smem[NHS * HALO_BYTES + 2 * B_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -1620,7 +1621,7 @@ __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
   const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;
 
   auto halo_part = [&](int c, int j0, int j1) {  // DMA rounds [j0, j1) of chunk c's halo
-    const unsigned Hs = lds0 + (c & 1) * HALO_BYTES + wid_u * 1024;
+    const unsigned Hs = lds0 + (NHS == 1 ? 0 : (c & 1)) * HALO_BYTES + wid_u * 1024;
 #pragma unroll
     for (int j = 0; j < NHMAX; ++j)
       if (j >= j0 && j < j1) dma16(xrs, goff[j] < 0 ? kOOB : (goff[j] + c * BK) * ES, Hs + j * NW * 1024);
@@ -1628,7 +1629,7 @@ __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
   auto b_tile = [&](int st) {  // weight K-tile of step st (chunk-major: tap fastest)
     const int c = st / ntap, t = st - c * ntap;
     const int kbase = t * g.C + c * BK;
-    const unsigned Bs = lds0 + 2 * HALO_BYTES + (st & 1) * B_BYTES + wid_u * 1024;
+    const unsigned Bs = lds0 + NHS * HALO_BYTES + (st & 1) * B_BYTES + wid_u * 1024;
 #pragma unroll
     for (int i = 0; i < RB; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs + i * NW * 1024);
   };
@@ -1643,8 +1644,8 @@ __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
     const int c = st / ntap, t = st - c * ntap;
     const int th = t / g.KW, tw = t - th * g.KW;
     const int toff = (th + dy) * g.hWp + (tw + dx);
-    const char* Hs = smem + (c & 1) * HALO_BYTES;
-    const char* Bs = smem + 2 * HALO_BYTES + (st & 1) * B_BYTES;
+    const char* Hs = smem + (NHS == 1 ? 0 : (c & 1)) * HALO_BYTES;
+    const char* Bs = smem + NHS * HALO_BYTES + (st & 1) * B_BYTES;
     if constexpr (PRELOAD) {
       uint4 af[2][TM], bfr[2][TN];
 #pragma unroll
@@ -1753,7 +1754,7 @@ __global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
 
 // Host geometry of the halo variant for a BM-row tile; false if the launch does not fit
 // (rows per tile not whole output rows, tiles straddling images unevenly, halo > LDS slot).
-bool halo_geometry(ConvGeom& g, int BM, int BN, int NW) {
+bool halo_geometry(ConvGeom& g, int BM, int BN, int NW, int hmax_rows) {
   if (g.up || g.mode != 0 || g.hm || g.cy || g.x2 || g.Wo <= 0 || BM % g.Wo != 0) return false;
   if (!g.deconv && g.stride != 1) return false;
   const int R = BM / g.Wo;
@@ -1766,8 +1767,7 @@ bool halo_geometry(ConvGeom& g, int BM, int BN, int NW) {
   g.hpw = g.deconv ? 1 : g.pad_w;
   g.hWp = g.Wo + g.hKW - 1;
   g.hL = (R / g.hSL) * (g.hSL + g.hKH - 1) * g.hWp;
-  const int hmax = ((160 * 1024 - 2 * BN * 128) / (2 * 128)) / 64 * 64;
-  if (g.hL > hmax) return false;
+  if (g.hL > hmax_rows) return false;
   g.hNHD = (g.hL + NW * 8 - 1) / (NW * 8);
   return true;
 }
@@ -1898,13 +1898,19 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   if constexpr (sizeof(T) == 2 && !DUAL) {
     // halo variant (tile 64 + h): whole output rows per tile, input window staged once per
     // K-chunk; falls through to the heuristic when the geometry does not fit
-    if (want >= 64 && want < 69 && g.C % bk_of_t<T>() == 0) {
-      static const int hBM[] = {256, 256, 256, 128, 128};
-      static const int hBN[] = {256, 128, 64, 128, 64};
-      static const int hNW[] = {8, 8, 4, 4, 4};
+    if (want >= 64 && want < 75 && (want & 7) != 7 && g.C % bk_of_t<T>() == 0) {
+      // 64..68: two halo slots (any C); 69, 70, 72: one slot (C == one K-chunk), smaller
+      // LDS so two blocks share a CU
       const int h = want - 64;
+      static const int hBM[] = {256, 256, 256, 128, 128, 256, 128, 0, 256};
+      static const int hBN[] = {256, 128, 64, 128, 64, 64, 64, 0, 128};
+      static const int hNW[] = {8, 8, 4, 4, 4, 4, 4, 0, 8};
+      static const int hHR[] = {halo_rows_max<256>(), halo_rows_max<128>(), halo_rows_max<64>(),
+                                halo_rows_max<128>(), halo_rows_max<64>(), 448, 320, 0, 448};
+      const bool one_slot = h >= 5;
       ConvGeom hg = g;
-      if (g.CoutPad % hBN[h] == 0 && halo_geometry(hg, hBM[h], hBN[h], hNW[h])) {
+      if (g.CoutPad % hBN[h] == 0 && (!one_slot || g.C == bk_of_t<T>()) &&
+          halo_geometry(hg, hBM[h], hBN[h], hNW[h], hHR[h])) {
         hg.ntiles = g.CoutPad / hBN[h];
         hg.mtiles = (g.M + hBM[h] - 1) / hBM[h];
         const int hb = hg.mtiles * hg.ntiles * nclass;
@@ -1913,7 +1919,16 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
           case 1: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 128, 8, 4>), dim3(hb), dim3(512), 0, s, hg); break;
           case 2: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 64, 4, 4>), dim3(hb), dim3(256), 0, s, hg); break;
           case 3: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 128, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
-          default: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
+          case 4: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
+          case 5:
+            hipLaunchKernelGGL((conv_halo_kernel<T, 256, 64, 4, 4, 448, 1>), dim3(hb), dim3(256), 0, s, hg);
+            break;
+          case 6:
+            hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2, 320, 1>), dim3(hb), dim3(256), 0, s, hg);
+            break;
+          default:
+            hipLaunchKernelGGL((conv_halo_kernel<T, 256, 128, 8, 4, 448, 1>), dim3(hb), dim3(512), 0, s, hg);
+            break;
         }
         return check_launch(what);
       }
@@ -1998,7 +2013,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 69 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -2048,7 +2063,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -2080,7 +2095,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -2112,7 +2127,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 69 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

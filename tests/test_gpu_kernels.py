@@ -420,6 +420,9 @@ HALO_CASES = [
     (5, 8, 8, 256, 256, 64, True),      # deconv classes, 4 images per tile, partial tile
     (2, 32, 32, 128, 256, 64, True),    # deconv, 8 rows per tile
     (2, 16, 16, 256, 128, 65, True),
+    (2, 64, 64, 64, 64, 69, False),     # single halo slot (C = one K-chunk), layer1 shape
+    (3, 32, 32, 64, 64, 70, False),
+    (3, 32, 32, 64, 128, 72, False),
 ]
 
 
