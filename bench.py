@@ -334,7 +334,7 @@ def main():
         traffic, src = pmc_traffic(args.layers, args.size, args.precision, args.groups)
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
                 'frac': round(achieved / peak, 4), 'traffic': traffic,
-                'kernel': 'conv stack (conv_igemm_kernel launches + pack + maxpool) per network replay',
+                'kernel': 'network per replay: fused stem (stem_pool_kernel) + conv stack (conv_igemm / conv_persist kernels, fused deconv+head)',
                 'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (gf, frames)}
         if traffic:
             roof['traffic_source'] = src + ' (PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward)'

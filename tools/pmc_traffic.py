@@ -14,7 +14,8 @@ import csv
 import json
 import sys
 
-NET_KERNELS = ('conv_igemm_kernel', 'maxpool_kernel', 'pack_s2d_kernel', 'pack_kernel')
+NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'conv_halo_kernel', 'stem_pool_kernel', 'maxpool_kernel',
+       'pack_s2d_kernel', 'pack_kernel')
 
 
 def load(path, counter):
@@ -34,9 +35,9 @@ def main():
     else:  # the last forward starts at the first input-pack launch of the final run of packs
         names = [x[1] for x in fetch]
         i = len(names) - 1
-        while i >= 0 and 'pack' not in names[i]:
+        while i >= 0 and not any(k in names[i] for k in ('pack', 'stem_pool')):
             i -= 1
-        while i > 0 and 'pack' in names[i - 1]:
+        while i > 0 and any(k in names[i - 1] for k in ('pack', 'stem_pool')):
             i -= 1
         per_fwd = len(names) - i
     f = fetch[-per_fwd:]

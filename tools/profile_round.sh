@@ -18,3 +18,6 @@ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv 
 python3 tools/pmc_traffic.py "$OUT"/pmc_fetch/run_counter_collection.csv "$OUT"/pmc_write/run_counter_collection.csv \
   > "$OUT/pmc_traffic_network.txt"
 echo profile done
+python3 tools/roofline_check.py "$OUT"/infer/run_kernel_trace.csv "$OUT"/infer_bench.log > "$OUT/roofline_check.txt"
+timeout -k 10 400 python3 tools/bench_layers.py --autotune > "$OUT/layers_autotuned.txt" 2>&1
+echo profile all done
