@@ -116,6 +116,11 @@ int posu_set_conv_persistent(int on);
  * folded into the register epilogue (1, default; bf16/f16) or on 64x256 tiles with the
  * head applied from LDS (0). */
 int posu_set_conv_head256(int on);
+/* Tuning knob: chained launches (posu_conv2d_chain_fwd / posu_conv1x1_dual_chain_fwd) with
+ * Cout2 <= 64 run on a 256x256 tile of eight 32-pixel x 256-channel waves, the next conv1
+ * from the register epilogue with its weights in LDS (1; bf16/f16), or on the 64x256
+ * LDS-epilogue tile (0, default). */
+int posu_set_conv_chain8(int on);
 /* Test hook: force one tile configuration for every conv launch that admits it
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K

@@ -304,7 +304,10 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   static_assert(ND * (S - 2) < 64, "vmcnt range");
   static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
   static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
-  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
+  // chained next conv1 on the 8x1-wave 256x256 tile: its weights [64][256] sit after the ring
+  constexpr bool CHAIN8 = WGN == 1 && BN == 256 && BM == 256 && NW == 8 && E == 8 && !PH;
+  constexpr int CW_BYTES = CHAIN8 ? 64 * 256 * 2 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>() + CW_BYTES];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -408,6 +411,18 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int kw_row = (cL * E) >> g.logC, ci_row = (cL * E) & (g.C - 1);
   const int nk = g.Kpad / BK;
   const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;  // weight row offset (elements) for i = 0
+  if constexpr (CHAIN8) {
+    if (g.cy) {  // [Cout2 <= 64][256] -> LDS rows of 512 B, 16-B chunk c of row r at c ^ (r & 15)
+      const u32x4 cws = make_srd(g.cw, g.Cout2 * g.ckp * ES);
+      const unsigned Cs0 = lds0 + ring_bytes<BM, BN, S>() + wid_u * 1024;
+#pragma unroll
+      for (int rd = 0; rd < 4; ++rd) {
+        const int r = rd * 16 + (tid >> 5), p = tid & 31;
+        const int off = r < g.Cout2 ? (r * g.ckp + ((p ^ (r & 15)) * 8)) * ES : kOOB;
+        dma16(cws, off, Cs0 + rd * NW * 1024);
+      }
+    }
+  }
 
   // global -> LDS (async DMA) for K-tile KT into ring slot BUF: exactly ND dma16 per thread
 #define POSU_DMA_TILE(KT, BUF)                                                                      \
@@ -701,7 +716,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // pixel per lane), so its partial heatmaps over its 64 channels are 2 MFMAs per m-tile;
   // the four column waves' partials are summed in LDS in a fixed order.
   constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && !PH && E == 8;
-  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && !g.cy && (!g.hm || HEAD256)) {
+  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && (!g.cy || CHAIN8) && (!g.hm || HEAD256)) {
     // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
     // holds 8 consecutive channels (16-B stores, half the store instructions):
     // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
@@ -709,6 +724,17 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     constexpr int TP = TN / 2;
     const bool head = HEAD256 && g.hm != nullptr;
+    // chained next conv1 (CHAIN8): every wave owns all 256 channels of its 32 pixels, so
+    // its rounded outputs (B fragments, k-groups in the swap order) times the LDS-resident
+    // weights give the next conv1 directly: cacc[i][t] = 16 out channels x 16 pixels
+    const bool chain = CHAIN8 && g.cy != nullptr;
+    f32x4 cacc[CHAIN8 ? TM : 1][4];
+    if constexpr (CHAIN8) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) cacc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     uint4 hwf[HEAD256 ? TP : 1];
     f32x4 hacc[HEAD256 ? TM : 1];
     if constexpr (HEAD256) {
@@ -772,6 +798,21 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (rp) v[e] += r[e];
           if (g.relu) v[e] = fmaxf(v[e], 0.f);
         }
+        if constexpr (CHAIN8) {
+          if (chain) {
+            const uint4 pk = O::store_vals(v);
+            if (mok) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
+            const char* Cs = smem + ring_bytes<BM, BN, S>();
+            const int c = jp * 4 + 2 * (q & 1) + (q >> 1);  // this lane's 8-channel chunk
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              if (16 * t >= g.Cout2) break;
+              const uint4 wf = *reinterpret_cast<const uint4*>(Cs + (16 * t + r16) * 512 + ((c ^ r16) << 4));
+              O::mma(cacc[i][t], wf, pk);  // rows = next-conv channels, cols = pixels
+            }
+            continue;
+          }
+        }
         if constexpr (HEAD256) {
           if (head) {
             const uint4 pk = O::store_vals(v);
@@ -787,6 +828,32 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
             __builtin_nontemporal_store(pv, reinterpret_cast<u32x4*>(yp + pix + cop[jp]));
           } else {
             *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
+          }
+        }
+      }
+    }
+    if constexpr (CHAIN8) {
+      if (chain) {  // BN + ReLU of the next conv1, paired tiles -> 16-B NHWC stores
+        T* __restrict__ cyp = reinterpret_cast<T*>(g.cy);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + rowA(i) + r16;
+#pragma unroll
+          for (int tp = 0; tp < 2; ++tp) {
+            const int co = 16 * (2 * tp + (q & 1)) + 8 * (q >> 1);
+            float v[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(cacc[i][2 * tp][e]),
+                                                               __float_as_uint(cacc[i][2 * tp + 1][e]), false, false);
+              v[e] = __uint_as_float(sw[0]);
+              v[4 + e] = __uint_as_float(sw[1]);
+            }
+            if (m < g.M && co < g.Cout2) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * g.cscale[co + e] + g.cshift[co + e], 0.f);
+              *reinterpret_cast<uint4*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = O::store_vals(v);
+            }
           }
         }
       }
@@ -1828,6 +1895,7 @@ int g_force = -1;   // forced tile configuration (tests), -1 = automatic
 long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
 int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
 int g_early_nk = 8;             // posu_set_conv_early_residual
+int g_chain8 = 0;               // chained conv1 on the 8x1-wave 256x256 tile (posu_set_conv_chain8)
 int g_head256 = 1;              // fused head on the 256x256 direct-epilogue tile (posu_set_conv_head256)
 int g_persist = 0;              // persistent K-tile stream by default (posu_set_conv_persistent)
 long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
@@ -1845,6 +1913,15 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
       launch_cfg<T, 256, 256, 8, 2, DUAL>(g, g.mtiles * nclass, 2, s);
+      return check_launch(what);
+    }
+  }
+  if constexpr (sizeof(T) == 2) {  // chained next conv1 on the 8x1-wave 256x256 tile
+    if (g.cy && !g.hm && g_chain8 && g.direct && g.Cout == 256 && g.Cout2 <= 64 && g.ckp == 256) {
+      g.ntiles = 1;
+      g.mtiles = (g.M + 255) / 256;
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 8, 2, DUAL>), dim3(g.mtiles * nclass), dim3(512), 0, s,
+                         g);
       return check_launch(what);
     }
   }
@@ -2030,6 +2107,11 @@ extern "C" int posu_set_conv_nt_threshold(long long bytes) {
 
 extern "C" int posu_set_conv_early_residual(int max_ktiles) {
   g_early_nk = max_ktiles;
+  return POSU_OK;
+}
+
+extern "C" int posu_set_conv_chain8(int on) {
+  g_chain8 = on ? 1 : 0;
   return POSU_OK;
 }
 

@@ -43,6 +43,7 @@ _SIGNATURES = {
     'posu_set_conv_early_residual': [_i],
     'posu_set_conv_persistent': [_i],
     'posu_set_conv_head256': [_i],
+    'posu_set_conv_chain8': [_i],
     'posu_stem_pool_fwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p],
     'posu_force_conv_config': [_i],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],

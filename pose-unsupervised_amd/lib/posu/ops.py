@@ -72,6 +72,11 @@ def set_conv_head256(on):
     call('posu_set_conv_head256', int(bool(on)))
 
 
+def set_conv_chain8(on):
+    """Chained next conv1 (Cout2 <= 64) on the 8x1-wave 256x256 register-epilogue tile."""
+    call('posu_set_conv_chain8', int(bool(on)))
+
+
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""

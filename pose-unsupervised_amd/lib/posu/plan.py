@@ -23,9 +23,11 @@ from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dua
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
-# Bottleneck tails that also compute the next block's conv1 (layer1 -> layer2.0).
-# Off by default: measured slower on R50@256 (the 64x256 chain tile re-reads the whole
-# 256-channel weight per 64-pixel block: 381 vs 341 us for block0 + the next conv1).
+# Bottleneck tails that also compute the next block's conv1: True = wherever chainable_to
+# allows (next conv1 <= 128 channels), False = never (default), 'auto' = only where the
+# register-epilogue chain applies (bf16 / fp16, next conv1 <= 64 channels).  Both measured
+# slower end to end on R50@256 (64x256 LDS chain tile: 381 vs 341 us for block0 + the next
+# conv1; register chain, posu_set_conv_chain8: 3.67 vs 3.38 ms per 128-frame forward).
 CHAIN_BLOCKS = False
 # fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
 FUSED_STEM = True
@@ -227,7 +229,8 @@ class PoseResNetPlan:
         if CHAIN_BLOCKS:
             blocks = [b for layer in self.layers for b in layer]
             for b, nxt in zip(blocks, blocks[1:]):
-                if b.chainable_to(nxt):
+                if b.chainable_to(nxt) and (CHAIN_BLOCKS is True or (
+                        code in (ops.BF16, ops.F16) and nxt.convs[0].cout <= 64)):
                     b.chain = nxt.convs[0]
         mods = list(net.deconv_layers)
         self.deconvs = []

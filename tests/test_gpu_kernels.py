@@ -503,13 +503,23 @@ def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
 
 @pytest.mark.parametrize('code,tol', [(F32, 1e-5), (BF16, 0.02), (F16, 0.005)])
 @pytest.mark.parametrize('dual,cout2', [(False, 64), (True, 64), (False, 128)])
-def test_chained_next_conv1_matches_two_launches(cuda, code, tol, dual, cout2):
+@pytest.mark.parametrize('chain8,shape', [(0, (3, 9, 7)), (1, (3, 9, 7)), (1, (4, 32, 33))])
+def test_chained_next_conv1_matches_two_launches(cuda, code, tol, dual, cout2, chain8, shape):
     """Block tail (+residual / downsample source) with the next block's 1x1 conv1 in the
-    same launch == the tail launch followed by a separate conv1 launch on its output."""
+    same launch == the tail launch followed by a separate conv1 launch on its output; on the
+    64x256 LDS-epilogue tile and (chain8, bf16/f16, cout2 <= 64) the 8x1-wave register tile."""
+    ops.set_conv_chain8(chain8)
+    try:
+        _chain_case(cuda, code, tol, dual, cout2, shape)
+    finally:
+        ops.set_conv_chain8(0)
+
+
+def _chain_case(cuda, code, tol, dual, cout2, shape):
     g = torch.Generator().manual_seed(9)
     dt = ops.torch_dtype(code)
     bk = ops.conv_bk(code)
-    n, h, w, mid, cin = 3, 9, 7, 64, 128
+    (n, h, w), mid, cin = shape, 64, 128
     a = torch.relu(torch.randn(n, h, w, mid, generator=g)).to(cuda, dt)
     x = torch.randn(n, h, w, cin if dual else 256, generator=g).to(cuda, dt)
     w3 = torch.randn(256, mid, 1, 1, generator=g) * 0.1

@@ -63,6 +63,11 @@ def main():
         from posu import plan as P
         for st in args.settings:
             apply(st)
+            kv = dict(x.split('=') for x in st.split(',') if x)
+            saved = P.CHAIN_BLOCKS
+            P.CHAIN_BLOCKS = {'off': False, 'on': True, 'auto': 'auto'}[kv.get('chain', 'auto')]
+            plan = P.PoseResNetPlan(net, plan.code)
+            P.CHAIN_BLOCKS = saved
             P._TUNE_CACHE.clear()
             plan.autotune(plan.pack_input(views), keep_features=False)
             torch.cuda.synchronize()
@@ -77,12 +82,12 @@ def main():
             with torch.cuda.graph(g):
                 plan.run(plan.pack_input(views), keep_features=False)
             torch.cuda.synchronize()
-            graphs[st] = g
+            graphs[st] = (g, plan)
         apply('')
         times = {st: [] for st in args.settings}
         for _ in range(args.rounds):
             for st in args.settings:
-                g = graphs[st]
+                g = graphs[st][0]
                 g.replay()
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
