@@ -40,11 +40,25 @@ class RawViews:
 
     def __init__(self, plan, views, hflip):
         self.plan, self.views, self.hflip = plan, views, hflip
-        n, _, self.h, self.w = views[0].shape
-        self.shape = (n * len(views), self.h, self.w, 3)
+        _, _, self.h, self.w = views[0].shape
+        self.shape = (sum(v.shape[0] for v in views), self.h, self.w, 3)
+        self.device = views[0].device
 
     def packed(self):
         return self.plan.pack_input(self.views, hflip=self.hflip, fused=False)
+
+    def __getitem__(self, sl):
+        """Batch slice (chunked runs): the views' rows [start, stop) of the stacked batch."""
+        if not isinstance(sl, slice) or sl.step not in (None, 1):
+            raise TypeError('RawViews supports contiguous batch slices only')
+        start, stop, _ = sl.indices(self.shape[0])
+        out, base = [], 0
+        for v in self.views:
+            a, b = max(start - base, 0), min(stop - base, v.shape[0])
+            if a < b:
+                out.append(v[a:b])
+            base += v.shape[0]
+        return RawViews(self.plan, out, self.hflip)
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -272,12 +286,13 @@ class PoseResNetPlan:
         """stem + max-pool: one fused launch per view for RawViews, else two launches."""
         code = self.code
         if isinstance(x, RawViews):
-            n = x.views[0].shape[0]
             out = torch.empty((x.shape[0], x.h // 4, x.w // 4, self.stem.cout), dtype=ops.torch_dtype(code),
-                              device=x.views[0].device)
-            for i, v in enumerate(x.views):
+                              device=x.device)
+            base = 0
+            for v in x.views:
                 ops.stem_pool(v, self.stem_fused_w, self.stem.scale, self.stem.shift, code,
-                              out=out[i * n:(i + 1) * n], hflip=x.hflip)
+                              out=out[base:base + v.shape[0]], hflip=x.hflip)
+                base += v.shape[0]
             return out
         return ops.maxpool3x3s2_nhwc(self.run_stem(x), code)
 
@@ -370,8 +385,6 @@ class PoseResNetPlan:
                 x = dc(x, code)
             hm, f = self._last_deconv_head(x, keep_features)
             return hm, (x1 if keep_features else None), f
-        if isinstance(x, RawViews):
-            x = x.packed()
         c = n // chunks
         dt = ops.torch_dtype(code)
         dev = x.device

@@ -119,6 +119,22 @@ def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks):
     torch.testing.assert_close(f1, f0, atol=1e-6, rtol=1e-6)
 
 
+def test_chunked_run_with_fused_stem_equals_whole_batch(cuda):
+    """bf16 at 256x256 hands the views to the fused stem (RawViews); chunked runs slice
+    them per chunk (a chunk may cover part of a view) and give the whole-batch result."""
+    from posu.plan import RawViews
+    net = _model(50, 256, 0, 'bf16', cuda)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 3, 256, seed=5)]
+    plan = net.plan(cuda)
+    x = plan.pack_input(views)
+    assert isinstance(x, RawViews) and x.shape[0] == 12
+    assert [v.shape[0] for v in x[2:7].views] == [1, 3, 1]
+    with torch.no_grad():
+        hm0, _, _ = plan.run(x, keep_features=False)
+        hm1, _, _ = plan.run(x, chunks=4, keep_features=False)
+    torch.testing.assert_close(hm1, hm0, atol=1e-3, rtol=0)
+
+
 @pytest.mark.parametrize('precision', ['fp32', 'bf16'])
 def test_chained_plan_equals_unchained_plan(cuda, precision):
     """The layer1 chains (block tail + next conv1 in one launch) change no result beyond
