@@ -1,3 +1,5 @@
+# Training-step A/B of the conv epilogue mode (register-direct vs LDS), 8 timed steps each:
+#   bash tools/train_epilogue_ab.sh   (on the GPU box, from the repo root)
 set -o pipefail
 for e in 1 0; do
 timeout -k 10 200 python -c "
