@@ -85,29 +85,35 @@ __global__ __launch_bounds__(NW * 64) void stem_pool_kernel(const float* __restr
   // ---- global -> registers first (the block's loads all in flight at once), then LDS
   constexpr int WCH = 64 * (kStemK / 8);                 // 16-B weight chunks
   constexpr int WIT = (WCH + NT - 1) / NT;
-  constexpr int XIT = (kWinRows * WP + NT - 1) / NT;     // window pixels per thread
   u32x4 wv[WIT];
 #pragma unroll
   for (int it = 0; it < WIT; ++it) {
     const int i = min(tid + it * NT, WCH - 1);  // clamped: duplicate chunks store the same bytes
     wv[it] = *reinterpret_cast<const u32x4*>(w + i * 8);
   }
-  // input window pixel (r, c) = input (r0 + r, c - 3), 3 channels + 0
+  // input window pixel (r, c) = input (r0 + r, c - 3), 3 channels + 0, read as 16-B groups
+  // of 4 input columns (4 gk - 4 .. 4 gk - 1) per plane: window columns 4 gk - 1 .. 4 gk + 2
   const size_t plane = static_cast<size_t>(H) * W;
   const float* __restrict__ xn = x + static_cast<size_t>(n) * 3 * plane;
-  float xv[XIT][3];
+  constexpr int GPR = NW * 8 + 2;                          // groups per window row (W / 4 + 2)
+  constexpr int XG = (kWinRows * GPR + NT - 1) / NT;       // groups per thread
+  float4 xv[XG][3];
 #pragma unroll
-  for (int it = 0; it < XIT; ++it) {
+  for (int it = 0; it < XG; ++it) {
     const int i = tid + it * NT;
-    const int r = i / WP, c = i - r * WP;
-    const int iy = r0 + r, ix = c - 3;
-    xv[it][0] = xv[it][1] = xv[it][2] = 0.f;
-    if (i < kWinRows * WP && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
-        static_cast<unsigned>(ix) < static_cast<unsigned>(W)) {
-      const size_t o = static_cast<size_t>(iy) * W + (hflip ? W - 1 - ix : ix);
-      xv[it][0] = xn[o];
-      xv[it][1] = xn[plane + o];
-      xv[it][2] = xn[2 * plane + o];
+    const int r = i / GPR, gk = i - r * GPR;
+    const int iy = r0 + r, c0 = 4 * (gk - 1);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) xv[it][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < kWinRows * GPR && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
+        static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
+      const size_t o = static_cast<size_t>(iy) * W + (hflip ? W - 4 - c0 : c0);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        float4 v = *reinterpret_cast<const float4*>(xn + p * plane + o);
+        if (hflip) v = make_float4(v.w, v.z, v.y, v.x);
+        xv[it][p] = v;
+      }
     }
   }
 #pragma unroll
@@ -117,11 +123,19 @@ __global__ __launch_bounds__(NW * 64) void stem_pool_kernel(const float* __restr
     *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = wv[it];
   }
 #pragma unroll
-  for (int it = 0; it < XIT; ++it) {
+  for (int it = 0; it < XG; ++it) {
     const int i = tid + it * NT;
-    if (i < kWinRows * WP)
-      *reinterpret_cast<uint2*>(win + i * 8) =
-          make_uint2(O::pack2(xv[it][0], xv[it][1]), O::pack2(xv[it][2], 0.f));
+    if (i >= kWinRows * GPR) continue;
+    const int r = i / GPR, gk = i - r * GPR;
+    const float a0[4] = {xv[it][0].x, xv[it][0].y, xv[it][0].z, xv[it][0].w};
+    const float a1[4] = {xv[it][1].x, xv[it][1].y, xv[it][1].z, xv[it][1].w};
+    const float a2[4] = {xv[it][2].x, xv[it][2].y, xv[it][2].z, xv[it][2].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int wc = 4 * gk - 1 + e;
+      if (wc >= 0 && wc < WP)
+        *reinterpret_cast<uint2*>(win + (r * WP + wc) * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
+    }
   }
   __syncthreads();
 
