@@ -283,7 +283,7 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 }
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false>
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false, bool PP = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int NT = NW * 64;
@@ -305,7 +305,9 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
   static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
   // chained next conv1 on the 8x1-wave 256x256 tile: its weights [64][256] sit after the ring
-  constexpr bool CHAIN8 = WGN == 1 && BN == 256 && BM == 256 && NW == 8 && E == 8 && !PH;
+  constexpr bool CHAIN8 = WGN == 1 && BN == 256 && BM == 256 && NW == 8 && E == 8 && !PH && !PP;
+  static_assert(!PP || (NW == 8 && WGM == 2 && S == 2 && !PH && RA % 2 == 0 && RB % 2 == 0),
+                "ping-pong loop: eight waves as two row halves, two slots");
   constexpr int CW_BYTES = CHAIN8 ? 64 * 256 * 2 : 0;
   __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>() + CW_BYTES];
 
@@ -355,6 +357,11 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // that lane fetches logical chunk cL = (tid & 7) ^ ((row >> 1) & 7), which is the
   // same for every i because ROWS*i does not touch bits 1..3 of the row.
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
+  // Ping-pong loop (PP): waves 0-3 stage tile rows [0, BM/2) of A and [0, BN/2) of B,
+  // waves 4-7 the other halves, piece i of wave w covering rows 32 i + 8 (w & 3) .. + 7 of
+  // its half (rows bits 1..3 -- the swizzle -- are those of the default mapping)
+  const int gp = static_cast<int>(wid_u) >> 2, wl = static_cast<int>(wid_u) & 3;
+  auto drow = [&](int i, int half) { return PP ? gp * half + 32 * i + 8 * wl + (lane >> 3) : (tid >> 3) + ROWS * i; };
   const int HoWo = g.Ho * g.Wo;
   int hb[RA], wb[RA], nb[RA];   // generic window gather
   int o1[RA], o2[RA];           // DUAL: byte offsets of the two 1x1 sources
@@ -362,7 +369,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   if constexpr (DUAL) x2rs = make_srd(g.x2, g.N * g.H2 * g.W2 * g.C2 * ES);
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
-    const int m = m0 + (tid >> 3) + ROWS * i;
+    const int m = m0 + drow(i, BM / 2);
     if (m < g.M) {
       const int n = m / HoWo, rem = m - n * HoWo;
       const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
@@ -571,7 +578,100 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
   // overwrites, which every wave finished reading in the previous iteration)
-  if constexpr (PH) {
+  if constexpr (PP) {
+    // Ping-pong loop: the two waves of a SIMD (w and w + 4, one per row half) alternate a
+    // "memory" phase -- this K-step's fragment reads + its share of the next K-tile's
+    // LDS-DMAs -- with a "matrix" phase on registers only, the halves one phase apart, so
+    // the matrix pipe always has one wave's MFMAs while the other issues its loads.
+    //   phase  waves 0-3                     waves 4-7
+    //   4t     read (t, k0), stage (t+1, h0)  MFMAs (t-1, k1)
+    //   4t+1   MFMAs (t, k0)                 read (t, k0), stage (t+1, h0)
+    //   4t+2   read (t, k1), stage (t+1, h1)  MFMAs (t, k0)
+    //   4t+3   MFMAs (t, k1), wait DMA        read (t, k1), stage (t+1, h1), wait DMA
+    // Slot (t+1) & 1 was last read at phase 4t-1, so the stages of t+1 start at 4t; every
+    // piece of t+1 is waited for by its issuing wave before the barrier ending phase 4t+3.
+    constexpr int HA = RA / 2, HB = RB / 2;
+    auto stage = [&](int kt, int buf, auto hc) {
+      constexpr int H = decltype(hc)::value;
+      const int kbase = kt * BK;
+      const unsigned As_ = lds0 + buf * STAGE + gp * (BM / 2) * 128 + wl * 1024;
+      const unsigned Bs_ = lds0 + buf * STAGE + A_BYTES + gp * (BN / 2) * 128 + wl * 1024;
+      if constexpr (DUAL) {
+        const bool first = kbase < g.K1;
+#pragma unroll
+        for (int i = H * HA; i < H * HA + HA; ++i) {
+          const int o = first ? o1[i] : o2[i];
+          const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
+          dma16(first ? xrs : x2rs, off, As_ + i * 4096);
+        }
+      } else {  // one tap per K-tile (launcher-checked)
+        const int tap = kbase >> g.logC;
+        const int th = tap / g.KW, tw = tap - th * g.KW;
+        const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));
+#pragma unroll
+        for (int i = H * HA; i < H * HA + HA; ++i) {
+          const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
+                          static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
+          dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * 4096);
+        }
+      }
+#pragma unroll
+      for (int i = H * HB; i < H * HB + HB; ++i)
+        dma16(wrs, ((n0 + drow(i, BN / 2)) * g.Kpad + cL * E + kbase) * ES, Bs_ + i * 4096);
+    };
+    using H0_ = std::integral_constant<int, 0>;
+    using H1_ = std::integral_constant<int, 1>;
+    auto barrier = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    uint4 af[TM], bfr[TN];
+    auto read = [&](int buf, int cb) {
+      const char* As_ = smem + buf * STAGE;
+      const char* Bs_ = As_ + A_BYTES;
+      const int c = 4 * cb + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));
+    };
+    auto mma = [&] {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
+    };
+    stage(0, 0, H0_{});
+    stage(0, 0, H1_{});
+    vm_wait<0>();
+    barrier();
+    if (gp) barrier();  // the second row half runs one phase behind
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      read(cur, 0);
+      if (more) stage(kt + 1, cur ^ 1, H0_{});
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      mma();
+      barrier();
+      read(cur, 1);
+      if (more) stage(kt + 1, cur ^ 1, H1_{});
+      if (gp) vm_wait<0>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      mma();
+      if (!gp) {
+        vm_wait<0>();
+        barrier();
+      } else if (more) {
+        barrier();
+      }
+    }
+  } else if constexpr (PH) {
     // Phased 256x256 loop: each K-tile is four phases, one output quadrant
     // (64 rows x 32 columns of the wave's tile, 16 MFMAs) per phase, each phase staging
     // one half-tile of the NEXT K-tile (2 LDS-DMAs per thread) beside its fragment reads
@@ -1948,9 +2048,21 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   }
   // per-call tile (autotuned plans) > test hook > heuristic; tile = cfg + 8 * variant,
   // variant 1 = single-slot ring (four-wave tiles), 2 = three-slot ring (where it fits)
-  const int want = tile >= 0 ? tile : g_force;
+  int want = tile >= 0 ? tile : g_force;
   int st = g_stages;
   bool ph = false;
+  // tiles 7 / 15: ping-pong loop on 256x256 / 256x128 (eight 128x64 / 128x32 waves),
+  // 2-byte dtypes, one-tap-per-K-tile gathers or two-source tails; else the heuristic
+  bool pp = false;
+  if (want == 7 || want == 15) {
+    const int c = want == 7 ? 5 : 6;
+    if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0 &&
+        (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0))) {
+      cfg = c;
+      pp = true;
+    }
+    want = -1;
+  }
   if (want >= 0 && want < 64) {
     const int c = want & 7;
     const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
@@ -1966,7 +2078,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   // direct NHWC epilogue, outputs addressable by a 32-bit buffer offset
   const bool persist_ok = sizeof(T) == 2 && g.mode == 0 && !g.hm && !g.cy &&
                           static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
-  const bool persist = persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
+  const bool persist = !pp && persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
@@ -2022,6 +2134,15 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
         case 5: launch_persist<T, 256, 256, 8, 2, DUAL>(g, nb, s); break;
         default: launch_persist<T, 256, 128, 8, 4, DUAL>(g, nb, s); break;
       }
+      return check_launch(what);
+    }
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (pp) {
+      if (cfg == 5)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, true>), dim3(nb), dim3(512), 0, s, g);
+      else
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 2, 2, DUAL, false, true>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
     }
   }
@@ -2090,7 +2211,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && (cfg & 7) != 7), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && ((cfg & 7) != 7 || cfg == 7 || cfg == 15)), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -2145,7 +2266,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -2177,7 +2298,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -2209,7 +2330,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && (tile & 7) != 7), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

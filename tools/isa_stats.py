@@ -18,12 +18,14 @@ def main():
         j = s.find('.Lfunc_end', i)
         body = s[i:j]
         meta = {}
-        for key in ('vgpr_count', 'agpr_count', 'sgpr_count', 'group_segment_fixed_size', 'private_segment_fixed_size',
-                    'vgpr_spill_count'):
-            mm = re.search(r'\.name:\s+' + re.escape(name) + r'[\s\S]{0,3000}?\.' + key + r':\s+(\d+)', s)
-            if not mm:
-                mm = re.search(r'\.' + key + r':\s+(\d+)[\s\S]{0,3000}?\.name:\s+' + re.escape(name) + r'\b', s)
-            meta[key] = mm.group(1) if mm else '?'
+        md = s[s.find('amdhsa.kernels'):]
+        for blk in re.split(r'\n  - ', md):  # one YAML entry per kernel
+            if re.search(r'\.name:\s+' + re.escape(name) + r'\s', blk):
+                for key in ('vgpr_count', 'agpr_count', 'sgpr_count', 'group_segment_fixed_size',
+                            'private_segment_fixed_size', 'vgpr_spill_count'):
+                    mm = re.search(r'\.' + key + r':\s+(\d+)', blk)
+                    meta[key] = mm.group(1) if mm else '?'
+                break
         waits = re.findall(r's_waitcnt\s+(.*)', body)
         vm = {}
         for w in waits:
