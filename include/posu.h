@@ -125,7 +125,8 @@ int posu_set_conv_chain8(int on);
  * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K
  * layers); + 16: a three-slot ring (two K-tiles in flight; not 5); 29: the phased
- * 256x256 loop; + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
+ * 256x256 loop; 7 / 15 (bf16/f16): the ping-pong loop on 256x256 / 256x128 (waves w and
+ * w + 4 of a SIMD one phase apart); + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
  * stride-1 convs and deconvs over whole output rows): the halo variant with tiles
  * 256x256, 256x128, 256x64, 128x128, 128x64; 69, 70, 72: single-halo-slot 256x64,
  * 128x64, 256x128 for C = one K-chunk); -1 restores the automatic choice. */
