@@ -126,7 +126,8 @@ int posu_set_conv_chain8(int on);
  * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K
  * layers); + 16: a three-slot ring (two K-tiles in flight; not 5); 29: the phased
  * 256x256 loop; 7 / 15 (bf16/f16): the ping-pong loop on 256x256 / 256x128 (waves w and
- * w + 4 of a SIMD one phase apart); + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
+ * w + 4 of a SIMD one phase apart); 23 / 31 (bf16/f16): 256x256 / 256x128 with waves 4-7
+ * staggered by half a K-tile; + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
  * stride-1 convs and deconvs over whole output rows): the halo variant with tiles
  * 256x256, 256x128, 256x64, 128x128, 128x64; 69, 70, 72: single-halo-slot 256x64,
  * 128x64, 256x128 for C = one K-chunk); -1 restores the automatic choice. */

@@ -283,8 +283,10 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 }
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false, bool PP = false>
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false, int LOOP = 0>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
+  constexpr bool PP = LOOP == 1;  // ping-pong halves
+  constexpr bool SG = LOOP == 2;  // waves 4-7 staggered by half a K-tile
   using O = Op<T>;
   constexpr int NT = NW * 64;
   constexpr int E = O::E;
@@ -671,6 +673,42 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         barrier();
       }
     }
+  } else if constexpr (SG) {
+    // Stagger (two-slot ring, one barrier per K-tile): waves 4-7 run half a K-tile behind
+    // waves 0-3 -- they keep the second k-step's fragments of K-tile t in registers and
+    // issue its MFMAs after the next barrier, while waves 0-3 wait for their first
+    // fragment reads; every read still happens before the barrier that frees its slot.
+    static_assert(S == 2 && NW == 8 && !PH, "stagger: eight waves, two slots");
+    const bool lag = wid_u >= 4;
+    uint4 hA[TM], hB[TN];
+    auto read = [&](const char* As_, const char* Bs_, int cb, uint4 (&a)[TM], uint4 (&b)[TN]) {
+      const int c = 4 * cb + q;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));
+    };
+    auto mma = [&](const uint4 (&a)[TM], const uint4 (&b)[TN]) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) O::mma(acc[i][j], b[j], a[i]);
+    };
+    POSU_DMA_TILE(0, 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      vm_wait<0>();
+      __syncthreads();
+      if (kt + 1 < nk) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
+      const char* As_ = smem + (kt & 1) * STAGE;
+      const char* Bs_ = As_ + A_BYTES;
+      uint4 af[TM], bfr[TN];
+      if (lag && kt > 0) mma(hA, hB);
+      read(As_, Bs_, 0, af, bfr);
+      mma(af, bfr);
+      read(As_, Bs_, 1, hA, hB);
+      if (!lag) mma(hA, hB);
+    }
+    if (lag) mma(hA, hB);
   } else if constexpr (PH) {
     // Phased 256x256 loop: each K-tile is four phases, one output quadrant
     // (64 rows x 32 columns of the wave's tile, 16 MFMAs) per phase, each phase staging
@@ -2012,7 +2050,9 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     if (g.hm && !g.cy && g_head256 && g.direct && g.CoutPad == 256) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
-      launch_cfg<T, 256, 256, 8, 2, DUAL>(g, g.mtiles * nclass, 2, s);
+      // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 2>), dim3(g.mtiles * nclass),
+                         dim3(512), 0, s, g);
       return check_launch(what);
     }
   }
@@ -2053,13 +2093,21 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   bool ph = false;
   // tiles 7 / 15: ping-pong loop on 256x256 / 256x128 (eight 128x64 / 128x32 waves),
   // 2-byte dtypes, one-tap-per-K-tile gathers or two-source tails; else the heuristic
-  bool pp = false;
+  // tiles 23 / 31: the staggered two-slot loop on 256x256 / 256x128 (any gather)
+  bool pp = false, sg = false;
   if (want == 7 || want == 15) {
     const int c = want == 7 ? 5 : 6;
     if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0 &&
         (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0))) {
       cfg = c;
       pp = true;
+    }
+    want = -1;
+  } else if (want == 23 || want == 31) {
+    const int c = want == 23 ? 5 : 6;
+    if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
+      cfg = c;
+      sg = true;
     }
     want = -1;
   }
@@ -2078,7 +2126,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   // direct NHWC epilogue, outputs addressable by a 32-bit buffer offset
   const bool persist_ok = sizeof(T) == 2 && g.mode == 0 && !g.hm && !g.cy &&
                           static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
-  const bool persist = !pp && persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
+  const bool persist = !pp && !sg && persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
@@ -2140,9 +2188,16 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   if constexpr (sizeof(T) == 2) {
     if (pp) {
       if (cfg == 5)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, true>), dim3(nb), dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 1>), dim3(nb), dim3(512), 0, s, g);
       else
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 2, 2, DUAL, false, true>), dim3(nb), dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 2, 2, DUAL, false, 1>), dim3(nb), dim3(512), 0, s, g);
+      return check_launch(what);
+    }
+    if (sg) {
+      if (cfg == 5)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 2>), dim3(nb), dim3(512), 0, s, g);
+      else
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, false, 2>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
     }
   }
@@ -2211,7 +2266,7 @@ using namespace posu;
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
 extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && ((cfg & 7) != 7 || cfg == 7 || cfg == 15)), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && ((cfg & 7) != 7 || cfg == 7 || cfg == 15 || cfg == 23 || cfg == 31)), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
   g_force = cfg;
   return POSU_OK;
 }
@@ -2266,7 +2321,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -2298,7 +2353,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -2330,7 +2385,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15)), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

@@ -73,15 +73,18 @@ class _Tuner:
 def _tile_candidates(cout):
     """Tile ids (include/posu.h): cfg 0..6, cfg + 8 = single-slot ring (four-wave tiles;
     short-K layers: more blocks per CU), cfg + 16 = three-slot ring (two K-tiles in flight),
-    cfg + 32 = persistent K-tile stream (epilogue stores overlap the next tile's fetch)."""
+    cfg + 32 = persistent K-tile stream (epilogue stores overlap the next tile's fetch),
+    23 / 31 = 256x256 / 256x128 with waves 4-7 staggered by half a K-tile."""
     cpad = (cout + 63) // 64 * 64
     c = [0, 1, 2]
     if cpad % 128 == 0:
         c += [3, 4, 6]
     if cpad % 256 == 0:
         c.append(5)
-    # + 32: the persistent K-tile stream (2-byte dtypes; others ignore the bit)
-    return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c]
+    # + 32: the persistent K-tile stream (2-byte dtypes; others ignore the bit);
+    # 23 / 31: the eight-wave tiles with waves 4-7 staggered by half a K-tile
+    sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)]
+    return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c] + sg
 
 
 def _tuned(key, cout, launch):

@@ -321,7 +321,7 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 29])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 23, 29, 31])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks and the
@@ -339,7 +339,7 @@ def test_every_tile_configuration_matches_torch(cuda, cfg, code):
         ops.force_conv_config(-1)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 15, 16, 29])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 15, 16, 23, 29, 31])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
     """The register-direct epilogue applies the same f32 arithmetic (BN, residual, ReLU,
@@ -456,8 +456,8 @@ def test_halo_variant_matches_gather_kernel(cuda, case, code):
 
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
-    """The phased 256x256 main loop (tile 29) and the ping-pong loops (tiles 7 / 15 on
-    256x256 / 256x128) keep each accumulator's K order, so their outputs equal the two-slot
+    """The phased 256x256 main loop (tile 29), the ping-pong loops (tiles 7 / 15 on
+    256x256 / 256x128) and the staggered loops (tiles 23 / 31) keep each accumulator's K order, so their outputs equal the two-slot
     loops (tiles 5 / 6) bit for bit: 3x3 + residual (ragged M), strided 1x1,
     ConvTranspose(4, s2) and the two-source Bottleneck tail."""
     dt = ops.torch_dtype(code)
@@ -477,7 +477,7 @@ def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
     wdc = (rnd(4, 256, 4 * 128).float() * 0.03).to(dt)
     assert (9 * 128) % bk == 0
     outs = {}
-    for t in (5, 29, 7, 6, 15):
+    for t in (5, 29, 7, 23, 6, 15, 31):
         outs[t] = [
             ops.conv2d_nhwc(x, w3, 256, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
             ops.conv2d_nhwc(x, w3[:, :128].contiguous(), 256, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
@@ -485,7 +485,7 @@ def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
             ops.conv1x1_dual_nhwc(x, x2, 2, wd, 256, sh, True, code, tile=t),
         ]
     torch.cuda.synchronize()
-    for t, base in ((29, 5), (7, 5), (15, 6)):
+    for t, base in ((29, 5), (7, 5), (23, 5), (15, 6), (31, 6)):
         for a, b in zip(outs[base], outs[t]):
             assert torch.equal(a, b), (t, float((a.float() - b.float()).abs().max()))
 
