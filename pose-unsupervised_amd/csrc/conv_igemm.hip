@@ -695,6 +695,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         for (int j = 0; j < TN; ++j) O::mma(acc[i][j], b[j], a[i]);
     };
     POSU_DMA_TILE(0, 0);
+    if (lag) __builtin_amdgcn_s_setprio(1);  // the lagging half wins issue arbitration (-2..-7 %)
     for (int kt = 0; kt < nk; ++kt) {
       vm_wait<0>();
       __syncthreads();
@@ -709,6 +710,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       if (!lag) mma(hA, hB);
     }
     if (lag) mma(hA, hB);
+    __builtin_amdgcn_s_setprio(0);
   } else if constexpr (PH) {
     // Phased 256x256 loop: each K-tile is four phases, one output quadrant
     // (64 rows x 32 columns of the wave's tile, 16 MFMAs) per phase, each phase staging
