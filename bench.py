@@ -267,7 +267,7 @@ def main():
             stage_geo(hm)
         torch.cuda.synchronize()
         if not args.no_autotune:  # per-layer conv tile choice, timed on the real operands
-            plan.autotune(plan.pack_input(views), chunks=args.chunks, keep_features=False)
+            plan.autotune(plan.pack_input(views), chunks=args.chunks, keep_features=False, reps=8)
             torch.cuda.synchronize()
         use_graph = not args.no_graph
         if use_graph:

@@ -2128,6 +2128,8 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   // direct NHWC epilogue, outputs addressable by a 32-bit buffer offset
   const bool persist_ok = sizeof(T) == 2 && g.mode == 0 && !g.hm && !g.cy &&
                           static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
+  // untuned eight-wave launches take the staggered loop (bit-exact with the plain one)
+  if (want < 0 && !g_persist && sizeof(T) == 2 && !pp && !ph && (cfg == 5 || cfg == 6)) sg = true;
   const bool persist = !pp && !sg && persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
