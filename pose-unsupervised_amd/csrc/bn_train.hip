@@ -10,6 +10,8 @@
 // follow torch.nn.BatchNorm2d: biased variance for normalisation, unbiased variance in
 // running_var, running = (1 - momentum) * running + momentum * batch, updated once per
 // segment in segment (= view) order like the reference's four backbone calls.
+#include <initializer_list>
+
 #include "posu_common.h"
 
 namespace posu {
@@ -24,12 +26,15 @@ struct RedShape {
 RedShape red_shape(int Pseg, int C, int E, int nseg) {
   RedShape r;
   r.CPR = C / E;
-  r.CB = std::min(r.CPR, 256);
+  r.CB = std::min(r.CPR, 64);  // one wave of channel chunks per pixel row: wide layers get more blocks
   r.PL = 256 / r.CB;
   r.CG = (r.CPR + r.CB - 1) / r.CB;
   int nb = std::max(1, 1024 / (r.CG * nseg));
   nb = std::min(nb, kMaxNB);
   nb = std::min(nb, std::max(1, Pseg / r.PL));
+  // f64 partials of wide, short layers (layer4: 2048 channels x 2048 pixels per view) stay
+  // below 1/8 of the input they reduce: at least 64 pixels per block
+  nb = std::min(nb, std::max(1, Pseg / 64));
   r.NB = nb;
   r.PPB = (Pseg + nb - 1) / nb;
   return r;
@@ -74,11 +79,12 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
   }
   if (active) {
     const int pbeg = blk * rs.PPB, pend = min(Pseg, pbeg + rs.PPB);
-    for (int p = pbeg + pl; p < pend; p += rs.PL) {
-      const size_t off = (static_cast<size_t>(seg) * Pseg + p) * C + ch * E;
+    const size_t sbase = static_cast<size_t>(seg) * Pseg * C + ch * E;
+    // one pixel's contribution, accumulated in pixel order (the sums do not depend on U)
+    auto acc = [&](const uint4& zq, const uint4& gq, const uint4& yq) {
       float v[E];
+      Vec<T>::unpack(zq, v);
       if constexpr (MODE == 0) {
-        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
 #pragma unroll
         for (int e = 0; e < E; ++e) {
           a[e] += v[e];
@@ -86,11 +92,10 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
         }
       } else {
         float gv[E];
-        Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + off), gv);
-        Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + off), v);
+        Vec<T>::unpack(gq, gv);
         if (y) {
           float yv[E];
-          Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + off), yv);
+          Vec<T>::unpack(yq, yv);
 #pragma unroll
           for (int e = 0; e < E; ++e) gv[e] = yv[e] > 0.f ? gv[e] : 0.f;
         } else if (msc) {  // ReLU mask recomputed from z (no residual): y > 0 <=> z*scale+shift > 0
@@ -103,6 +108,27 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
           b[e] += gv[e] * ((v[e] - mu[e]) * rd[e]);
         }
       }
+    };
+    // U pixels per step with all their loads issued first (memory-level parallelism)
+    constexpr int U = MODE == 0 ? 8 : 4;
+    const uint4 zero = make_uint4(0, 0, 0, 0);
+    int p = pbeg + pl;
+    for (; p + (U - 1) * rs.PL < pend; p += U * rs.PL) {
+      uint4 zq[U], gq[U], yq[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t off = sbase + static_cast<size_t>(p + u * rs.PL) * C;
+        zq[u] = *reinterpret_cast<const uint4*>(z + off);
+        gq[u] = MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero;
+        yq[u] = MODE == 1 && y ? *reinterpret_cast<const uint4*>(y + off) : zero;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc(zq[u], gq[u], yq[u]);
+    }
+    for (; p < pend; p += rs.PL) {
+      const size_t off = sbase + static_cast<size_t>(p) * C;
+      acc(*reinterpret_cast<const uint4*>(z + off), MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero,
+          MODE == 1 && y ? *reinterpret_cast<const uint4*>(y + off) : zero);
     }
   }
 #pragma unroll
@@ -215,6 +241,158 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ z, 
     }
     *reinterpret_cast<uint4*>(y + i * E) = Vec<T>::pack(v);
   }
+}
+
+// Segment-major variants (C / E divides 256): blockIdx.y = segment, a thread's channel
+// chunk never changes (the grid stride is a multiple of 256), so the per-channel
+// parameters live in registers; U chunks per step with their loads issued first.
+// Same arithmetic per element as the kernels above.
+constexpr int kSegU = 4;
+
+// E consecutive per-channel f32 parameters as 16-B loads (E = 4 or 8; every parameter
+// row starts at a multiple of 8 channels of a 16-B aligned allocation)
+template <int E>
+__device__ __forceinline__ void ldparams(const float* __restrict__ p, float* v) {
+#pragma unroll
+  for (int i = 0; i < E / 4; ++i) {
+    const float4 q = reinterpret_cast<const float4*>(p)[i];
+    v[4 * i] = q.x;
+    v[4 * i + 1] = q.y;
+    v[4 * i + 2] = q.z;
+    v[4 * i + 3] = q.w;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_apply_seg_kernel(const T* __restrict__ z, int Pseg, int C,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           const T* __restrict__ res, int relu, T* __restrict__ y) {
+  constexpr int E = Vec<T>::E, U = kSegU;
+  const int CPR = C / E, seg = blockIdx.y;
+  const int c0 = (threadIdx.x % CPR) * E;
+  float sc[E], sh[E];
+  ldparams<E>(scale + seg * C + c0, sc);
+  ldparams<E>(shift + seg * C + c0, sh);
+  const int n = Pseg * CPR, stride = gridDim.x * 256;
+  const T* __restrict__ zs = z + static_cast<size_t>(seg) * Pseg * C;
+  const T* __restrict__ rs = res ? res + static_cast<size_t>(seg) * Pseg * C : nullptr;
+  T* __restrict__ ys = y + static_cast<size_t>(seg) * Pseg * C;
+  auto one = [&](int i, const uint4& zq, const uint4& rq) {
+    float v[E], r[E];
+    Vec<T>::unpack(zq, v);
+    if (rs) Vec<T>::unpack(rq, r);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      float t = v[e] * sc[e] + sh[e];
+      if (rs) t += r[e];
+      v[e] = relu ? fmaxf(t, 0.f) : t;
+    }
+    *reinterpret_cast<uint4*>(ys + static_cast<size_t>(i) * E) = Vec<T>::pack(v);
+  };
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  int i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    uint4 zq[U], rq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      zq[u] = *reinterpret_cast<const uint4*>(zs + static_cast<size_t>(i + u * stride) * E);
+      rq[u] = rs ? *reinterpret_cast<const uint4*>(rs + static_cast<size_t>(i + u * stride) * E) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(i + u * stride, zq[u], rq[u]);
+  }
+  for (; i < n; i += stride)
+    one(i, *reinterpret_cast<const uint4*>(zs + static_cast<size_t>(i) * E),
+        rs ? *reinterpret_cast<const uint4*>(rs + static_cast<size_t>(i) * E) : zero);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restrict__ gy, const T* __restrict__ y,
+                                                               const float* __restrict__ msc,
+                                                               const float* __restrict__ msh,
+                                                               const T* __restrict__ z, int Pseg, int C,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const float* __restrict__ coef, T* __restrict__ dz,
+                                                               T* __restrict__ gres) {
+  constexpr int E = Vec<T>::E, U = kSegU;
+  const int CPR = C / E, seg = blockIdx.y;
+  const int c0 = (threadIdx.x % CPR) * E;
+  float mu[E], rd[E], k1[E], mg[E], mgx[E], ks[E], kh[E];
+  ldparams<E>(mean + seg * C + c0, mu);
+  ldparams<E>(rstd + seg * C + c0, rd);
+  ldparams<E>(coef + (seg * 3 + 0) * C + c0, k1);
+  ldparams<E>(coef + (seg * 3 + 1) * C + c0, mg);
+  ldparams<E>(coef + (seg * 3 + 2) * C + c0, mgx);
+  if (msc) {
+    ldparams<E>(msc + seg * C + c0, ks);
+    ldparams<E>(msh + seg * C + c0, kh);
+  } else {
+#pragma unroll
+    for (int e = 0; e < E; ++e) ks[e] = kh[e] = 0.f;
+  }
+  const int n = Pseg * CPR, stride = gridDim.x * 256;
+  const size_t sb = static_cast<size_t>(seg) * Pseg * C;
+  auto one = [&](int i, const uint4& gq, const uint4& zq, const uint4& yq) {
+    const size_t off = sb + static_cast<size_t>(i) * E;
+    float g[E], v[E];
+    Vec<T>::unpack(gq, g);
+    Vec<T>::unpack(zq, v);
+    if (y) {
+      float yv[E];
+      Vec<T>::unpack(yq, yv);
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
+    } else if (msc) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = v[e] * ks[e] + kh[e] > 0.f ? g[e] : 0.f;
+    }
+    if (gres) *reinterpret_cast<uint4*>(gres + off) = Vec<T>::pack(g);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const float xh = (v[e] - mu[e]) * rd[e];
+      v[e] = k1[e] * (g[e] - mg[e] - xh * mgx[e]);
+    }
+    *reinterpret_cast<uint4*>(dz + off) = Vec<T>::pack(v);
+  };
+  const uint4 zero = make_uint4(0, 0, 0, 0);
+  int i = blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < n; i += U * stride) {
+    uint4 gq[U], zq[U], yq[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t off = sb + static_cast<size_t>(i + u * stride) * E;
+      gq[u] = *reinterpret_cast<const uint4*>(gy + off);
+      zq[u] = *reinterpret_cast<const uint4*>(z + off);
+      yq[u] = y ? *reinterpret_cast<const uint4*>(y + off) : zero;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) one(i + u * stride, gq[u], zq[u], yq[u]);
+  }
+  for (; i < n; i += stride) {
+    const size_t off = sb + static_cast<size_t>(i) * E;
+    one(i, *reinterpret_cast<const uint4*>(gy + off), *reinterpret_cast<const uint4*>(z + off),
+        y ? *reinterpret_cast<const uint4*>(y + off) : zero);
+  }
+}
+
+// blocks per segment of a segment-major launch: at least 16 chunks per thread (the
+// per-channel parameters are loaded once per thread), at most about 1024 blocks in all
+inline int seg_blocks(int Pseg, int C, int E, int nseg) {
+  const long long chunks = static_cast<long long>(Pseg) * (C / E);
+  const long long need = (chunks + 256LL * 16 - 1) / (256LL * 16);
+  const long long cap = std::max(1, 1024 / nseg);
+  return static_cast<int>(std::max(1LL, std::min(need, cap)));
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<size_t>(p) & 15) == 0; }
+
+inline bool seg_major(int C, int E, int nseg, int Pseg, std::initializer_list<const void*> params) {
+  for (const void* p : params)
+    if (p && !aligned16(p)) return false;
+  const int cpr = C / E;
+  return cpr > 0 && 256 % cpr == 0 && nseg <= 65535 && static_cast<long long>(Pseg) * cpr < (1LL << 31);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
@@ -431,8 +609,15 @@ extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C
   POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_bn_apply: bad shape");
   hipStream_t s = as_stream(stream);
   const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
+  const int E = chunk_elems(dtype);
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
+    if (seg_major(C, E, nseg, Pseg, {scale, shift})) {
+      hipLaunchKernelGGL(bn_apply_seg_kernel<T>, dim3(seg_blocks(Pseg, C, E, nseg), nseg), dim3(256), 0, s,
+                         static_cast<const T*>(z), Pseg, C, scale, shift, static_cast<const T*>(residual), relu,
+                         static_cast<T*>(y));
+      return;
+    }
     hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(z), Pseg,
                        C, scale, shift, static_cast<const T*>(residual), relu, static_cast<T*>(y), total);
   });
@@ -465,6 +650,14 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
                      rstd, coef, dgamma, dbeta);
   with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
+    const int E = chunk_elems(dtype);
+    if (seg_major(C, E, nseg, Pseg, {mean, rstd, coef, relu_scale, relu_shift})) {
+      hipLaunchKernelGGL(bn_bwd_apply_seg_kernel<T>, dim3(seg_blocks(Pseg, C, E, nseg), nseg), dim3(256), 0, s,
+                         static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale, relu_shift,
+                         static_cast<const T*>(z), Pseg, C, mean, rstd, coef, static_cast<T*>(dz),
+                         static_cast<T*>(gres));
+      return;
+    }
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(gy),
                        static_cast<const T*>(y), relu_scale, relu_shift, static_cast<const T*>(z), Pseg, C, mean, rstd, coef,
                        static_cast<T*>(dz), static_cast<T*>(gres), total);

@@ -133,9 +133,10 @@ def _bn_ref(z, nseg, gamma, beta, rm, rv, res, relu):
 @pytest.mark.parametrize('c,nseg,residual,relu', [(64, 4, False, True), (256, 2, True, True),
                                                   (2048, 1, False, False), (128, 4, True, True)])
 @pytest.mark.parametrize('code', [F32, BF16])
-def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, relu, code):
+@pytest.mark.parametrize('size', [(2, 9, 7), (3, 24, 20)])  # the larger one runs the unrolled loops
+def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, relu, code, size):
     g = torch.Generator().manual_seed(14)
-    b, h, w = 2, 9, 7
+    b, h, w = size
     dt = ops.torch_dtype(code)
     # activations representable in the compute dtype, so the reference sees the same
     # inputs (and the same ReLU mask) as the kernels

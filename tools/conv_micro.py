@@ -28,9 +28,12 @@ CASES = {
     'l1c3r': ('conv', 64, 64, 64, 256, 1, 1, 0),  # with the residual add (Bottleneck tail)
     'l2c2': ('conv', 32, 32, 128, 128, 3, 1, 1),
     'l2c3': ('conv', 32, 32, 128, 512, 1, 1, 0),
+    'l2c3r': ('conv', 32, 32, 128, 512, 1, 1, 0),
+    'l2c1': ('conv', 32, 32, 512, 128, 1, 1, 0),
     'l3c1': ('conv', 16, 16, 1024, 256, 1, 1, 0),
     'l3c2': ('conv', 16, 16, 256, 256, 3, 1, 1),
     'l3c3': ('conv', 16, 16, 256, 1024, 1, 1, 0),
+    'l3c3r': ('conv', 16, 16, 256, 1024, 1, 1, 0),
     'l4c2': ('conv', 8, 8, 512, 512, 3, 1, 1),
     'deconv1': ('deconv', 8, 8, 2048, 256, 4, 2, 1),
     'deconv2': ('deconv', 16, 16, 256, 256, 4, 2, 1),
