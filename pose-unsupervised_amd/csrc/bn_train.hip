@@ -29,7 +29,7 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
   r.CB = std::min(r.CPR, 64);  // one wave of channel chunks per pixel row: wide layers get more blocks
   r.PL = 256 / r.CB;
   r.CG = (r.CPR + r.CB - 1) / r.CB;
-  int nb = std::max(1, 1024 / (r.CG * nseg));
+  int nb = std::max(1, 512 / (r.CG * nseg));  // <= 128 partial blocks per view of 4: one load round per finalize lane
   nb = std::min(nb, kMaxNB);
   nb = std::min(nb, std::max(1, Pseg / r.PL));
   // f64 partials of wide, short layers (layer4: 2048 channels x 2048 pixels per view) stay
@@ -158,30 +158,46 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
   }
 }
 
-// ---- finalize: one block per FCH channels, FLN lanes sum the partial blocks of a
-// segment (16 strided loads per lane in flight), fixed-order LDS combine.
-constexpr int FCH = 16, FLN = 16;
+// ---- finalize: one block per FCH channels, FLN lanes sum the partial blocks of up to
+// FSEG segments at once (every load of the pass in flight together: the partials are a few
+// hundred KiB, so this pass is latency-bound), fixed-order LDS combine.  Per segment the
+// summation order is the blocks' order, whatever the grouping.
+constexpr int FCH = 8, FLN = 32, FSEG = 4;
 
-__device__ __forceinline__ void reduce_seg(const double* __restrict__ part, int seg, int NB, int C, int c, bool valid,
-                                           int cl, int ln, double (*red)[FLN][FCH], double& s, double& q) {
-  double a = 0.0, b = 0.0;
+__device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int seg0, int ns, int NB, int C, int c,
+                                            bool valid, int cl, int ln, double (*red)[FSEG][FLN][FCH], double* s,
+                                            double* q) {
+  double a[FSEG], b[FSEG];
+#pragma unroll
+  for (int k = 0; k < FSEG; ++k) a[k] = b[k] = 0.0;
   if (valid) {
-    const double* base = part + static_cast<size_t>(seg) * NB * 2 * C;
+    const double* base = part + static_cast<size_t>(seg0) * NB * 2 * C + c;
 #pragma unroll 4
     for (int blk = ln; blk < NB; blk += FLN) {
-      a += base[static_cast<size_t>(blk) * 2 * C + c];
-      b += base[static_cast<size_t>(blk) * 2 * C + C + c];
+#pragma unroll
+      for (int k = 0; k < FSEG; ++k)
+        if (k < ns) {
+          const double* p = base + (static_cast<size_t>(k) * NB + blk) * 2 * C;
+          a[k] += p[0];
+          b[k] += p[C];
+        }
     }
   }
-  red[0][ln][cl] = a;
-  red[1][ln][cl] = b;
+#pragma unroll
+  for (int k = 0; k < FSEG; ++k) {
+    red[0][k][ln][cl] = a[k];
+    red[1][k][ln][cl] = b[k];
+  }
   __syncthreads();
-  s = 0.0;
-  q = 0.0;
   if (ln == 0)
-    for (int l = 0; l < FLN; ++l) {
-      s += red[0][l][cl];
-      q += red[1][l][cl];
+#pragma unroll
+    for (int k = 0; k < FSEG; ++k) {
+      s[k] = 0.0;
+      q[k] = 0.0;
+      for (int l = 0; l < FLN; ++l) {
+        s[k] += red[0][k][l][cl];
+        q[k] += red[1][k][l][cl];
+      }
     }
   __syncthreads();
 }
@@ -193,27 +209,32 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
                                                                 float* running_var, float* __restrict__ mean,
                                                                 float* __restrict__ rstd, float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
-  __shared__ double red[2][FLN][FCH];
+  __shared__ double red[2][FSEG][FLN][FCH];
   const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
-  for (int seg = 0; seg < nseg; ++seg) {  // in segment order: running stats compose like V calls
-    double sum, sq;
-    reduce_seg(part, seg, NB, C, c, valid, cl, ln, red, sum, sq);
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    double sums[FSEG], sqs[FSEG];
+    const int ns = min(FSEG, nseg - seg0);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sums, sqs);
     if (ln != 0 || !valid) continue;
-    const double mu = sum / n;
-    const double var = fmax(sq / n - mu * mu, 0.0);
-    const double r = 1.0 / sqrt(var + static_cast<double>(eps));
-    const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-    mean[seg * C + c] = static_cast<float>(mu);
-    rstd[seg * C + c] = static_cast<float>(r);
-    scale[seg * C + c] = static_cast<float>(gm * r);
-    shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
-    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mu);
-    if (running_var)
-      running_var[c] = (1.f - momentum) * running_var[c] +
-                       momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+    for (int k = 0; k < ns; ++k) {  // in segment order: running stats compose like V calls
+      const int seg = seg0 + k;
+      const double sum = sums[k], sq = sqs[k];
+      const double mu = sum / n;
+      const double var = fmax(sq / n - mu * mu, 0.0);
+      const double r = 1.0 / sqrt(var + static_cast<double>(eps));
+      const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+      mean[seg * C + c] = static_cast<float>(mu);
+      rstd[seg * C + c] = static_cast<float>(r);
+      scale[seg * C + c] = static_cast<float>(gm * r);
+      shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
+      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mu);
+      if (running_var)
+        running_var[c] = (1.f - momentum) * running_var[c] +
+                         momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+    }
   }
 }
 
@@ -400,22 +421,27 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
                                                               const float* __restrict__ rstd,
                                                               float* __restrict__ coef, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  __shared__ double red[2][FLN][FCH];
+  __shared__ double red[2][FSEG][FLN][FCH];
   const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
   double tg = 0.0, tgx = 0.0;
-  for (int seg = 0; seg < nseg; ++seg) {
-    double sg, sgx;
-    reduce_seg(part, seg, NB, C, c, valid, cl, ln, red, sg, sgx);
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    double sgs[FSEG], sgxs[FSEG];
+    const int ns = min(FSEG, nseg - seg0);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sgs, sgxs);
     if (ln != 0 || !valid) continue;
-    tg += sg;
-    tgx += sgx;
-    const float gm = gamma ? gamma[c] : 1.f;
-    coef[(seg * 3 + 0) * C + c] = gm * rstd[seg * C + c];
-    coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
-    coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
+    for (int k = 0; k < ns; ++k) {
+      const int seg = seg0 + k;
+      const double sg = sgs[k], sgx = sgxs[k];
+      tg += sg;
+      tgx += sgx;
+      const float gm = gamma ? gamma[c] : 1.f;
+      coef[(seg * 3 + 0) * C + c] = gm * rstd[seg * C + c];
+      coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
+      coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
+    }
   }
   if (ln == 0 && valid) {
     if (dgamma) dgamma[c] = static_cast<float>(tgx);
@@ -467,12 +493,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 
 __global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double* __restrict__ part, int NB, int C,
                                                                    float* __restrict__ out) {
-  __shared__ double red[2][FLN][FCH];
+  __shared__ double red[2][FSEG][FLN][FCH];
   const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
   const int c = blockIdx.x * FCH + cl;
-  double s, q;
-  reduce_seg(part, 0, NB, C, c, c < C, cl, ln, red, s, q);
-  if (ln == 0 && c < C) out[c] = static_cast<float>(s);
+  double s[FSEG], q[FSEG];
+  reduce_segs(part, 0, 1, NB, C, c, c < C, cl, ln, red, s, q);
+  if (ln == 0 && c < C) out[c] = static_cast<float>(s[0]);
 }
 
 // ---- max-pool 3x3 / s2 / p1 backward (PyTorch's tie rule: the first maximum in

@@ -131,7 +131,8 @@ def _bn_ref(z, nseg, gamma, beta, rm, rv, res, relu):
 
 
 @pytest.mark.parametrize('c,nseg,residual,relu', [(64, 4, False, True), (256, 2, True, True),
-                                                  (2048, 1, False, False), (128, 4, True, True)])
+                                                  (2048, 1, False, False), (128, 4, True, True),
+                                                  (64, 6, True, True)])  # 6 segments: two finalize passes
 @pytest.mark.parametrize('code', [F32, BF16])
 @pytest.mark.parametrize('size', [(2, 9, 7), (3, 24, 20)])  # the larger one runs the unrolled loops
 def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, relu, code, size):
