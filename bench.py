@@ -1,25 +1,41 @@
 """Benchmark of the 4-view hot path (BASELINE.json metric: 4-view 256x256 frames/sec,
-fwd + triangulate).
+fwd + triangulate; MPJPE-mm vs ref).
 
 One step = one batch of 32 groups x 4 views (128 frames, 256x256, synthetic N(0,1)
 crops already resident in HBM) through
     PoseResNet-50 forward (bf16 MFMA kernels) -> soft-argmax + crop affine
     -> epipolar loss -> fp64 DLT triangulation,
-captured as two hipGraphs (network | decode+geometry) and replayed.  With --gpus N
-(launched by torch.distributed.run) every rank processes its own 32 groups (weak
-scaling, no data-path collective); time = max over ranks.
+captured as two hipGraphs per input batch (network | decode+geometry) and replayed.
+The timed steps rotate over --batches distinct input batches (3 x 100 MB of crops, more
+than the 256 MiB Infinity Cache holds), so no step reads inputs an earlier step left
+on-die.
 
-Also reported, on the same JSON line:
-  roofline     -- the conv stack (implicit-GEMM MFMA kernels): 14.47 GFLOP/frame x 128
-                  frames per network replay / its HIP-event time, against the dense bf16
-                  MFMA peak (2.5 PFLOP/s);
-  cpu_baseline -- the CPU oracle (torch-CPU fp32 restatement of the reference path + the
-                  numpy pymvg-style triangulation) timed on the host cores on a bounded
-                  sample, rank 0 at N = 1 only.
+Multi-GPU: `python bench.py --gpus N` starts N ranks itself (one process per GPU,
+torch.distributed.run, 127.0.0.1 rendezvous) before this process touches the GPU; the
+driver's `python -m torch.distributed.run ... bench.py --gpus N` lands directly in the
+rank code.  Every rank processes its own 32 groups per step (weak scaling, no data-path
+collective; the reference's DistributedSampler sharding, lib/utils/utils.py:134-141),
+`dist.get_world_size() == N` is asserted, time = max over ranks, value = all ranks'
+frames / that time.
+
+Also reported, on the same JSON line (rank 0):
+  roofline       -- the network (fused stem + implicit-GEMM MFMA conv stack + fused
+                    deconv/head): 14.47 GFLOP/frame x 128 frames per replay / its
+                    HIP-event time on the launch stream, against the dense bf16 peak;
+  mpjpe_vs_ref_mm -- the bench chain's triangulated joints against the CPU oracle chain
+                    (fp32 reference network + soft-argmax + affine + fp64 triangulation)
+                    on the same first input batch, as run/test/test_triangulate.py:98-102
+                    computes MPJPE (mean / std / max per-joint error, mm);
+  fp32_mode      -- frames/s of the same pipeline with the exact-f32 kernels (parity mode);
+  cpu_baseline   -- that oracle chain timed on the host cores (rank 0 at N = 1): the full
+                    32 x 4 batch (configs[2]) and batch 1 (configs[0]).
+`--dry-run` runs the launcher and the rank plumbing on CPU (gloo) without any GPU work.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -48,18 +64,104 @@ def parse():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--groups', type=int, default=32, help='4-view groups per GPU per step')
+    ap.add_argument('--batches', type=int, default=3, help='distinct input batches rotated over the timed steps')
     ap.add_argument('--layers', type=int, default=50)
     ap.add_argument('--size', type=int, default=256)
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
+    ap.add_argument('--tune-file', default='',
+                    help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
+                         'after autotuning -- profile runs load it so traces hold no trial launches')
     ap.add_argument('--chunks', type=int, default=1,
                     help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-mpjpe', action='store_true', help='skip the oracle-chain MPJPE check')
+    ap.add_argument('--fp32-steps', type=int, default=5, help='timed steps of the fp32 parity mode (0: skip)')
+    ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
     return ap.parse_args()
 
 
+# ------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(args):
+    """One process per GPU, started before this process makes any HIP call (the
+    reference's mp.spawn + init_process_group, run/pose2d/train.py:129-135)."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(args.gpus),
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    env.setdefault('OMP_NUM_THREADS', '1')
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args, backend, device=None):
+    """-> (rank, local, world, dist or None); asserts the job has exactly --gpus ranks."""
+    from posu import dist as pdist
+    rank, local, world = pdist.env_rank()
+    if world != args.gpus:
+        raise SystemExit('bench.py: WORLD_SIZE=%d but --gpus %d' % (world, args.gpus))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        pdist.init(backend, device=device)
+        got = dist.get_world_size()
+        assert got == args.gpus, 'process group has %d ranks, expected %d' % (got, args.gpus)
+    return rank, local, world, dist
+
+
+def gather_per_rank(values, dist, device='cpu'):
+    """All ranks' small float vectors (rank order), e.g. [frames, seconds]."""
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
+    if dist is None:
+        return [t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def dry_run_main(args):
+    """The rank plumbing of the real run on CPU (gloo): world size check, per-rank group
+    shards, barrier-bracketed timing, max over ranks, all ranks' frames.  No GPU work: the
+    per-step work is a stand-in (a small CPU matmul per group), so `value` is not a
+    measurement of the hot path and the line says so."""
+    from posu import dist as pdist
+    rank, local, world, dist = init_ranks(args, 'gloo')
+    groups = pdist.shard_groups(args.groups * world, rank, world)
+    a = torch.randn(64, 64)
+
+    def step():
+        for _ in groups:
+            a.mm(a)
+    for _ in range(args.warmup):
+        step()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if dist is not None:
+        dist.barrier()
+    elapsed = pdist.max_over_ranks(time.perf_counter() - t0)
+    per_rank = gather_per_rank([4 * len(groups) * args.steps, elapsed], dist)
+    if rank == 0:
+        print(json.dumps({'metric': METRIC + ' [dry run: launcher plumbing only, no GPU work]',
+                          'value': pdist.throughput(4 * len(groups), args.steps, world, elapsed), 'unit': 'frames/s',
+                          'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup, 'dry_run': True,
+                          'per_rank_frames': [int(p[0]) for p in per_rank], 'groups_per_rank': len(groups)}))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ model / oracle
 def build_model(layers, size, precision, device):
     from models.pose_resnet import get_pose_net
     from posu import synthetic as syn
@@ -68,10 +170,15 @@ def build_model(layers, size, precision, device):
     return net.to(device).eval()
 
 
+def input_views(groups, size, rank, b, device):
+    from posu import synthetic as syn
+    return [v.to(device) for v in syn.synthetic_views(4, groups, size, seed=100 + 16 * rank + b)]
+
+
 def pmc_traffic(layers, size, precision, groups):
     """HBM bytes of one network forward from the newest committed PMC reduction
-    (profiles/<round>/pmc_traffic_network.txt, tools/profile_round.sh), for the default
-    workload it was measured on; None otherwise."""
+    (profiles/<round>/pmc_traffic_network.txt, written by tools/profile_round.sh with the
+    commit it was measured at), for the default workload; (None, None) otherwise."""
     if (layers, size, precision, groups) != (50, 256, 'bf16', 32):
         return None, None
     import glob
@@ -80,59 +187,317 @@ def pmc_traffic(layers, size, precision, groups):
         return None, None
     with open(files[-1]) as f:
         d = json.loads(f.readline())
-    return d['traffic_bytes'], os.path.relpath(files[-1], REPO)
+    return d['traffic_bytes'], {'file': os.path.relpath(files[-1], REPO), 'commit': d.get('commit')}
 
 
-def cpu_baseline(layers, size, seconds):
-    """Oracle chain on the host cores for a bounded sample of the same workload."""
+def oracle_chain(sd, layers, size, views_cpu, host, full=False):
+    """CPU oracle of the whole step on one batch: fp32 reference network -> soft-argmax ->
+    crop affine -> FundamentalLoss -> fp64 triangulation.  Returns X [G, J, 3] (full: a
+    dict with the heatmaps, image-px joints [V, G, J, 2], the loss and X)."""
     from oracle import geometry_ref as G
     from oracle import pose_resnet_ref as PR
+    ng = views_cpu[0].shape[0]
+    hm, _, _ = PR.pose_resnet_forward(torch.cat(views_cpu, 0), sd, layers)
+    sa = G.softargmax2d(hm)
+    img = G.transform_back(sa, host['centers'].reshape(-1, 2), host['scales'].reshape(-1, 2), [size // 4] * 2)
+    joints = [img[v * ng:(v + 1) * ng] for v in range(4)]
+    loss = G.fundamental_loss(joints, [torch.ones(ng, 16, 1)] * 4, host['subjects'], host['F_dict'])
+    p2d = torch.stack(joints, 1).reshape(ng * 4, 16, 2).double().numpy()   # group-major, view-minor
+    X = G.triangulate_poses(host['cams'], p2d)
+    if full:
+        return {'heatmaps': hm, 'joints': torch.stack(joints), 'loss': float(loss), 'X': X}
+    return X
+
+
+def cpu_baseline(layers, size, groups, seconds):
+    """The oracle chain on the host cores: the full configs[2] batch (groups x 4 frames,
+    repeated until `seconds` have passed, at least once) and configs[0] (batch 1,
+    forward only).  Returns (cpu_baseline dict, the first full batch's oracle outputs)."""
     from models.pose_resnet import get_pose_net
+    from oracle import pose_resnet_ref as PR
     from posu import synthetic as syn
+    from posu.pipeline import synthetic_meta
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(layers, size))
-    ng = 1  # one 4-view group per iteration
-    meta_host = _cpu_meta(ng, size)
-    views = syn.synthetic_views(4, ng, size, seed=0)
-    x = torch.cat(views, 0)
-
-    def one():
-        hm, _, _ = PR.pose_resnet_forward(x, sd, layers)
-        sa = G.softargmax2d(hm)
-        img = G.transform_back(sa, meta_host['centers'], meta_host['scales'], [size // 4, size // 4])
-        joints = [img[v * ng:(v + 1) * ng] for v in range(4)]
-        G.fundamental_loss(joints, [torch.ones(ng, 16, 1)] * 4, meta_host['subjects'], meta_host['F_dict'])
-        p2d = torch.stack(joints, 1).reshape(ng * 4, 16, 2).double().numpy()
-        G.triangulate_poses(meta_host['cams'], p2d)
-    one()
-    frames, t0 = 0, time.perf_counter()
+    _, host = synthetic_meta(groups, 'cpu', image_size=size)
+    views = syn.synthetic_views(4, groups, size, seed=100)
+    frames, ref, t0 = 0, None, time.perf_counter()
     while True:
-        one()
-        frames += 4 * ng
+        out = oracle_chain(sd, layers, size, views, host, full=ref is None)
+        ref = out if ref is None else ref
+        frames += 4 * groups
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {'value': frames / el, 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d frames (%d 4-view groups, 1 group per iteration) of the same R%d@%d workload through '
-                      'the CPU oracle: torch-CPU fp32 forward + soft-argmax + transform_back + FundamentalLoss + '
-                      'numpy DLT/SVD triangulation, %.1f s' % (frames, frames // 4, layers, size, el)}
+    x1 = syn.synthetic_views(1, 1, size, seed=7)[0]
+    PR.pose_resnet_forward(x1, sd, layers)
+    n1, t1 = 0, time.perf_counter()
+    while n1 < 3 or time.perf_counter() - t1 < min(3.0, seconds / 4):
+        PR.pose_resnet_forward(x1, sd, layers)
+        n1 += 1
+    c1_ms = (time.perf_counter() - t1) / n1 * 1e3
+    ref['host'] = host
+    return ({'value': round(frames / el, 3), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+             'sample': '%d frames = %d pass(es) of the full %dx4 batch (R%d@%d) through the CPU oracle chain: '
+                       'torch-CPU fp32 forward + soft-argmax + transform_back + FundamentalLoss + numpy DLT/SVD '
+                       'triangulation, %.1f s' % (frames, frames // (4 * groups), groups, layers, size, el),
+             'batch1_forward_ms': round(c1_ms, 2), 'batch1_frames_per_s': round(1e3 / c1_ms, 3)}, ref)
 
 
-def _cpu_meta(ng, size):
-    from posu import synthetic as syn
-    from multiviews.cameras import project_pose
-    cams = syn.group_cameras(ng)
-    poses = syn.synthetic_poses3d(ng)
-    centers = np.zeros((4 * ng, 2))
-    for g in range(ng):
-        for v in range(4):
-            centers[v * ng + g] = project_pose(poses[g, :1], cams[g * 4 + v])[0]
-    return {'cams': cams, 'centers': centers, 'scales': np.full((4 * ng, 2), 5.0),
-            'subjects': syn.group_subjects(ng), 'F_dict': syn.fundamental_dict()}
+def compare_with_reference(out, ref, meta, dev):
+    """The bench chain's outputs on its first input batch (heatmaps, image-px joints
+    [V, G, J, 2], epipolar loss, X) against the CPU oracle chain's (the checker).
+
+    * heatmaps / joints / loss: direct differences.
+    * triangulation_same_2d: X from the device kernel vs the oracle's triangulation of the
+      SAME device joints -- the triangulation's own parity (BASELINE's 1e-2 mm gate).
+    * mpjpe (the bench line's mpjpe_vs_ref_mm): the pipeline's 2-D deviation from the
+      reference chain, d = joints - joints_ref, laid on consistent geometry -- the
+      synthetic 3-D poses projected into the group's cameras (p) -- and triangulated:
+      device kernel on p + d against the oracle on p, per-joint error (mm) with
+      run/test/test_triangulate.py:98-102's arithmetic.  The raw end-to-end X of a
+      random-weight network is no measure: its four views' soft-argmax joints are
+      mutually inconsistent, so the DLT solution sits near the plane at infinity and
+      moves by metres for sub-pixel input changes (kept as raw_end_to_end for the record)."""
+    from oracle import geometry_ref as G
+    from posu import ops
+    from posu.metrics import mpjpe_stats
+    host = ref['host']
+    V, ng, J = 4, ref['joints'].shape[1], ref['joints'].shape[2]
+    hm_err = (out['hm0'] - ref['heatmaps']).abs()
+    jerr = np.linalg.norm(out['coords0'] - ref['joints'].numpy(), axis=-1)
+    p2d = out['coords0'].transpose(1, 0, 2, 3).reshape(ng * V, J, 2).astype(np.float64)
+    tri = mpjpe_stats(out['X0'], G.triangulate_poses(host['cams'], p2d))
+    proj = np.stack([np.stack([G.project_pose(host['poses3d'][g], host['cams'][g * V + v]) for g in range(ng)])
+                     for v in range(V)])                                             # [V, G, J, 2]
+    d = out['coords0'].astype(np.float64) - ref['joints'].numpy().astype(np.float64)
+    Xb = ops.triangulate_dlt(meta.M, meta.intr, torch.from_numpy(proj + d).to(dev), None, undistort=True,
+                             view_major=True).cpu().numpy()
+    Xr = G.triangulate_poses(host['cams'], proj.transpose(1, 0, 2, 3).reshape(ng * V, J, 2))
+    st = mpjpe_stats(Xb, Xr)
+    raw = mpjpe_stats(out['X0'], ref['X'])
+    r6 = lambda v: float('%.6g' % v)  # noqa: E731
+    return {'mean': r6(st['mean']), 'std': r6(st['std']), 'max': r6(st['max']),
+            'heatmap_abs_err': {'max': r6(hm_err.max()), 'mean': r6(hm_err.mean())},
+            'joints_px_err': {'max': r6(jerr.max()), 'mean': r6(jerr.mean())},
+            'epipolar_loss_rel_err': r6(abs(out['loss0'] / ref['loss'] - 1)),
+            'triangulation_same_2d_mm': {'mean': r6(tri['mean']), 'max': r6(tri['max'])},
+            'raw_end_to_end_mm': {'mean': r6(raw['mean']), 'max': r6(raw['max'])}}
 
 
+# ------------------------------------------------------------------ inference
+class Replayer:
+    """Network and decode+geometry stages of one input batch, captured as two hipGraphs."""
+
+    def __init__(self, plan, views, meta, groups, chunks, use_graph, dev):
+        from posu import ops
+        self.plan, self.views, self.meta, self.groups, self.chunks = plan, views, meta, groups, chunks
+        self.ops = ops
+        self.use_graph = use_graph
+        self.dev = dev
+
+    def stage_net(self):
+        return self.plan.run(self.plan.pack_input(self.views), chunks=self.chunks, keep_features=False)[0]
+
+    def stage_geo(self, hm):
+        ops, meta = self.ops, self.meta
+        coords = ops.softargmax2d(hm, beta=100.0, affine=meta.affines).view(4, self.groups, hm.shape[1], 2)
+        loss = ops.epipolar_loss(coords, meta.weights, meta.F, meta.subj)
+        X = ops.triangulate_dlt(meta.M, meta.intr, coords, None, undistort=True, view_major=True)
+        return coords, loss, X
+
+    def capture(self):
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.stage_geo(self.stage_net())
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        torch.cuda.synchronize()
+        self.g_net, self.g_geo = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_net):
+            self.hm = self.stage_net()
+        with torch.cuda.graph(self.g_geo, pool=self.g_net.pool()):
+            self.out = self.stage_geo(self.hm)
+        torch.cuda.synchronize()
+
+    def run_net(self):
+        if self.use_graph:
+            self.g_net.replay()
+            return self.hm
+        self.hm = self.stage_net()
+        return self.hm
+
+    def run_geo(self, hm):
+        if self.use_graph:
+            self.g_geo.replay()
+            return self.out
+        self.out = self.stage_geo(hm)
+        return self.out
+
+
+def load_tiles(path):
+    from posu import plan as pl
+    with open(path) as f:
+        table = json.load(f)
+    for entry in table['tiles']:
+        pl._TUNE_CACHE[tuple(_tup(entry['key']))] = entry['tile']
+    return len(table['tiles'])
+
+
+def _tup(x):
+    return tuple(_tup(v) for v in x) if isinstance(x, list) else x
+
+
+def save_tiles(path):
+    from posu import plan as pl
+    with open(path, 'w') as f:
+        json.dump({'tiles': [{'key': list(k), 'tile': t} for k, t in pl.tuned_tiles().items()]}, f)
+
+
+def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, dist=None):
+    """Build, (auto)tune, capture and time the pipeline in one precision; returns a dict."""
+    from posu.pipeline import synthetic_meta
+    net = build_model(args.layers, args.size, precision, dev)
+    meta, _ = synthetic_meta(args.groups, dev, image_size=args.size)
+    plan = net.plan(dev)
+    reps = [Replayer(plan, input_views(args.groups, args.size, rank, b, dev), meta, args.groups, args.chunks,
+                     not args.no_graph, dev) for b in range(nbatch)]
+    tuned = None
+    with torch.no_grad():
+        for r in reps:  # eager warmup (plan packing, allocator)
+            r.stage_geo(r.stage_net())
+        torch.cuda.synchronize()
+        if autotune:
+            if args.tune_file and os.path.exists(args.tune_file):
+                tuned = 'loaded %d layer tiles from %s' % (load_tiles(args.tune_file), args.tune_file)
+            else:
+                plan.autotune(plan.pack_input(reps[0].views), chunks=args.chunks, keep_features=False, reps=8)
+                torch.cuda.synchronize()
+                tuned = 'autotuned in-run'
+                if args.tune_file:
+                    save_tiles(args.tune_file)
+        use_graph = not args.no_graph
+        if use_graph:
+            try:
+                for r in reps:
+                    r.capture()
+            except Exception as e:  # report, then time eagerly
+                print('graph capture failed (%s); timing eager launches' % e, file=sys.stderr)
+                use_graph = False
+                for r in reps:
+                    r.use_graph = False
+        for i in range(warmup):
+            r = reps[i % nbatch]
+            r.run_geo(r.run_net())
+        stream = torch.cuda.current_stream(dev)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+               torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            r = reps[i % nbatch]
+            ev[i][0].record(stream)
+            hm = r.run_net()
+            ev[i][1].record(stream)
+            r.run_geo(hm)
+            ev[i][2].record(stream)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        net_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+        geo_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+        # the first batch's outputs, for the MPJPE check
+        r = reps[0]
+        coords, loss, X = r.run_geo(r.run_net())
+        torch.cuda.synchronize()
+    return {'elapsed': elapsed, 'net_ms': net_ms, 'geo_ms': geo_ms, 'X0': X.detach().cpu().numpy().copy(),
+            'coords0': coords.detach().cpu().numpy().copy(), 'hm0': r.hm.detach().cpu().clone(),
+            'use_graph': use_graph, 'tuned': tuned, 'loss0': float(loss), 'meta': r.meta}
+
+
+def infer_main(args):
+    from posu import dist as pdist
+    _, local, world = pdist.env_rank()
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
+    frames = 4 * args.groups
+    res = time_pipeline(args, args.precision, dev, rank, args.steps, args.warmup, args.batches,
+                        not args.no_autotune, dist)
+    elapsed = pdist.max_over_ranks(res['elapsed'], device=dev)
+    value = pdist.throughput(frames, args.steps, world, elapsed)
+    per_rank = gather_per_rank([frames * args.steps, res['elapsed']], dist, device=dev)
+    gf = GFLOP_PER_FRAME.get((args.layers, args.size))
+    peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS  # fp16 dense peak == bf16
+    roof = None
+    if gf is not None:
+        achieved = gf * frames / (res['net_ms'] * 1e-3) / 1e3  # TFLOP/s
+        traffic, src = pmc_traffic(args.layers, args.size, args.precision, args.groups)
+        roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
+                'frac': round(achieved / peak, 4), 'traffic': traffic,
+                'kernel': 'network per replay: fused stem (stem_pool_kernel) + conv stack (conv_igemm / '
+                          'conv_persist kernels, fused deconv+head)',
+                'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (gf, frames)}
+        if traffic:
+            roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward')
+            roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
+    fp32 = None
+    if args.fp32_steps > 0 and args.precision != 'fp32':
+        r32 = time_pipeline(args, 'fp32', dev, rank, args.fp32_steps, 2, args.batches, False, dist)
+        el32 = pdist.max_over_ranks(r32['elapsed'], device=dev)
+        fp32 = {'value': round(pdist.throughput(frames, args.fp32_steps, world, el32), 2), 'unit': 'frames/s',
+                'network_ms': round(r32['net_ms'], 3), 'steps': args.fp32_steps,
+                'roofline_frac_f32': (round(gf * frames / (r32['net_ms'] * 1e-3) / 1e3 / PEAK_F32_TFLOPS, 4)
+                                      if gf else None)}
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    cpu, mpjpe = None, None
+    if world == 1 and not (args.no_cpu_baseline and args.no_mpjpe):
+        cpu, ref = cpu_baseline(args.layers, args.size, args.groups,
+                                0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds)
+        if args.no_cpu_baseline:
+            cpu = None
+        if not args.no_mpjpe:
+            mpjpe = compare_with_reference(res, ref, res['meta'], dev)
+            mpjpe['what'] = ('%s pipeline vs the fp32 CPU oracle chain on the first input batch; mean/std/max: its '
+                             '2-D joint deviation laid on the synthetic poses\' projections and triangulated (mm, '
+                             'test_triangulate.py:98-102 arithmetic) -- see bench.compare_with_reference'
+                             % args.precision)
+            if fp32 is not None:
+                fp32['mpjpe_vs_ref_mm'] = compare_with_reference(r32, ref, r32['meta'], dev)
+    line = {
+        'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
+        'config': {'workload': '4-view H36M-like batch %dx4 at %dx%d: PoseResNet-%d forward + soft-argmax/affine '
+                               '+ epipolar loss + fp64 DLT triangulation (BASELINE configs[2])'
+                               % (args.groups, args.size, args.size, args.layers),
+                   'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
+                   'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
+                   'hipgraph': res['use_graph'], 'chunks': args.chunks, 'tiles': res['tuned'] or 'heuristic',
+                   'input_batches_rotated': args.batches},
+        'network_ms': round(res['net_ms'], 4), 'decode_geometry_ms': round(res['geo_ms'], 4),
+        'groups_per_s': round(value / 4, 2), 'per_rank_frames': [int(p[0]) for p in per_rank],
+        'per_rank_seconds': [round(p[1], 5) for p in per_rank],
+        'mpjpe_vs_ref_mm': mpjpe, 'fp32_mode': fp32,
+        'roofline': roof, 'cpu_baseline': cpu,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+# ------------------------------------------------------------------ training
 def train_main(args):
     """configs[3]: one training step = 4-view batch (groups x 4 frames per GPU) through the
     reference's step (core/function.py:154-366): train-mode forward with per-view BN,
@@ -144,13 +509,11 @@ def train_main(args):
     from core.loss import JointsMSELoss, FundamentalLoss
     from models.multiview_pose_resnet import get_multiview_pose_net
     from utils.transforms import integral_preds_image_th
-    rank, local, world = pdist.env_rank()
+    from posu import ops
+    _, local, _ = pdist.env_rank()
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        pdist.init('nccl', device=dev)
+    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
     cfg = syn.make_cfg(num_layers=args.layers, image_size=args.size)
     net = build_model(args.layers, args.size, args.precision, dev).train()
     model = get_multiview_pose_net(net, cfg)
@@ -158,7 +521,7 @@ def train_main(args):
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local,
                                                           bucket_cap_mb=64)
     nb, nv, hs = args.groups, 4, args.size // 4
-    views = [v.to(dev) for v in syn.synthetic_views(nv, nb, args.size, seed=100 + rank)]
+    views = input_views(nb, args.size, rank, 0, dev)
     meta, _ = synthetic_meta(nb, dev, image_size=args.size)
     g = torch.Generator().manual_seed(7 + rank)
     ys, xs = torch.meshgrid(torch.arange(hs, dtype=torch.float32), torch.arange(hs, dtype=torch.float32),
@@ -178,7 +541,6 @@ def train_main(args):
         for v in range(nv):
             loss = loss + mse(raw[v], target[v], weight)
         coords = integral_preds_image_th(torch.cat(raw, 0), meta.affines).view(nv, nb, 16, 2)
-        from posu import ops
         loss = loss + 1e-3 * ops.epipolar_loss(coords, None, fund.F, subj)
         opt.zero_grad(set_to_none=True)
         loss.backward()
@@ -198,6 +560,7 @@ def train_main(args):
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_rank = gather_per_rank([nv * nb * args.steps, elapsed], dist, device=dev)
     elapsed = pdist.max_over_ranks(elapsed, device=dev)
     frames = nv * nb
     value = pdist.throughput(frames, args.steps, world, elapsed)
@@ -221,6 +584,7 @@ def train_main(args):
                                    % (nb, args.size, args.size, args.layers),
                        'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                        'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce)' % world},
+            'per_rank_frames': [int(p[0]) for p in per_rank],
             'loss': round(float(loss), 5), 'roofline': roof, 'cpu_baseline': None,
         }
         print(json.dumps(line))
@@ -230,139 +594,13 @@ def train_main(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(args))   # before anything touches the GPU
+    if args.dry_run:
+        return dry_run_main(args)
     if args.mode == 'train':
         return train_main(args)
-    from posu import dist as pdist
-    rank, local, world = pdist.env_rank()
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        pdist.init('nccl', device=dev)
-
-    from posu import synthetic as syn
-    from posu.pipeline import synthetic_meta
-    from posu import ops
-
-    net = build_model(args.layers, args.size, args.precision, dev)
-    meta, _ = synthetic_meta(args.groups, dev, image_size=args.size)
-    views = [v.to(dev) for v in syn.synthetic_views(4, args.groups, args.size, seed=100 + rank)]
-    plan = net.plan(dev)
-    frames = 4 * args.groups
-
-    # two stages so the network can be timed on its own with events between replays
-    def stage_net():
-        return plan.run(plan.pack_input(views), chunks=args.chunks, keep_features=False)[0]
-
-    def stage_geo(hm):
-        coords = ops.softargmax2d(hm, beta=100.0, affine=meta.affines).view(4, args.groups, hm.shape[1], 2)
-        loss = ops.epipolar_loss(coords, meta.weights, meta.F, meta.subj)
-        X = ops.triangulate_dlt(meta.M, meta.intr, coords, None, undistort=True, view_major=True)
-        return coords, loss, X
-
-    with torch.no_grad():
-        for _ in range(3):  # eager warmup (plan packing, allocator)
-            hm = stage_net()
-            stage_geo(hm)
-        torch.cuda.synchronize()
-        if not args.no_autotune:  # per-layer conv tile choice, timed on the real operands
-            plan.autotune(plan.pack_input(views), chunks=args.chunks, keep_features=False, reps=8)
-            torch.cuda.synchronize()
-        use_graph = not args.no_graph
-        if use_graph:
-            try:
-                s = torch.cuda.Stream(dev)
-                s.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(s):
-                    for _ in range(2):
-                        hm = stage_net()
-                        stage_geo(hm)
-                torch.cuda.current_stream(dev).wait_stream(s)
-                torch.cuda.synchronize()
-                g_net, g_geo = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_net):
-                    hm_static = stage_net()
-                with torch.cuda.graph(g_geo, pool=g_net.pool()):
-                    out_static = stage_geo(hm_static)
-                torch.cuda.synchronize()
-            except Exception as e:  # report, then time eagerly
-                print('graph capture failed (%s); timing eager launches' % e, file=sys.stderr)
-                use_graph = False
-
-        def run_net():
-            if use_graph:
-                g_net.replay()
-                return hm_static
-            return stage_net()
-
-        def run_geo(hm):
-            if use_graph:
-                g_geo.replay()
-                return out_static
-            return stage_geo(hm)
-
-        for _ in range(args.warmup):
-            run_geo(run_net())
-        stream = torch.cuda.current_stream(dev)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-               torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            ev[i][0].record(stream)
-            hm = run_net()
-            ev[i][1].record(stream)
-            run_geo(hm)
-            ev[i][2].record(stream)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        net_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-        geo_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
-
-    elapsed = pdist.max_over_ranks(elapsed, device=dev)
-    value = pdist.throughput(frames, args.steps, world, elapsed)
-    gf = GFLOP_PER_FRAME.get((args.layers, args.size))
-    peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS  # fp16 dense peak == bf16
-    roof = None
-    if gf is not None:
-        achieved = gf * frames / (net_ms * 1e-3) / 1e3  # TFLOP/s
-        traffic, src = pmc_traffic(args.layers, args.size, args.precision, args.groups)
-        roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
-                'frac': round(achieved / peak, 4), 'traffic': traffic,
-                'kernel': 'network per replay: fused stem (stem_pool_kernel) + conv stack (conv_igemm / conv_persist kernels, fused deconv+head)',
-                'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (gf, frames)}
-        if traffic:
-            roof['traffic_source'] = src + ' (PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward)'
-            roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
-    if rank != 0:
-        if dist is not None:
-            dist.destroy_process_group()
-        return
-    cpu = None
-    if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.layers, args.size, args.cpu_baseline_seconds)
-    line = {
-        'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
-        'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
-        'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision, 'data': 'synthetic',
-        'config': {'workload': '4-view H36M-like batch %dx4 at %dx%d: PoseResNet-%d forward + soft-argmax/affine '
-                               '+ epipolar loss + fp64 DLT triangulation (BASELINE configs[2])'
-                               % (args.groups, args.size, args.size, args.layers),
-                   'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
-                   'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
-                   'hipgraph': use_graph, 'chunks': args.chunks, 'autotuned_tiles': not args.no_autotune},
-        'network_ms': round(net_ms, 4), 'decode_geometry_ms': round(geo_ms, 4),
-        'groups_per_s': round(value / 4, 2),
-        'roofline': roof, 'cpu_baseline': cpu,
-    }
-    print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    return infer_main(args)
 
 
 if __name__ == '__main__':

@@ -40,7 +40,10 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
   return r;
 }
 
-// MODE 0: (sum z, sum z^2)            -- forward statistics / channel sums
+// MODE 0: (sum (z - K), sum (z - K)^2) -- forward statistics / channel sums; K = the
+//         segment's first pixel when kout is non-null (shifted sums: a channel whose
+//         mean is large against its spread keeps its variance in the f32 partials),
+//         else 0.  Block 0 of each segment stores K to kout [nseg][C].
 // MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0] (y optional)
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z, const T* __restrict__ gy,
@@ -48,7 +51,8 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
                                                          const float* __restrict__ msh,
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, int Pseg, int C,
-                                                         RedShape rs, double* __restrict__ part) {
+                                                         RedShape rs, double* __restrict__ part,
+                                                         float* __restrict__ kout) {
   constexpr int E = Vec<T>::E;
   __shared__ double red[2][256][E];
   const int tid = threadIdx.x;
@@ -77,6 +81,16 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       }
     }
   }
+  float kv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) kv[e] = 0.f;
+  if (MODE == 0 && kout && active) {
+    Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + static_cast<size_t>(seg) * Pseg * C + ch * E), kv);
+    if (blk == 0 && pl == 0) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) kout[seg * C + ch * E + e] = kv[e];
+    }
+  }
   if (active) {
     const int pbeg = blk * rs.PPB, pend = min(Pseg, pbeg + rs.PPB);
     const size_t sbase = static_cast<size_t>(seg) * Pseg * C + ch * E;
@@ -87,8 +101,9 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       if constexpr (MODE == 0) {
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-          a[e] += v[e];
-          b[e] += v[e] * v[e];
+          const float d = v[e] - kv[e];
+          a[e] += d;
+          b[e] += d * d;
         }
       } else {
         float gv[E];
@@ -205,7 +220,8 @@ __device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
                                                                 int Pseg, int C, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
-                                                                float momentum, float* running_mean,
+                                                                float momentum, const float* __restrict__ kshift,
+                                                                float* running_mean,
                                                                 float* running_var, float* __restrict__ mean,
                                                                 float* __restrict__ rstd, float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
@@ -221,9 +237,10 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
     if (ln != 0 || !valid) continue;
     for (int k = 0; k < ns; ++k) {  // in segment order: running stats compose like V calls
       const int seg = seg0 + k;
-      const double sum = sums[k], sq = sqs[k];
-      const double mu = sum / n;
-      const double var = fmax(sq / n - mu * mu, 0.0);
+      const double sum = sums[k], sq = sqs[k];  // shifted by K = kshift[seg][c]
+      const double dm = sum / n;
+      const double mu = static_cast<double>(kshift[seg * C + c]) + dm;
+      const double var = fmax(sq / n - dm * dm, 0.0);
       const double r = 1.0 / sqrt(var + static_cast<double>(eps));
       const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
       mean[seg * C + c] = static_cast<float>(mu);
@@ -413,7 +430,10 @@ inline bool seg_major(int C, int E, int nseg, int Pseg, std::initializer_list<co
   for (const void* p : params)
     if (p && !aligned16(p)) return false;
   const int cpr = C / E;
-  return cpr > 0 && 256 % cpr == 0 && nseg <= 65535 && static_cast<long long>(Pseg) * cpr < (1LL << 31);
+  // the loops index chunks in int: i + (U - 1) * stride and i + U * stride must stay below
+  // 2^31 for the largest i < Pseg * cpr (stride <= 1024 blocks * 256 threads)
+  const long long n = static_cast<long long>(Pseg) * cpr;
+  return cpr > 0 && 256 % cpr == 0 && nseg <= 65535 && n + static_cast<long long>(kSegU) * 1024 * 256 < (1LL << 31);
 }
 
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
@@ -617,15 +637,18 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
   POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_fwd: workspace too small");
   hipStream_t s = as_stream(stream);
   double* part = static_cast<double*>(workspace);
+  // the per-segment shifts K live where the backward keeps its coefficients
+  float* kshift = reinterpret_cast<float*>(static_cast<char*>(workspace) + partial_bytes(nseg, C));
   const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
-                       static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part);
+                       static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part,
+                       kshift);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
   hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
-                     gamma, beta, eps, momentum, running_mean, running_var, mean, rstd, scale, shift);
+                     gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
   return check_launch("posu_bn_train_fwd");
 }
 
@@ -669,7 +692,7 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
                        static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale,
-                       relu_shift, mean, rstd, Pseg, C, rs, part);
+                       relu_shift, mean, rstd, Pseg, C, rs, part, nullptr);
   });
   POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
@@ -703,7 +726,7 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, 1), dim3(256), 0, s, static_cast<const T*>(x),
-                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part);
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
   hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);

@@ -49,15 +49,25 @@ class FundamentalLoss:
         self.nviews = 1 + max(max(k[1], k[2]) for k in keys)
         self.pairs = list(itertools.permutations(range(self.nviews), 2))
         table = np.zeros((len(self.subjects), len(self.pairs), 3, 3), dtype=np.float32)
+        self._missing = {}  # subject -> first (subject, i, j) key absent from the dict
         for si, s in enumerate(self.subjects):
             for pi, (i, j) in enumerate(self.pairs):
                 if (s, i, j) in fundamental_matrix_dict:
                     table[si, pi] = np.asarray(fundamental_matrix_dict[(s, i, j)], dtype=np.float32)
+                else:
+                    self._missing.setdefault(s, (s, i, j))
         self.F = torch.from_numpy(table).to(device)
         self._subj_index = {s: i for i, s in enumerate(self.subjects)}
 
     def subject_indices(self, subjects):
-        idx = np.array([self._subj_index[s] for s in np.asarray(subjects).tolist()], dtype=np.int32)
+        """Rows of the F table; a subject without an entry, or with a (subject, i, j) pair
+        missing from the dict, raises KeyError like the reference's dict lookup
+        (loss.py:127) -- never a silent zero matrix."""
+        subjects = np.asarray(subjects).tolist()
+        for s in subjects:
+            if s in self._missing:
+                raise KeyError(self._missing[s])
+        idx = np.array([self._subj_index[s] for s in subjects], dtype=np.int32)
         return torch.from_numpy(idx).to(self.device)
 
     def __call__(self, joints_2d_list, target_weight, meta):

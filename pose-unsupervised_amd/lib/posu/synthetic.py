@@ -98,6 +98,32 @@ def synthetic_state_dict(template, seed=0, bn_stats=None):
     return out
 
 
+def reference_init_state_dict(template, seed=0):
+    """The reference's random init (get_pose_net(is_train=True) without a pretrained file,
+    pose_resnet.py:234-247) drawn from numpy PCG64 instead of torch's global RNG, so the
+    same tensors come out on every machine: conv / deconv weights N(0, 0.001), BN weight 1,
+    bias 0, running stats (0, 1); the final conv's bias keeps PyTorch's default Conv2d
+    init, U(-1/sqrt(fan_in), 1/sqrt(fan_in)), which that init leaves in place."""
+    out = {}
+    for name, t in template.items():
+        shape = tuple(t.shape)
+        r = _rng(name, seed)
+        if name.endswith('num_batches_tracked'):
+            out[name] = torch.zeros((), dtype=torch.long)
+            continue
+        if len(shape) == 4:
+            v = r.normal(0.0, 0.001, size=shape)
+        elif name.endswith('running_var') or (name.endswith('weight') and len(shape) == 1):
+            v = np.ones(shape)
+        elif name.startswith('final_layer') and name.endswith('bias'):
+            fan_in = template[name[:-4] + 'weight'][0].numel()
+            v = r.uniform(-1.0, 1.0, size=shape) / np.sqrt(fan_in)
+        else:
+            v = np.zeros(shape)
+        out[name] = torch.from_numpy(v.astype(np.float32))
+    return out
+
+
 def load_bn_stats(num_layers, image_size):
     path = bn_stats_file(num_layers, image_size)
     if not os.path.exists(path):

@@ -303,10 +303,58 @@ def train_step_golden(ref_pr, ref_tf, ref_loss, num_layers=50, image_size=128, n
     print('train step r%d@%d: mse %.6g fund %.6g' % (num_layers, image_size, mse.item(), fund.item()))
 
 
+ADAM_STEPS = 6
+
+
+def adam_golden(ref_pr, ref_loss, num_layers=18, image_size=128, nviews=4, batch=2, init_seed=123):
+    """Seeded reference optimisation trajectory: the reference's random init
+    (pose_resnet.py:234-247: N(0, 0.001) weights, BN 1 / 0) drawn from numpy
+    (posu.synthetic.reference_init_state_dict -- torch's CPU RNG kernels can draw different
+    floats on another host CPU, the GPU box's), then ADAM_STEPS steps of
+    torch.optim.Adam(lr=1e-3) on the per-view JointsMSELoss(use_target_weight) of fixed
+    synthetic targets in the reference's train mode (per-view BN batch statistics,
+    core/function.py:154-182, 365-367).  Also recorded: the sums of the tensors the
+    reference's own get_pose_net(is_train=True) draws after torch.manual_seed(init_seed)
+    here, which the build's get_pose_net must reproduce bit for bit on this host."""
+    cfg = syn.make_cfg(num_layers=num_layers, image_size=image_size)
+    torch.manual_seed(init_seed)
+    seeded = ref_pr.get_pose_net(cfg, is_train=True)
+    torch_init_sums = np.array([float(p.detach().double().sum()) for p in seeded.parameters()])
+    net = ref_pr.get_pose_net(cfg, is_train=False)
+    net.load_state_dict(syn.reference_init_state_dict(net.state_dict(), seed=init_seed))
+    init_sums = np.array([float(p.detach().double().sum()) for p in net.parameters()])
+    net.train()
+    views = syn.synthetic_views(nviews, batch, image_size, seed=init_seed + 1)
+    hms = image_size // 4
+    targets = peaked_heatmaps(nviews * batch, 16, hms, hms, seed=init_seed + 2).reshape(nviews, batch, 16, hms, hms)
+    tw = (np.random.default_rng(init_seed + 3).uniform(size=(nviews, batch, 16, 1)) > 0.15).astype(np.float32)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    crit = ref_loss.JointsMSELoss(use_target_weight=True)
+    losses, norms = [], []
+    for _ in range(ADAM_STEPS):
+        outs = [net(v)[0] for v in views]
+        loss = sum(crit(outs[v], torch.from_numpy(targets[v]), torch.from_numpy(tw[v])) for v in range(nviews))
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+        norms.append([float(p.detach().norm()) for p in net.parameters()])
+    np.savez_compressed(os.path.join(HERE, 'adam_r%d_%d.npz' % (num_layers, image_size)),
+                        num_layers=num_layers, image_size=image_size, nviews=nviews, batch=batch,
+                        init_seed=init_seed, lr=1e-3, init_sums=init_sums, torch_init_sums=torch_init_sums,
+                        targets=targets, target_weight=tw,
+                        losses=np.array(losses), param_norms=np.array(norms),
+                        param_names=np.array([n for n, _ in net.named_parameters()]))
+    print('adam r%d@%d: losses %s' % (num_layers, image_size, ['%.6f' % v for v in losses]))
+
+
 def main():
     torch.manual_seed(0)
     torch.set_num_threads(8)
     ref_pr, ref_tf, ref_inf, ref_loss, ref_cam = _import_reference()
+    if len(sys.argv) > 1 and sys.argv[1] == 'adam':  # only the Adam trajectory
+        adam_golden(ref_pr, ref_loss)
+        return
     pose_resnet_golden(ref_pr, 50, 256, batch=2, seed=0)
     pose_resnet_golden(ref_pr, 18, 128, batch=2, seed=1)
     pose_resnet_golden(ref_pr, 152, 384, batch=1, seed=2)
@@ -315,6 +363,7 @@ def main():
     camera_golden(ref_cam)
     train_step_golden(ref_pr, ref_tf, ref_loss)
     flip_golden(ref_tf)
+    adam_golden(ref_pr, ref_loss)
 
 
 if __name__ == '__main__':

@@ -160,6 +160,45 @@ def test_synthetic_state_dict_is_deterministic_and_keyed_like_the_reference():
         abs(sum(p.numel() for p in net.parameters()) - 34.0e6) < 0.1e6
 
 
+def test_seeded_init_weights_draw_the_reference_tensors(golden):
+    """get_pose_net(is_train=True) after torch.manual_seed(s) draws bit-identical tensors
+    to the reference's (pose_resnet.py:234-247, module construction order included) on the
+    host the golden was made on (torch's CPU RNG kernels may draw differently on another
+    CPU, so the GPU trajectory test starts from the numpy-drawn init below)."""
+    from models.pose_resnet import get_pose_net
+    g = golden('adam_r18_128.npz')
+    torch.manual_seed(int(g['init_seed']))
+    net = get_pose_net(syn.make_cfg(num_layers=int(g['num_layers']), image_size=int(g['image_size'])), is_train=True)
+    assert [n for n, _ in net.named_parameters()] == list(g['param_names'])
+    sums = np.array([float(p.detach().double().sum()) for p in net.parameters()])
+    if not np.array_equal(sums, g['torch_init_sums']):
+        t = torch.empty(1000)
+        torch.manual_seed(0)
+        t.normal_()
+        pytest.skip('torch CPU RNG draws differ on this host (first normal %.9g)' % float(t[0]))
+    # the numpy-drawn init of the Adam trajectory golden
+    net.load_state_dict(syn.reference_init_state_dict(net.state_dict(), seed=int(g['init_seed'])))
+    sums = np.array([float(p.detach().double().sum()) for p in net.parameters()])
+    np.testing.assert_allclose(sums, g['init_sums'], rtol=1e-10, atol=1e-12)
+
+
+def test_fundamental_loss_missing_pair_raises_like_the_reference():
+    """The reference looks F up per (subject, i, j) (loss.py:127): a missing key is a
+    KeyError, not a zero matrix."""
+    from core.loss import FundamentalLoss
+    F = syn.fundamental_dict()
+    fl = FundamentalLoss(syn.make_cfg(), fundamental_matrix_dict=F, device=torch.device('cpu'))
+    assert fl.subject_indices([9, 11]).tolist() == [fl.subjects.index(9), fl.subjects.index(11)]
+    broken = dict(F)
+    del broken[(11, 2, 1)]
+    fl = FundamentalLoss(syn.make_cfg(), fundamental_matrix_dict=broken, device=torch.device('cpu'))
+    fl.subject_indices([9, 9])  # subject 9 is complete
+    with pytest.raises(KeyError):
+        fl.subject_indices([9, 11])
+    with pytest.raises(KeyError):
+        fl.subject_indices([5])
+
+
 def test_forward_refuses_cpu_tensors():
     from models.pose_resnet import get_pose_net
     net = get_pose_net(syn.make_cfg(num_layers=18, image_size=64), is_train=False).eval()

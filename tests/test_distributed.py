@@ -51,3 +51,28 @@ def test_two_rank_sharding_timing_and_mpjpe():
     np.testing.assert_allclose(res[0][2], ref, rtol=1e-12)
     np.testing.assert_allclose(res[1][2], ref, rtol=1e-12)
     assert res[0][3] == 2 * 128 * 20 / 2.0
+
+
+def test_bench_launcher_starts_one_rank_per_gpu_dry_run():
+    """`python bench.py --gpus 2` starts its own two ranks (torch.distributed.run, before any
+    GPU call) and the rank code checks the world size: the same launcher and rank path the
+    driver's 1->8 GPU scaling run takes, here with gloo and no GPU work (--dry-run)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS='1')
+    env.pop('WORLD_SIZE', None)
+    out = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '2', '--dry-run', '--steps', '3',
+                          '--warmup', '1', '--groups', '5'], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out.stdout  # rank 0 prints one line
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == 2 and d['dry_run']
+    assert d['per_rank_frames'] == [4 * 5 * 3, 4 * 5 * 3]
+    # a rank launched with a WORLD_SIZE that disagrees with --gpus refuses to run
+    bad = subprocess.run([sys.executable, os.path.join(repo, 'bench.py'), '--gpus', '2', '--dry-run'],
+                         capture_output=True, text=True, timeout=120,
+                         env=dict(env, WORLD_SIZE='1', RANK='0', LOCAL_RANK='0'))
+    assert bad.returncode != 0 and 'WORLD_SIZE=1 but --gpus 2' in bad.stderr

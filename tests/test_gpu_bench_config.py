@@ -1,0 +1,104 @@
+"""Parity at the benchmarked configuration (BASELINE configs[2]): exactly the plan
+bench.py times -- R50@256, 32 groups x 4 views, per-layer autotuned tiles (bf16), the fused
+stem / deconv+head launches, the two hipGraphs -- against the CPU oracle chain (fp32
+reference network -> soft-argmax -> crop affine -> FundamentalLoss -> fp64 triangulation)
+on bench's first input batch, compared by bench.compare_with_reference (the numbers the
+bench line reports as mpjpe_vs_ref_mm):
+
+  heatmap error; joint error in image px; epipolar-loss relative error;
+  triangulation_same_2d_mm -- the device triangulation vs the oracle's on the same 2-D
+      joints (BASELINE.json: 1e-2 mm);
+  mean / max (mm) -- the pipeline's 2-D deviation from the reference chain laid on the
+      synthetic poses' projections and triangulated (run/test/test_triangulate.py:98-102).
+
+The raw end-to-end X of a random-weight network is not gated: its views' soft-argmax
+joints do not correspond, so the DLT solution is ill-conditioned (see compare_with_reference).
+
+Gates: fp32 (parity mode) -- heatmaps 1e-3 (BASELINE.json), triangulation 1e-2 mm on the
+same 2-D joints, loss 1e-5 relative, joints and pipeline mm within measured bands.  bf16
+(benchmarked mode) -- bands from the measured deviation: soft-argmax at
+beta = 100 on the peakless heatmaps of a random-weight network turns bf16's ~0.02 heatmap
+deviation into joint moves of tens of pixels."""
+import numpy as np
+import pytest
+import torch
+
+import bench
+from posu import synthetic as syn
+from posu.pipeline import synthetic_meta
+
+pytestmark = pytest.mark.gpu
+
+GROUPS, LAYERS, SIZE = 32, 50, 256
+BANDS = {  # measured on MI355X (round 2: fp32 hm 2.3e-5 / px 0.005 / mm 0.029; bf16 hm 0.21 / px 38 / mm 472)
+    'fp32': {'hm_max': 1e-3, 'tri_max': 1e-2, 'loss_rel': 1e-5, 'px_mean': 0.02, 'mm_mean': 0.1},
+    'bf16': {'hm_max': 0.5, 'hm_mean': 0.05, 'tri_max': 1e-2, 'loss_rel': 1e-2, 'px_mean': 100.0, 'mm_mean': 1000.0},
+}
+
+
+@pytest.fixture(scope='module')
+def oracle_run():
+    from models.pose_resnet import get_pose_net
+    torch.set_num_threads(16)
+    net = get_pose_net(syn.make_cfg(num_layers=LAYERS, image_size=SIZE), is_train=False)
+    sd = syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(LAYERS, SIZE))
+    _, host = synthetic_meta(GROUPS, 'cpu', image_size=SIZE)
+    views = syn.synthetic_views(4, GROUPS, SIZE, seed=100)   # = bench.input_views(rank 0, batch 0)
+    ref = bench.oracle_chain(sd, LAYERS, SIZE, views, host, full=True)
+    ref['host'] = host
+    # the reference path's own fp32 error: the same forward in fp64 (the oracle is
+    # dtype-generic), heatmaps and soft-argmax coordinates
+    from oracle import geometry_ref as G
+    from oracle import pose_resnet_ref as PR
+    hm64, _, _ = PR.pose_resnet_forward(torch.cat(views, 0).double(), {k: v.double() if v.is_floating_point() else v
+                                                                      for k, v in sd.items()}, LAYERS)
+    ref['hm64'] = hm64
+    ref['sa64'] = G.softargmax2d(hm64)
+    return ref
+
+
+def _bench_plan_outputs(cuda, precision, autotune):
+    from posu import plan as P
+    net = bench.build_model(LAYERS, SIZE, precision, cuda)
+    meta, _ = synthetic_meta(GROUPS, cuda, image_size=SIZE)
+    plan = net.plan(cuda)
+    rep = bench.Replayer(plan, bench.input_views(GROUPS, SIZE, 0, 0, cuda), meta, GROUPS, 1, True, cuda)
+    with torch.no_grad():
+        rep.stage_geo(rep.stage_net())
+        if autotune:
+            plan.autotune(plan.pack_input(rep.views), keep_features=False, reps=2)
+            assert len(P.tuned_tiles()) > 20
+        rep.capture()
+        rep.run_geo(rep.run_net())
+        coords, loss, X = rep.run_geo(rep.run_net())
+        torch.cuda.synchronize()
+    return {'hm0': rep.hm.cpu(), 'coords0': coords.cpu().numpy(), 'loss0': float(loss), 'X0': X.cpu().numpy(),
+            'meta': meta}
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precision):
+    out = _bench_plan_outputs(cuda, precision, autotune=precision != 'fp32')
+    c = bench.compare_with_reference(out, oracle_run, out['meta'], cuda)
+    print('%s bench config vs oracle: %s' % (precision, c))
+    b = BANDS[precision]
+    assert np.isfinite(out['X0']).all()
+    assert c['heatmap_abs_err']['max'] < b['hm_max']
+    if 'hm_mean' in b:
+        assert c['heatmap_abs_err']['mean'] < b['hm_mean']
+    assert c['triangulation_same_2d_mm']['max'] < b['tri_max']
+    assert c['epipolar_loss_rel_err'] < b['loss_rel']
+    assert c['joints_px_err']['mean'] < b['px_mean']
+    assert c['mean'] < b['mm_mean']
+    # against fp64: the HIP path's error next to the reference fp32 path's own error
+    from oracle import geometry_ref as G
+    ours_hm = (out['hm0'].double() - oracle_run['hm64']).abs().max().item()
+    ref_hm = (oracle_run['heatmaps'].double() - oracle_run['hm64']).abs().max().item()
+    ours_sa = (G.softargmax2d(out['hm0']).double() - oracle_run['sa64']).norm(dim=-1)
+    ref_sa = (G.softargmax2d(oracle_run['heatmaps']).double() - oracle_run['sa64']).norm(dim=-1)
+    print('vs fp64: heatmap max |err| ours %.3g, reference fp32 path %.3g; soft-argmax heatmap-px err mean/max '
+          'ours %.3g / %.3g, reference fp32 path %.3g / %.3g'
+          % (ours_hm, ref_hm, ours_sa.mean(), ours_sa.max(), ref_sa.mean(), ref_sa.max()))
+    if precision == 'fp32':  # within a small factor of the reference's own fp32 precision
+        assert ours_hm < 4 * ref_hm + 1e-6
+        assert ours_sa.mean() < 4 * ref_sa.mean() + 1e-5

@@ -111,29 +111,53 @@ def test_step_along_negative_gradient_reduces_the_loss(cuda, precision):
     assert loss0.item() - loss1 > 0.5 * predicted
 
 
-def test_adam_steps_run(cuda):
-    """The reference's optimizer (Adam, lr 1e-3) over a few steps of the HIP training path."""
+# Adam trajectory bands (relative, per step) against the reference's seeded trajectory.
+# fp32: the exact-f32 kernels reproduce the reference step by step; Adam's first update is
+# ~lr*sign(g), so only gradients near zero can flip and the band stays small.  bf16: the
+# forward itself deviates ~1e-3 relative, which the later steps carry along.
+ADAM_RTOL = {'fp32': 2e-3, 'bf16': 3e-2}
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_adam_trajectory_matches_reference(cuda, golden, precision):
+    """The reference's optimisation (torch.optim.Adam, lr 1e-3, N(0, 0.001) init from a
+    seeded get_pose_net(is_train=True)) over 6 steps of the HIP training path, against
+    the trajectory the reference's own modules took on CPU (tests/golden/adam_r18_128.npz).
+    The first Adam step RAISES the loss in the reference too (an update of ~lr per weight
+    on N(0, 1e-3) weights overshoots), so the check is the trajectory, not monotonicity.
+    The init is the reference's distribution drawn from numpy (reference_init_state_dict)
+    so that the same tensors come out on the GPU box's CPU."""
     from core.loss import JointsMSELoss
     from models.multiview_pose_resnet import get_multiview_pose_net
     from models.pose_resnet import get_pose_net
-    cfg = syn.make_cfg(num_layers=18, image_size=128)
-    net = get_pose_net(cfg, is_train=True, precision='bf16').to(cuda).train()
+    g = golden('adam_r18_128.npz')
+    nl, size, nv, b, seed = (int(g[k]) for k in ('num_layers', 'image_size', 'nviews', 'batch', 'init_seed'))
+    cfg = syn.make_cfg(num_layers=nl, image_size=size)
+    net = get_pose_net(cfg, is_train=False, precision=precision)
+    net.load_state_dict(syn.reference_init_state_dict(net.state_dict(), seed=seed))
+    # same tensors as the golden's init (the sums differ only by the host's reduction order)
+    np.testing.assert_allclose([float(p.detach().double().sum()) for p in net.parameters()], g['init_sums'],
+                               rtol=1e-10, atol=1e-12)
+    net = net.to(cuda).train()
     model = get_multiview_pose_net(net, cfg)
-    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 128, seed=41)]
-    ys, xs = torch.meshgrid(torch.arange(32.), torch.arange(32.), indexing='ij')
-    c = torch.rand(8, 16, 2, generator=torch.Generator().manual_seed(42)) * 24 + 4
-    tgt = torch.exp(-((ys - c[..., 1, None, None]) ** 2 + (xs - c[..., 0, None, None]) ** 2) / 8.0)
-    tgt = tgt.to(cuda).view(4, 2, 16, 32, 32)
-    w = torch.ones(2, 16, 1, device=cuda)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    views = [v.to(cuda) for v in syn.synthetic_views(nv, b, size, seed=seed + 1)]
+    tgt = torch.from_numpy(g['targets']).to(cuda)
+    tw = torch.from_numpy(g['target_weight']).to(cuda)
+    opt = torch.optim.Adam(net.parameters(), lr=float(g['lr']))
     crit = JointsMSELoss(use_target_weight=True)
-    losses = []
-    for _ in range(6):
+    losses, norms = [], []
+    for _ in range(len(g['losses'])):
         out, _, _, _ = model(views)
-        loss = sum(crit(o, tgt[v], w) for v, o in enumerate(out))
+        loss = sum(crit(o, tgt[v], tw[v]) for v, o in enumerate(out))
         opt.zero_grad()
         loss.backward()
         opt.step()
         losses.append(loss.item())
-    print('losses', losses)
-    assert all(np.isfinite(losses)) and min(losses[1:]) < losses[0]
+        norms.append([float(p.detach().norm()) for p in net.parameters()])
+    rel = np.abs(np.array(losses) / g['losses'] - 1)
+    nrel = np.abs(np.array(norms) / g['param_norms'] - 1).max(axis=1)
+    print('%s losses %s\n  ref %s\n  rel %s\n  worst param-norm rel per step %s'
+          % (precision, np.round(losses, 6), np.round(g['losses'], 6), rel, nrel))
+    assert np.all(np.isfinite(losses))
+    assert rel.max() < ADAM_RTOL[precision], rel
+    assert nrel.max() < ADAM_RTOL[precision], nrel

@@ -200,3 +200,24 @@ def test_maxpool_backward_with_ties_matches_autograd(cuda, code):
     dt = ops.torch_dtype(code)
     gx = T.maxpool3x3s2_bwd(_nhwc(x.detach(), cuda, dt), _nhwc(gy, cuda, dt))
     torch.testing.assert_close(_nchw(gx), gx_ref, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize('code', [F32])
+def test_bn_train_statistics_with_a_large_mean_offset(cuda, code):
+    """Channels whose mean is large against their spread (|mean| / std ~ 1e4): the partial
+    sums are taken about the segment's first pixel, so the variance survives f32 partials
+    (a plain E[z^2] - mean^2 loses it entirely at this ratio)."""
+    g = torch.Generator().manual_seed(31)
+    nseg, b, c, h, w = 2, 4, 64, 24, 20
+    dt = ops.torch_dtype(code)
+    offset = torch.linspace(-300, 300, c).view(1, c, 1, 1)
+    z = (offset + 0.03 * torch.randn(nseg * b, c, h, w, generator=g)).to(dt).float()
+    gamma, beta = torch.ones(c), torch.zeros(c)
+    rm, rv = torch.zeros(c, device=cuda), torch.ones(c, device=cuda)
+    mean, rstd, sc, sh = T.bn_train_fwd(_nhwc(z, cuda, dt), nseg, gamma.to(cuda), beta.to(cuda), 1e-5, 0.1, rm, rv)
+    torch.cuda.synchronize()
+    zs = z.double().view(nseg, b, c, h, w)
+    mu = zs.mean(dim=(1, 3, 4))
+    var = zs.var(dim=(1, 3, 4), unbiased=False)
+    torch.testing.assert_close(mean.cpu().double().view(nseg, c), mu, atol=1e-4, rtol=1e-6)
+    torch.testing.assert_close(rstd.cpu().double().view(nseg, c), 1 / torch.sqrt(var + 1e-5), atol=0, rtol=2e-3)
