@@ -84,54 +84,17 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
  *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied).
  *   tile (here and in posu_conv1x1_dual_fwd / posu_deconv4x4s2_fwd): -1 = the
- *   built-in heuristic, cfg + 8 * variant = a fixed tile configuration (numbering of
- *   posu_force_conv_config); the Python plan picks it per layer by timing every
- *   admissible configuration once (PoseResNetPlan.autotune). */
+ *   built-in heuristic, else a fixed tile configuration cfg + 8 * variant:
+ *     cfg 0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128 (four waves),
+ *         5: 256x256, 6: 256x128 (eight waves);
+ *     variant 1: single-slot LDS ring (cfg 0-4), 2: three-slot ring (cfg != 5);
+ *     + 32 (bf16 / f16): the persistent K-tile stream;
+ *     23 / 31 (bf16 / f16): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile.
+ *   The tile only changes speed (every configuration computes the same sums in the same
+ *   K order); the Python plan picks it per layer by timing every admissible
+ *   configuration once (PoseResNetPlan.autotune).  The library keeps no mutable state:
+ *   every knob is an argument. */
 int posu_conv_bk(int dtype);
-/* Tuning knob: depth of the LDS-DMA ring of the convolution kernels (2 or 3
- * K-tiles; process-wide, default 2). */
-int posu_set_conv_stages(int stages);
-/* Tuning knob: allow the eight-wave 256x256 / 256x128 tiles for layers with
- * Cout >= 128 (1, default) or restrict to the four-wave tiles (0). */
-int posu_set_conv_tiles(int big);
-/* Diagnostics: when buf (device, int64[4 * blocks]) is non-null, every conv launch's
- * blocks record s_memtime at start, at the end of the main loop and at exit, and their
- * HW_ID register; null (default) turns the stamps off. */
-int posu_debug_conv_stamps(void* buf);
-/* Tuning knob: NHWC conv outputs (no chained conv / fused head) are stored straight from
- * the MFMA accumulators (1, default), the same with non-temporal stores (2: faster for the
- * layer alone, slower end to end because the next layer then reads from beyond L2), or
- * staged through LDS as 16-B rows (0). */
-int posu_set_conv_epilogue(int direct);
-/* Tuning knob: with epilogue mode 2, outputs smaller than `bytes` keep plain stores (they
- * can stay in L2 for the next layer). Default 0. */
-int posu_set_conv_nt_threshold(long long bytes);
-/* Tuning knob: residual-add launches with at most `max_ktiles` K-tiles load their residual
- * before the operand fetch (small tiles, direct epilogue); 0 disables. Default 8. */
-int posu_set_conv_early_residual(int max_ktiles);
-/* Tuning knob: launches without an explicit tile run the persistent K-tile-stream
- * variant (1) or one block per tile (0, default); explicit tiles select it with +32. */
-int posu_set_conv_persistent(int on);
-/* Tuning knob: posu_deconv4x4s2_head_fwd runs on the eight-wave 256x256 tile with the head
- * folded into the register epilogue (1, default; bf16/f16) or on 64x256 tiles with the
- * head applied from LDS (0). */
-int posu_set_conv_head256(int on);
-/* Tuning knob: chained launches (posu_conv2d_chain_fwd / posu_conv1x1_dual_chain_fwd) with
- * Cout2 <= 64 run on a 256x256 tile of eight 32-pixel x 256-channel waves, the next conv1
- * from the register epilogue with its weights in LDS (1; bf16/f16), or on the 64x256
- * LDS-epilogue tile (0, default). */
-int posu_set_conv_chain8(int on);
-/* Test hook: force one tile configuration for every conv launch that admits it
- * (0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128, 5: 256x256 (8 waves),
- * 6: 256x128 (8 waves); + 8: configurations 0..4 with a single-slot LDS ring (short-K
- * layers); + 16: a three-slot ring (two K-tiles in flight; not 5); 29: the phased
- * 256x256 loop; 7 / 15 (bf16/f16): the ping-pong loop on 256x256 / 256x128 (waves w and
- * w + 4 of a SIMD one phase apart); 23 / 31 (bf16/f16): 256x256 / 256x128 with waves 4-7
- * staggered by half a K-tile; + 32 (bf16/f16): the persistent K-tile stream; 64..68 (bf16/f16,
- * stride-1 convs and deconvs over whole output rows): the halo variant with tiles
- * 256x256, 256x128, 256x64, 128x128, 128x64; 69, 70, 72: single-halo-slot 256x64,
- * 128x64, 256x128 for C = one K-chunk); -1 restores the automatic choice. */
-int posu_force_conv_config(int cfg);
 /* Fused stem (replaces lib/models/pose_resnet.py:192-195, conv1 -> bn1 -> relu ->
  * maxpool, and the input pack): x NCHW f32 [N, 3, H, W] (the reference's input tensor,
  * mirrored along W when hflip), w packed [64][224] dtype (k = kh*32 + kw*4 + c, zero for
@@ -167,24 +130,6 @@ int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C,
 int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
                          const void* w, int Cout, const float* scale,
                          const float* shift, int relu, void* y, int tile, void* stream);
-
-/* A Bottleneck's last conv (Cout == 256, + residual + ReLU; or the two-source
- * conv3|downsample tail) chained with the NEXT block's conv1 (1x1, stride 1, folded BN
- * cscale/cshift, ReLU; Cout2 <= 128, multiple of 16) on the same output tile: y is
- * written as by posu_conv2d_fwd / posu_conv1x1_dual_fwd and cy = relu(conv1x1(y) *
- * cscale + cshift) [N, Ho, Wo, Cout2] is computed from the rounded y in LDS, so the next
- * block never re-reads y for its conv1 (pose_resnet.py:79-99 -> the next block's
- * conv1).  cw: packed [round_up(Cout2, 64)][256] dtype. */
-int posu_conv2d_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
-                          int Cout, int KH, int KW, int stride, int pad, const float* scale,
-                          const float* shift, const void* residual, int relu, void* y,
-                          const void* cw, int Cout2, const float* cscale, const float* cshift,
-                          void* cy, void* stream);
-int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int H, int W, int C,
-                                const void* x2, int H2, int W2, int C2, int stride2,
-                                const void* w, int Cout, const float* shift, int relu, void* y,
-                                const void* cw, int Cout2, const float* cscale,
-                                const float* cshift, void* cy, void* stream);
 
 /* Cross-view Aggregation (multiview_pose_resnet.py:16-58, ChannelWiseFC / Aggregation,
  * NETWORK.AGGRE): the V(V-1) per-pair [HW x HW] matrices form one block matrix with

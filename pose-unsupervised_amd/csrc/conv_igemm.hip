@@ -61,26 +61,12 @@ struct ConvGeom {
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out, 2: f32 rows blocked by vblk columns
   int vblk;          // mode 2: out[(co / vblk)][m][co % vblk] (view-major heatmaps of a GEMM)
-  // fused 1x1 head (mode 0, BN == Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
-  // chained 1x1 conv (mode 0, BN == Cout == 256): cy[m][co] = relu(cscale[co] *
-  // sum_c cw[co][c] y[m][c] + cshift[co]) -- the next Bottleneck's conv1 on this tile
-  const void* cw;    // packed [>= Cout2 rows][ckp] (dtype)
-  const float* cscale;
-  const float* cshift;
-  void* cy;
-  int Cout2, ckp;
+  // fused 1x1 head (mode 0, Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
   const void* hw;    // packed head weight [>= 16 rows][hkp] (dtype)
   const float* hbias;
   float* hm;
   int J, hkp;
   int mtiles, ntiles;
-  int early_nk;      // early residual prefetch for launches of at most this many K-tiles
-  int direct;        // mode 0 without chain/head: store straight from the accumulators
-  long long* stamps;  // diagnostics: per block s_memtime at start / main-loop end / exit (or null)
-  // halo kernel: output rows per tile R = BM / Wo, segment length SL (rows of one image
-  // inside a tile), halo window KHh x KWh around each output pixel, halo pitch HWp,
-  // halo LDS rows HL, DMA rounds NHD
-  int hR, hSL, hKH, hKW, hWp, hL, hNHD, hph, hpw;
 };
 
 template <typename T>
@@ -168,6 +154,9 @@ constexpr int pass_rows() {
 }
 
 constexpr int kOOB = 0x7ffffff0;  // buffer offset past num_records: the load returns zeros
+// residual-add launches with at most this many K-tiles load their residual before the
+// operand fetch (direct epilogue), so its HBM latency overlaps the main loop
+constexpr int kEarlyNK = 8;
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -283,10 +272,9 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 }
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool PH = false, int LOOP = 0>
+// SG: eight-wave tiles with waves 4-7 staggered by half a K-tile (two-slot ring).
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
-  constexpr bool PP = LOOP == 1;  // ping-pong halves
-  constexpr bool SG = LOOP == 2;  // waves 4-7 staggered by half a K-tile
   using O = Op<T>;
   constexpr int NT = NW * 64;
   constexpr int E = O::E;
@@ -301,27 +289,19 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int PR = pass_rows<BM, BN, S>();
   constexpr bool PRELOAD = TM + TN <= 8;  // both k-steps' fragments fit the VGPR budget
-  constexpr bool CHAINABLE = BN == 256 && BM == 64 && NW == 4 && PR == BM;
   static_assert(S >= 1 && S <= 4, "1..4 stages");
   static_assert(ND * (S - 2) < 64, "vmcnt range");
   static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
   static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
-  // chained next conv1 on the 8x1-wave 256x256 tile: its weights [64][256] sit after the ring
-  constexpr bool CHAIN8 = WGN == 1 && BN == 256 && BM == 256 && NW == 8 && E == 8 && !PH && !PP;
-  static_assert(!PP || (NW == 8 && WGM == 2 && S == 2 && !PH && RA % 2 == 0 && RB % 2 == 0),
-                "ping-pong loop: eight waves as two row halves, two slots");
-  constexpr int CW_BYTES = CHAIN8 ? 64 * 256 * 2 : 0;
-  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>() + CW_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WGN, wn = wid % WGN;
   const int r16 = lane & 15, q = lane >> 4;
-  // tile row of the wave's m-tile i / tile column of its n-tile j.  Phased loop (PH):
-  // m-tiles 0-3 of every wave lie in tile rows 0-127 and 4-7 in 128-255 (n-tiles 0-1 in
-  // columns 0-127, 2-3 in 128-255), so each LDS half-tile feeds one quadrant phase.
-  auto rowA = [&](int i) { return PH ? (i >> 2) * 128 + wm * 64 + (i & 3) * 16 : wm * WTM + i * 16; };
-  auto colB = [&](int j) { return PH ? (j >> 1) * 128 + wn * 32 + (j & 1) * 16 : wn * WTN + j * 16; };
+  // tile row of the wave's m-tile i / tile column of its n-tile j
+  auto rowA = [&](int i) { return wm * WTM + i * 16; };
+  auto colB = [&](int j) { return wn * WTN + j * 16; };
 
   // XCD-aware tile order: blocks b and b+8 share an XCD; give each XCD a
   // contiguous run of tiles so neighbouring tiles (same A rows) share its L2.
@@ -359,11 +339,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // that lane fetches logical chunk cL = (tid & 7) ^ ((row >> 1) & 7), which is the
   // same for every i because ROWS*i does not touch bits 1..3 of the row.
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
-  // Ping-pong loop (PP): waves 0-3 stage tile rows [0, BM/2) of A and [0, BN/2) of B,
-  // waves 4-7 the other halves, piece i of wave w covering rows 32 i + 8 (w & 3) .. + 7 of
-  // its half (rows bits 1..3 -- the swizzle -- are those of the default mapping)
-  const int gp = static_cast<int>(wid_u) >> 2, wl = static_cast<int>(wid_u) & 3;
-  auto drow = [&](int i, int half) { return PP ? gp * half + 32 * i + 8 * wl + (lane >> 3) : (tid >> 3) + ROWS * i; };
+  auto drow = [&](int i) { return (tid >> 3) + ROWS * i; };
   const int HoWo = g.Ho * g.Wo;
   int hb[RA], wb[RA], nb[RA];   // generic window gather
   int o1[RA], o2[RA];           // DUAL: byte offsets of the two 1x1 sources
@@ -371,7 +347,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   if constexpr (DUAL) x2rs = make_srd(g.x2, g.N * g.H2 * g.W2 * g.C2 * ES);
 #pragma unroll
   for (int i = 0; i < RA; ++i) {
-    const int m = m0 + drow(i, BM / 2);
+    const int m = m0 + drow(i);
     if (m < g.M) {
       const int n = m / HoWo, rem = m - n * HoWo;
       const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
@@ -420,18 +396,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int kw_row = (cL * E) >> g.logC, ci_row = (cL * E) & (g.C - 1);
   const int nk = g.Kpad / BK;
   const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;  // weight row offset (elements) for i = 0
-  if constexpr (CHAIN8) {
-    if (g.cy) {  // [Cout2 <= 64][256] -> LDS rows of 512 B, 16-B chunk c of row r at c ^ (r & 15)
-      const u32x4 cws = make_srd(g.cw, g.Cout2 * g.ckp * ES);
-      const unsigned Cs0 = lds0 + ring_bytes<BM, BN, S>() + wid_u * 1024;
-#pragma unroll
-      for (int rd = 0; rd < 4; ++rd) {
-        const int r = rd * 16 + (tid >> 5), p = tid & 31;
-        const int off = r < g.Cout2 ? (r * g.ckp + ((p ^ (r & 15)) * 8)) * ES : kOOB;
-        dma16(cws, off, Cs0 + rd * NW * 1024);
-      }
-    }
-  }
 
   // global -> LDS (async DMA) for K-tile KT into ring slot BUF: exactly ND dma16 per thread
 #define POSU_DMA_TILE(KT, BUF)                                                                      \
@@ -542,14 +506,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const long long t_start = g.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
   // Early residual prefetch (short-K Bottleneck tails): the residual chunks, in the direct
   // epilogue's lane layout, are loaded before the first operand DMA, so their HBM latency
   // overlaps the operand fetch instead of following the main loop.
-  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16 && !PH;
+  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16;
   constexpr int ETM = EARLY ? TM : 1, ETP = EARLY ? TN / 2 : 1;
-  const bool early = EARLY && g.res && g.direct && g.mode == 0 && !g.hm && !g.cy && nk <= g.early_nk;
+  const bool early = EARLY && g.res && g.mode == 0 && !g.hm && nk <= kEarlyNK;
   uint4 rve[ETM][ETP];
   auto out_pix = [&](int i, bool& mok) -> size_t {  // element offset of the pixel of row i
     const int m = m0 + rowA(i) + r16;
@@ -580,105 +543,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
   // overwrites, which every wave finished reading in the previous iteration)
-  if constexpr (PP) {
-    // Ping-pong loop: the two waves of a SIMD (w and w + 4, one per row half) alternate a
-    // "memory" phase -- this K-step's fragment reads + its share of the next K-tile's
-    // LDS-DMAs -- with a "matrix" phase on registers only, the halves one phase apart, so
-    // the matrix pipe always has one wave's MFMAs while the other issues its loads.
-    //   phase  waves 0-3                     waves 4-7
-    //   4t     read (t, k0), stage (t+1, h0)  MFMAs (t-1, k1)
-    //   4t+1   MFMAs (t, k0)                 read (t, k0), stage (t+1, h0)
-    //   4t+2   read (t, k1), stage (t+1, h1)  MFMAs (t, k0)
-    //   4t+3   MFMAs (t, k1), wait DMA        read (t, k1), stage (t+1, h1), wait DMA
-    // Slot (t+1) & 1 was last read at phase 4t-1, so the stages of t+1 start at 4t; every
-    // piece of t+1 is waited for by its issuing wave before the barrier ending phase 4t+3.
-    constexpr int HA = RA / 2, HB = RB / 2;
-    auto stage = [&](int kt, int buf, auto hc) {
-      constexpr int H = decltype(hc)::value;
-      const int kbase = kt * BK;
-      const unsigned As_ = lds0 + buf * STAGE + gp * (BM / 2) * 128 + wl * 1024;
-      const unsigned Bs_ = lds0 + buf * STAGE + A_BYTES + gp * (BN / 2) * 128 + wl * 1024;
-      if constexpr (DUAL) {
-        const bool first = kbase < g.K1;
-#pragma unroll
-        for (int i = H * HA; i < H * HA + HA; ++i) {
-          const int o = first ? o1[i] : o2[i];
-          const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
-          dma16(first ? xrs : x2rs, off, As_ + i * 4096);
-        }
-      } else {  // one tap per K-tile (launcher-checked)
-        const int tap = kbase >> g.logC;
-        const int th = tap / g.KW, tw = tap - th * g.KW;
-        const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));
-#pragma unroll
-        for (int i = H * HA; i < H * HA + HA; ++i) {
-          const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
-                          static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
-          dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * 4096);
-        }
-      }
-#pragma unroll
-      for (int i = H * HB; i < H * HB + HB; ++i)
-        dma16(wrs, ((n0 + drow(i, BN / 2)) * g.Kpad + cL * E + kbase) * ES, Bs_ + i * 4096);
-    };
-    using H0_ = std::integral_constant<int, 0>;
-    using H1_ = std::integral_constant<int, 1>;
-    auto barrier = [] {
-      __builtin_amdgcn_sched_barrier(0);
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    };
-    uint4 af[TM], bfr[TN];
-    auto read = [&](int buf, int cb) {
-      const char* As_ = smem + buf * STAGE;
-      const char* Bs_ = As_ + A_BYTES;
-      const int c = 4 * cb + q;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, c));
-#pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, c));
-    };
-    auto mma = [&] {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
-    };
-    stage(0, 0, H0_{});
-    stage(0, 0, H1_{});
-    vm_wait<0>();
-    barrier();
-    if (gp) barrier();  // the second row half runs one phase behind
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      const bool more = kt + 1 < nk;
-      read(cur, 0);
-      if (more) stage(kt + 1, cur ^ 1, H0_{});
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier();
-      mma();
-      barrier();
-      read(cur, 1);
-      if (more) stage(kt + 1, cur ^ 1, H1_{});
-      if (gp) vm_wait<0>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      barrier();
-      mma();
-      if (!gp) {
-        vm_wait<0>();
-        barrier();
-      } else if (more) {
-        barrier();
-      }
-    }
-  } else if constexpr (SG) {
+  if constexpr (SG) {
     // Stagger (two-slot ring, one barrier per K-tile): waves 4-7 run half a K-tile behind
     // waves 0-3 -- they keep the second k-step's fragments of K-tile t in registers and
     // issue its MFMAs after the next barrier, while waves 0-3 wait for their first
     // fragment reads; every read still happens before the barrier that frees its slot.
-    static_assert(S == 2 && NW == 8 && !PH, "stagger: eight waves, two slots");
+    static_assert(S == 2 && NW == 8, "stagger: eight waves, two slots");
     const bool lag = wid_u >= 4;
     uint4 hA[TM], hB[TN];
     auto read = [&](const char* As_, const char* Bs_, int cb, uint4 (&a)[TM], uint4 (&b)[TN]) {
@@ -711,115 +581,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
     if (lag) mma(hA, hB);
     __builtin_amdgcn_s_setprio(0);
-  } else if constexpr (PH) {
-    // Phased 256x256 loop: each K-tile is four phases, one output quadrant
-    // (64 rows x 32 columns of the wave's tile, 16 MFMAs) per phase, each phase staging
-    // one half-tile of the NEXT K-tile (2 LDS-DMAs per thread) beside its fragment reads
-    // and MFMAs; counted vmcnt(4) keeps two half-tiles in flight across the barriers.
-    //   phase  quadrant  reads (LDS->VGPR)     stages (K-tile t+1)   waits for
-    //   1      (0,0)     A rows 0-127, B 0-127  A rows 0-127          B 128-255 (t)
-    //   2      (0,1)     B 128-255              B 0-127               A 128-255 (t)
-    //   3      (1,1)     A rows 128-255         B 128-255             -
-    //   4      (1,0)     -                      A rows 128-255        A, B 0-127 (t+1)
-    // A slot is restaged four phases after its last read (WAR-safe with one barrier
-    // per phase); a DMA is read only after its issuing waves' vmcnt and a barrier.
-    static_assert(BM == 256 && BN == 256 && NW == 8 && WGM == 2 && S == 2 && RA == 4 && RB == 4,
-                  "phased loop: 256x256 tile, 8 waves, 2 slots");
-    auto stage_a = [&](int kt, int buf, auto i0c) {
-      constexpr int I0 = decltype(i0c)::value;
-      const int kbase = kt * BK;
-      const unsigned As_ = lds0 + buf * STAGE + wid_u * 1024;
-      if constexpr (DUAL) {
-        const bool first = kbase < g.K1;
-#pragma unroll
-        for (int i = I0; i < I0 + 2; ++i) {
-          const int o = first ? o1[i] : o2[i];
-          const int off = o == kOOB ? kOOB : o + (first ? kbase : kbase - g.K1) * ES;
-          dma16(first ? xrs : x2rs, off, As_ + i * NW * 1024);
-        }
-      } else {  // fast gather only (one tap per K-tile)
-        const int tap = kbase >> g.logC;
-        const int th = tap / g.KW, tw = tap - th * g.KW;
-        const int toff = (th * g.W + tw) * g.C + (kbase & (g.C - 1));
-#pragma unroll
-        for (int i = I0; i < I0 + 2; ++i) {
-          const bool ok = static_cast<unsigned>(hb[i] + th) < static_cast<unsigned>(g.H) &&
-                          static_cast<unsigned>(wb[i] + tw) < static_cast<unsigned>(g.W);
-          dma16(xrs, ok ? (pbase[i] + toff) * ES : kOOB, As_ + i * NW * 1024);
-        }
-      }
-    };
-    auto stage_b = [&](int kt, int buf, auto i0c) {
-      constexpr int I0 = decltype(i0c)::value;
-      const unsigned Bs_ = lds0 + buf * STAGE + A_BYTES + wid_u * 1024;
-#pragma unroll
-      for (int i = I0; i < I0 + 2; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kt * BK) * ES, Bs_ + i * NW * 1024);
-    };
-    using I0_ = std::integral_constant<int, 0>;
-    using I2_ = std::integral_constant<int, 2>;
-    uint4 af[4][2], bq0[2][2], bq1[2][2];
-    auto read_a = [&](const char* As_, int mi) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-          af[ii][cb] = *reinterpret_cast<const uint4*>(As_ + swz(rowA(mi * 4 + ii) + r16, 4 * cb + q));
-    };
-    auto read_b = [&](const char* Bs_, int ni, uint4 (&bq)[2][2]) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj)
-          bq[jj][cb] = *reinterpret_cast<const uint4*>(Bs_ + swz(colB(ni * 2 + jj) + r16, 4 * cb + q));
-    };
-    auto mma_q = [&](int mi, int ni, uint4 (&bq)[2][2]) {
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-          for (int jj = 0; jj < 2; ++jj) O::mma(acc[mi * 4 + ii][ni * 2 + jj], bq[jj][cb], af[ii][cb]);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    auto barrier = [] {
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    stage_a(0, 0, I0_{});
-    stage_b(0, 0, I0_{});
-    stage_b(0, 0, I2_{});
-    stage_a(0, 0, I2_{});
-    vm_wait<4>();
-    barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1, nxt = cur ^ 1;
-      const bool more = kt + 1 < nk;
-      const char* As_ = smem + cur * STAGE;
-      const char* Bs_ = As_ + A_BYTES;
-      read_a(As_, 0);
-      read_b(Bs_, 0, bq0);
-      if (more) stage_a(kt + 1, nxt, I0_{});
-      mma_q(0, 0, bq0);
-      if (more) vm_wait<4>();
-      else vm_wait<2>();
-      barrier();
-      read_b(Bs_, 1, bq1);
-      if (more) stage_b(kt + 1, nxt, I0_{});
-      mma_q(0, 1, bq1);
-      if (more) vm_wait<4>();
-      else vm_wait<0>();
-      barrier();
-      read_a(As_, 1);
-      if (more) stage_b(kt + 1, nxt, I2_{});
-      mma_q(1, 1, bq1);
-      barrier();
-      if (more) stage_a(kt + 1, nxt, I2_{});
-      mma_q(1, 0, bq0);
-      if (more) vm_wait<4>();
-      barrier();
-    }
   } else if constexpr (S == 1) {
     // single slot (short-K layers): a quarter of the LDS of a 2-slot ring, so more
     // blocks share a CU and one block's epilogue overlaps another's operand fetch
@@ -846,17 +607,16 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   }
 #undef POSU_DMA_TILE
 #undef POSU_COMPUTE
-  const long long t_loop = g.stamps ? __builtin_amdgcn_s_memtime() : 0;
 
-  // ---- direct epilogue (NHWC outputs without a chained conv): each lane stores its 4
+  // ---- direct epilogue (NHWC outputs): each lane stores its 4
   // consecutive channels of one pixel straight from the accumulators (BN, residual,
   // ReLU applied in registers) -- no LDS round trip, no barriers
   // 256x256 tiles also carry the fused 1x1 head (pose_resnet.py:126-132, 203): each
   // wave's rounded outputs are already MFMA B fragments (8 consecutive channels of one
   // pixel per lane), so its partial heatmaps over its 64 channels are 2 MFMAs per m-tile;
   // the four column waves' partials are summed in LDS in a fixed order.
-  constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && !PH && E == 8;
-  if (E == 8 && TN % 2 == 0 && g.direct && g.mode == 0 && (!g.cy || CHAIN8) && (!g.hm || HEAD256)) {
+  constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && E == 8;
+  if (E == 8 && TN % 2 == 0 && g.mode == 0 && (!g.hm || HEAD256)) {
     // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
     // holds 8 consecutive channels (16-B stores, half the store instructions):
     // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
@@ -864,17 +624,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     constexpr int TP = TN / 2;
     const bool head = HEAD256 && g.hm != nullptr;
-    // chained next conv1 (CHAIN8): every wave owns all 256 channels of its 32 pixels, so
-    // its rounded outputs (B fragments, k-groups in the swap order) times the LDS-resident
-    // weights give the next conv1 directly: cacc[i][t] = 16 out channels x 16 pixels
-    const bool chain = CHAIN8 && g.cy != nullptr;
-    f32x4 cacc[CHAIN8 ? TM : 1][4];
-    if constexpr (CHAIN8) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) cacc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
     uint4 hwf[HEAD256 ? TP : 1];
     f32x4 hacc[HEAD256 ? TM : 1];
     if constexpr (HEAD256) {
@@ -938,21 +687,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (rp) v[e] += r[e];
           if (g.relu) v[e] = fmaxf(v[e], 0.f);
         }
-        if constexpr (CHAIN8) {
-          if (chain) {
-            const uint4 pk = O::store_vals(v);
-            if (mok) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
-            const char* Cs = smem + ring_bytes<BM, BN, S>();
-            const int c = jp * 4 + 2 * (q & 1) + (q >> 1);  // this lane's 8-channel chunk
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-              if (16 * t >= g.Cout2) break;
-              const uint4 wf = *reinterpret_cast<const uint4*>(Cs + (16 * t + r16) * 512 + ((c ^ r16) << 4));
-              O::mma(cacc[i][t], wf, pk);  // rows = next-conv channels, cols = pixels
-            }
-            continue;
-          }
-        }
         if constexpr (HEAD256) {
           if (head) {
             const uint4 pk = O::store_vals(v);
@@ -961,41 +695,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
             continue;
           }
         }
-        if (mok && cop[jp] < g.Cout) {
-          const uint4 pk = O::store_vals(v);
-          if (g.direct == 2) {  // streaming store: do not keep the output lines in L2
-            const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
-            __builtin_nontemporal_store(pv, reinterpret_cast<u32x4*>(yp + pix + cop[jp]));
-          } else {
-            *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
-          }
-        }
-      }
-    }
-    if constexpr (CHAIN8) {
-      if (chain) {  // BN + ReLU of the next conv1, paired tiles -> 16-B NHWC stores
-        T* __restrict__ cyp = reinterpret_cast<T*>(g.cy);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int m = m0 + rowA(i) + r16;
-#pragma unroll
-          for (int tp = 0; tp < 2; ++tp) {
-            const int co = 16 * (2 * tp + (q & 1)) + 8 * (q >> 1);
-            float v[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(cacc[i][2 * tp][e]),
-                                                               __float_as_uint(cacc[i][2 * tp + 1][e]), false, false);
-              v[e] = __uint_as_float(sw[0]);
-              v[4 + e] = __uint_as_float(sw[1]);
-            }
-            if (m < g.M && co < g.Cout2) {
-#pragma unroll
-              for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * g.cscale[co + e] + g.cshift[co + e], 0.f);
-              *reinterpret_cast<uint4*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = O::store_vals(v);
-            }
-          }
-        }
+        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
       }
     }
     if constexpr (HEAD256) {
@@ -1021,7 +721,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         }
       }
     }
-  } else if (g.direct && g.mode == 0 && !g.hm && !g.cy) {
+  } else if (g.mode == 0 && !g.hm) {
     T* __restrict__ yp = reinterpret_cast<T*>(g.y);
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     float sc[TN][4], sh[TN][4];
@@ -1072,12 +772,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         }
         const uint4 pk = O::store_vals(v);
         if constexpr (E == 4) {
-          if (g.direct == 2) {
-            const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
-            __builtin_nontemporal_store(pv, reinterpret_cast<u32x4*>(yp + pix + co));
-          } else {
-            *reinterpret_cast<uint4*>(yp + pix + co) = pk;
-          }
+          *reinterpret_cast<uint4*>(yp + pix + co) = pk;
         } else {
           *reinterpret_cast<uint2*>(yp + pix + co) = make_uint2(pk.x, pk.y);
         }
@@ -1171,72 +866,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
           for (int e = 0; e < E; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        const uint4 packed = O::store_vals(v);
-        *reinterpret_cast<uint4*>(yp + off[it]) = packed;
-        if constexpr (CHAINABLE) {
-          if (g.cy) {  // the chained conv reads exactly the stored (rounded) values
-            float vr[E];
-            O::load_vals(packed, vr);
-#pragma unroll
-            for (int e = 0; e < E; e += 4)
-              *reinterpret_cast<float4*>(Cs + row * LD + cc * E + e) = make_float4(vr[e], vr[e + 1], vr[e + 2],
-                                                                                   vr[e + 3]);
-          }
-        }
-      }
-      if constexpr (CHAINABLE) {
-        if (g.cy) {
-          __syncthreads();
-          // next block's conv1 (1x1) on the tile in LDS: wave w takes pixel rows
-          // 16w..16w+15 (the MFMA B operand), all Cout2 channels (A = weights), K = 256
-          constexpr int MAXT = 8;
-          f32x4 cacc[MAXT];
-#pragma unroll
-          for (int j = 0; j < MAXT; ++j) cacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-          const T* __restrict__ cwp = reinterpret_cast<const T*>(g.cw);
-          const int ntc = g.Cout2 / 16;
-          const int prow = wid * 16 + r16;
-          for (int kc = 0; kc < BN / (4 * E); ++kc) {
-            const int c = 4 * kc + q;
-            float av[E];
-#pragma unroll
-            for (int e = 0; e < E; e += 4) {
-              const float4 t4 = *reinterpret_cast<const float4*>(Cs + prow * LD + c * E + e);
-              av[e] = t4.x;
-              av[e + 1] = t4.y;
-              av[e + 2] = t4.z;
-              av[e + 3] = t4.w;
-            }
-            const uint4 a = O::store_vals(av);
-#pragma unroll
-            for (int j = 0; j < MAXT; ++j)
-              if (j < ntc) {
-                const uint4 b = *reinterpret_cast<const uint4*>(cwp + static_cast<size_t>(j * 16 + r16) * g.ckp + c * E);
-                O::mma(cacc[j], b, a);  // rows = channels, cols = pixels
-              }
-          }
-          const int m = m0 + prow;
-          if (m < g.M) {
-            T* __restrict__ cyp = reinterpret_cast<T*>(g.cy);
-#pragma unroll
-            for (int j = 0; j < MAXT; ++j)
-              if (j < ntc) {
-                const int co = j * 16 + q * 4;
-                float v[E];
-#pragma unroll
-                for (int e = 0; e < E; ++e) v[e] = 0.f;
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                  v[e] = fmaxf(cacc[j][e] * g.cscale[co + e] + g.cshift[co + e], 0.f);
-                if constexpr (E == 4) {
-                  *reinterpret_cast<uint4*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = O::store_vals(v);
-                } else {  // 4 two-byte values: the low 8 bytes of a packed chunk
-                  const uint4 pk = O::store_vals(v);
-                  *reinterpret_cast<uint2*>(cyp + static_cast<size_t>(m) * g.Cout2 + co) = make_uint2(pk.x, pk.y);
-                }
-              }
-          }
-        }
+        *reinterpret_cast<uint4*>(yp + off[it]) = O::store_vals(v);
       }
     } else if (g.mode == 2) {
       // f32 GEMM rows, column blocks of vblk stored as separate [M][vblk] planes
@@ -1332,13 +962,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
   }
   }  // LDS epilogue
-  if (g.stamps && tid == 0) {
-    long long* st = g.stamps + 4 * static_cast<size_t>(blockIdx.x);
-    st[0] = t_start;
-    st[1] = t_loop;
-    st[2] = __builtin_amdgcn_s_memtime();
-    st[3] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID (wave, SIMD, CU, SE)
-  }
+
 }
 
 // ---------------------------------------------------------------------------------
@@ -1737,248 +1361,6 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
   }
 }
 
-// ---------------------------------------------------------------------------------
-// Halo variant for stride-1 KHxKW convolutions and the ConvTranspose(4, s2) parity
-// classes (2-byte dtypes, direct epilogue).  A tile is R = BM / Wo whole output rows;
-// per 64-channel K-chunk its input window -- the R rows plus the (KH-1)-row / (KW-1)-column
-// halo, one segment per image the rows belong to -- is staged ONCE in LDS and every tap
-// reads its A fragments from it at a tap-uniform row offset, instead of gathering BM rows
-// per tap (9x fewer A bytes over the L2->LDS path for 3x3, 4x for a deconv class).  The
-// K order is chunk-major (all taps of a chunk, then the next chunk); the weights stream
-// one [BN][64] K-tile per tap through a two-slot ring, the next chunk's halo is DMA'd in
-// per-tap parts into the other halo slot while the current chunk computes.
-template <int BN>
-constexpr int halo_rows_max() {  // LDS rows of one halo slot: 2 halo + 2 weight slots in 160 KiB
-  return ((160 * 1024 - 2 * BN * 128) / (2 * 128)) / 64 * 64;
-}
-
-template <typename T, int BM, int BN, int NW, int WGM, int HR = halo_rows_max<BN>(), int NHS = 2>
-__global__ __launch_bounds__(NW * 64) void conv_halo_kernel(ConvGeom g) {
-  using O = Op<T>;
-  constexpr int E = O::E;
-  constexpr int ES = static_cast<int>(sizeof(T));
-  constexpr int BK = 8 * E;
-  constexpr int WGN = NW / WGM;
-  constexpr int WTM = BM / WGM, WTN = BN / WGN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int ROWS = NW * 8;
-  constexpr int RB = BN / ROWS;
-  constexpr int HMAX = HR;  // halo LDS rows per slot; NHS = 1: one slot (a single K-chunk)
-  constexpr int NHMAX = HMAX / ROWS;
-  constexpr int HALO_BYTES = HMAX * 128, B_BYTES = BN * 128;
-  constexpr int TP = TN / 2;
-  constexpr bool PRELOAD = TM + TN <= 8;
-  static_assert(E == 8 && TN % 2 == 0, "halo variant: 2-byte dtypes, paired n-tiles");
-  static_assert(NHS * HALO_BYTES + 2 * B_BYTES <= 160 * 1024, "LDS budget");
-  static_assert(HR % ROWS == 0, "halo slot = whole DMA rounds");
-  __shared__ __attribute__((aligned(16))) char smem[NHS * HALO_BYTES + 2 * B_BYTES];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WGN, wn = wid % WGN;
-  const int r16 = lane & 15, q = lane >> 4;
-
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-  const int wg = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-  const int nt = wg % g.ntiles;
-  const int rest = wg / g.ntiles;
-  const int mt = g.deconv ? rest >> 2 : rest;
-  const int cls = g.deconv ? rest & 3 : 0;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int dy = g.deconv ? cls >> 1 : 0, dx = g.deconv ? cls & 1 : 0;
-  const int osc = g.deconv ? 2 : 1;
-  const T* __restrict__ wp = reinterpret_cast<const T*>(g.w);
-  if (g.deconv) wp += static_cast<size_t>(cls) * g.CoutPad * g.Kpad;
-
-  const u32x4 xrs = make_srd(g.x, g.N * g.H * g.W * g.C * ES);
-  const u32x4 wrs = make_srd(wp, g.CoutPad * g.Kpad * ES);
-  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
-  const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
-  const int cL = (tid & 7) ^ ((tid >> 4) & 7);
-
-  // ---- halo DMA sources: LDS row L = j * ROWS + (tid >> 3) of a slot <-> halo pixel
-  const int rho0 = m0 / g.Wo;                    // first output row (n * Ho + oy) of the tile
-  const int HS = g.hSL + g.hKH - 1;              // halo rows per segment
-  int goff[NHMAX];
-#pragma unroll
-  for (int j = 0; j < NHMAX; ++j) {
-    const int L = j * ROWS + (tid >> 3);
-    const int hr = L / g.hWp, hx = L - hr * g.hWp;
-    const int k = hr / HS, r = hr - k * HS;
-    const int rho = rho0 + k * g.hSL;            // first output row of segment k
-    const int n = rho / g.Ho, oys = rho - n * g.Ho;
-    const int iy = oys - g.hph + r, ix = hx - g.hpw;
-    const bool ok = L < g.hL && n < g.N && static_cast<unsigned>(iy) < static_cast<unsigned>(g.H) &&
-                    static_cast<unsigned>(ix) < static_cast<unsigned>(g.W);
-    goff[j] = ok ? ((n * g.H + iy) * g.W + ix) * g.C + cL * E : -1;
-  }
-  // ---- A fragment rows: halo LDS row of each m-tile row's pixel (tap offset added later)
-  int lbase[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int ml = wm * WTM + i * 16 + r16;      // row within the tile
-    const int rl = ml / g.Wo, ox = ml - rl * g.Wo;
-    const int k = rl / g.hSL, rr2 = rl - k * g.hSL;
-    lbase[i] = (k * HS + rr2) * g.hWp + ox;
-  }
-  const int nchunk = g.C / BK;
-  const int ntap = g.KH * g.KW;
-  const int nsteps = nchunk * ntap;
-  const int wbrow = (n0 + (tid >> 3)) * g.Kpad + cL * E;
-
-  auto halo_part = [&](int c, int j0, int j1) {  // DMA rounds [j0, j1) of chunk c's halo
-    const unsigned Hs = lds0 + (NHS == 1 ? 0 : (c & 1)) * HALO_BYTES + wid_u * 1024;
-#pragma unroll
-    for (int j = 0; j < NHMAX; ++j)
-      if (j >= j0 && j < j1) dma16(xrs, goff[j] < 0 ? kOOB : (goff[j] + c * BK) * ES, Hs + j * NW * 1024);
-  };
-  auto b_tile = [&](int st) {  // weight K-tile of step st (chunk-major: tap fastest)
-    const int c = st / ntap, t = st - c * ntap;
-    const int kbase = t * g.C + c * BK;
-    const unsigned Bs = lds0 + NHS * HALO_BYTES + (st & 1) * B_BYTES + wid_u * 1024;
-#pragma unroll
-    for (int i = 0; i < RB; ++i) dma16(wrs, (wbrow + ROWS * i * g.Kpad + kbase) * ES, Bs + i * NW * 1024);
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute = [&](int st) {
-    const int c = st / ntap, t = st - c * ntap;
-    const int th = t / g.KW, tw = t - th * g.KW;
-    const int toff = (th + dy) * g.hWp + (tw + dx);
-    const char* Hs = smem + (NHS == 1 ? 0 : (c & 1)) * HALO_BYTES;
-    const char* Bs = smem + NHS * HALO_BYTES + (st & 1) * B_BYTES;
-    if constexpr (PRELOAD) {
-      uint4 af[2][TM], bfr[2][TN];
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int cc = 4 * cb + q;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[cb][j] = *reinterpret_cast<const uint4*>(Bs + swz(wn * WTN + j * 16 + r16, cc));
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[cb][i] = *reinterpret_cast<const uint4*>(Hs + swz(lbase[i] + toff, cc));
-      }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[cb][j], af[cb][i]);
-    } else {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int cc = 4 * cb + q;
-        uint4 af[TM], bfr[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) af[i] = *reinterpret_cast<const uint4*>(Hs + swz(lbase[i] + toff, cc));
-#pragma unroll
-        for (int j = 0; j < TN; ++j) bfr[j] = *reinterpret_cast<const uint4*>(Bs + swz(wn * WTN + j * 16 + r16, cc));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) O::mma(acc[i][j], bfr[j], af[i]);
-      }
-    }
-  };
-  auto barrier = [] {
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-
-  halo_part(0, 0, g.hNHD);
-  b_tile(0);
-  vm_wait<0>();
-  barrier();
-  for (int st = 0; st < nsteps; ++st) {
-    const int c = st / ntap, t = st - c * ntap;
-    if (st + 1 < nsteps) b_tile(st + 1);
-    if (c + 1 < nchunk) {  // part t of the next chunk's halo
-      const int j0 = (t * g.hNHD) / ntap, j1 = ((t + 1) * g.hNHD) / ntap;
-      halo_part(c + 1, j0, j1);
-    }
-    compute(st);
-    vm_wait<0>();
-    barrier();
-  }
-
-  // ---- direct epilogue (as conv_igemm_kernel's): paired n-tiles, 16-B NHWC stores
-  T* __restrict__ yp = reinterpret_cast<T*>(g.y);
-  const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
-  const int HoWo = g.Ho * g.Wo;
-  int cop[TP];
-  float sc[TP][8], sh[TP][8];
-#pragma unroll
-  for (int jp = 0; jp < TP; ++jp) {
-    cop[jp] = n0 + wn * WTN + (2 * jp + (q & 1)) * 16 + 8 * (q >> 1);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int co = cop[jp] + e;
-      sc[jp][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
-      sh[jp][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WTM + i * 16 + r16;
-    const bool mok = m < g.M;
-    const int mm = mok ? m : 0;
-    const int n = mm / HoWo, rem = mm - n * HoWo;
-    const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-    const size_t pix = (static_cast<size_t>(n * g.out_H + oy * osc + dy) * g.out_W + (ox * osc + dx)) * g.Cout;
-    uint4 rv[TP];
-#pragma unroll
-    for (int jp = 0; jp < TP; ++jp) {
-      rv[jp] = make_uint4(0, 0, 0, 0);
-      if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
-    }
-#pragma unroll
-    for (int jp = 0; jp < TP; ++jp) {
-      float v[8], r[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
-                                                         __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
-        v[e] = __uint_as_float(sw[0]);
-        v[4 + e] = __uint_as_float(sw[1]);
-      }
-      O::load_vals(rv[jp], r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        v[e] = v[e] * sc[jp][e] + sh[jp][e];
-        if (rp) v[e] += r[e];
-        if (g.relu) v[e] = fmaxf(v[e], 0.f);
-      }
-      if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
-    }
-  }
-}
-
-// Host geometry of the halo variant for a BM-row tile; false if the launch does not fit
-// (rows per tile not whole output rows, tiles straddling images unevenly, halo > LDS slot).
-bool halo_geometry(ConvGeom& g, int BM, int BN, int NW, int hmax_rows) {
-  if (g.up || g.mode != 0 || g.hm || g.cy || g.x2 || g.Wo <= 0 || BM % g.Wo != 0) return false;
-  if (!g.deconv && g.stride != 1) return false;
-  const int R = BM / g.Wo;
-  if (!(R % g.Ho == 0 || g.Ho % R == 0)) return false;
-  g.hR = R;
-  g.hSL = std::min(R, g.Ho);
-  g.hKH = g.deconv ? 3 : g.KH;
-  g.hKW = g.deconv ? 3 : g.KW;
-  g.hph = g.deconv ? 1 : g.pad_h;
-  g.hpw = g.deconv ? 1 : g.pad_w;
-  g.hWp = g.Wo + g.hKW - 1;
-  g.hL = (R / g.hSL) * (g.hSL + g.hKH - 1) * g.hWp;
-  if (g.hL > hmax_rows) return false;
-  g.hNHD = (g.hL + NW * 8 - 1) / (NW * 8);
-  return true;
-}
-
 int cu_count() {
   static const int n = [] {
     int dev = 0, v = 0;
@@ -2024,157 +1406,83 @@ void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
   hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 2, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
 }
 
-template <typename T>
-constexpr int bk_of_t() {
-  return 128 / static_cast<int>(sizeof(T));
-}
 
-int g_stages = 2;   // ring depth (posu_set_conv_stages)
-int g_big = 1;      // 256 x 256 / 256 x 128 eight-wave tiles for wide layers (posu_set_conv_tiles)
-int g_force = -1;   // forced tile configuration (tests), -1 = automatic
-long long* g_stamps = nullptr;  // diagnostics (posu_debug_conv_stamps)
-int g_direct = 1;               // register-direct epilogue (posu_set_conv_epilogue)
-int g_early_nk = 8;             // posu_set_conv_early_residual
-int g_chain8 = 0;               // chained conv1 on the 8x1-wave 256x256 tile (posu_set_conv_chain8)
-int g_head256 = 1;              // fused head on the 256x256 direct-epilogue tile (posu_set_conv_head256)
-int g_persist = 0;              // persistent K-tile stream by default (posu_set_conv_persistent)
-long long g_nt_min_bytes = 0;   // smallest output that takes streaming stores (posu_set_conv_nt_threshold)
+// Tile configurations (the `tile` argument of the conv entry points): cfg + 8 * variant,
+//   cfg 0: 256x64, 1: 128x64, 2: 64x64, 3: 128x128, 4: 64x128 (four waves),
+//       5: 256x256, 6: 256x128 (eight waves);
+//   variant 1: single-slot LDS ring (cfg 0-4; short-K layers: more blocks per CU),
+//   variant 2: three-slot ring (cfg != 5),
+//   +32 (2-byte dtypes): the persistent K-tile stream (conv_persist_kernel);
+//   23 / 31 (2-byte dtypes): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile
+//   (also what the heuristic runs for those shapes);
+//   -1: the built-in heuristic.
+bool tile_ok(int tile) {
+  if (tile == -1 || tile == 23 || tile == 31) return true;
+  if (tile < 0 || tile >= 64) return false;
+  const int c = tile & 7, v = (tile >> 3) & 3;
+  return c <= 6 && v <= 2 && !(v == 1 && c > 4) && !(v == 2 && c == 5);
+}
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
-  g.stamps = g_stamps;
-  g.early_nk = g_early_nk;
-  g.direct = g_direct;
-  if (g.direct == 2 &&  // streaming stores only for outputs that would not stay in L2 anyway
-      static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * static_cast<int>(sizeof(T)) < g_nt_min_bytes)
-    g.direct = 1;
   if constexpr (sizeof(T) == 2) {  // fused head on the eight-wave 256x256 tile, direct epilogue
-    if (g.hm && !g.cy && g_head256 && g.direct && g.CoutPad == 256) {
+    if (g.hm && g.CoutPad == 256) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
       // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 2>), dim3(g.mtiles * nclass),
-                         dim3(512), 0, s, g);
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(g.mtiles * nclass), dim3(512), 0,
+                         s, g);
       return check_launch(what);
     }
   }
-  if constexpr (sizeof(T) == 2) {  // chained next conv1 on the 8x1-wave 256x256 tile
-    if (g.cy && !g.hm && g_chain8 && g.direct && g.Cout == 256 && g.Cout2 <= 64 && g.ckp == 256) {
-      g.ntiles = 1;
-      g.mtiles = (g.M + 255) / 256;
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 8, 2, DUAL>), dim3(g.mtiles * nclass), dim3(512), 0, s,
-                         g);
-      return check_launch(what);
-    }
-  }
-  if (g.hm || g.cy) {  // fused head / chained conv: one block owns all 256 output channels
+  if (g.hm) {  // fused head (f32): one 64x256 block owns all 256 output channels, head from LDS
     g.ntiles = 1;
     g.mtiles = (g.M + 63) / 64;
     hipLaunchKernelGGL((conv_igemm_kernel<T, 64, 256, 4, 1, 2, DUAL>), dim3(g.mtiles * nclass), dim3(256), 0, s, g);
     return check_launch(what);
   }
-  // tile choice: 64-channel layers take 256 x 64 tiles (four waves stacked along M,
-  // 64 x 64 each); wider layers 256 x 256 / 256 x 128 with eight 128 x 64 waves when
-  // the grid still gives every CU a block, else 128 x 128; grids that would not give
-  // every CU two blocks drop to 64-row tiles.
+  // heuristic: 64-channel layers take 256 x 64 tiles (four waves stacked along M, 64 x 64
+  // each); wider layers 256 x 256 with eight 128 x 64 waves when the grid still gives
+  // every CU a block, else 128 x 128; grids that would not give every CU two blocks drop
+  // to 64-row tiles.
   auto blocks = [&](int bm, int bn) {
     return static_cast<long long>((g.M + bm - 1) / bm) * (g.CoutPad / bn) * nclass;
   };
   int cfg;
   if (g.CoutPad % 128 != 0) {
     cfg = blocks(256, 64) >= 1024 ? 0 : (blocks(128, 64) >= 512 ? 1 : 2);
-  } else if (g_big && g.CoutPad % 256 == 0 && blocks(256, 256) >= 256) {
+  } else if (g.CoutPad % 256 == 0 && blocks(256, 256) >= 256) {
     cfg = 5;
   } else {  // 128-channel layers: 256 x 128 measured slower than 128 x 128 (layer2 c1/c2, R50@256)
     cfg = blocks(128, 128) >= 512 ? 3 : 4;
   }
-  // per-call tile (autotuned plans) > test hook > heuristic; tile = cfg + 8 * variant,
-  // variant 1 = single-slot ring (four-wave tiles), 2 = three-slot ring (where it fits)
-  int want = tile >= 0 ? tile : g_force;
-  int st = g_stages;
-  bool ph = false;
-  // tiles 7 / 15: ping-pong loop on 256x256 / 256x128 (eight 128x64 / 128x32 waves),
-  // 2-byte dtypes, one-tap-per-K-tile gathers or two-source tails; else the heuristic
-  // tiles 23 / 31: the staggered two-slot loop on 256x256 / 256x128 (any gather)
-  bool pp = false, sg = false;
-  if (want == 7 || want == 15) {
-    const int c = want == 7 ? 5 : 6;
-    if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0 &&
-        (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0))) {
-      cfg = c;
-      pp = true;
-    }
-    want = -1;
-  } else if (want == 23 || want == 31) {
-    const int c = want == 23 ? 5 : 6;
+  int st = 2;
+  bool sg = false, persist = false;
+  if (tile == 23 || tile == 31) {
+    const int c = tile == 23 ? 5 : 6;
     if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
       cfg = c;
       sg = true;
     }
-    want = -1;
-  }
-  if (want >= 0 && want < 64) {
-    const int c = want & 7;
+  } else if (tile >= 0) {
+    const int c = tile & 7, v = (tile >> 3) & 3;
     const bool wide_ok = g.CoutPad % 128 == 0 && (c != 5 || g.CoutPad % 256 == 0);
     if (c <= 2 || wide_ok) {
       cfg = c;
-      const int v = want >> 3;
       st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
-      // variant 3: phased 256x256 loop (one-tap-per-K-tile gathers and two-source tails)
-      ph = (v & 3) == 3 && c == 5 && (DUAL || (g.C % bk_of_t<T>() == 0 && g.up == 0));
+      // persistent K-tile stream: 2-byte dtypes, direct NHWC epilogue, outputs addressable
+      // by a 32-bit buffer offset
+      persist = (tile & 32) != 0 && sizeof(T) == 2 && g.mode == 0 &&
+                static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
     }
+  } else if (sizeof(T) == 2 && (cfg == 5 || cfg == 6)) {
+    sg = true;  // untuned eight-wave launches take the staggered loop (bit-exact with the plain one)
   }
-  // persistent K-tile stream (tile bit 32, or the process-wide knob): 2-byte dtypes,
-  // direct NHWC epilogue, outputs addressable by a 32-bit buffer offset
-  const bool persist_ok = sizeof(T) == 2 && g.mode == 0 && !g.hm && !g.cy &&
-                          static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
-  // untuned eight-wave launches take the staggered loop (bit-exact with the plain one)
-  if (want < 0 && !g_persist && sizeof(T) == 2 && !pp && !ph && (cfg == 5 || cfg == 6)) sg = true;
-  const bool persist = !pp && !sg && persist_ok && (want >= 0 ? (want & 32) != 0 : g_persist != 0);
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
   static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
-  if constexpr (sizeof(T) == 2 && !DUAL) {
-    // halo variant (tile 64 + h): whole output rows per tile, input window staged once per
-    // K-chunk; falls through to the heuristic when the geometry does not fit
-    if (want >= 64 && want < 75 && (want & 7) != 7 && g.C % bk_of_t<T>() == 0) {
-      // 64..68: two halo slots (any C); 69, 70, 72: one slot (C == one K-chunk), smaller
-      // LDS so two blocks share a CU
-      const int h = want - 64;
-      static const int hBM[] = {256, 256, 256, 128, 128, 256, 128, 0, 256};
-      static const int hBN[] = {256, 128, 64, 128, 64, 64, 64, 0, 128};
-      static const int hNW[] = {8, 8, 4, 4, 4, 4, 4, 0, 8};
-      static const int hHR[] = {halo_rows_max<256>(), halo_rows_max<128>(), halo_rows_max<64>(),
-                                halo_rows_max<128>(), halo_rows_max<64>(), 448, 320, 0, 448};
-      const bool one_slot = h >= 5;
-      ConvGeom hg = g;
-      if (g.CoutPad % hBN[h] == 0 && (!one_slot || g.C == bk_of_t<T>()) &&
-          halo_geometry(hg, hBM[h], hBN[h], hNW[h], hHR[h])) {
-        hg.ntiles = g.CoutPad / hBN[h];
-        hg.mtiles = (g.M + hBM[h] - 1) / hBM[h];
-        const int hb = hg.mtiles * hg.ntiles * nclass;
-        switch (h) {
-          case 0: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 256, 8, 2>), dim3(hb), dim3(512), 0, s, hg); break;
-          case 1: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 128, 8, 4>), dim3(hb), dim3(512), 0, s, hg); break;
-          case 2: hipLaunchKernelGGL((conv_halo_kernel<T, 256, 64, 4, 4>), dim3(hb), dim3(256), 0, s, hg); break;
-          case 3: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 128, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
-          case 4: hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2>), dim3(hb), dim3(256), 0, s, hg); break;
-          case 5:
-            hipLaunchKernelGGL((conv_halo_kernel<T, 256, 64, 4, 4, 448, 1>), dim3(hb), dim3(256), 0, s, hg);
-            break;
-          case 6:
-            hipLaunchKernelGGL((conv_halo_kernel<T, 128, 64, 4, 2, 320, 1>), dim3(hb), dim3(256), 0, s, hg);
-            break;
-          default:
-            hipLaunchKernelGGL((conv_halo_kernel<T, 256, 128, 8, 4, 448, 1>), dim3(hb), dim3(512), 0, s, hg);
-            break;
-        }
-        return check_launch(what);
-      }
-    }
-  }
   if constexpr (sizeof(T) == 2) {
     if (persist) {
       switch (cfg) {
@@ -2188,20 +1496,11 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       }
       return check_launch(what);
     }
-  }
-  if constexpr (sizeof(T) == 2) {
-    if (pp) {
-      if (cfg == 5)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 1>), dim3(nb), dim3(512), 0, s, g);
-      else
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 2, 2, DUAL, false, 1>), dim3(nb), dim3(512), 0, s, g);
-      return check_launch(what);
-    }
     if (sg) {
       if (cfg == 5)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, 2>), dim3(nb), dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       else
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, false, 2>), dim3(nb), dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
     }
   }
@@ -2211,10 +1510,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     case 2: launch_cfg<T, 64, 64, 4, 2, DUAL>(g, nb, st, s); break;
     case 3: launch_cfg<T, 128, 128, 4, 2, DUAL>(g, nb, st, s); break;
     case 4: launch_cfg<T, 64, 128, 4, 2, DUAL>(g, nb, st, s); break;
-    case 5:
-      if (ph) hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
-      else launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s);
-      break;
+    case 5: launch_cfg<T, 256, 256, 8, 2, DUAL>(g, nb, 2, s); break;
     default: launch_cfg<T, 256, 128, 8, 4, DUAL>(g, nb, st == 3 ? 3 : 2, s); break;
   }
   return check_launch(what);
@@ -2269,63 +1565,11 @@ using namespace posu;
 
 extern "C" int posu_conv_bk(int dtype) { return bk_of(dtype); }
 
-extern "C" int posu_force_conv_config(int cfg) {
-  POSU_REQUIRE(cfg == -1 || (cfg >= 0 && cfg < 75 && ((cfg & 7) != 7 || cfg == 7 || cfg == 15 || cfg == 23 || cfg == 31)), "posu_force_conv_config: -1 (auto) or cfg + 8 * variant");
-  g_force = cfg;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_epilogue(int direct) {
-  g_direct = direct < 0 ? 0 : direct > 2 ? 2 : direct;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_nt_threshold(long long bytes) {
-  g_nt_min_bytes = bytes;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_early_residual(int max_ktiles) {
-  g_early_nk = max_ktiles;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_chain8(int on) {
-  g_chain8 = on ? 1 : 0;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_head256(int on) {
-  g_head256 = on ? 1 : 0;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_persistent(int on) {
-  g_persist = on ? 1 : 0;
-  return POSU_OK;
-}
-
-extern "C" int posu_debug_conv_stamps(void* buf) {
-  g_stamps = static_cast<long long*>(buf);
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_tiles(int big) {
-  g_big = big ? 1 : 0;
-  return POSU_OK;
-}
-
-extern "C" int posu_set_conv_stages(int stages) {
-  POSU_REQUIRE(stages == 2 || stages == 3, "posu_set_conv_stages: 2 or 3");
-  g_stages = stages;
-  return POSU_OK;
-}
-
 extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_conv2d_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile_ok(tile), "posu_conv2d_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -2357,7 +1601,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_conv1x1_dual_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile_ok(tile), "posu_conv1x1_dual_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -2389,7 +1633,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile == -1 || (tile >= 0 && tile < 75 && ((tile & 7) != 7 || tile == 7 || tile == 15 || tile == 23 || tile == 31)), "posu_deconv4x4s2_fwd: tile must be -1 (auto) or cfg + 8 * variant");
+  POSU_REQUIRE(tile_ok(tile), "posu_deconv4x4s2_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
@@ -2490,89 +1734,6 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
   g.out_H = H;
   g.out_W = W;
   return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
-}
-
-// Bottleneck tail + the next block's conv1 in one launch (layer1: Cout 256): the block
-// output y is written as usual and, from the same tile in LDS, cy = relu(bn(conv1x1(y)))
-// (pose_resnet.py:79-99: out of block b feeds conv1 of block b + 1), so y is not read
-// back from HBM by the next block.
-namespace posu {
-namespace {
-int attach_chain(ConvGeom& g, int dtype, const void* cw, int Cout2, const float* cscale, const float* cshift, void* cy,
-                 const char* what) {
-  POSU_REQUIRE(cw && cscale && cshift && cy, std::string(what) + ": null chained operand");
-  POSU_REQUIRE(g.Cout == 256 && g.relu && Cout2 > 0 && Cout2 % 16 == 0 && Cout2 <= 128,
-               std::string(what) + ": needs Cout == 256, ReLU, and 16 <= Cout2 <= 128 (multiple of 16)");
-  g.cw = cw;
-  g.Cout2 = Cout2;
-  g.cscale = cscale;
-  g.cshift = cshift;
-  g.cy = cy;
-  g.ckp = round_up(g.Cout, bk_of(dtype));
-  return POSU_OK;
-}
-}  // namespace
-}  // namespace posu
-
-extern "C" int posu_conv2d_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
-                                     int KH, int KW, int stride, int pad, const float* scale, const float* shift,
-                                     const void* residual, int relu, void* y, const void* cw, int Cout2,
-                                     const float* cscale, const float* cshift, void* cy, void* stream) {
-  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_chain_fwd")) return st;
-  POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_chain_fwd: bad window");
-  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  POSU_REQUIRE(Ho > 0 && Wo > 0, "posu_conv2d_chain_fwd: empty output");
-  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
-  g.scale = scale;
-  g.shift = shift;
-  g.res = residual;
-  g.y = y;
-  g.Ho = Ho;
-  g.Wo = Wo;
-  g.M = N * Ho * Wo;
-  g.K = KH * KW * C;
-  g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = KH;
-  g.KW = KW;
-  g.stride = stride;
-  g.pad_h = pad;
-  g.pad_w = pad;
-  g.relu = relu;
-  g.out_H = Ho;
-  g.out_W = Wo;
-  if (int st = attach_chain(g, dtype, cw, Cout2, cscale, cshift, cy, "posu_conv2d_chain_fwd")) return st;
-  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_chain_fwd");
-}
-
-extern "C" int posu_conv1x1_dual_chain_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2,
-                                           int H2, int W2, int C2, int stride2, const void* w, int Cout,
-                                           const float* shift, int relu, void* y, const void* cw, int Cout2,
-                                           const float* cscale, const float* cshift, void* cy, void* stream) {
-  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_chain_fwd")) return st;
-  if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_chain_fwd")) return st;
-  const int BK = bk_of(dtype);
-  POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_chain_fwd: C and C2 must be multiples of the K-tile");
-  POSU_REQUIRE(stride2 > 0 && (H - 1) * stride2 < H2 && (W - 1) * stride2 < W2,
-               "posu_conv1x1_dual_chain_fwd: source-2 grid too small for the output grid");
-  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
-  g.x2 = x2;
-  g.H2 = H2;
-  g.W2 = W2;
-  g.C2 = C2;
-  g.stride2 = stride2;
-  g.K1 = C;
-  g.shift = shift;
-  g.y = y;
-  g.Ho = H;
-  g.Wo = W;
-  g.M = N * H * W;
-  g.K = C + C2;
-  g.Kpad = C + C2;
-  g.relu = relu;
-  g.out_H = H;
-  g.out_W = W;
-  if (int st = attach_chain(g, dtype, cw, Cout2, cscale, cshift, cy, "posu_conv1x1_dual_chain_fwd")) return st;
-  return dispatch<true>(dtype, g, 1, stream, "posu_conv1x1_dual_chain_fwd");
 }
 
 // Plain GEMM on the conv kernel (1x1 window over M "pixels" of K channels):

@@ -8,11 +8,18 @@ posu_flip_back launch per view), weighted-MSE loss, PCK accuracy, and
 (``preds[k::nviews]``) exactly as the reference stores them.  Everything stays on the
 device until the final copy of predictions and heatmaps.
 
+With NETWORK.AGGRE the cross-view Aggregation runs too (models.multiview_pose_resnet),
+TEST.FUSE_OUTPUT routes the outputs (``fuse_routing``), and the loss carries the
+reference's AGGRE terms (function.py:597-609): the consistent loss between the raw and
+aggregated heatmaps of the H36M samples (LOSS.USE_CONSISTENT_LOSS, plain mean MSE) and,
+with DATASET.PSEUDO_LABEL_PATH, the weighted MSE of the routed outputs against the
+pseudo-label targets times LOSS.MSE_LOSS_WEIGHT.
+
 ``validate`` keeps the reference signature (function.py:529-536) and its outputs: the
 ``heatmaps_locations_<subset>_<type>.h5`` file that run/test/test_triangulate.py reads
 (keys heatmaps / locations / joint_names_order, u2a-selected joints) and
-``dataset.evaluate``'s perf indicator.  Debug-image dumps, tensorboard and the
-AGGRE fusion routing are not part of this build (AGGRE raises at model construction).
+``dataset.evaluate``'s perf indicator.  Debug-image dumps and tensorboard are not part
+of this build.
 """
 import logging
 import os
@@ -41,6 +48,16 @@ def fuse_routing(raw_features, aggre_features, is_aggre, meta):
     return output
 
 
+def select_out_h36m(raw_features, aggre_features, meta):
+    """function.py:47-61: per view, the raw and aggregated heatmaps of the H36M samples."""
+    raw_h36m, agg_h36m = [], []
+    for r, a, m in zip(raw_features, aggre_features, meta):
+        idx = torch.tensor([s == 'h36m' for s in m['source']], dtype=torch.bool, device=r.device)
+        raw_h36m.append(r[idx])
+        agg_h36m.append(a[idx])
+    return raw_h36m, agg_h36m
+
+
 def _run_model(model, views, hflip):
     """model(views) -> (per-view heatmaps, aggregated heatmaps or []); the flip test's
     mirrored input is packed by the HIP input-pack kernel when the model is this build's."""
@@ -59,7 +76,7 @@ def _run_model(model, views, hflip):
 
 
 def validate_batch(config, model, input, target=None, weight=None, meta=None, flip_pairs=None,
-                   criterion=None):
+                   criterion=None, criterion_dict=None):
     """One batch of the reference's validate loop.
 
     input: V x [N, 3, H, W] cuda f32; target / weight: V x [N, J, h, w] / [N, J, 1] (optional);
@@ -82,10 +99,24 @@ def validate_batch(config, model, input, target=None, weight=None, meta=None, fl
         res = {'output': output, 'loss': None, 'acc': None, 'cnt': None}
         if target is not None:
             target = [t.to(device) for t in target]
+            criterion = criterion or (criterion_dict or {}).get('mse_weights')
             if criterion is not None and weight is not None:
+                weight = [w.to(device) for w in weight]
                 loss = 0
                 for t, w, r in zip(target, weight, raw):   # on the raw outputs (function.py:589-595)
-                    loss = loss + criterion(r, t, w.to(device))
+                    loss = loss + criterion(r, t, w)
+                if config.NETWORK.AGGRE:                   # function.py:597-609
+                    if getattr(config.LOSS, 'USE_CONSISTENT_LOSS', False):
+                        raw_h36m, agg_h36m = select_out_h36m(raw, agg, meta)
+                        assert len(raw_h36m[0]) == len(agg_h36m[0])
+                        if len(raw_h36m[0]) != 0:
+                            rh, ah = torch.cat(raw_h36m, dim=0), torch.cat(agg_h36m, dim=0)
+                            # torch.nn.MSELoss(reduction='mean') = the joints MSE (a sum of
+                            # per-joint means) / J, on the HIP reduction kernel
+                            loss = loss + ops.joints_mse(rh.contiguous(), ah.contiguous(), None) / rh.shape[1]
+                    if getattr(config.DATASET, 'PSEUDO_LABEL_PATH', ''):
+                        for t, w, o in zip(target, weight, output):
+                            loss = loss + criterion(o, t, w) * config.LOSS.MSE_LOSS_WEIGHT
                 res['loss'] = float(loss)
             accs, cnts = [], []
             for o, t in zip(output, target):
@@ -137,8 +168,7 @@ def validate(config, loader, dataset, model_dict, criterion_dict, output_dir, wr
     for i, (input, target, weight, meta) in enumerate(loader):
         input = [view.to(device, non_blocking=False) for view in input]
         r = validate_batch(config, model_dict['base_model'], input, target, weight, meta,
-                           flip_pairs=getattr(dataset, 'flip_pairs', None),
-                           criterion=criterion_dict.get('mse_weights'))
+                           flip_pairs=getattr(dataset, 'flip_pairs', None), criterion_dict=criterion_dict)
         nimgs = r['preds'].shape[0]
         all_preds[idx:idx + nimgs] = r['preds']
         all_heatmaps[idx:idx + nimgs] = r['heatmaps']

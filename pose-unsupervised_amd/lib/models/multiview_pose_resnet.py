@@ -17,25 +17,30 @@ import torch
 import torch.nn as nn
 
 from posu import ops
-from posu.aggregate import aggregate
+from posu.aggregate import aggregate, channel_fc
 
 
 class ChannelWiseFC(nn.Module):
     """multiview_pose_resnet.py:16-29: out[n, c] = in[n, c].flatten() @ weight."""
 
-    def __init__(self, size):
+    def __init__(self, size, precision='fp32'):
         super(ChannelWiseFC, self).__init__()
         self.weight = nn.Parameter(torch.Tensor(size, size))
         self.weight.data.uniform_(0, 0.1)
+        self.precision = precision
 
     def forward(self, input):
-        raise NotImplementedError('ChannelWiseFC runs inside Aggregation (one fused GEMM for all view pairs)')
+        """One MFMA rows GEMM ([N*C, HW] x [HW, HW]); inside Aggregation all twelve run as
+        one block-matrix GEMM instead."""
+        if not input.is_cuda:
+            raise RuntimeError('ChannelWiseFC runs on the MI355X HIP path only: input must be a cuda tensor')
+        return channel_fc(input, self.weight, ops.dtype_code(self.precision))
 
 
 class Aggregation(nn.Module):
     """multiview_pose_resnet.py:32-58: warped_i = sum_{o != i} fc_(i,o)(x_o) / (V - 1)."""
 
-    def __init__(self, cfg, weights=[0.4, 0.2, 0.2, 0.2], precision='bf16'):
+    def __init__(self, cfg, weights=[0.4, 0.2, 0.2, 0.2], precision='fp32'):
         super(Aggregation, self).__init__()
         NUM_NETS = 12
         size = int(cfg.NETWORK.HEATMAP_SIZE[0])
@@ -43,7 +48,7 @@ class Aggregation(nn.Module):
         self.precision = precision
         self.aggre = nn.ModuleList()
         for i in range(NUM_NETS):
-            self.aggre.append(ChannelWiseFC(size * size))
+            self.aggre.append(ChannelWiseFC(size * size, precision))
 
     def forward(self, inputs):
         for t in inputs:
@@ -81,5 +86,5 @@ class MultiViewPose(nn.Module):
 
 
 def get_multiview_pose_net(PoseResNet, CFG):
-    Aggre = Aggregation(CFG, precision=getattr(PoseResNet, 'precision', 'bf16')) if CFG.NETWORK.AGGRE else None
+    Aggre = Aggregation(CFG, precision=getattr(PoseResNet, 'precision', 'fp32')) if CFG.NETWORK.AGGRE else None
     return MultiViewPose(PoseResNet, Aggre, CFG)

@@ -10,11 +10,15 @@ The modules hold the parameters in the reference's NCHW fp32 layout; forward run
 :class:`posu.plan.PoseResNetPlan` (NHWC, MFMA implicit-GEMM kernels, BN folded into
 the conv epilogues) that is re-packed whenever a parameter or buffer changes.
 
-Compute dtype: ``precision='bf16'`` (default, bf16 operands / f32 accumulate),
-``'fp16'`` (IEEE fp16 operands / f32 accumulate, the fp16 setting of BASELINE
-configs[4]) or ``'fp32'`` (exact-f32 MFMA; the parity mode).  Heatmaps are always returned as NCHW
-float32; ``layer1_out`` / ``deconv_out`` are returned as NCHW-shaped channels-last
-views of the NHWC activations in the compute dtype (zero-copy).
+Compute dtype: ``precision='fp32'`` (the default: exact-f32 MFMA, the reference's fp32
+numerics -- heatmaps within 1e-3 of the reference, so an unchanged reference script gets
+reference results), ``'bf16'`` (opt-in fast mode: bf16 operands / f32 accumulate,
+~16x the fp32 MFMA rate; heatmaps deviate ~0.02 mean / 0.15 max from the fp32 path on
+R50@256) or ``'fp16'`` (IEEE fp16 operands / f32 accumulate, the fp16
+setting of BASELINE configs[4]).  Heatmaps are always returned as NCHW float32;
+``layer1_out`` / ``deconv_out`` are returned as NCHW-shaped channels-last views of the
+NHWC activations in the compute dtype (zero-copy; fp32 in the default mode, like the
+reference's).
 
 Training mode (``model.train()``) runs posu.train_plan: batch-statistics BN per view,
 differentiable through one autograd Function whose backward is the HIP kernel chain;
@@ -75,7 +79,7 @@ _DECONV_CFG = {4: (1, 0), 3: (1, 1), 2: (0, 0)}  # kernel -> (padding, output_pa
 
 class PoseResNet(nn.Module):
 
-    def __init__(self, block, layers, cfg, precision='bf16', **kwargs):
+    def __init__(self, block, layers, cfg, precision='fp32', **kwargs):
         super(PoseResNet, self).__init__()
         extra = cfg.POSE_RESNET
         self.inplanes = 64
@@ -198,7 +202,8 @@ resnet_spec = {18: (BasicBlock, [2, 2, 2, 2]),
 
 
 def get_pose_net(cfg, is_train, **kwargs):
-    """Reference factory (pose_resnet.py:257-267); extra kwarg ``precision`` = 'bf16' | 'fp16' | 'fp32'."""
+    """Reference factory (pose_resnet.py:257-267); extra kwarg ``precision`` = 'fp32' (default,
+    reference numerics) | 'bf16' | 'fp16' (opt-in fast modes)."""
     block_class, layers = resnet_spec[cfg.POSE_RESNET.NUM_LAYERS]
     model = PoseResNet(block_class, layers, cfg, **kwargs)
     if is_train:

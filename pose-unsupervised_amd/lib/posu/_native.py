@@ -35,22 +35,8 @@ _SIGNATURES = {
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
     'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_conv_bk': [_i],
-    'posu_set_conv_stages': [_i],
-    'posu_set_conv_tiles': [_i],
-    'posu_debug_conv_stamps': [_p],
-    'posu_set_conv_epilogue': [_i],
-    'posu_set_conv_nt_threshold': [_ll],
-    'posu_set_conv_early_residual': [_i],
-    'posu_set_conv_persistent': [_i],
-    'posu_set_conv_head256': [_i],
-    'posu_set_conv_chain8': [_i],
     'posu_stem_pool_fwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p],
-    'posu_force_conv_config': [_i],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
-    'posu_conv2d_chain_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _p, _i, _p, _p, _p,
-                              _p],
-    'posu_conv1x1_dual_chain_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _i, _p, _p, _i, _p, _p,
-                                    _p, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p],
     'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],

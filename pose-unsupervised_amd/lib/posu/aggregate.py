@@ -106,3 +106,46 @@ def aggregate(views, weights, code):
     hm_vm = torch.stack([t.float() for t in views], 0)
     out = _AggregateFn.apply(hm_vm, code, *weights)
     return list(out.unbind(0))
+
+
+class _ChannelFCFn(torch.autograd.Function):
+    """ChannelWiseFC.forward (multiview_pose_resnet.py:23-28): out[n, c] = in[n, c].flatten() @ W
+    as one rows GEMM (posu_gemm_rows_f32); backward dX = dOut . W^T (same kernel, W as the
+    packed operand) and dW = X^T . dOut (the 1x1 weight-gradient kernel over M rows)."""
+
+    @staticmethod
+    def forward(ctx, inp, weight, code):
+        n, c, h, w = inp.shape
+        hw = h * w
+        x = pack_rows(inp.float().reshape(1, n * c, hw), code)                      # [M, HW]
+        wt = weight.detach().float().t().contiguous().to(ops.torch_dtype(code))    # [p][q]
+        out = gemm_rows(x, wt, hw, hw, code)                                         # [1, M, HW]
+        ctx.save_for_backward(x, weight)
+        ctx.code, ctx.shape = code, (n, c, h, w)
+        return out.reshape(n, c, h, w)
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, weight = ctx.saved_tensors
+        code = ctx.code
+        n, c, h, w = ctx.shape
+        hw, m = h * w, n * c
+        g = pack_rows(gout.float().reshape(1, m, hw), code)
+        dinp = dw = None
+        if ctx.needs_input_grad[0]:
+            wq = weight.detach().float().contiguous().to(ops.torch_dtype(code))     # [q][p]
+            dinp = gemm_rows(g, wq, hw, hw, code).reshape(n, c, h, w)
+        if ctx.needs_input_grad[1]:
+            dbt = T.conv2d_wgrad(g.view(m, 1, 1, hw), x.view(m, 1, 1, hw), hw, 1, 1, 1, 0, code).view(hw, hw)
+            dw = dbt.t().contiguous()
+        return dinp, dw, None
+
+
+def channel_fc(inp, weight, code):
+    """[N, C, H, W] cuda heatmaps x ChannelWiseFC weight [HW, HW] -> [N, C, H, W] f32.
+    H*W must be a power of two (the rows GEMM's K; 64x64 / 32x32 heatmaps)."""
+    require_cuda(inp, weight)
+    hw = inp.shape[2] * inp.shape[3]
+    if hw & (hw - 1) or hw < 64:
+        raise NotImplementedError('ChannelWiseFC on the HIP path needs H*W a power of two >= 64 (got %d)' % hw)
+    return _ChannelFCFn.apply(inp, weight, code)

@@ -31,52 +31,6 @@ def conv_bk(code):
     return nat.load().posu_conv_bk(code)
 
 
-def force_conv_config(cfg):
-    """Test hook: force a conv tile configuration (see include/posu.h), -1 = automatic."""
-    call('posu_force_conv_config', int(cfg))
-
-
-def set_conv_tiles(big):
-    """Enable (True) / disable the eight-wave 256-row tiles for wide layers."""
-    call('posu_set_conv_tiles', int(bool(big)))
-
-
-def set_conv_stages(stages):
-    """Depth of the conv kernels' LDS-DMA ring (2 or 3 K-tiles in flight)."""
-    call('posu_set_conv_stages', int(stages))
-
-
-def set_conv_epilogue(direct):
-    """NHWC conv epilogue: 1 = straight from the accumulators (default), 2 = the same with
-    non-temporal (streaming) stores, 0 = through LDS."""
-    call('posu_set_conv_epilogue', int(direct))
-
-
-def set_conv_nt_threshold(nbytes):
-    """Outputs below nbytes keep plain (L2-allocating) stores under epilogue mode 2."""
-    call('posu_set_conv_nt_threshold', int(nbytes))
-
-
-def set_conv_early_residual(max_ktiles):
-    """Residual prefetch before the operand fetch for launches of <= max_ktiles K-tiles."""
-    call('posu_set_conv_early_residual', int(max_ktiles))
-
-
-def set_conv_persistent(on):
-    """Persistent K-tile-stream conv variant for launches without an explicit tile."""
-    call('posu_set_conv_persistent', int(bool(on)))
-
-
-def set_conv_head256(on):
-    """Fused deconv + head on the 256x256 direct-epilogue tile (1) or the 64x256 LDS tile (0)."""
-    call('posu_set_conv_head256', int(bool(on)))
-
-
-def set_conv_chain8(on):
-    """Chained next conv1 (Cout2 <= 64) on the 8x1-wave 256x256 register-epilogue tile."""
-    call('posu_set_conv_chain8', int(bool(on)))
-
-
 # ---------------------------------------------------------------- layout ops
 def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     """[N, C, H, W] f32 -> [N, H, W, cpad] (zero channels above C); hflip mirrors W."""
@@ -132,32 +86,6 @@ def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, ti
     call('posu_conv1x1_dual_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
          None, ptr(shift), int(relu), ptr(out), int(tile), stream_of(x.device))
     return out
-
-
-def conv2d_chain_nhwc(x, wpk, cout, k, stride, pad, scale, shift, residual, code, cw, cout2, cscale, cshift,
-                      out=None):
-    """Block tail conv (+residual, ReLU) and the next block's 1x1 conv1 in one launch:
-    returns (y [N, Ho, Wo, cout], cy [N, Ho, Wo, cout2])."""
-    n, h, w, c = x.shape
-    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    if out is None:
-        out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
-    cy = torch.empty((n, ho, wo, cout2), dtype=x.dtype, device=x.device)
-    call('posu_conv2d_chain_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, k, k, stride, pad, ptr(scale), ptr(shift),
-         ptr(residual), 1, ptr(out), ptr(cw), cout2, ptr(cscale), ptr(cshift), ptr(cy), stream_of(x.device))
-    return out, cy
-
-
-def conv1x1_dual_chain_nhwc(x, x2, stride2, wpk, cout, shift, code, cw, cout2, cscale, cshift, out=None):
-    """Two-source Bottleneck tail (conv3|downsample, ReLU) chained with the next conv1."""
-    n, h, w, c = x.shape
-    _, h2, w2, c2 = x2.shape
-    if out is None:
-        out = torch.empty((n, h, w, cout), dtype=x.dtype, device=x.device)
-    cy = torch.empty((n, h, w, cout2), dtype=x.dtype, device=x.device)
-    call('posu_conv1x1_dual_chain_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
-         ptr(shift), 1, ptr(out), ptr(cw), cout2, ptr(cscale), ptr(cshift), ptr(cy), stream_of(x.device))
-    return out, cy
 
 
 def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):

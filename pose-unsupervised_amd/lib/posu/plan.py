@@ -23,12 +23,6 @@ from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dua
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
-# Bottleneck tails that also compute the next block's conv1: True = wherever chainable_to
-# allows (next conv1 <= 128 channels), False = never (default), 'auto' = only where the
-# register-epilogue chain applies (bf16 / fp16, next conv1 <= 64 channels).  Both measured
-# slower end to end on R50@256 (64x256 LDS chain tile: 381 vs 341 us for block0 + the next
-# conv1; register chain, posu_set_conv_chain8: 3.67 vs 3.38 ms per 128-frame forward).
-CHAIN_BLOCKS = False
 # fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
 FUSED_STEM = True
 
@@ -159,14 +153,13 @@ class _DualTail:
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'chain')
+    __slots__ = ('convs', 'down', 'dual')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
         self.convs = []
         self.down = None
         self.dual = None
-        self.chain = None   # the next block's conv1, computed in this block's tail launch
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -183,35 +176,16 @@ class _Block:
     def cout(self):
         return self.dual.cout if self.dual is not None else self.convs[-1].cout
 
-    def chainable_to(self, nxt):
-        """This block's tail can also compute `nxt`'s conv1 (posu_conv2d_chain_fwd): all 256
-        output channels in one tile, and a 1x1 / stride-1 next conv1 of <= 128 channels."""
-        c1 = nxt.convs[0]
-        return (self.cout == 256 and c1.k == 1 and c1.stride == 1 and c1.pad == 0 and c1.relu
-                and c1.cout <= 128 and c1.cout % 16 == 0 and c1.w.shape[1] == 256)
-
-    def __call__(self, x, code, out=None, pre=None):
-        """-> (block output, the next block's conv1 output if chained else None).
-        pre: this block's conv1 output, already computed by the previous block."""
-        y = pre if pre is not None else x
-        first = 1 if pre is not None else 0
-        ch = self.chain
+    def __call__(self, x, code, out=None):
+        y = x
         if self.dual is not None:
-            for c in self.convs[first:]:
+            for c in self.convs:
                 y = c(y, code)
-            if ch is not None:
-                dl = self.dual
-                return ops.conv1x1_dual_chain_nhwc(y, x, dl.stride2, dl.w, dl.cout, dl.shift, code, ch.w, ch.cout,
-                                                   ch.scale, ch.shift, out=out)
-            return self.dual(y, x, code, out=out), None
+            return self.dual(y, x, code, out=out)
         res = self.down(x, code) if self.down is not None else x
-        for c in self.convs[first:-1]:
+        for c in self.convs[:-1]:
             y = c(y, code)
-        last = self.convs[-1]
-        if ch is not None:
-            return ops.conv2d_chain_nhwc(y, last.w, last.cout, last.k, last.stride, last.pad, last.scale,
-                                         last.shift, res, code, ch.w, ch.cout, ch.scale, ch.shift, out=out)
-        return last(y, code, residual=res, out=out), None
+        return self.convs[-1](y, code, residual=res, out=out)
 
 
 class _Deconv:
@@ -243,12 +217,6 @@ class PoseResNetPlan:
         self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, STEM_S2D_PAD, bk, ops.torch_dtype(code))
         self.layers = [[_Block(b, code, bk) for b in layer] for layer in
                        (net.layer1, net.layer2, net.layer3, net.layer4)]
-        if CHAIN_BLOCKS:
-            blocks = [b for layer in self.layers for b in layer]
-            for b, nxt in zip(blocks, blocks[1:]):
-                if b.chainable_to(nxt) and (CHAIN_BLOCKS is True or (
-                        code in (ops.BF16, ops.F16) and nxt.convs[0].cout <= 64)):
-                    b.chain = nxt.convs[0]
         mods = list(net.deconv_layers)
         self.deconvs = []
         for i in range(0, len(mods), 3):
@@ -316,20 +284,18 @@ class PoseResNetPlan:
         """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
         code = self.code
         x = self.stem_pool(x)
-        pre = None
         for li in (0, 1):
             layer = self.layers[li]
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
                 if li == 0 and last and keep is not None:
-                    x, pre = blk(x, code, out=keep, pre=pre)
+                    x = blk(x, code, out=keep)
                 elif li == 1 and last and out is not None:
-                    x, pre = blk(x, code, out=out, pre=pre)
+                    x = blk(x, code, out=out)
                 else:
-                    x, pre = blk(x, code, pre=pre)
+                    x = blk(x, code)
             if li == 0:
                 x1 = x
-        assert pre is None
         return x, x1
 
     def _last_deconv_head(self, x, keep_f, hm_out=None, f_out=None):
@@ -378,10 +344,9 @@ class PoseResNetPlan:
         if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
             x = self.stem_pool(x)
             x1 = None
-            pre = None
             for li, layer in enumerate(self.layers):
                 for blk in layer:
-                    x, pre = blk(x, code, pre=pre)
+                    x = blk(x, code)
                 if li == 0:
                     x1 = x
             for dc in self.deconvs[:-1]:
@@ -404,10 +369,9 @@ class PoseResNetPlan:
             sl = slice(k * c, (k + 1) * c)
             self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
         y = x2
-        pre = None
         for layer in self.layers[2:]:
             for blk in layer:
-                y, pre = blk(y, code, pre=pre)
+                y = blk(y, code)
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)

@@ -328,22 +328,33 @@ def adam_golden(ref_pr, ref_loss, num_layers=18, image_size=128, nviews=4, batch
     hms = image_size // 4
     targets = peaked_heatmaps(nviews * batch, 16, hms, hms, seed=init_seed + 2).reshape(nviews, batch, 16, hms, hms)
     tw = (np.random.default_rng(init_seed + 3).uniform(size=(nviews, batch, 16, 1)) > 0.15).astype(np.float32)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
-    crit = ref_loss.JointsMSELoss(use_target_weight=True)
-    losses, norms = [], []
-    for _ in range(ADAM_STEPS):
-        outs = [net(v)[0] for v in views]
-        loss = sum(crit(outs[v], torch.from_numpy(targets[v]), torch.from_numpy(tw[v])) for v in range(nviews))
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-        losses.append(loss.item())
-        norms.append([float(p.detach().norm()) for p in net.parameters()])
+    def trajectory(model, dtype):
+        model = model.to(dtype)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        crit = ref_loss.JointsMSELoss(use_target_weight=True)
+        losses, norms = [], []
+        for _ in range(ADAM_STEPS):
+            outs = [model(v.to(dtype))[0] for v in views]
+            loss = sum(crit(outs[v], torch.from_numpy(targets[v]).to(dtype), torch.from_numpy(tw[v]).to(dtype))
+                       for v in range(nviews))
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+            norms.append([float(p.detach().norm()) for p in model.parameters()])
+        return losses, norms
+    import copy
+    net64 = copy.deepcopy(net)
+    losses, norms = trajectory(net, torch.float32)
+    # the same trajectory in fp64: the reference's own fp32 rounding moves an Adam
+    # trajectory (sign-like first steps on near-zero gradients), measured against this
+    losses64, norms64 = trajectory(net64, torch.float64)
     np.savez_compressed(os.path.join(HERE, 'adam_r%d_%d.npz' % (num_layers, image_size)),
                         num_layers=num_layers, image_size=image_size, nviews=nviews, batch=batch,
                         init_seed=init_seed, lr=1e-3, init_sums=init_sums, torch_init_sums=torch_init_sums,
                         targets=targets, target_weight=tw,
                         losses=np.array(losses), param_norms=np.array(norms),
+                        losses_f64=np.array(losses64), param_norms_f64=np.array(norms64),
                         param_names=np.array([n for n, _ in net.named_parameters()]))
     print('adam r%d@%d: losses %s' % (num_layers, image_size, ['%.6f' % v for v in losses]))
 

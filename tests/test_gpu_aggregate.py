@@ -52,3 +52,29 @@ def test_fuse_routing_blends_h36m_samples_only(cuda):
         torch.testing.assert_close(o[0], 3 / 5 * aa[0] + 2 / 5 * rr[0])
         torch.testing.assert_close(o[1], rr[1])
     assert fuse_routing(r, a, False, meta) is r
+
+
+@pytest.mark.parametrize('precision,tol', [('fp32', 1e-5), ('bf16', 2e-2)])
+def test_channel_wise_fc_forward_and_backward_match_matmul(cuda, precision, tol):
+    """ChannelWiseFC.forward on its own (multiview_pose_resnet.py:23-28): reshape to
+    [N*C, H*W] @ weight, against the same torch ops in fp32 on CPU, with gradients."""
+    from models.multiview_pose_resnet import ChannelWiseFC
+    g = torch.Generator().manual_seed(3)
+    fc = ChannelWiseFC(16 * 16, precision=precision)
+    with torch.no_grad():
+        fc.weight.copy_(torch.rand(256, 256, generator=g) * 0.1)
+    x = torch.randn(3, 16, 16, 16, generator=g)
+    gy = torch.randn(3, 16, 16, 16, generator=g)
+    xr = x.clone().requires_grad_(True)
+    wr = fc.weight.detach().clone().requires_grad_(True)
+    ref = torch.matmul(xr.reshape(48, 256), wr).reshape(3, 16, 16, 16)
+    (ref * gy).sum().backward()
+    fc = fc.to(cuda)
+    xd = x.to(cuda).requires_grad_(True)
+    out = fc(xd)
+    (out * gy.to(cuda)).sum().backward()
+    s = ref.abs().max().item()
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), atol=tol * s, rtol=0)
+    np.testing.assert_allclose(xd.grad.cpu().numpy(), xr.grad.numpy(), atol=tol * xr.grad.abs().max().item(), rtol=0)
+    np.testing.assert_allclose(fc.weight.grad.cpu().numpy(), wr.grad.numpy(), atol=tol * wr.grad.abs().max().item(),
+                               rtol=0)

@@ -12,7 +12,7 @@ from posu._native import BF16, F16, F32
 pytestmark = pytest.mark.gpu
 
 
-def _conv_case(cuda, code, n, cin, h, w, cout, k, stride, pad, residual, relu, seed=0):
+def _conv_case(cuda, code, n, cin, h, w, cout, k, stride, pad, residual, relu, seed=0, tile=-1):
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
@@ -32,7 +32,7 @@ def _conv_case(cuda, code, n, cin, h, w, cout, k, stride, pad, residual, relu, s
     xd = xd.to(cuda, dt)
     wp = packing.pack_conv_weight(wt.to(cuda), cin_pad, ops.conv_bk(code), dt)
     rd = res.permute(0, 2, 3, 1).contiguous().to(cuda, dt) if residual else None
-    out = ops.conv2d_nhwc(xd, wp, cout, k, k, stride, pad, sc.to(cuda), sh.to(cuda), rd, relu, code)
+    out = ops.conv2d_nhwc(xd, wp, cout, k, k, stride, pad, sc.to(cuda), sh.to(cuda), rd, relu, code, tile=tile)
     torch.cuda.synchronize()
     return out.float().cpu().permute(0, 3, 1, 2), ref
 
@@ -271,16 +271,12 @@ def test_dual_1x1_tail_matches_torch(cuda, code, tol, stride):
 
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 @pytest.mark.parametrize('keep_f', [True, False])
-@pytest.mark.parametrize('head256,shape', [(1, (3, 5, 6, 16)), (0, (3, 5, 6, 16)), (1, (2, 24, 20, 13))])
-def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f, head256, shape):
-    """Last deconv + BN + ReLU + 1x1 head in one launch, on the 256x256 register-epilogue
-    tile (head256=1; partial heatmaps of the four column waves summed in LDS) and on the
-    64x256 LDS tile; ragged M, several tiles, J < 16."""
-    ops.set_conv_head256(head256)
-    try:
-        _fused_deconv_head_case(cuda, code, tol, keep_f, shape)
-    finally:
-        ops.set_conv_head256(1)
+@pytest.mark.parametrize('shape', [(3, 5, 6, 16), (2, 24, 20, 13)])
+def test_fused_deconv_head_matches_unfused(cuda, code, tol, keep_f, shape):
+    """Last deconv + BN + ReLU + 1x1 head in one launch: bf16 / f16 on the 256x256
+    register-epilogue tile (partial heatmaps of the four column waves summed in LDS), f32
+    on the 64x256 LDS tile; ragged M, several tiles, J < 16."""
+    _fused_deconv_head_case(cuda, code, tol, keep_f, shape)
 
 
 def _fused_deconv_head_case(cuda, code, tol, keep_f, shape):
@@ -313,63 +309,31 @@ def _fused_deconv_head_case(cuda, code, tol, keep_f, shape):
 
 @pytest.mark.parametrize('case', CONV_CASES[1:5])
 def test_conv2d_three_stage_ring_matches_torch(cuda, case):
-    ops.set_conv_stages(3)
-    try:
-        got, ref = _conv_case(cuda, F32, *case)
-    finally:
-        ops.set_conv_stages(2)
+    got, ref = _conv_case(cuda, F32, *case, tile=16 + (1 if case[4] < 128 else 3))
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 23, 29, 31])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 22, 23, 31, 32, 37])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
-    """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks and the
-    single- / three-slot variants) on ragged shapes: 3x3 with residual, 1x1 strided."""
+    """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks, the single- /
+    three-slot variants, the staggered and persistent loops) on ragged shapes: 3x3 with
+    residual, 1x1 strided."""
     cout = 256 if (cfg & 7) in (3, 4, 5, 6, 7) else 64
-    ops.force_conv_config(cfg)
-    try:
-        for case in [(2, 64, 17, 15, cout, 3, 1, 1, True, True), (3, 128, 12, 12, cout, 1, 2, 0, False, False)]:
-            got, ref = _conv_case(cuda, code, *case)
-            if code == F32:
-                torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
-            else:
-                assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
-    finally:
-        ops.force_conv_config(-1)
+    for case in [(2, 64, 17, 15, cout, 3, 1, 1, True, True), (3, 128, 12, 12, cout, 1, 2, 0, False, False)]:
+        got, ref = _conv_case(cuda, code, *case, tile=cfg)
+        if code == F32:
+            torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+        else:
+            assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 15, 16, 23, 29, 31])
-@pytest.mark.parametrize('code', [F32, BF16, F16])
-def test_direct_epilogue_bit_exact_vs_lds_epilogue(cuda, cfg, code):
-    """The register-direct epilogue applies the same f32 arithmetic (BN, residual, ReLU,
-    one rounding) as the LDS-staged one: outputs equal bit for bit, for every tile shape,
-    ragged M and the deconv parity scatter."""
-    dt = ops.torch_dtype(code)
-    g = torch.Generator(device=cuda).manual_seed(11)
-    cout = 256
-    sc = torch.rand(cout, device=cuda, generator=g) + 0.5
-    sh = torch.randn(cout, device=cuda, generator=g) * 0.1
-    x = torch.randn(5, 19, 23, 128, device=cuda, generator=g).to(dt)
-    res = torch.randn(5, 19, 23, cout, device=cuda, generator=g).to(dt)
-    w3 = (torch.randn(cout, 9 * 128, device=cuda, generator=g) * 0.03).to(dt)
-    wdc = (torch.randn(4, cout, 4 * 128, device=cuda, generator=g) * 0.03).to(dt)
-    outs = {}
-    ops.force_conv_config(cfg)
-    try:
-        for direct in (0, 1, 2, 3):
-            ops.set_conv_epilogue(min(direct, 2))
-            ops.set_conv_early_residual(0 if direct < 3 else 64)
-            outs[direct] = [ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, res, True, code),
-                            ops.conv2d_nhwc(x, w3, cout, 3, 3, 1, 1, sc, sh, None, False, code),
-                            ops.deconv4x4s2_nhwc(x, wdc, cout, sc, sh, True, code)]
-        torch.cuda.synchronize()
-    finally:
-        ops.set_conv_epilogue(1)
-        ops.set_conv_early_residual(8)
-        ops.force_conv_config(-1)
-    for a, b, c, d in zip(outs[0], outs[1], outs[2], outs[3]):
-        assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+def test_invalid_tile_is_refused(cuda):
+    x = torch.zeros(1, 8, 8, 64, device=cuda, dtype=torch.bfloat16)
+    w = torch.zeros(64, 64, device=cuda, dtype=torch.bfloat16)
+    for bad in (7, 15, 29, 64, 70, 40 + 5):
+        with pytest.raises(RuntimeError, match='tile must be'):
+            ops.conv2d_nhwc(x, w, 64, 1, 1, 1, 0, None, None, None, False, BF16, tile=bad)
 
 
 @pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
@@ -410,56 +374,12 @@ def test_persistent_stream_bit_exact_vs_one_block_per_tile(cuda, cfg, code):
         assert torch.equal(a, b)
 
 
-HALO_CASES = [
-    # n, h, w, cin, cout, halo tile, deconv
-    (3, 16, 16, 256, 256, 64, False),   # one image per 256-row tile (layer3 shape)
-    (3, 32, 32, 128, 128, 65, False),   # 8 rows of a 32-wide image per tile (layer2)
-    (2, 64, 64, 64, 64, 66, False),     # 4 rows of a 64-wide image (layer1)
-    (5, 8, 8, 512, 512, 67, False),     # two 8x8 images per 128-row tile, last tile partial
-    (3, 16, 16, 256, 256, 68, False),
-    (5, 8, 8, 256, 256, 64, True),      # deconv classes, 4 images per tile, partial tile
-    (2, 32, 32, 128, 256, 64, True),    # deconv, 8 rows per tile
-    (2, 16, 16, 256, 128, 65, True),
-    (2, 64, 64, 64, 64, 69, False),     # single halo slot (C = one K-chunk), layer1 shape
-    (3, 32, 32, 64, 64, 70, False),
-    (3, 32, 32, 64, 128, 72, False),
-]
-
-
-@pytest.mark.parametrize('case', HALO_CASES)
-@pytest.mark.parametrize('code', [BF16, F16])
-def test_halo_variant_matches_gather_kernel(cuda, case, code):
-    """Halo tiles (64..68): the input window staged once per K-chunk and read at tap
-    offsets gives the gathered kernel's result up to the f32 summation order (chunk-major
-    K): 3x3 + residual on every tile shape, multi-image and partial tiles, deconv classes."""
-    n, h, w, cin, cout, tile, deconv = case
-    dt = ops.torch_dtype(code)
-    g = torch.Generator(device=cuda).manual_seed(3)
-    x = torch.randn(n, h, w, cin, device=cuda, generator=g).to(dt)
-    sc = torch.rand(cout, device=cuda, generator=g) + 0.5
-    sh = torch.randn(cout, device=cuda, generator=g) * 0.1
-    if deconv:
-        wt = (torch.randn(4, cout, 4 * cin, device=cuda, generator=g) * (1.0 / (4 * cin)) ** 0.5).to(dt)
-        got = ops.deconv4x4s2_nhwc(x, wt, cout, sc, sh, True, code, tile=tile)
-        ref = ops.deconv4x4s2_nhwc(x, wt, cout, sc, sh, True, code, tile=-1)
-    else:
-        wt = (torch.randn(cout, 9 * cin, device=cuda, generator=g) * (1.0 / (9 * cin)) ** 0.5).to(dt)
-        res = torch.randn(n, h, w, cout, device=cuda, generator=g).to(dt)
-        got = ops.conv2d_nhwc(x, wt, cout, 3, 3, 1, 1, sc, sh, res, True, code, tile=tile)
-        ref = ops.conv2d_nhwc(x, wt, cout, 3, 3, 1, 1, sc, sh, res, True, code, tile=-1)
-    torch.cuda.synchronize()
-    d = (got.float() - ref.float()).abs()
-    tol = (0.02 if code == BF16 else 0.004) * (1 + ref.float().abs())
-    assert bool((d <= tol).all()), float(d.max())
-    assert float(d.mean()) < (2e-3 if code == BF16 else 3e-4)
-
-
 @pytest.mark.parametrize('code', [F32, BF16, F16])
-def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
-    """The phased 256x256 main loop (tile 29), the ping-pong loops (tiles 7 / 15 on
-    256x256 / 256x128) and the staggered loops (tiles 23 / 31) keep each accumulator's K order, so their outputs equal the two-slot
-    loops (tiles 5 / 6) bit for bit: 3x3 + residual (ragged M), strided 1x1,
-    ConvTranspose(4, s2) and the two-source Bottleneck tail."""
+def test_staggered_tiles_bit_exact_vs_two_slot(cuda, code):
+    """The staggered loops (tiles 23 / 31: waves 4-7 half a K-tile behind) keep each
+    accumulator's K order, so their outputs equal the two-slot loops (tiles 5 / 6) bit for
+    bit: 3x3 + residual (ragged M), strided 1x1, ConvTranspose(4, s2) and the two-source
+    Bottleneck tail.  (f32 has no staggered loop: its 23 / 31 run as 5 / 6.)"""
     dt = ops.torch_dtype(code)
     g = torch.Generator(device=cuda).manual_seed(5)
     sc = torch.rand(256, device=cuda, generator=g) + 0.5
@@ -477,7 +397,7 @@ def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
     wdc = (rnd(4, 256, 4 * 128).float() * 0.03).to(dt)
     assert (9 * 128) % bk == 0
     outs = {}
-    for t in (5, 29, 7, 23, 6, 15, 31):
+    for t in (5, 23, 6, 31):
         outs[t] = [
             ops.conv2d_nhwc(x, w3, 256, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
             ops.conv2d_nhwc(x, w3[:, :128].contiguous(), 256, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
@@ -485,7 +405,7 @@ def test_phased_256_tile_bit_exact_vs_two_slot(cuda, code):
             ops.conv1x1_dual_nhwc(x, x2, 2, wd, 256, sh, True, code, tile=t),
         ]
     torch.cuda.synchronize()
-    for t, base in ((29, 5), (7, 5), (23, 5), (15, 6), (31, 6)):
+    for t, base in ((23, 5), (31, 6)):
         for a, b in zip(outs[base], outs[t]):
             assert torch.equal(a, b), (t, float((a.float() - b.float()).abs().max()))
 
@@ -501,49 +421,6 @@ def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
         assert (got - ref).abs().max().item() <= 0.03 * ref.abs().max().item() + 0.02
     else:
         torch.testing.assert_close(got, ref, atol=tol, rtol=tol)
-
-
-@pytest.mark.parametrize('code,tol', [(F32, 1e-5), (BF16, 0.02), (F16, 0.005)])
-@pytest.mark.parametrize('dual,cout2', [(False, 64), (True, 64), (False, 128)])
-@pytest.mark.parametrize('chain8,shape', [(0, (3, 9, 7)), (1, (3, 9, 7)), (1, (4, 32, 33))])
-def test_chained_next_conv1_matches_two_launches(cuda, code, tol, dual, cout2, chain8, shape):
-    """Block tail (+residual / downsample source) with the next block's 1x1 conv1 in the
-    same launch == the tail launch followed by a separate conv1 launch on its output; on the
-    64x256 LDS-epilogue tile and (chain8, bf16/f16, cout2 <= 64) the 8x1-wave register tile."""
-    ops.set_conv_chain8(chain8)
-    try:
-        _chain_case(cuda, code, tol, dual, cout2, shape)
-    finally:
-        ops.set_conv_chain8(0)
-
-
-def _chain_case(cuda, code, tol, dual, cout2, shape):
-    g = torch.Generator().manual_seed(9)
-    dt = ops.torch_dtype(code)
-    bk = ops.conv_bk(code)
-    (n, h, w), mid, cin = shape, 64, 128
-    a = torch.relu(torch.randn(n, h, w, mid, generator=g)).to(cuda, dt)
-    x = torch.randn(n, h, w, cin if dual else 256, generator=g).to(cuda, dt)
-    w3 = torch.randn(256, mid, 1, 1, generator=g) * 0.1
-    sc = (torch.rand(256, generator=g) + 0.5).to(cuda)
-    sh = (torch.randn(256, generator=g) * 0.1).to(cuda)
-    w1 = torch.randn(cout2, 256, 1, 1, generator=g) * 0.06
-    s1 = (torch.rand(cout2, generator=g) + 0.5).to(cuda)
-    b1 = (torch.randn(cout2, generator=g) * 0.1).to(cuda)
-    cw = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
-    if dual:
-        wd = torch.randn(256, cin, 1, 1, generator=g) * 0.1
-        sd = (torch.rand(256, generator=g) + 0.5).to(cuda)
-        wp = packing.pack_dual_1x1_weight(w3.to(cuda), sc, wd.to(cuda), sd, dt)
-        y, cy = ops.conv1x1_dual_chain_nhwc(a, x, 1, wp, 256, sh, code, cw, cout2, s1, b1)
-        y_ref = ops.conv1x1_dual_nhwc(a, x, 1, wp, 256, sh, True, code)
-    else:
-        wp = packing.pack_conv_weight(w3.to(cuda), mid, bk, dt)
-        y, cy = ops.conv2d_chain_nhwc(a, wp, 256, 1, 1, 0, sc, sh, x, code, cw, cout2, s1, b1)
-        y_ref = ops.conv2d_nhwc(a, wp, 256, 1, 1, 1, 0, sc, sh, x, True, code)
-    cy_ref = ops.conv2d_nhwc(y_ref, cw, cout2, 1, 1, 1, 0, s1, b1, None, True, code)
-    torch.testing.assert_close(y, y_ref, atol=0, rtol=0)        # same kernel math for the tail
-    torch.testing.assert_close(cy.float(), cy_ref.float(), atol=tol, rtol=tol)
 
 
 @pytest.mark.parametrize('distortion', [False, True])

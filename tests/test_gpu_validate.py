@@ -101,3 +101,44 @@ def test_validate_batch_with_flip_test_matches_oracle(cuda, golden):
         np.testing.assert_allclose(res['preds'][k::4, :, 2:], mv, atol=1e-6, rtol=0)
     assert res['loss'] is not None and np.isfinite(res['loss'])
     assert 0.0 <= res['acc'] <= 1.0
+
+
+def test_validate_batch_aggre_loss_terms(cuda):
+    """AGGRE validation loss (function.py:589-609): JointsMSE on the raw outputs + the
+    consistent loss (plain mean MSE between raw and aggregated heatmaps of the H36M samples)
+    + the pseudo-label MSE of the fused outputs x MSE_LOSS_WEIGHT, against the same sums
+    taken with torch ops on CPU from the model's own raw / aggregated heatmaps."""
+    from core.function import fuse_routing, validate_batch
+    from core.loss import JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    size, n = 64, 3
+    cfg = syn.make_cfg(num_layers=18, image_size=size)
+    cfg.NETWORK.AGGRE = True
+    cfg.TEST.FUSE_OUTPUT = True
+    cfg.LOSS.USE_CONSISTENT_LOSS = True
+    cfg.LOSS.MSE_LOSS_WEIGHT = 0.7
+    cfg.DATASET.PSEUDO_LABEL_PATH = 'pseudo.pkl'
+    net = get_pose_net(cfg, is_train=False, precision='fp32')
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=2))
+    net = net.to(cuda).eval()
+    model = get_multiview_pose_net(net, cfg).to(cuda)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, n, size, seed=35)]
+    meta = [{'center': torch.full((n, 2), 500.0, dtype=torch.float64), 'scale': torch.full((n, 2), 5.0,
+             dtype=torch.float64), 'source': ['h36m', 'mpii', 'h36m']} for _ in range(4)]
+    g = torch.Generator().manual_seed(36)
+    target = [torch.rand(n, 16, 16, 16, generator=g) for _ in range(4)]
+    weight = [(torch.rand(n, 16, 1, generator=g) > 0.2).float() for _ in range(4)]
+    crit = {'mse_weights': JointsMSELoss(use_target_weight=True)}
+    res = validate_batch(cfg, model, views, target, weight, meta, criterion_dict=crit)
+    with torch.no_grad():
+        raw, agg, _, _ = model(views)
+        out = fuse_routing(raw, agg, True, meta)
+    raw = [r.cpu() for r in raw]
+    agg = [a.cpu() for a in agg]
+    out = [o.cpu() for o in out]
+    ref = sum(G.joints_mse(r, t, w) for r, t, w in zip(raw, target, weight))
+    sel = torch.tensor([True, False, True])
+    ref = ref + torch.nn.functional.mse_loss(torch.cat([r[sel] for r in raw]), torch.cat([a[sel] for a in agg]))
+    ref = ref + sum(G.joints_mse(o, t, w) for o, t, w in zip(out, target, weight)) * 0.7
+    np.testing.assert_allclose(res['loss'], float(ref), rtol=1e-5)

@@ -36,16 +36,12 @@ def main():
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--precision', default='bf16')
     ap.add_argument('--reps', type=int, default=20)
-    ap.add_argument('--stages', type=int, default=2)
-    ap.add_argument('--big', type=int, default=1)
     ap.add_argument('--autotune', action='store_true', help='per-layer tile autotuning first')
     args = ap.parse_args()
     import bench
     dev = torch.device('cuda', 0)
     net = bench.build_model(args.layers, args.size, args.precision, dev)
     plan = net.plan(dev)
-    ops.set_conv_stages(args.stages)
-    ops.set_conv_tiles(args.big)
     code = plan.code
     esz = 2 if code == ops.BF16 else 4
     x_in = [torch.randn(args.batch, 3, args.size, args.size, device=dev)]
@@ -118,25 +114,6 @@ def main():
     hm = ops.head1x1_nchw(x, plan.head_w, plan.njoints, plan.head_b, code)
     rec('head', lambda: ops.head1x1_nchw(x, plan.head_w, plan.njoints, plan.head_b, code),
         2 * hm.numel() * x.shape[3], x.numel() * esz + hm.numel() * 4)
-    # chained tails (block tail + next block's conv1 in one launch) vs the two launches
-    xin = p
-    blocks = [b for layer in plan.layers for b in layer]
-    for bi, (b, nxt) in enumerate(zip(blocks, blocks[1:])):
-        y_pre = xin
-        out_blk, _ = b(xin, code) if b.chain is None else (None, None)
-        if b.chain is not None:
-            chained = lambda b=b, x=xin: b(x, code)
-            saved = b.chain
-            b.chain = None
-            sep = lambda b=b, x=xin, nxt=nxt: nxt.convs[0](b(x, code)[0], code)
-            us_sep = timeit(sep, args.reps)
-            b.chain = saved
-            us_ch = timeit(chained, args.reps)
-            print('chain block%-3d  tail+next-c1 %8.1f us   chained %8.1f us' % (bi, us_sep, us_ch), flush=True)
-            out_blk = b(xin, code)[0]
-        xin = out_blk if out_blk is not None else b(xin, code)[0]
-        if bi > 12:
-            break
     tot = sum(r[1] for r in rows)
     fl = sum(r[2] for r in rows)
     print('TOTAL %.1f us  %.1f TF (conv FLOPs / all launch time)' % (tot, fl / tot / 1e6))
