@@ -131,6 +131,24 @@ int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int W, int C,
                          const void* w, int Cout, const float* scale,
                          const float* shift, int relu, void* y, int tile, void* stream);
 
+/* Fused Bottleneck block, eval mode (lib/models/pose_resnet.py:61-99 with the BNs folded):
+ *   y = relu( conv3(relu(conv2_3x3(relu(conv1(x) * s1 + b1)) * s2 + b2)) * s3 + b3 + x )
+ * in one launch that streams each image's rows once: the two planes-wide intermediates stay
+ * in LDS / registers, x is read from HBM once (conv1 input and residual) and y written
+ * once.  Identity residual (no downsample), stride 1.  Built for layer1 of PoseResNet at
+ * 256x256: W = 64, C = 256, P = 64; dtype BF16 / F16.
+ *   x, y: [N, H, W, C] (y must not alias x);
+ *   w1: [P][C] with the input channels permuted: column 32 s + 8 q + e holds channel
+ *       32 s + 16 (q & 1) + 8 (q >> 1) + e, s1/b1 [P] f32;
+ *   w2: [P][9 * P] (posu_conv2d_fwd packing of conv2, k = (kh * 3 + kw) * P + ci), s2/b2 [P];
+ *   w3: [C][P] with the input channels of every 32-block permuted: column 32 b + 8 q + e
+ *       holds input channel 32 b + 16 (e >> 2) + 4 q + (e & 3) (the order in which conv2's
+ *       accumulators become conv3's MFMA operand), s3/b3 [C]. */
+int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
+                        const float* s1, const float* b1, const void* w2, const float* s2,
+                        const float* b2, const void* w3, const float* s3, const float* b3, void* y,
+                        void* stream);
+
 /* Cross-view Aggregation (multiview_pose_resnet.py:16-58, ChannelWiseFC / Aggregation,
  * NETWORK.AGGRE): the V(V-1) per-pair [HW x HW] matrices form one block matrix with
  * zero diagonal blocks (scaled by 1/(V-1)), so all V aggregated views are ONE GEMM:

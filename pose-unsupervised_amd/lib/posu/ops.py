@@ -88,6 +88,16 @@ def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, ti
     return out
 
 
+def bottleneck_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
+    """Fused identity-residual Bottleneck (posu_bottleneck_fwd): x [N, H, W, C] -> y."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    call('posu_bottleneck_fwd', code, ptr(x), n, h, w, c, w1.shape[0], ptr(w1), ptr(s1), ptr(b1), ptr(w2), ptr(s2),
+         ptr(b2), ptr(w3), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
+    return out
+
+
 def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):
     n, h, w, c = x.shape
     if out is None:

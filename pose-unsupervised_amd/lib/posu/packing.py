@@ -27,6 +27,45 @@ def pack_conv_weight(w, cin_pad, bk, dtype):
     return out.to(dtype).contiguous()
 
 
+def bottleneck_conv3_order(planes):
+    """Input-channel order of the fused Bottleneck's conv3 K (csrc/bottleneck.hip): column
+    32 b + 8 q + e reads channel 32 b + 16 (e >> 2) + 4 q + (e & 3) -- the order in which
+    lane (pixel, q) of conv2's 16x16 accumulators (channels 4q..4q+3 of two n-tiles) forms
+    an MFMA k-step."""
+    idx = []
+    for b in range(planes // 32):
+        for q in range(4):
+            for e in range(8):
+                idx.append(32 * b + 16 * (e >> 2) + 4 * q + (e & 3))
+    return idx
+
+
+def bottleneck_conv1_order(cin):
+    """Input-channel order of the fused Bottleneck's conv1 K: column 32 s + 8 q + e reads
+    channel 32 s + 16 (q & 1) + 8 (q >> 1) + e, so lane q's x fragment of k-step s is the
+    8-channel chunk its conv3 epilogue adds as the residual of output pair s."""
+    return [32 * s + 16 * (q & 1) + 8 * (q >> 1) + e for s in range(cin // 32) for q in range(4) for e in range(8)]
+
+
+def pack_bottleneck_conv1_weight(w, dtype):
+    """conv1 weight [P, C, 1, 1] -> [P][C] with the K columns in bottleneck_conv1_order."""
+    p, cin = w.shape[:2]
+    if cin % 32 or w.shape[2:] != (1, 1):
+        raise NotImplementedError('fused Bottleneck conv1: 1x1 kernel, input channels a multiple of 32')
+    order = torch.tensor(bottleneck_conv1_order(cin), device=w.device)
+    return w.detach().float().reshape(p, cin)[:, order].to(dtype).contiguous()
+
+
+def pack_bottleneck_conv3_weight(w, dtype):
+    """conv3 weight [C, P, 1, 1] -> [C][P] with the K columns in bottleneck_conv3_order."""
+    cout, p = w.shape[:2]
+    if p % 32 or w.shape[2:] != (1, 1):
+        raise NotImplementedError('fused Bottleneck conv3: 1x1 kernel, planes a multiple of 32')
+    wf = w.detach().float().reshape(cout, p)
+    order = torch.tensor(bottleneck_conv3_order(p), device=w.device)
+    return wf[:, order].to(dtype).contiguous()
+
+
 def pack_stem_s2d_weight(w, cpad, bk, dtype):
     """7x7 / stride 2 / pad 3 stem weight [Cout, Cin, 7, 7] -> the equivalent 4x4 / stride 1 /
     top-left pad 2 weight over the 2x2 space-to-depth input (channel (dy*2+dx)*Cin + c):

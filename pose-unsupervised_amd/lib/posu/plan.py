@@ -17,8 +17,8 @@ torch.cuda.CUDAGraph (hipGraph) by the caller.
 import torch
 
 from . import ops
-from .packing import (fold_bn, pack_conv_weight, pack_deconv4x4_weight, pack_dual_1x1_weight,
-                      pack_stem_fused_weight, pack_stem_s2d_weight)
+from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_conv_weight, pack_deconv4x4_weight,
+                      pack_dual_1x1_weight, pack_stem_fused_weight, pack_stem_s2d_weight)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
@@ -152,14 +152,20 @@ class _DualTail:
             mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out, tile=t))
 
 
+# identity-residual Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch
+# (posu_bottleneck_fwd) in bf16 / fp16 plans; False runs the three convolutions
+FUSED_BOTTLENECK = True
+
+
 class _Block:
-    __slots__ = ('convs', 'down', 'dual')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
         self.convs = []
         self.down = None
         self.dual = None
+        self.w1f = self.w3f = None   # conv1 / conv3 packed for the fused kernel (permuted K)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -171,6 +177,15 @@ class _Block:
             self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
         if ds is not None:
             self.down = _Conv(ds[0], ds[1], False, code, bk)
+        elif code in (ops.BF16, ops.F16) and len(names) == 3 and self._fusable_shape():
+            self.w1f = pack_bottleneck_conv1_weight(blk.conv1.weight, ops.torch_dtype(code))
+            self.w3f = pack_bottleneck_conv3_weight(blk.conv3.weight, ops.torch_dtype(code))
+
+    def _fusable_shape(self):
+        c1, c2, c3 = self.convs
+        return (c1.k == 1 and c1.stride == 1 and c1.cout == 64 and c1.w.shape == (64, 256) and
+                c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.cout == 64 and c2.w.shape == (64, 576) and
+                c3.k == 1 and c3.stride == 1 and c3.cout == 256)
 
     @property
     def cout(self):
@@ -182,6 +197,10 @@ class _Block:
             for c in self.convs:
                 y = c(y, code)
             return self.dual(y, x, code, out=out)
+        if self.w3f is not None and FUSED_BOTTLENECK and x.shape[2] == 64:
+            c1, c2, c3 = self.convs
+            return ops.bottleneck_nhwc(x, self.w1f, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3f, c3.scale,
+                                       c3.shift, code, out=out)
         res = self.down(x, code) if self.down is not None else x
         for c in self.convs[:-1]:
             y = c(y, code)

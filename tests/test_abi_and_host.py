@@ -249,3 +249,30 @@ def test_dual_tail_weight_folds_both_bn_branches():
     feat = torch.cat([a.permute(0, 2, 3, 1), x[:, :, ::2, ::2].permute(0, 2, 3, 1)], dim=3)
     got = (feat @ wp[:cout].t()).permute(0, 3, 1, 2)
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
+
+
+def test_bottleneck_conv3_order_is_the_accumulator_fragment_order():
+    """conv2's 16x16x32 accumulators (lane (p, q): channels 4q..4q+3 of n-tiles 2b and 2b+1)
+    read as conv3's B fragment (lane (p, q): k = 8q + e) map k-step b's k = 8q + e to channel
+    32b + 16(e >> 2) + 4q + (e & 3); the packed conv3 weight reads the same channel there, so
+    the product sums every channel exactly once."""
+    order = packing.bottleneck_conv3_order(64)
+    assert sorted(order) == list(range(64))
+    for b in range(2):
+        for q in range(4):
+            acc_channels = [32 * b + 4 * q + e for e in range(4)] + [32 * b + 16 + 4 * q + e for e in range(4)]
+            assert order[32 * b + 8 * q:32 * b + 8 * q + 8] == acc_channels
+    w = torch.randn(256, 64, 1, 1)
+    wp = packing.pack_bottleneck_conv3_weight(w, torch.float32)
+    t = torch.randn(64)
+    torch.testing.assert_close(wp @ t[order], w.view(256, 64) @ t)
+    # conv1: lane q of k-step s reads the residual chunk of output pair s (epilogue lane q:
+    # channels 32 s + 16 (q & 1) + 8 (q >> 1) .. + 7)
+    o1 = packing.bottleneck_conv1_order(256)
+    assert sorted(o1) == list(range(256))
+    for s in range(8):
+        for q in range(4):
+            assert o1[32 * s + 8 * q:32 * s + 8 * q + 8] == [32 * s + 16 * (q & 1) + 8 * (q >> 1) + e for e in range(8)]
+    w1 = torch.randn(64, 256, 1, 1)
+    x = torch.randn(256)
+    torch.testing.assert_close(packing.pack_bottleneck_conv1_weight(w1, torch.float32) @ x[o1], w1.view(64, 256) @ x)

@@ -1,0 +1,103 @@
+"""The fused Bottleneck launch (posu_bottleneck_fwd, csrc/bottleneck.hip) against the
+three-launch path on the same device and against torch fp32 on CPU (eval-mode
+Bottleneck, reference lib/models/pose_resnet.py:61-99), plus the whole R50 plan with the
+fused layer1 blocks against the unfused plan."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from posu import ops, packing, synthetic as syn
+from posu._native import BF16, F16
+
+pytestmark = pytest.mark.gpu
+
+
+def _block_params(g, c=256, p=64):
+    def bn(ch):
+        return (torch.rand(ch, generator=g) + 0.5, torch.randn(ch, generator=g) * 0.1)
+    w1 = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    w2 = torch.randn(p, p, 3, 3, generator=g) * (2.0 / (9 * p)) ** 0.5
+    w3 = torch.randn(c, p, 1, 1, generator=g) * (2.0 / p) ** 0.5 * 0.3
+    return w1, bn(p), w2, bn(p), w3, bn(c)
+
+
+def _torch_block(x, w1, bn1, w2, bn2, w3, bn3):
+    t = F.relu(F.conv2d(x, w1) * bn1[0].view(1, -1, 1, 1) + bn1[1].view(1, -1, 1, 1))
+    t = F.relu(F.conv2d(t, w2, padding=1) * bn2[0].view(1, -1, 1, 1) + bn2[1].view(1, -1, 1, 1))
+    t = F.conv2d(t, w3) * bn3[0].view(1, -1, 1, 1) + bn3[1].view(1, -1, 1, 1)
+    return F.relu(t + x)
+
+
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64)])
+def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
+    g = torch.Generator().manual_seed(17 + h)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g)
+    x = torch.randn(n, 256, h, 64, generator=g)
+    dt = ops.torch_dtype(code)
+    xq = x.to(dt).float()   # the input as the device sees it
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    bk = ops.conv_bk(code)
+    xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 64, bk, dt)
+    p3 = packing.pack_conv_weight(w3.to(cuda), 64, bk, dt)
+    p3f = packing.pack_bottleneck_conv3_weight(w3.to(cuda), dt)
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
+    p1f = packing.pack_bottleneck_conv1_weight(w1.to(cuda), dt)
+    fused = ops.bottleneck_nhwc(xd, p1f, s[0], s[1], p2, s[2], s[3], p3f, s[4], s[5], code)
+    t1 = ops.conv2d_nhwc(xd, p1, 64, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    t2 = ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    three = ops.conv2d_nhwc(t2, p3, 256, 1, 1, 1, 0, s[4], s[5], xd, True, code)
+    torch.cuda.synchronize()
+    # conv1 / conv3 sum their channels in other orders: t1 may differ in its last bit, which
+    # conv2 / conv3 carry along (a flipped t1 bit enters 576 products of conv2, a flipped t2
+    # bit 64 of conv3): on average a small fraction of an ulp, ~10 ulps at the worst element
+    # of the 5 x 64 x 64 x 256 case
+    d = (fused.float() - three.float()).abs()
+    ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * three.float().abs().clamp_min(2.0 ** -4)
+    assert float(d.mean()) < 0.05 * float(ulp.mean()), float(d.mean())
+    assert bool((d <= 16 * ulp).all()), float((d / ulp).max())
+    got = fused.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs()
+    tol = 0.05 if code == BF16 else 0.01
+    assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
+
+
+def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
+    x = torch.zeros(1, 8, 32, 256, device=cuda, dtype=torch.bfloat16)
+    w = torch.zeros(64, 256, device=cuda, dtype=torch.bfloat16)
+    s = torch.ones(256, device=cuda)
+    with pytest.raises(RuntimeError, match='W = 64'):
+        ops.bottleneck_nhwc(x, w, s, s, w, s, s, w, s, s, BF16)
+    x = torch.zeros(1, 8, 64, 256, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match='alias'):
+        ops.bottleneck_nhwc(x, w, s, s, w, s, s, w, s, s, BF16, out=x)
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp16'])
+def test_plan_with_fused_layer1_matches_unfused_plan(cuda, precision):
+    import posu.plan as P
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
+    net = net.to(cuda).eval()
+    plan = net.plan(cuda)
+    assert sum(b.w3f is not None for b in plan.layers[0]) == 2   # layer1 blocks 1 and 2
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=12)]
+    saved = P.FUSED_BOTTLENECK
+    try:
+        with torch.no_grad():
+            P.FUSED_BOTTLENECK = True
+            hm1, x11, _ = plan.run(plan.pack_input(views))
+            P.FUSED_BOTTLENECK = False
+            hm0, x10, _ = plan.run(plan.pack_input(views))
+    finally:
+        P.FUSED_BOTTLENECK = saved
+    torch.cuda.synchronize()
+    dx = (x11.float() - x10.float()).abs().max().item()
+    dh = (hm1 - hm0).abs()
+    print('%s fused vs unfused plan: layer1 out max %.3g, heatmaps max %.3g mean %.3g'
+          % (precision, dx, dh.max(), dh.mean()))
+    assert dx < (0.1 if precision == 'bf16' else 0.02)
+    assert dh.mean() < (0.01 if precision == 'bf16' else 0.002)

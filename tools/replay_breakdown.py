@@ -1,0 +1,56 @@
+"""Per-launch timeline of network replays from a rocprofv3 kernel-trace CSV.
+
+    python tools/replay_breakdown.py gpurun_out/prof/run_kernel_trace.csv [--last 5]
+
+A replay = the dispatches from one stem_pool_kernel up to (not including) the next
+soft-argmax kernel.  Prints, for the chosen replays, each launch's median duration (us)
+with its kernel name, and the replay's launch-time sum and wall span (first start to last
+end: the sum plus the gaps between launches)."""
+import argparse
+import csv
+import re
+import statistics
+
+
+def short(name):
+    name = name.replace('(anonymous namespace)::', '').replace('posu::', '')
+    name = re.sub(r'\(.*', '', name)
+    return name[:100]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('csv')
+    ap.add_argument('--last', type=int, default=5, help='replays (from the end of the trace) to aggregate')
+    a = ap.parse_args()
+    rows = []
+    with open(a.csv) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
+    rows.sort()
+    replays, cur = [], None
+    for s, e, n in rows:
+        if 'stem_pool_kernel' in n:
+            cur = [(s, e, n)]
+            replays.append(cur)
+        elif cur is not None:
+            if 'softargmax' in n:
+                cur = None
+            else:
+                cur.append((s, e, n))
+    replays = [r for r in replays if len(r) == len(replays[-1])][-a.last:]
+    if not replays:
+        raise SystemExit('no replay found')
+    k = len(replays[0])
+    print('%d replays of %d launches' % (len(replays), k))
+    tot = 0.0
+    for i in range(k):
+        d = statistics.median((r[i][1] - r[i][0]) / 1e3 for r in replays)
+        tot += d
+        print('%3d %9.1f us  %s' % (i, d, short(replays[0][i][2])))
+    span = statistics.median((r[-1][1] - r[0][0]) / 1e3 for r in replays)
+    print('sum of launches %.1f us, replay span %.1f us (gaps %.1f us)' % (tot, span, span - tot))
+
+
+if __name__ == '__main__':
+    main()
