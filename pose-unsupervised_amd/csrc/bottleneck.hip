@@ -77,15 +77,9 @@ constexpr int kXP = 134144;             // conv1 partial sums: 8 waves x [64 lan
 constexpr int kXT = 150528;             // t2 exchange: 8 waves x [64 lanes][16 B]       8192 B
 constexpr int kLds = 158720;
 
-// workgroup barrier that also publishes this wave's LDS writes (lgkmcnt(0) first); LDS-DMA
-// and global loads stay in flight across it
 __device__ __forceinline__ void raw_barrier() {
   if (kAbl & 8) return;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();
 }
 
 __device__ __forceinline__ void ld8(const float* p, float* v) {  // 8 f32 from LDS

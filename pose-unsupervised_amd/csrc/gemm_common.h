@@ -115,6 +115,17 @@ __device__ __forceinline__ void dma16(u32x4 srd, int voff, unsigned lds) {
       : "memory");
 }
 
+// workgroup barrier that also publishes this wave's LDS writes and retires its LDS reads
+// (lgkmcnt(0) first); LDS-DMA and global loads stay in flight across it -- unlike
+// __syncthreads(), whose fence waits for them too
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // wait until at most N of this wave's vector-memory ops are outstanding
 template <int N>
 __device__ __forceinline__ void vm_wait() {

@@ -1,0 +1,90 @@
+"""Times conv tile configurations on the compute-heavy R50@256 batch-128 layer shapes (bf16,
+HIP events, min over rounds) and checks that loops with the same K order agree bit for bit.
+
+    python tools/tile_micro.py [--tiles 5,23,29] [--reps 10] [--rounds 3]
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, 'pose-unsupervised_amd', 'lib'), REPO]
+
+import torch  # noqa: E402
+
+from posu import ops  # noqa: E402
+
+BF16 = 1
+# name, kind, (n, h, w, cin), cout, k
+SHAPES = [
+    ('deconv3 32->64', 'deconv', (128, 32, 32, 256), 256, 4),
+    ('deconv2 16->32', 'deconv', (128, 16, 16, 256), 256, 4),
+    ('deconv1 8->16', 'deconv', (128, 8, 8, 2048), 256, 4),
+    ('l3 c2 3x3 16x16x256', 'conv', (128, 16, 16, 256), 256, 3),
+    ('l4 c2 3x3 8x8x512', 'conv', (128, 8, 8, 512), 512, 3),
+    ('l2 c2 3x3 32x32x128', 'conv', (128, 32, 32, 128), 128, 3),
+    ('l3 c1 1x1 16x16x1024', 'conv', (128, 16, 16, 1024), 256, 1),
+    ('l4 c3 1x1 8x8x512', 'conv', (128, 8, 8, 512), 2048, 1),
+]
+
+
+def timeit(fn, reps, rounds):
+    best = 1e9
+    for _ in range(rounds):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) * 1e3 / reps)
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--tiles', default='5,23,29')
+    ap.add_argument('--reps', type=int, default=10)
+    ap.add_argument('--rounds', type=int, default=3)
+    a = ap.parse_args()
+    tiles = [int(t) for t in a.tiles.split(',')]
+    dev = torch.device('cuda', 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    dt = torch.bfloat16
+    bk = ops.conv_bk(BF16)
+    for name, kind, (n, h, w, cin), cout, k in SHAPES:
+        x = torch.randn(n, h, w, cin, device=dev, generator=g).to(dt)
+        sc = torch.rand(cout, device=dev, generator=g) + 0.5
+        sh = torch.randn(cout, device=dev, generator=g) * 0.1
+        if kind == 'deconv':
+            wk = (torch.randn(4, cout, 4 * cin, device=dev, generator=g) * 0.03).to(dt)
+            flop = 2.0 * n * (2 * h) * (2 * w) * cout * 4 * cin
+            fn = lambda t, x=x, wk=wk, cout=cout, sc=sc, sh=sh: ops.deconv4x4s2_nhwc(x, wk, cout, sc, sh, True, BF16, tile=t)
+        else:
+            kk = k * k * cin
+            kp = (kk + bk - 1) // bk * bk
+            wk = torch.zeros(cout, kp, device=dev, dtype=dt)
+            wk[:, :kk] = (torch.randn(cout, kk, device=dev, generator=g) * 0.03).to(dt)
+            flop = 2.0 * n * h * w * cout * kk
+            fn = lambda t, x=x, wk=wk, cout=cout, k=k, sc=sc, sh=sh: ops.conv2d_nhwc(
+                x, wk, cout, k, k, 1, k // 2, sc, sh, None, True, BF16, tile=t)
+        outs, line = {}, []
+        for t in tiles:
+            try:
+                outs[t] = fn(t)
+            except RuntimeError as e:
+                line.append('%d: n/a' % t)
+                continue
+            us = timeit(lambda: fn(t), a.reps, a.rounds)
+            line.append('%d: %7.1f us %6.0f TF' % (t, us, flop / us / 1e6))
+        torch.cuda.synchronize()
+        ref = outs.get(tiles[0])
+        same = ' '.join('%d=%s' % (t, 'eq' if torch.equal(ref, o) else 'DIFF %.3g' % float((ref.float() - o.float()).abs().max()))
+                        for t, o in outs.items() if t != tiles[0]) if ref is not None else ''
+        print('%-24s %s | %s' % (name, ' | '.join(line), same))
+
+
+if __name__ == '__main__':
+    main()
