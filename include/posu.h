@@ -149,6 +149,22 @@ int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, in
                         const float* b2, const void* w3, const float* s3, const float* b3, void* y,
                         void* stream);
 
+/* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
+ * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn
+ * share one accumulator (as in posu_conv1x1_dual_fwd),
+ *   y = relu( [w3*s3 | wd*sd] . [t2 ; x] + shift3 ),  t2 = conv2 output as above,
+ * x read once (conv1 input and downsample input), y written once.  W = 64, C = P = 64,
+ * 4P = 256 output channels; dtype BF16 / F16.
+ *   x: [N, H, W, C]; y: [N, H, W, 4P] (must not alias x);
+ *   w1: [P][C] (natural channel order), s1/b1 [P]; w2, s2, b2 as posu_bottleneck_fwd;
+ *   w3d: [4P][2P]: columns 0..P-1 = conv3 weight * s3 with the posu_bottleneck_fwd column
+ *        permutation of w3, columns P..2P-1 = downsample weight * sd (natural order);
+ *   shift3: [4P] f32 = b3 + bd. */
+int posu_bottleneck_down_fwd(int dtype, const void* x, int N, int H, int W, int C, int P,
+                             const void* w1, const float* s1, const float* b1, const void* w2,
+                             const float* s2, const float* b2, const void* w3d, const float* shift3,
+                             void* y, void* stream);
+
 /* Cross-view Aggregation (multiview_pose_resnet.py:16-58, ChannelWiseFC / Aggregation,
  * NETWORK.AGGRE): the V(V-1) per-pair [HW x HW] matrices form one block matrix with
  * zero diagonal blocks (scaled by 1/(V-1)), so all V aggregated views are ONE GEMM:

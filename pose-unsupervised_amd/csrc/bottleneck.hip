@@ -15,9 +15,9 @@
 //            rows ahead; its half of w1 held in VGPRs for the whole strip) into all 64
 //            outputs, hands the partner's two n-tiles over in LDS (f32) and finishes its
 //            own two (sum of the halves in the order half 0 + half 1, BN1, ReLU) into a
-//            3-row LDS ring [row][64 px][64 ch] (rows outside the image are zeros =
+//            3-row LDS ring [row][66 px][64 ch] (rows outside the image are zeros =
 //            conv2's padding), so every conv1 row is computed once.
-//   conv2    3x3 over ring rows y-1, y, y+1 (x-padding = zeroed fragments), output n-tiles
+//   conv2    3x3 over ring rows y-1, y, y+1 (x-padding = two zero columns of the ring), output n-tiles
 //            2h, 2h+1, w2 [9][64][64] resident in LDS; BN2 + ReLU stay in registers,
 //            rounded: the two n-tiles ARE conv3's B fragment of k-step h (lane (p, q) holds
 //            channels 4q..4q+3 of each, a permuted channel order in which conv3's weights are
@@ -51,9 +51,10 @@ struct BottleGeom {
   const void* w2;  // [64][576], k = (kh * 3 + kw) * 64 + ci
   const float* s2;
   const float* b2;
-  const void* w3;  // [256][64], K permuted (bottleneck_conv3_order)
-  const float* s3;
-  const float* b3;
+  const void* w3;  // [256][64], K permuted (bottleneck_conv3_order); DOWN: [256][128] =
+                   // [w3 * s3 permuted | wd * sd], the dual tail's folded weights
+  const float* s3;  // DOWN: unused
+  const float* b3;  // DOWN: b3 + bd
   int N, H;
   int strips;      // strips per image
   int rows;        // rows per strip (H / strips)
@@ -71,11 +72,13 @@ constexpr int kAbl = POSU_BNECK_ABLATE;
 constexpr int kP = 64, kW = 64, kC = 256;
 constexpr int kW2 = 0;                  // w2: 9 taps x [64 co][128 B]                73728 B
 constexpr int kW3 = 73728;              // w3: [256 co][128 B]                         32768 B
-constexpr int kT1 = 106496;             // t1 ring: 3 x [64 px][128 B]                 24576 B
-constexpr int kBN = 131072;             // s1 b1 s2 b2 (64 each), s3 b3 (256 each) f32   3072 B
-constexpr int kXP = 134144;             // conv1 partial sums: 8 waves x [64 lanes][8 f32] 16384 B
-constexpr int kXT = 150528;             // t2 exchange: 8 waves x [64 lanes][16 B]       8192 B
-constexpr int kLds = 158720;
+constexpr int kT1 = 106496;             // t1 ring: 3 x [66 px][128 B] (px -1, 64 zero)  25344 B
+constexpr int kSlot = 66 * 128;
+constexpr int kBN = kT1 + 3 * kSlot;    // s1 b1 s2 b2 (64 each), s3 b3 (256 each) f32   3072 B
+constexpr int kXP = kBN + 3072;         // conv1 partial sums: 8 waves x [64 lanes][8 f32] 16384 B
+constexpr int kXT = kXP + 16384;        // t2 exchange: 8 waves x [64 lanes][16 B]       8192 B
+constexpr int kLds = kXT + 8192;        // 159488
+static_assert(kLds <= 160 * 1024, "LDS");
 
 __device__ __forceinline__ void raw_barrier() {
   if (kAbl & 8) return;
@@ -89,11 +92,17 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {  // 8 f32 from L
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <typename T>
+// DOWN: the first block of layer1 (x [N, H, 64, 64], a downsample branch instead of the
+// identity): conv1 split over N (K = 64, no partial hand-off), the downsample's MFMAs from the
+// x fragments of row y join conv3's accumulators, weights [w3*s3 | wd*sd] (wd in VGPRs).
+template <typename T, bool DOWN>
 __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
   using O = Op<T>;
   constexpr int ES = static_cast<int>(sizeof(T));
   static_assert(ES == 2, "bf16 / f16 activations");
+  constexpr int kCi = DOWN ? 64 : kC;        // block input channels
+  constexpr int NF = DOWN ? 2 : 4;           // x fragments per lane and row
+  constexpr int kW3K = DOWN ? 2 * kP : kP;   // row length of the packed conv3 weight
   __shared__ __attribute__((aligned(16))) char smem[kLds];
 
   const int tid = threadIdx.x;
@@ -119,14 +128,14 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
   // ---- prologue: w2 / w3 -> LDS (LDS-DMA, swizzled rows), BN params -> LDS, w1 -> VGPRs
   {
     const u32x4 w2s = make_srd(g.w2, kP * 9 * kP * ES);
-    const u32x4 w3s = make_srd(g.w3, kC * kP * ES);
+    const u32x4 w3s = make_srd(g.w3, kC * kW3K * ES);
     const int cL = (tid & 7) ^ ((tid >> 4) & 7), drow = tid >> 3;
 #pragma unroll
     for (int t = 0; t < 9; ++t)
       dma16(w2s, (drow * (9 * kP) + t * kP + cL * 8) * ES, lds0 + kW2 + t * 8192 + wid_u * 1024);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      dma16(w3s, ((drow + 64 * i) * kP + cL * 8) * ES, lds0 + kW3 + i * 8192 + wid_u * 1024);
+      dma16(w3s, ((drow + 64 * i) * kW3K + cL * 8) * ES, lds0 + kW3 + i * 8192 + wid_u * 1024);
     float* bw = reinterpret_cast<float*>(smem + kBN);
     if (tid < 64) {
       bw[tid] = g.s1[tid];
@@ -135,18 +144,44 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
       bw[192 + tid] = g.b2[tid];
     }
     if (tid < 256) {
-      bw[256 + tid] = g.s3[tid];
+      bw[256 + tid] = DOWN ? 1.f : g.s3[tid];
       bw[512 + tid] = g.b3[tid];
     }
+    // conv2's x-padding: ring columns px = -1 and px = 64 (rows 0 and 65 of each slot) stay zero
+    if (tid < 48) {
+      const int sl = tid >> 4, side = (tid >> 3) & 1, ch = tid & 7;
+      *reinterpret_cast<uint4*>(smem + kT1 + sl * kSlot + side * 65 * 128 + ch * 16) = make_uint4(0, 0, 0, 0);
+    }
   }
-  uint4 w1f[4][4];  // [k-step 4h + s][n-tile]: rows 16 j + r16, permuted K columns 32 s + 8 q .. + 7
+  // [k-step 4h + s][jj]: n-tile (jj + 2h) & 3 -- this wave's own two n-tiles first, then the
+  // partner's -- rows 16 j + r16, permuted K columns 32 s + 8 q .. + 7
+  // DOWN: [k-step s][jj] = n-tile 2h + jj over the whole K = 64 (natural channel order)
+  uint4 w1f[4][4];
   {
     const T* w1 = reinterpret_cast<const T*>(g.w1);
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        w1f[s][j] = *reinterpret_cast<const uint4*>(w1 + (16 * j + r16) * kC + 32 * (4 * h + s) + 8 * q);
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (DOWN) {
+          if (s < 2 && j < 2) w1f[s][j] = *reinterpret_cast<const uint4*>(w1 + (16 * (2 * h + j) + r16) * kCi + 32 * s + 8 * q);
+        } else {
+          w1f[s][j] = *reinterpret_cast<const uint4*>(w1 + (16 * ((j + 2 * h) & 3) + r16) * kC + 32 * (4 * h + s) + 8 * q);
+        }
+      }
+  }
+  // DOWN: the downsample's weights wd * sd, rows 128 h + 64 qh + 16 j + r16 (this wave's
+  // output channels), natural K columns 64 + 32 s + 8 q .. + 7 of the packed [256][128]
+  uint4 wdf[2][2][4];
+  if constexpr (DOWN) {
+    const T* w3 = reinterpret_cast<const T*>(g.w3);
+#pragma unroll
+    for (int qh = 0; qh < 2; ++qh)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          wdf[qh][s][j] = *reinterpret_cast<const uint4*>(w3 + (128 * h + 64 * qh + 16 * j + r16) * kW3K + kP + 32 * s + 8 * q);
   }
 
   // x row r -> this lane's 4 fragments of this wave's channel half (k-steps 4h .. 4h+3).
@@ -155,32 +190,45 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
   // bookkeeping assume the shorter path at the join and wait for the prefetch it just issued.
   // x / y through buffer descriptors: the row offset is wave-uniform (soffset, an SGPR) and
   // the lane's offset a loop constant, so the loop holds no 64-bit addresses in VGPRs
-  const int act_bytes = g.N * H * kW * kC * ES;
-  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g.x), 0, act_bytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(g.y, 0, act_bytes, 0x00020000);
-  const int lane_off = (px * kC + 128 * h + cq) * ES;   // + 64 B per k-step
-  constexpr int kRowBytes = kW * kC * ES;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g.x), 0, g.N * H * kW * kCi * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(g.y, 0, g.N * H * kW * kC * ES, 0x00020000);
+  const int lane_off = (px * kC + 128 * h + cq) * ES;   // y (and identity x): + 64 B per k-step
+  const int lane_offx = DOWN ? (px * kCi + 8 * q) * ES : lane_off;
+  constexpr int kRowBytes = kW * kC * ES, kRowBytesX = kW * kCi * ES;
   const int rmax = (yb < H - 1 ? yb : H - 1);
   auto load_row = [&](int r, uint4(&f)[4]) {
     const int rr = r < 0 ? 0 : (r > rmax ? rmax : r);
-    const int roff = __builtin_amdgcn_readfirstlane((n * H + rr) * kRowBytes);
+    const int roff = __builtin_amdgcn_readfirstlane((n * H + rr) * kRowBytesX);
     if (kAbl & 32) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) f[s] = make_uint4(rr, s, lane, 1);
+      for (int s = 0; s < NF; ++s) f[s] = make_uint4(rr, s, lane, 1);
       return;
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_off + 64 * s, roff, (kAbl & 128) ? 2 : 0);
+    for (int s = 0; s < NF; ++s) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_offx + 64 * s, roff, (kAbl & 128) ? 2 : 0);
       f[s] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
   // conv1 of x row r over this wave's channel half, all 64 outputs; the partner's two n-tiles
   // go to the exchange slot, this wave's two stay in acc
+  // (DOWN: this wave's two n-tiles over the whole K, nothing handed over)
   auto conv1_part = [&](int r, const uint4(&f)[4], f32x4(&acc)[2]) {
     f32x4 a[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (DOWN) {
+      if (r >= 0 && r < H) {
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) O::mma(a[j], w1f[s][j], f[s]);
+      }
+      acc[0] = a[0];
+      acc[1] = a[1];
+      return;
+    }
     if (r >= 0 && r < H) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -190,24 +238,25 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
           else O::mma(a[j], w1f[s][j], f[s]);
         }
     }
-    // (selects, not a[2 * h]: a runtime index would put the array in scratch)
-    *reinterpret_cast<f32x4*>(xp_mine) = h ? a[0] : a[2];
-    *reinterpret_cast<f32x4*>(xp_mine + 4) = h ? a[1] : a[3];
-    acc[0] = h ? a[2] : a[0];
-    acc[1] = h ? a[3] : a[1];
+    *reinterpret_cast<f32x4*>(xp_mine) = a[2];
+    *reinterpret_cast<f32x4*>(xp_mine + 4) = a[3];
+    acc[0] = a[0];
+    acc[1] = a[1];
   };
   // full sums of n-tiles 2h, 2h+1 (half 0 + half 1), BN1 + ReLU into ring slot r % 3
   // (zeros outside the image)
   auto conv1_fin = [&](int r, const f32x4(&acc)[2]) {
-    char* slot = smem + kT1 + ((r + 3) % 3) * 8192;
+    char* slot = smem + kT1 + ((r + 3) % 3) * kSlot;
     const bool ok = r >= 0 && r < H;
-    const f32x4 pa = *reinterpret_cast<const f32x4*>(xp_part);
-    const f32x4 pb = *reinterpret_cast<const f32x4*>(xp_part + 4);
-    f32x4 t0, t1;
+    f32x4 t0 = acc[0], t1 = acc[1];
+    if constexpr (!DOWN) {
+      const f32x4 pa = *reinterpret_cast<const f32x4*>(xp_part);
+      const f32x4 pb = *reinterpret_cast<const f32x4*>(xp_part + 4);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {  // in the order half 0 + half 1 on both waves
-      t0[e] = h == 0 ? acc[0][e] + pa[e] : pa[e] + acc[0][e];
-      t1[e] = h == 0 ? acc[1][e] + pb[e] : pb[e] + acc[1][e];
+      for (int e = 0; e < 4; ++e) {  // half 0 + half 1 (f32 addition commutes exactly)
+        t0[e] += pa[e];
+        t1[e] += pb[e];
+      }
     }
     const int c0 = 16 * (2 * h + (q & 1)) + 8 * (q >> 1);
     float v[8], sc[8], sh[8];
@@ -221,7 +270,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     ld8(bn + 64 + c0, sh);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ok ? fmaxf(v[e] * sc[e] + sh[e], 0.f) : 0.f;
-    *reinterpret_cast<uint4*>(slot + swz(px, c0 >> 3)) = O::store_vals(v);
+    *reinterpret_cast<uint4*>(slot + swz(px + 1, c0 >> 3)) = O::store_vals(v);
   };
   // conv2 of output row y, n-tiles 2h, 2h+1, over ring rows y-1..y+1; BN2 + ReLU, rounded:
   // conv3's B fragment of k-step h (channels 32 h + 4 q .. +3 and 32 h + 16 + 4 q .. +3)
@@ -233,17 +282,15 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     for (int t = 0; t < 9; ++t) {
       if (t == 5) mid();
       const int dy = t / 3, dx = t % 3;
-      const char* slot = smem + kT1 + ((y - 1 + dy + 3) % 3) * 8192;
+      const char* slot = smem + kT1 + ((y - 1 + dy + 3) % 3) * kSlot;
       const char* Wt = smem + kW2 + t * 8192;
-      const int xs = px + dx - 1;
-      const bool ok = static_cast<unsigned>(xs) < static_cast<unsigned>(kW);
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         uint4 wf[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) wf[j] = *reinterpret_cast<const uint4*>(Wt + swz(16 * (2 * h + j) + r16, 4 * cb + q));
-        const uint4 tv = *reinterpret_cast<const uint4*>(slot + swz(ok ? xs : 0, 4 * cb + q));
-        const uint4 tf = ok ? tv : make_uint4(0, 0, 0, 0);
+        // ring column px + dx = input pixel px + dx - 1 (columns 0 and 65 are the zero padding)
+        const uint4 tf = *reinterpret_cast<const uint4*>(slot + swz(px + dx, 4 * cb + q));
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (kAbl & 1) acc2[j][0] += __uint_as_float(wf[j].x ^ tf.y);
@@ -299,6 +346,12 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
           else O::mma(acc3[j], wf, tb[kb]);
         }
       }
+      if constexpr (DOWN) {  // + the downsample of x row y (res = its fragments)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O::mma(acc3[j], wdf[qh][s][j], res[s]);
+      }
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
         const int s = 2 * qd + jp, c0 = 32 * s + cq;
@@ -310,11 +363,16 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
           v[e] = __uint_as_float(sw[0]);
           v[4 + e] = __uint_as_float(sw[1]);
         }
-        ld8(bn + 256 + c0, sc);
         ld8(bn + 512 + c0, sh);
-        O::load_vals(res[2 * qh + jp], r);
+        if constexpr (DOWN) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + sh[e], 0.f);
+        } else {
+          ld8(bn + 256 + c0, sc);
+          O::load_vals(res[2 * qh + jp], r);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+        }
         // channels c0 .. c0 + 7 = 128 h + 32 (2 qh + jp) + cq, packed HERE (the empty asm
         // keeps the compiler from sinking the packing, and 8 live f32 per value, into the
         // next row's step where the value is stored: 98 spilled VGPRs without it)
@@ -337,11 +395,11 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
   load_row(ya + 1, xb);
   load_row(ya + 2, xc);
   conv1_part(ya - 1, xd, c1);
-  raw_barrier();
+  if (!DOWN) raw_barrier();
   conv1_fin(ya - 1, c1);
-  raw_barrier();          // partial slots free again
+  if (!DOWN) raw_barrier();  // partial slots free again
   conv1_part(ya, xa, c1);
-  raw_barrier();
+  if (!DOWN) raw_barrier();
   conv1_fin(ya, c1);
 
   // one output row, three barriers: (a) conv1 partials of row y+1 exchanged, (b) ring rows
@@ -352,7 +410,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     conv1_part(y + 1, rb, c1);
     load_row(y + 3, rd);
     if (fl) flush(0);
-    raw_barrier();
+    if (!DOWN) raw_barrier();  // (DOWN: no partials; barrier (c) of the last step freed the slot)
     conv1_fin(y + 1, c1);
     if (fl) flush(1);
     raw_barrier();
@@ -388,19 +446,22 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
 
 using namespace posu;
 
-extern "C" int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
-                                   const float* s1, const float* b1, const void* w2, const float* s2, const float* b2,
-                                   const void* w3, const float* s3, const float* b3, void* y, void* stream) {
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_bottleneck_fwd: dtype must be BF16 or F16");
-  POSU_REQUIRE(x && w1 && s1 && b1 && w2 && s2 && b2 && w3 && s3 && b3 && y, "posu_bottleneck_fwd: null pointer");
-  POSU_REQUIRE(x != y, "posu_bottleneck_fwd: the output must not alias the input");
-  POSU_REQUIRE(W == kW && C == kC && P == kP,
-               "posu_bottleneck_fwd: built for W = 64, C = 256, planes = 64 (layer1 of PoseResNet at 256x256)");
-  POSU_REQUIRE(N > 0 && H > 0, "posu_bottleneck_fwd: empty input");
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
-               "posu_bottleneck_fwd: activation exceeds the 2 GiB addressing range");
+namespace {
+int bottleneck_launch(bool down, int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
+                      const float* s1, const float* b1, const void* w2, const float* s2, const float* b2,
+                      const void* w3, const float* s3, const float* b3, void* y, void* stream, const char* what) {
+  const std::string wh(what);
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, wh + ": dtype must be BF16 or F16");
+  POSU_REQUIRE(x && w1 && s1 && b1 && w2 && s2 && b2 && w3 && (s3 || down) && b3 && y, wh + ": null pointer");
+  POSU_REQUIRE(x != y, wh + ": the output must not alias the input");
+  POSU_REQUIRE(W == kW && C == (down ? 64 : kC) && P == kP,
+               wh + (down ? ": built for W = 64, C = 64, planes = 64 (layer1 block 0 of PoseResNet at 256x256)"
+                          : ": built for W = 64, C = 256, planes = 64 (layer1 of PoseResNet at 256x256)"));
+  POSU_REQUIRE(N > 0 && H > 0, wh + ": empty input");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * kC * 2 < (1LL << 31) - 256,
+               wh + ": activation exceeds the 2 GiB addressing range");
   for (const void* p : {x, static_cast<const void*>(y), w1, w2, w3})
-    POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, "posu_bottleneck_fwd: pointers must be 16-byte aligned");
+    POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, wh + ": pointers must be 16-byte aligned");
   BottleGeom g{};
   g.x = x;
   g.y = y;
@@ -421,9 +482,29 @@ extern "C" int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W
   g.strips = strips;
   g.rows = H / strips;
   hipStream_t s = as_stream(stream);
-  if (dtype == POSU_BF16)
-    hipLaunchKernelGGL(bottleneck64_kernel<uint16_t>, dim3(N * strips), dim3(512), 0, s, g);
-  else
-    hipLaunchKernelGGL(bottleneck64_kernel<f16_t>, dim3(N * strips), dim3(512), 0, s, g);
-  return check_launch("posu_bottleneck_fwd");
+  const dim3 grid(N * strips), block(512);
+  if (dtype == POSU_BF16) {
+    if (down) hipLaunchKernelGGL((bottleneck64_kernel<uint16_t, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((bottleneck64_kernel<uint16_t, false>), grid, block, 0, s, g);
+  } else {
+    if (down) hipLaunchKernelGGL((bottleneck64_kernel<f16_t, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((bottleneck64_kernel<f16_t, false>), grid, block, 0, s, g);
+  }
+  return check_launch(what);
+}
+}  // namespace
+
+extern "C" int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
+                                   const float* s1, const float* b1, const void* w2, const float* s2, const float* b2,
+                                   const void* w3, const float* s3, const float* b3, void* y, void* stream) {
+  return bottleneck_launch(false, dtype, x, N, H, W, C, P, w1, s1, b1, w2, s2, b2, w3, s3, b3, y, stream,
+                           "posu_bottleneck_fwd");
+}
+
+extern "C" int posu_bottleneck_down_fwd(int dtype, const void* x, int N, int H, int W, int C, int P,
+                                        const void* w1, const float* s1, const float* b1, const void* w2,
+                                        const float* s2, const float* b2, const void* w3d, const float* shift3,
+                                        void* y, void* stream) {
+  return bottleneck_launch(true, dtype, x, N, H, W, C, P, w1, s1, b1, w2, s2, b2, w3d, nullptr, shift3, y, stream,
+                           "posu_bottleneck_down_fwd");
 }

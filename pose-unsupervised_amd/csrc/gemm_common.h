@@ -27,8 +27,7 @@ struct Op<uint16_t> {  // bf16
   static __device__ __forceinline__ uint4 store_vals(const float* v) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<uint32_t>(f2bf(v[2 * i])) | (static_cast<uint32_t>(f2bf(v[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = f2bf2(v[2 * i], v[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

@@ -44,6 +44,15 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return __builtin_bit_cast(uint16_t, h);
 }
 
+// two f32 -> packed bf16x2 (round to nearest even, as f2bf): ONE v_cvt_pk_bf16_f32, where
+// two f2bf calls cost two conversions and an OR
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+  const f32x2v v = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
+}
+
 // wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
@@ -90,8 +99,7 @@ struct Vec<uint16_t> {
   static __device__ __forceinline__ uint4 pack(const float* v) {
     uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      w[i] = static_cast<uint32_t>(f2bf(v[2 * i])) | (static_cast<uint32_t>(f2bf(v[2 * i + 1])) << 16);
+    for (int i = 0; i < 4; ++i) w[i] = f2bf2(v[2 * i], v[2 * i + 1]);
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
 };

@@ -40,7 +40,7 @@ struct StemOp<uint16_t> {
                                                   0, 0, 0);
   }
   static __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return static_cast<uint32_t>(f2bf(a)) | (static_cast<uint32_t>(f2bf(b)) << 16);
+    return f2bf2(a, b);
   }
   static __device__ __forceinline__ float round(float a) { return bf2f(f2bf(a)); }
 };

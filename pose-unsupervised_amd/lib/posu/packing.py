@@ -66,6 +66,14 @@ def pack_bottleneck_conv3_weight(w, dtype):
     return wf[:, order].to(dtype).contiguous()
 
 
+def pack_bottleneck_down_weight(dual_w, planes):
+    """Packed two-source tail weight [C][>= 2P] ([w3*s3 | wd*sd], pack_dual_1x1_weight) ->
+    [C][2P] for posu_bottleneck_down_fwd: the conv3 columns 0..P-1 in bottleneck_conv3_order,
+    the downsample columns P..2P-1 unchanged."""
+    order = torch.tensor(bottleneck_conv3_order(planes) + list(range(planes, 2 * planes)), device=dual_w.device)
+    return dual_w[:, order].contiguous()
+
+
 def pack_stem_s2d_weight(w, cpad, bk, dtype):
     """7x7 / stride 2 / pad 3 stem weight [Cout, Cin, 7, 7] -> the equivalent 4x4 / stride 1 /
     top-left pad 2 weight over the 2x2 space-to-depth input (channel (dy*2+dx)*Cin + c):

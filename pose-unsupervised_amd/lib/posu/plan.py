@@ -17,7 +17,8 @@ torch.cuda.CUDAGraph (hipGraph) by the caller.
 import torch
 
 from . import ops
-from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_conv_weight, pack_deconv4x4_weight,
+from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
+                      pack_conv_weight, pack_deconv4x4_weight,
                       pack_dual_1x1_weight, pack_stem_fused_weight, pack_stem_s2d_weight)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
@@ -152,13 +153,14 @@ class _DualTail:
             mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out, tile=t))
 
 
-# identity-residual Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch
-# (posu_bottleneck_fwd) in bf16 / fp16 plans; False runs the three convolutions
+# Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch each in bf16 / fp16 plans
+# (posu_bottleneck_fwd; the first block, with its downsample, posu_bottleneck_down_fwd);
+# False runs the convolutions
 FUSED_BOTTLENECK = True
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -166,12 +168,19 @@ class _Block:
         self.down = None
         self.dual = None
         self.w1f = self.w3f = None   # conv1 / conv3 packed for the fused kernel (permuted K)
+        self.w3d = None              # the fused first block's [w3*s3 | wd*sd] (permuted conv3 K)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
             for nm in names[:2]:
                 self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
             self.dual = _DualTail(blk.conv3, blk.bn3, ds[0], ds[1], code)
+            c1, c2 = self.convs
+            if code in (ops.BF16, ops.F16) and self.dual.stride2 == 1 and self.dual.cout == 256 and \
+                    c1.k == 1 and c1.stride == 1 and c1.w.shape == (64, 64) and \
+                    c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (64, 576) and \
+                    self.dual.w.shape[1] >= 128:
+                self.w3d = pack_bottleneck_down_weight(self.dual.w, 64)
             return
         for nm in names:
             self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
@@ -193,6 +202,10 @@ class _Block:
 
     def __call__(self, x, code, out=None):
         y = x
+        if self.w3d is not None and FUSED_BOTTLENECK and x.shape[2] == 64 and x.shape[3] == 64:
+            c1, c2 = self.convs
+            return ops.bottleneck_down_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3d,
+                                            self.dual.shift, code, out=out)
         if self.dual is not None:
             for c in self.convs:
                 y = c(y, code)

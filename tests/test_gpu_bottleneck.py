@@ -1,7 +1,8 @@
-"""The fused Bottleneck launch (posu_bottleneck_fwd, csrc/bottleneck.hip) against the
-three-launch path on the same device and against torch fp32 on CPU (eval-mode
-Bottleneck, reference lib/models/pose_resnet.py:61-99), plus the whole R50 plan with the
-fused layer1 blocks against the unfused plan."""
+"""The fused Bottleneck launches (posu_bottleneck_fwd / posu_bottleneck_down_fwd,
+csrc/bottleneck.hip) against the unfused launches on the same device and against torch fp32
+on CPU (eval-mode Bottleneck, reference lib/models/pose_resnet.py:61-99, downsample
+pose_resnet.py:136-141), plus the whole R50 plan with the fused layer1 blocks against the
+unfused plan."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -64,6 +65,48 @@ def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
     assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64)])
+def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n, h):
+    """Layer1 block 0: 64 input channels, downsample 1x1 + BN as the residual branch."""
+    g = torch.Generator().manual_seed(29 + h)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=64)
+    w3 = torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5 * 0.3
+    bn3 = (torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1)
+    wd = torch.randn(256, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5 * 0.3
+    bnd = (torch.rand(256, generator=g) + 0.5, torch.randn(256, generator=g) * 0.1)
+    x = torch.randn(n, 64, h, 64, generator=g).abs()   # a maxpool output of ReLUs
+    dt = ops.torch_dtype(code)
+    xq = x.to(dt).float()
+    t = F.relu(F.conv2d(xq, w1) * bn1[0].view(1, -1, 1, 1) + bn1[1].view(1, -1, 1, 1))
+    t = F.relu(F.conv2d(t, w2, padding=1) * bn2[0].view(1, -1, 1, 1) + bn2[1].view(1, -1, 1, 1))
+    ref = F.relu(F.conv2d(t, w3) * bn3[0].view(1, -1, 1, 1) + bn3[1].view(1, -1, 1, 1) +
+                 F.conv2d(xq, wd) * bnd[0].view(1, -1, 1, 1) + bnd[1].view(1, -1, 1, 1))
+    bk = ops.conv_bk(code)
+    xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 64, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 64, bk, dt)
+    s = [v.to(cuda) for v in (bn1[0], bn1[1], bn2[0], bn2[1])]
+    pdual = packing.pack_dual_1x1_weight(w3.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), dt)
+    shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
+    fused = ops.bottleneck_down_nhwc(xd, p1, s[0], s[1], p2, s[2], s[3],
+                                     packing.pack_bottleneck_down_weight(pdual, 64), shift, code)
+    t1 = ops.conv2d_nhwc(xd, p1, 64, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    t2 = ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    unfused = ops.conv1x1_dual_nhwc(t2, xd, 1, pdual, 256, shift, True, code)
+    torch.cuda.synchronize()
+    # conv1 sums in the unfused order; conv3 in a permuted one (last-bit differences of t2
+    # products only)
+    d = (fused.float() - unfused.float()).abs()
+    ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * unfused.float().abs().clamp_min(2.0 ** -4)
+    assert float(d.mean()) < 0.05 * float(ulp.mean()), float(d.mean())
+    assert bool((d <= 16 * ulp).all()), float((d / ulp).max())
+    got = fused.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs()
+    tol = 0.05 if code == BF16 else 0.01
+    assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
+
+
 def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 32, 256, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 256, device=cuda, dtype=torch.bfloat16)
@@ -73,6 +116,8 @@ def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 64, 256, device=cuda, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError, match='alias'):
         ops.bottleneck_nhwc(x, w, s, s, w, s, s, w, s, s, BF16, out=x)
+    with pytest.raises(RuntimeError, match='C = 64'):   # the first-block kernel takes 64 channels
+        ops.bottleneck_down_nhwc(x, w, s, s, w, s, s, w, s, BF16)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp16'])
@@ -84,6 +129,7 @@ def test_plan_with_fused_layer1_matches_unfused_plan(cuda, precision):
     net = net.to(cuda).eval()
     plan = net.plan(cuda)
     assert sum(b.w3f is not None for b in plan.layers[0]) == 2   # layer1 blocks 1 and 2
+    assert plan.layers[0][0].w3d is not None                     # layer1 block 0
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=12)]
     saved = P.FUSED_BOTTLENECK
     try:

@@ -73,16 +73,39 @@ def main():
         ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, BF16, out=t2)
         ops.conv2d_nhwc(t2, p3, 256, 1, 1, 1, 0, s[4], s[5], x, True, BF16, out=y3)
 
+    # the first block (64 input channels, downsample as the residual branch)
+    x0 = torch.randn(a.n, 64, 64, 64, generator=g).abs().to(dev, dt)
+    w10 = torch.randn(64, 64, 1, 1, generator=g) * 0.1
+    wd = torch.randn(256, 64, 1, 1, generator=g) * 0.1
+    p10 = packing.pack_conv_weight(w10.to(dev), 64, bk, dt)
+    pdual = packing.pack_dual_1x1_weight(w3.to(dev), s[4], wd.to(dev), s[4], dt)
+    p3d = packing.pack_bottleneck_down_weight(pdual, 64)
+    y0 = torch.empty(a.n, 64, 64, 256, device=dev, dtype=dt)
+    y03 = torch.empty_like(y0)
+
+    def fused_down():
+        ops.bottleneck_down_nhwc(x0, p10, s[0], s[1], p2, s[2], s[3], p3d, s[5], BF16, out=y0)
+
+    def three_down():
+        ops.conv2d_nhwc(x0, p10, 64, 1, 1, 1, 0, s[0], s[1], None, True, BF16, out=t1)
+        ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, BF16, out=t2)
+        ops.conv1x1_dual_nhwc(t2, x0, 1, pdual, 256, s[5], True, BF16, out=y03)
+
     nbytes = 2 * x.numel() * 2
-    cases = (('fused', fused),) if a.lib else (('fused', fused), ('three launches', three))
-    for name, fn in cases:
+    nb0 = (x0.numel() + y0.numel()) * 2
+    cases = [('fused', fused, nbytes), ('fused first', fused_down, nb0)]
+    if not a.lib:
+        cases += [('three launches', three, nbytes), ('first, unfused', three_down, nb0)]
+    for name, fn, nb in cases:
         us = timeit(fn, a.reps, a.rounds)
-        print('%-16s %8.1f us  %5.2f TB/s (algorithmic x + y)' % (name, us, nbytes / us / 1e6))
+        print('%-16s %8.1f us  %5.2f TB/s (algorithmic x + y)' % (name, us, nb / us / 1e6))
     if a.lib:
         return
     torch.cuda.synchronize()
     d = (y.float() - y3.float()).abs()
     print('fused vs three: max %.4g mean %.4g' % (float(d.max()), float(d.mean())))
+    d = (y0.float() - y03.float()).abs()
+    print('fused first vs unfused: max %.4g mean %.4g' % (float(d.max()), float(d.mean())))
 
 
 if __name__ == '__main__':
