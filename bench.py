@@ -443,8 +443,8 @@ def infer_main(args):
         traffic, src = pmc_traffic(args.layers, args.size, args.precision, args.groups)
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
                 'frac': round(achieved / peak, 4), 'traffic': traffic,
-                'kernel': 'network per replay: fused stem (stem_pool_kernel) + conv stack (conv_igemm / '
-                          'conv_persist kernels, fused deconv+head)',
+                'kernel': 'network per replay: fused stem (stem_pool_kernel) + fused layer1 Bottlenecks '
+                          '(bottleneck64_kernel) + conv stack (conv_igemm / conv_persist kernels, fused deconv+head)',
                 'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (gf, frames)}
         if traffic:
             roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward')

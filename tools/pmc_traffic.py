@@ -7,15 +7,18 @@
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced streaming reads, so it
 is doubled; WRITE_SIZE is exact for 16-B stores.  Infinity-Cache hits are counted too.
+The JSON line carries the commit the passes ran at (env POSU_COMMIT, set by
+tools/profile_round.sh).
 Takes the LAST forward's network launches (pack + conv stack + maxpool), found from the
 last run of input-pack launches unless a launch count is given.
 """
 import csv
 import json
+import os
 import sys
 
-NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'conv_halo_kernel', 'stem_pool_kernel', 'maxpool_kernel',
-       'pack_s2d_kernel', 'pack_kernel')
+NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck64_kernel', 'stem_pool_kernel', 'maxpool_kernel',
+               'pack_s2d_kernel', 'pack_kernel')
 
 
 def load(path, counter):
@@ -45,7 +48,7 @@ def main():
     fb = sum(x[2] for x in f) * 2 * 1024
     wb = sum(x[2] for x in w) * 1024
     print(json.dumps({'launches': len(f), 'fetch_bytes_corrected': fb, 'write_bytes': wb,
-                      'traffic_bytes': fb + wb}))
+                      'traffic_bytes': fb + wb, 'commit': os.environ.get('POSU_COMMIT')}))
     for a, b in zip(f, w):
         print('%-60s fetch %8.1f MB  write %8.1f MB' % (a[1][:60], a[2] * 2 * 1024 / 1e6, b[2] * 1024 / 1e6))
 
