@@ -67,7 +67,7 @@ def _bench_plan_outputs(cuda, precision, autotune):
         rep.stage_geo(rep.stage_net())
         if autotune:
             plan.autotune(plan.pack_input(rep.views), keep_features=False, reps=2)
-            assert len(P.tuned_tiles()) > 20
+            assert len(P.tuned_tiles()) >= 15   # every unfused conv geometry of the R50 plan
         rep.capture()
         rep.run_geo(rep.run_net())
         coords, loss, X = rep.run_geo(rep.run_net())
