@@ -30,9 +30,14 @@ from posu.pipeline import synthetic_meta
 pytestmark = pytest.mark.gpu
 
 GROUPS, LAYERS, SIZE = 32, 50, 256
-BANDS = {  # measured on MI355X (round 2: fp32 hm 2.3e-5 / px 0.005 / mm 0.029; bf16 hm 0.21 / px 38 / mm 472)
+# measured on MI355X (round 2: fp32 hm 2.3e-5 / px 0.005 / mm 0.029; bf16 hm 0.19-0.21 / px 38-39).
+# bf16 has no mm gate: with random weights the heatmaps are flat noise and soft-argmax at
+# beta = 100 turns a 0.02 heatmap difference into a jump between noise maxima (tens of px),
+# which the DLT over four mutually inconsistent views turns into metres (472-3269 mm mean
+# between runs of the same code) -- the fp32 mode is the parity configuration.
+BANDS = {
     'fp32': {'hm_max': 1e-3, 'tri_max': 1e-2, 'loss_rel': 1e-5, 'px_mean': 0.02, 'mm_mean': 0.1},
-    'bf16': {'hm_max': 0.5, 'hm_mean': 0.05, 'tri_max': 1e-2, 'loss_rel': 1e-2, 'px_mean': 100.0, 'mm_mean': 1000.0},
+    'bf16': {'hm_max': 0.5, 'hm_mean': 0.05, 'tri_max': 1e-2, 'loss_rel': 1e-2, 'px_mean': 100.0, 'mm_mean': None},
 }
 
 
@@ -89,7 +94,8 @@ def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precisio
     assert c['triangulation_same_2d_mm']['max'] < b['tri_max']
     assert c['epipolar_loss_rel_err'] < b['loss_rel']
     assert c['joints_px_err']['mean'] < b['px_mean']
-    assert c['mean'] < b['mm_mean']
+    if b['mm_mean'] is not None:
+        assert c['mean'] < b['mm_mean']
     # against fp64: the HIP path's error next to the reference fp32 path's own error
     from oracle import geometry_ref as G
     ours_hm = (out['hm0'].double() - oracle_run['hm64']).abs().max().item()
