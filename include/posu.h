@@ -63,6 +63,31 @@ int posu_pack_nchw_to_nhwc(int dtype, const float* x, int N, int C, int H, int W
 int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W,
                        void* y, int Cpad, int hflip, void* stream);
 
+/* Batched weight packing (training: the parameters change every optimizer step).  One
+ * launch packs every job of a device-resident table: fp32 PyTorch weights -> the layouts the
+ * conv kernels read, in `dtype` (replaces per-layer torch packing; the modes restate
+ * lib/posu/packing.py):
+ *   POSU_PACK_CONV:   Conv2d [cout][cin][kh][kw] -> [rows][kpad], k = tap * pitch + ci
+ *                     (posu_conv2d_fwd's w; pitch = the channel stride of the packed K);
+ *   POSU_PACK_DGRAD:  the same weight flipped and transposed -> [rows >= cin][kpad],
+ *                     k = tap * pitch + co, value w[co][ci][kh-1-th][kw-1-tw] (co < cout only;
+ *                     posu_conv2d_dgrad's weight);
+ *   POSU_PACK_DECONV: ConvTranspose2d [cin][cout][4][4] -> [4 classes][rows][kpad],
+ *                     k = (ty*2 + tx) * cin + ci (posu_deconv4x4s2_fwd's w).
+ * Zero outside the source.  block_start: the job's first block; blocks per job =
+ * posu_pack_job_blocks(mode, rows, kpad); total_blocks = their sum. */
+#define POSU_PACK_CONV 0
+#define POSU_PACK_DGRAD 1
+#define POSU_PACK_DECONV 2
+typedef struct posu_pack_job {
+  const float* src;
+  void* dst;
+  long long block_start;
+  int mode, cout, cin, kh, kw, pitch, rows, kpad;
+} posu_pack_job;
+long long posu_pack_job_blocks(int mode, int rows, int kpad);
+int posu_pack_weights(int dtype, const posu_pack_job* jobs, int njobs, long long total_blocks, void* stream);
+
 /* NHWC activations -> NCHW fp32 (for returning x1 / f in the reference
  * layout: lib/models/pose_resnet.py:205). */
 int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,

@@ -31,6 +31,8 @@ _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
+    'posu_pack_job_blocks': [_i, _i, _i],
+    'posu_pack_weights': [_i, _p, _i, _ll, _p],
     'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],
     'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
@@ -72,6 +74,7 @@ _SIGNATURES = {
     'posu_maxpool3x3s2_bwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _ll, _p],
 }
 _RESTYPES = {'posu_last_error': ctypes.c_char_p, 'posu_conv2d_wgrad_workspace': ctypes.c_longlong,
+             'posu_pack_job_blocks': ctypes.c_longlong,
              'posu_bn_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong}
 
 

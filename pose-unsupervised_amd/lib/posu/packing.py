@@ -8,6 +8,7 @@
 * Eval-mode BatchNorm2d -> per-channel (scale, shift) f32, folded in fp64:
   scale = gamma / sqrt(var + eps), shift = beta - mean * scale (+ conv bias * scale).
 """
+import numpy as np
 import torch
 
 COUT_ALIGN = 64
@@ -155,3 +156,70 @@ def pack_conv_dgrad_weight(w, bk, dtype):
     (see posu_conv2d_dgrad)."""
     wt = w.detach().float().flip(2, 3).transpose(0, 1)
     return pack_conv_weight(wt, wt.shape[1], bk, dtype)
+
+
+# ---- batched packing (posu_pack_weights): every weight of a training step in one launch
+PACK_CONV, PACK_DGRAD, PACK_DECONV = 0, 1, 2
+_JOB = np.dtype([('src', '<u8'), ('dst', '<u8'), ('block_start', '<i8'), ('mode', '<i4'), ('cout', '<i4'),
+                 ('cin', '<i4'), ('kh', '<i4'), ('kw', '<i4'), ('pitch', '<i4'), ('rows', '<i4'), ('kpad', '<i4')],
+                align=True)
+assert _JOB.itemsize == 56   # sizeof(posu_pack_job)
+
+
+class BatchedPacker:
+    """Packs a fixed set of fp32 parameters into preallocated kernel-layout buffers with one
+    posu_pack_weights launch (the per-layer torch packs above, restated in HIP).  add() returns
+    the destination buffer (stable across steps); run() re-packs from the parameters' current
+    values.  The job table is rebuilt if a parameter's storage moved."""
+
+    def __init__(self, code, device):
+        self.code, self.device = code, device
+        self.jobs, self.srcs, self.dsts = [], [], []
+        self.table, self.total, self._ptrs = None, 0, None
+
+    def add(self, mode, w, cout, cin, kh, kw, pitch, rows, kpad):
+        from . import ops
+        from ._native import load
+        if w.dtype != torch.float32 or not w.is_contiguous():
+            raise TypeError('batched packing reads contiguous f32 parameters')
+        n = rows * kpad * (4 if mode == PACK_DECONV else 1)
+        dst = torch.empty(((4, rows, kpad) if mode == PACK_DECONV else (rows, kpad)), dtype=ops.torch_dtype(self.code),
+                          device=self.device)
+        assert dst.numel() == n
+        blocks = int(load().posu_pack_job_blocks(mode, rows, kpad))
+        self.jobs.append([mode, cout, cin, kh, kw, pitch, rows, kpad, blocks])
+        self.srcs.append(w)
+        self.dsts.append(dst)
+        self.table = None
+        return dst
+
+    def conv(self, w, cin_pad, bk):
+        cout, cin, kh, kw = w.shape
+        return self.add(PACK_CONV, w, cout, cin, kh, kw, cin_pad, round_up(cout, COUT_ALIGN),
+                        round_up(kh * kw * cin_pad, bk))
+
+    def dgrad(self, w, bk, cout_pitch=None):
+        cout, cin, kh, kw = w.shape
+        pitch = cout_pitch or cout
+        return self.add(PACK_DGRAD, w, cout, cin, kh, kw, pitch, round_up(cin, COUT_ALIGN), round_up(kh * kw * pitch, bk))
+
+    def deconv(self, w, bk):
+        cin, cout = w.shape[:2]
+        return self.add(PACK_DECONV, w, cout, cin, 4, 4, cin, round_up(cout, COUT_ALIGN), round_up(4 * cin, bk))
+
+    def _build(self):
+        arr = np.zeros(len(self.jobs), dtype=_JOB)
+        start = 0
+        for i, (job, w, d) in enumerate(zip(self.jobs, self.srcs, self.dsts)):
+            mode, cout, cin, kh, kw, pitch, rows, kpad, blocks = job
+            arr[i] = (w.data_ptr(), d.data_ptr(), start, mode, cout, cin, kh, kw, pitch, rows, kpad)
+            start += blocks
+        self.table = torch.from_numpy(arr.view(np.uint8)).to(self.device)
+        self.total = start
+        self._ptrs = [w.data_ptr() for w in self.srcs]
+
+    def run(self):
+        from ._native import call, ptr, stream_of
+        if self.table is None or self._ptrs != [w.data_ptr() for w in self.srcs]:
+            self._build()
+        call('posu_pack_weights', self.code, ptr(self.table), len(self.jobs), self.total, stream_of(self.device))

@@ -19,12 +19,13 @@ update (in view order), as in the reference's four backbone calls.
 
 Parameters stay NCHW f32 in the nn.Modules (so optimizers, DDP and checkpoints are
 unchanged); they are packed into the kernels' layouts in the compute dtype once per
-step, and their gradients come back f32 in the modules' layouts.
+step -- every weight of the network in ONE posu_pack_weights launch into buffers allocated
+once (packing.BatchedPacker) -- and their gradients come back f32 in the modules' layouts.
 """
 import torch
 
 from . import ops, train_ops as T
-from .packing import pack_conv_dgrad_weight, pack_conv_weight, pack_deconv4x4_weight
+from .packing import BatchedPacker
 
 STEM_CIN_PAD = 8
 HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
@@ -46,9 +47,9 @@ class _ConvBN:
     def params(self):
         return [self.conv.weight, self.bn.weight, self.bn.bias]
 
-    def pack(self, code, bk, dt, need_dgrad=True):
-        self.w = pack_conv_weight(self.conv.weight, self.cin_pad, bk, dt)
-        self.wt = pack_conv_dgrad_weight(self.conv.weight, bk, dt) if need_dgrad else None
+    def pack(self, packer, bk, need_dgrad=True):
+        self.w = packer.conv(self.conv.weight, self.cin_pad, bk)
+        self.wt = packer.dgrad(self.conv.weight, bk) if need_dgrad else None
 
     def forward(self, x, nseg, code, residual=None):
         z = ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, None, None, None, False,
@@ -130,10 +131,10 @@ class _DeconvBN:
     def params(self):
         return [self.dc.weight, self.bn.weight, self.bn.bias]
 
-    def pack(self, code, bk, dt):
-        self.w = pack_deconv4x4_weight(self.dc.weight, bk, dt)
+    def pack(self, packer, bk):
+        self.w = packer.deconv(self.dc.weight, bk)
         # data gradient = conv 4x4 / s2 / p1 with the [Cin][Cout] weight read as conv weights
-        self.wd = pack_conv_weight(self.dc.weight, self.cout, bk, dt)
+        self.wd = packer.conv(self.dc.weight, self.cout, bk)
 
     def forward(self, x, nseg, code):
         z = ops.deconv4x4s2_nhwc(x, self.w, self.cout, None, None, False, code)
@@ -166,6 +167,7 @@ class TrainPlan:
         if fl.kernel_size != (1, 1):
             raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
         self.head = fl
+        self.packer = None
         self.njoints = fl.weight.shape[0]
         if self.njoints > HEAD_CPAD:
             raise NotImplementedError('more than %d joints' % HEAD_CPAD)
@@ -178,22 +180,28 @@ class TrainPlan:
         return out
 
     def pack(self):
-        code = self.code
-        bk, dt = ops.conv_bk(code), ops.torch_dtype(code)
-        self.stem.pack(code, bk, dt, need_dgrad=False)
-        for layer in self.layers:
-            for b in layer:
-                for u in b.all_units():
-                    u.pack(code, bk, dt)
-        for d in self.deconvs:
-            d.pack(code, bk, dt)
+        """Re-pack every weight from the parameters' current values (one launch); the job
+        table and the packed buffers are built on the first call."""
+        if self.packer is None or self.packer.device != self.head.weight.device:
+            code = self.code
+            bk = ops.conv_bk(code)
+            pk = BatchedPacker(code, self.head.weight.device)
+            self.stem.pack(pk, bk, need_dgrad=False)
+            for layer in self.layers:
+                for b in layer:
+                    for u in b.all_units():
+                        u.pack(pk, bk)
+            for d in self.deconvs:
+                d.pack(pk, bk)
+            fl = self.head
+            self.head_w = pk.conv(fl.weight, fl.weight.shape[1], bk)
+            # dgrad of the head over HEAD_CPAD gradient channels (zero above njoints)
+            self.head_wt = pk.dgrad(fl.weight, bk, cout_pitch=HEAD_CPAD)
+            self.packer = pk
         fl = self.head
-        self.head_w = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, dt)
-        wpad = torch.zeros((HEAD_CPAD,) + tuple(fl.weight.shape[1:]), dtype=torch.float32, device=fl.weight.device)
-        wpad[:self.njoints] = fl.weight.detach()
-        self.head_wt = pack_conv_dgrad_weight(wpad, bk, dt)
         self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None else
                        torch.zeros(self.njoints, device=fl.weight.device))
+        self.packer.run()
 
     def forward(self, x_nchw, nseg):
         """x [nseg*B, 3, H, W] f32 -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC, saved)."""

@@ -221,3 +221,41 @@ def test_bn_train_statistics_with_a_large_mean_offset(cuda, code):
     var = zs.var(dim=(1, 3, 4), unbiased=False)
     torch.testing.assert_close(mean.cpu().double().view(nseg, c), mu, atol=1e-4, rtol=1e-6)
     torch.testing.assert_close(rstd.cpu().double().view(nseg, c), 1 / torch.sqrt(var + 1e-5), atol=0, rtol=2e-3)
+
+
+@pytest.mark.parametrize('code', [F32, BF16, F16])
+def test_batched_weight_packing_equals_the_torch_packs(cuda, code):
+    """posu_pack_weights (one launch for the whole training step) against packing.py's torch
+    restatements, bit for bit: conv (padded stem channels, 3x3, 1x1), conv data-gradient
+    (flipped + transposed, and the head's padded gradient channels), deconv parity classes and
+    the deconv's data-gradient conv view."""
+    g = torch.Generator(device=cuda).manual_seed(3)
+    dt, bk = ops.torch_dtype(code), ops.conv_bk(code)
+    w_stem = torch.randn(64, 3, 7, 7, device=cuda, generator=g)
+    w3 = torch.randn(96, 40, 3, 3, device=cuda, generator=g)
+    w1 = torch.randn(130, 64, 1, 1, device=cuda, generator=g)
+    wdc = torch.randn(72, 48, 4, 4, device=cuda, generator=g)     # ConvTranspose2d [Cin][Cout][4][4]
+    wh = torch.randn(17, 256, 1, 1, device=cuda, generator=g)
+    pk = packing.BatchedPacker(code, cuda)
+    outs = [
+        (pk.conv(w_stem, 8, bk), packing.pack_conv_weight(w_stem, 8, bk, dt)),
+        (pk.conv(w3, 40, bk), packing.pack_conv_weight(w3, 40, bk, dt)),
+        (pk.dgrad(w3, bk), packing.pack_conv_dgrad_weight(w3, bk, dt)),
+        (pk.conv(w1, 64, bk), packing.pack_conv_weight(w1, 64, bk, dt)),
+        (pk.dgrad(w1, bk), packing.pack_conv_dgrad_weight(w1, bk, dt)),
+        (pk.deconv(wdc, bk), packing.pack_deconv4x4_weight(wdc, bk, dt)),
+        (pk.conv(wdc, 48, bk), packing.pack_conv_weight(wdc, 48, bk, dt)),
+    ]
+    wpad = torch.zeros(64, 256, 1, 1, device=cuda)
+    wpad[:17] = wh
+    outs.append((pk.dgrad(wh, bk, cout_pitch=64), packing.pack_conv_dgrad_weight(wpad, bk, dt)))
+    pk.run()
+    torch.cuda.synchronize()
+    for i, (got, ref) in enumerate(outs):
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        assert torch.equal(got, ref), (i, float((got.float() - ref.float()).abs().max()))
+    # the parameters change in place (an optimizer step): run() re-packs the new values
+    with torch.no_grad():
+        w3.mul_(-0.5)
+    pk.run()
+    assert torch.equal(outs[1][0], packing.pack_conv_weight(w3, 40, bk, dt))
