@@ -166,7 +166,8 @@ def build_model(layers, size, precision, device):
     from models.pose_resnet import get_pose_net
     from posu import synthetic as syn
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False, precision=precision)
-    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(layers, size)))
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
+                                                 bn_stats=syn.load_bn_stats(layers, size)))
     return net.to(device).eval()
 
 
@@ -220,7 +221,8 @@ def cpu_baseline(layers, size, groups, seconds):
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
-    sd = syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(layers, size))
+    sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
+                                  bn_stats=syn.load_bn_stats(layers, size))
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
     views = syn.synthetic_views(4, groups, size, seed=100)
     frames, ref, t0 = 0, None, time.perf_counter()

@@ -62,17 +62,17 @@ def oracle_run():
     return ref
 
 
-def _bench_plan_outputs(cuda, precision, autotune):
+def _bench_plan_outputs(cuda, precision, autotune, layers=LAYERS, size=SIZE, groups=GROUPS):
     from posu import plan as P
-    net = bench.build_model(LAYERS, SIZE, precision, cuda)
-    meta, _ = synthetic_meta(GROUPS, cuda, image_size=SIZE)
+    net = bench.build_model(layers, size, precision, cuda)
+    meta, _ = synthetic_meta(groups, cuda, image_size=size)
     plan = net.plan(cuda)
-    rep = bench.Replayer(plan, bench.input_views(GROUPS, SIZE, 0, 0, cuda), meta, GROUPS, 1, True, cuda)
+    rep = bench.Replayer(plan, bench.input_views(groups, size, 0, 0, cuda), meta, groups, 1, True, cuda)
     with torch.no_grad():
         rep.stage_geo(rep.stage_net())
         if autotune:
             plan.autotune(plan.pack_input(rep.views), keep_features=False, reps=2)
-            assert len(P.tuned_tiles()) >= 15   # every unfused conv geometry of the R50 plan
+            assert len(P.tuned_tiles()) >= 15   # every unfused conv geometry of the plan
         rep.capture()
         rep.run_geo(rep.run_net())
         coords, loss, X = rep.run_geo(rep.run_net())
@@ -108,3 +108,26 @@ def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precisio
     if precision == 'fp32':  # within a small factor of the reference's own fp32 precision
         assert ours_hm < 4 * ref_hm + 1e-6
         assert ours_sa.mean() < 4 * ref_sa.mean() + 1e-5
+
+
+def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda):
+    """configs[4]'s per-GPU pipeline (R152 backbone at 384x384, fp16 compute, fp64
+    triangulation) on one 4-view group, through bench's replay path (hipGraph, fused stem;
+    layer1 stays unfused at 96x96 maps), against the fp32 CPU oracle chain."""
+    layers, size, groups = 152, 384, 1
+    from models.pose_resnet import get_pose_net
+    torch.set_num_threads(16)
+    net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
+    sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
+                                  bn_stats=syn.load_bn_stats(layers, size))
+    _, host = synthetic_meta(groups, 'cpu', image_size=size)
+    views = syn.synthetic_views(4, groups, size, seed=100)
+    ref = bench.oracle_chain(sd, layers, size, views, host, full=True)
+    ref['host'] = host
+    out = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=groups)
+    c = bench.compare_with_reference(out, ref, out['meta'], cuda)
+    print('R152@384 fp16 pipeline vs oracle: %s' % c)
+    assert np.isfinite(out['X0']).all()
+    assert c['heatmap_abs_err']['mean'] < 0.05 and c['heatmap_abs_err']['max'] < 0.5
+    assert c['triangulation_same_2d_mm']['max'] < 1e-2      # the DLT itself: BASELINE's 1e-2 mm
+    assert c['epipolar_loss_rel_err'] < 0.1
