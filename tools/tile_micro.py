@@ -1,7 +1,7 @@
 """Times conv tile configurations on the compute-heavy R50@256 batch-128 layer shapes (bf16,
 HIP events, min over rounds) and checks that loops with the same K order agree bit for bit.
 
-    python tools/tile_micro.py [--tiles 5,23,29] [--reps 10] [--rounds 3]
+    python tools/tile_micro.py [--tiles 5,23,37] [--reps 10] [--rounds 3] [--lib PATH]
 """
 import argparse
 import os
@@ -12,7 +12,7 @@ sys.path[:0] = [os.path.join(REPO, 'pose-unsupervised_amd', 'lib'), REPO]
 
 import torch  # noqa: E402
 
-from posu import ops  # noqa: E402
+from posu import _native, ops  # noqa: E402
 
 BF16 = 1
 # name, kind, (n, h, w, cin), cout, k
@@ -45,11 +45,14 @@ def timeit(fn, reps, rounds):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument('--tiles', default='5,23,29')
+    ap.add_argument('--tiles', default='5,23,37')
+    ap.add_argument('--lib', default=None, help='another build of libposeu.so (experiments)')
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=3)
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(',')]
+    if a.lib:
+        _native._LIB_PATH = os.path.abspath(a.lib)
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev).manual_seed(0)
     dt = torch.bfloat16
