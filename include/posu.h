@@ -43,6 +43,7 @@ extern "C" {
 
 /* ---------------------------------------------------------------- runtime */
 const char* posu_last_error(void);
+/* 5: stateless conv knobs (4) + the fused layer1 Bottleneck kernels and batched weight packing */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
