@@ -186,6 +186,16 @@ int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, in
  *   w3d: [4P][2P]: columns 0..P-1 = conv3 weight * s3 with the posu_bottleneck_fwd column
  *        permutation of w3, columns P..2P-1 = downsample weight * sd (natural order);
  *   shift3: [4P] f32 = b3 + bd. */
+/* The identity Bottleneck of layer2 (lib/models/pose_resnet.py:61-99) as one launch, with the
+ * weights streamed through LDS (they do not fit): W = 32, C = 512, P = 128, H % 4 == 0; dtype
+ * BF16 / F16.  x, y: [N, H, W, C] (no alias); w1 [P][C], w2 [P][9P], w3 [C][P] in
+ * posu_conv2d_fwd's packing (natural channel order); s/b as posu_bottleneck_fwd.  Same K
+ * order per accumulator as the three convolutions. */
+int posu_bottleneck2_fwd(int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
+                         const float* s1, const float* b1, const void* w2, const float* s2,
+                         const float* b2, const void* w3, const float* s3, const float* b3, void* y,
+                         void* stream);
+
 int posu_bottleneck_down_fwd(int dtype, const void* x, int N, int H, int W, int C, int P,
                              const void* w1, const float* s1, const float* b1, const void* w2,
                              const float* s2, const float* b2, const void* w3d, const float* shift3,

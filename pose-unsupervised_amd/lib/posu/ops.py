@@ -98,6 +98,16 @@ def bottleneck_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
     return out
 
 
+def bottleneck2_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
+    """Fused identity Bottleneck of layer2 (posu_bottleneck2_fwd): x [N, H, 32, 512] -> y."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    call('posu_bottleneck2_fwd', code, ptr(x), n, h, w, c, w1.shape[0], ptr(w1), ptr(s1), ptr(b1), ptr(w2),
+         ptr(s2), ptr(b2), ptr(w3), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
+    return out
+
+
 def bottleneck_down_nhwc(x, w1, s1, b1, w2, s2, b2, w3d, shift3, code, out=None):
     """Fused first Bottleneck of layer1 with its downsample (posu_bottleneck_down_fwd):
     x [N, H, W, C] -> y [N, H, W, w3d.shape[0]]."""

@@ -107,6 +107,38 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
     assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12)])
+def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
+    """Layer2's identity block (32-wide maps, 512 channels, planes 128; weights streamed
+    through LDS): bit-identical to the three unfused launches (same K order per accumulator,
+    same epilogue arithmetic) and within the dtype's tolerance of torch fp32."""
+    g = torch.Generator().manual_seed(41 + h)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=512, p=128)
+    x = torch.randn(n, 512, h, 32, generator=g)
+    dt = ops.torch_dtype(code)
+    xq = x.to(dt).float()
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    bk = ops.conv_bk(code)
+    xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 512, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 128, bk, dt)
+    p3 = packing.pack_conv_weight(w3.to(cuda), 128, bk, dt)
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
+    fused = ops.bottleneck2_nhwc(xd, p1, s[0], s[1], p2, s[2], s[3], p3, s[4], s[5], code)
+    t1 = ops.conv2d_nhwc(xd, p1, 128, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    t2 = ops.conv2d_nhwc(t1, p2, 128, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    three = ops.conv2d_nhwc(t2, p3, 512, 1, 1, 1, 0, s[4], s[5], xd, True, code)
+    torch.cuda.synchronize()
+    d = (fused.float() - three.float()).abs()
+    print('layer2 fused vs three launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
+    assert torch.equal(fused, three)
+    got = fused.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs()
+    tol = 0.05 if code == BF16 else 0.01
+    assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
+
+
 def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 32, 256, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 256, device=cuda, dtype=torch.bfloat16)
@@ -118,10 +150,19 @@ def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
         ops.bottleneck_nhwc(x, w, s, s, w, s, s, w, s, s, BF16, out=x)
     with pytest.raises(RuntimeError, match='C = 64'):   # the first-block kernel takes 64 channels
         ops.bottleneck_down_nhwc(x, w, s, s, w, s, s, w, s, BF16)
+    x2 = torch.zeros(1, 6, 32, 512, device=cuda, dtype=torch.bfloat16)
+    w1 = torch.zeros(128, 512, device=cuda, dtype=torch.bfloat16)
+    w2 = torch.zeros(128, 1152, device=cuda, dtype=torch.bfloat16)
+    w3 = torch.zeros(512, 128, device=cuda, dtype=torch.bfloat16)
+    s2 = torch.ones(512, device=cuda)
+    with pytest.raises(RuntimeError, match='multiple of 4'):
+        ops.bottleneck2_nhwc(x2, w1, s2, s2, w2, s2, s2, w3, s2, s2, BF16)
+    with pytest.raises(RuntimeError, match='W = 32'):
+        ops.bottleneck2_nhwc(x, w1, s2, s2, w2, s2, s2, w3, s2, s2, BF16)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp16'])
-def test_plan_with_fused_layer1_matches_unfused_plan(cuda, precision):
+def test_plan_with_fused_bottlenecks_matches_unfused_plan(cuda, precision):
     import posu.plan as P
     from models.pose_resnet import get_pose_net
     net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision=precision)
@@ -130,6 +171,7 @@ def test_plan_with_fused_layer1_matches_unfused_plan(cuda, precision):
     plan = net.plan(cuda)
     assert sum(b.w3f is not None for b in plan.layers[0]) == 2   # layer1 blocks 1 and 2
     assert plan.layers[0][0].w3d is not None                     # layer1 block 0
+    assert [b.l2 for b in plan.layers[1]] == [False, True, True, True]   # layer2's identity blocks
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=12)]
     saved = P.FUSED_BOTTLENECK
     try:

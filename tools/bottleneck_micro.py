@@ -91,11 +91,33 @@ def main():
         ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, BF16, out=t2)
         ops.conv1x1_dual_nhwc(t2, x0, 1, pdual, 256, s[5], True, BF16, out=y03)
 
+    # layer2's identity block (32-wide maps, 512 channels, planes 128)
+    xl2 = torch.randn(a.n, 32, 32, 512, generator=g).to(dev, dt)
+    q1 = packing.pack_conv_weight((torch.randn(128, 512, 1, 1, generator=g) * 0.06).to(dev), 512, bk, dt)
+    q2 = packing.pack_conv_weight((torch.randn(128, 128, 3, 3, generator=g) * 0.03).to(dev), 128, bk, dt)
+    q3 = packing.pack_conv_weight((torch.randn(512, 128, 1, 1, generator=g) * 0.1).to(dev), 128, bk, dt)
+    sl = [torch.rand(c, device=dev) + 0.5 for c in (128, 128, 512)]
+    bl = [torch.randn(c, device=dev) * 0.1 for c in (128, 128, 512)]
+    yl2 = torch.empty_like(xl2)
+    u1 = torch.empty(a.n, 32, 32, 128, device=dev, dtype=dt)
+    u2 = torch.empty_like(u1)
+    yl23 = torch.empty_like(xl2)
+
+    def fused_l2():
+        ops.bottleneck2_nhwc(xl2, q1, sl[0], bl[0], q2, sl[1], bl[1], q3, sl[2], bl[2], BF16, out=yl2)
+
+    def three_l2():
+        ops.conv2d_nhwc(xl2, q1, 128, 1, 1, 1, 0, sl[0], bl[0], None, True, BF16, out=u1)
+        ops.conv2d_nhwc(u1, q2, 128, 3, 3, 1, 1, sl[1], bl[1], None, True, BF16, out=u2)
+        ops.conv2d_nhwc(u2, q3, 512, 1, 1, 1, 0, sl[2], bl[2], xl2, True, BF16, out=yl23)
+
     nbytes = 2 * x.numel() * 2
     nb0 = (x0.numel() + y0.numel()) * 2
-    cases = [('fused', fused, nbytes), ('fused first', fused_down, nb0)]
+    nb2 = 2 * xl2.numel() * 2
+    cases = [('fused', fused, nbytes), ('fused first', fused_down, nb0), ('fused layer2', fused_l2, nb2)]
     if not a.lib:
-        cases += [('three launches', three, nbytes), ('first, unfused', three_down, nb0)]
+        cases += [('three launches', three, nbytes), ('first, unfused', three_down, nb0),
+                  ('layer2, unfused', three_l2, nb2)]
     for name, fn, nb in cases:
         us = timeit(fn, a.reps, a.rounds)
         print('%-16s %8.1f us  %5.2f TB/s (algorithmic x + y)' % (name, us, nb / us / 1e6))
@@ -106,6 +128,8 @@ def main():
     print('fused vs three: max %.4g mean %.4g' % (float(d.max()), float(d.mean())))
     d = (y0.float() - y03.float()).abs()
     print('fused first vs unfused: max %.4g mean %.4g' % (float(d.max()), float(d.mean())))
+    d = (yl2.float() - yl23.float()).abs()
+    print('fused layer2 vs unfused: max %.4g mean %.4g' % (float(d.max()), float(d.mean())))
 
 
 if __name__ == '__main__':
