@@ -16,6 +16,9 @@ BF16 = 1
 F64 = 2
 F16 = 3
 
+# the ABI revision this binding declares (include/posu.h); load() refuses any other library
+ABI_VERSION = 5
+
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
 _lib = None
@@ -100,6 +103,9 @@ def load():
             fn = getattr(lib, name)  # AttributeError = a declared symbol is missing
             fn.argtypes = args
             fn.restype = _RESTYPES.get(name, ctypes.c_int)
+        if lib.posu_abi_version() != ABI_VERSION:
+            raise RuntimeError('libposeu.so has ABI %d, the binding expects %d: rebuild it'
+                               % (lib.posu_abi_version(), ABI_VERSION))
         _lib = lib
         return lib
 
