@@ -76,7 +76,8 @@ int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W,
  *   POSU_PACK_DECONV: ConvTranspose2d [cin][cout][4][4] -> [4 classes][rows][kpad],
  *                     k = (ty*2 + tx) * cin + ci (posu_deconv4x4s2_fwd's w).
  * Zero outside the source.  block_start: the job's first block; blocks per job =
- * posu_pack_job_blocks(mode, rows, kpad); total_blocks = their sum. */
+ * posu_pack_job_blocks(the job's mode .. kpad fields) (-1: kpad not a multiple of 8, a
+ * deconv other than 4x4, or a non-positive size); total_blocks = their sum. */
 #define POSU_PACK_CONV 0
 #define POSU_PACK_DGRAD 1
 #define POSU_PACK_DECONV 2
@@ -86,7 +87,7 @@ typedef struct posu_pack_job {
   long long block_start;
   int mode, cout, cin, kh, kw, pitch, rows, kpad;
 } posu_pack_job;
-long long posu_pack_job_blocks(int mode, int rows, int kpad);
+long long posu_pack_job_blocks(int mode, int cout, int cin, int kh, int kw, int pitch, int rows, int kpad);
 int posu_pack_weights(int dtype, const posu_pack_job* jobs, int njobs, long long total_blocks, void* stream);
 
 /* NHWC activations -> NCHW fp32 (for returning x1 / f in the reference

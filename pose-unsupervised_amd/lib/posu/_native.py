@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -34,7 +34,7 @@ _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
-    'posu_pack_job_blocks': [_i, _i, _i],
+    'posu_pack_job_blocks': [_i, _i, _i, _i, _i, _i, _i, _i],
     'posu_pack_weights': [_i, _p, _i, _ll, _p],
     'posu_pack_s2d_nchw': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_nhwc_to_nchw_f32': [_i, _p, _i, _i, _i, _i, _p, _p],

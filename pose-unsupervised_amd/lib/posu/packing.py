@@ -186,7 +186,9 @@ class BatchedPacker:
         dst = torch.empty(((4, rows, kpad) if mode == PACK_DECONV else (rows, kpad)), dtype=ops.torch_dtype(self.code),
                           device=self.device)
         assert dst.numel() == n
-        blocks = int(load().posu_pack_job_blocks(mode, rows, kpad))
+        blocks = int(load().posu_pack_job_blocks(mode, cout, cin, kh, kw, pitch, rows, kpad))
+        if blocks <= 0:
+            raise ValueError('posu_pack_weights cannot pack this weight (mode %d, %s)' % (mode, tuple(w.shape)))
         self.jobs.append([mode, cout, cin, kh, kw, pitch, rows, kpad, blocks])
         self.srcs.append(w)
         self.dsts.append(dst)

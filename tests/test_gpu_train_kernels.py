@@ -259,3 +259,28 @@ def test_batched_weight_packing_equals_the_torch_packs(cuda, code):
         w3.mul_(-0.5)
     pk.run()
     assert torch.equal(outs[1][0], packing.pack_conv_weight(w3, 40, bk, dt))
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_batched_weight_packing_network_sizes(cuda, code):
+    """The LDS-tiled packing paths at PoseResNet-50 sizes (several rows / tiles per block,
+    multi-tile deconv classes) against the torch restatements, bit for bit."""
+    g = torch.Generator(device=cuda).manual_seed(5)
+    dt, bk = ops.torch_dtype(code), ops.conv_bk(code)
+    w3 = torch.randn(512, 512, 3, 3, device=cuda, generator=g)
+    w1 = torch.randn(256, 1024, 1, 1, device=cuda, generator=g)
+    wdc = torch.randn(2048, 256, 4, 4, device=cuda, generator=g)
+    pk = packing.BatchedPacker(code, cuda)
+    outs = [
+        (pk.conv(w3, 512, bk), packing.pack_conv_weight(w3, 512, bk, dt)),
+        (pk.dgrad(w3, bk), packing.pack_conv_dgrad_weight(w3, bk, dt)),
+        (pk.conv(w1, 1024, bk), packing.pack_conv_weight(w1, 1024, bk, dt)),
+        (pk.dgrad(w1, bk), packing.pack_conv_dgrad_weight(w1, bk, dt)),
+        (pk.deconv(wdc, bk), packing.pack_deconv4x4_weight(wdc, bk, dt)),
+        (pk.conv(wdc, 256, bk), packing.pack_conv_weight(wdc, 256, bk, dt)),
+    ]
+    pk.run()
+    torch.cuda.synchronize()
+    for i, (got, ref) in enumerate(outs):
+        assert got.shape == ref.shape, (i, got.shape, ref.shape)
+        assert torch.equal(got, ref), (i, float((got.float() - ref.float()).abs().max()))
