@@ -28,7 +28,37 @@ from . import ops, train_ops as T
 from .packing import BatchedPacker
 
 STEM_CIN_PAD = 8
+# weight gradients on a side stream, overlapping the data-gradient chain (_Grads)
+SIDE_STREAM_WGRAD = True
 HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
+
+
+class _Grads(dict):
+    """parameter -> gradient; weight gradients run on a side stream (`side`), off the
+    backward's critical path: the data-gradient chain (BN backward -> dgrad -> next layer)
+    stays on the current stream while the compute-bound weight-gradient GEMMs fill the CUs
+    the HBM-bound BatchNorm passes leave idle.  join() makes the current stream wait for them."""
+
+    def __init__(self, side):
+        super().__init__()
+        self.side = side
+
+    def wgrad(self, param, fn, *inputs):
+        if self.side is None:
+            self[param] = fn()
+            return
+        main = torch.cuda.current_stream(inputs[0].device)
+        self.side.wait_stream(main)
+        with torch.cuda.stream(self.side):
+            g = fn()
+        for t in inputs:        # read on the side stream: not reused by main-stream allocations early
+            t.record_stream(self.side)
+        g.record_stream(main)   # consumed on the main stream after join()
+        self[param] = g
+
+    def join(self, device):
+        if self.side is not None:
+            torch.cuda.current_stream(device).wait_stream(self.side)
 
 
 class _ConvBN:
@@ -67,7 +97,8 @@ class _ConvBN:
         relu_from = (sc, sh) if (self.relu and not has_res) else None
         dz, gres, dgam, dbet = T.bn_train_bwd(gy, mask_y, z, nseg, mean, rstd, self.bn.weight, want_gres=want_gres,
                                               relu_from=relu_from)
-        grads[self.conv.weight] = T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad, code)
+        grads.wgrad(self.conv.weight, lambda: T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad,
+                                                             code), dz, x)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
         dx = None
@@ -147,7 +178,7 @@ class _DeconvBN:
     def backward(self, gy, saved, nseg, code, grads):
         x, z, mean, rstd, sc, sh = saved
         dz, _, dgam, dbet = T.bn_train_bwd(gy, None, z, nseg, mean, rstd, self.bn.weight, relu_from=(sc, sh))
-        grads[self.dc.weight] = T.deconv4x4s2_wgrad(x, dz, code)
+        grads.wgrad(self.dc.weight, lambda: T.deconv4x4s2_wgrad(x, dz, code), x, dz)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
         return ops.conv2d_nhwc(dz, self.wd, self.cin, 4, 4, 2, 1, None, None, None, False, code)
@@ -168,6 +199,7 @@ class TrainPlan:
             raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
         self.head = fl
         self.packer = None
+        self.side = None
         self.njoints = fl.weight.shape[0]
         if self.njoints > HEAD_CPAD:
             raise NotImplementedError('more than %d joints' % HEAD_CPAD)
@@ -237,12 +269,15 @@ class TrainPlan:
     def backward(self, dhm, saved, nseg):
         """dL/dheatmaps (NCHW f32) -> {parameter: gradient (f32, parameter layout)}."""
         code = self.code
-        grads = {}
+        dev = dhm.device
+        if SIDE_STREAM_WGRAD and self.side is None:
+            self.side = torch.cuda.Stream(dev)
+        grads = _Grads(self.side if SIDE_STREAM_WGRAD else None)
         f = saved['head_in']
         gh = ops.pack_nchw_to_nhwc(dhm, code, HEAD_CPAD)
         fl = self.head
-        dwh = T.conv2d_wgrad(gh, f, f.shape[3], 1, 1, 1, 0, code)
-        grads[fl.weight] = dwh[:self.njoints].contiguous()
+        grads.wgrad(fl.weight, lambda: T.conv2d_wgrad(gh, f, f.shape[3], 1, 1, 1, 0, code)[:self.njoints].contiguous(),
+                    gh, f)
         if fl.bias is not None:
             grads[fl.bias] = T.channel_sum(gh)[:self.njoints].contiguous()
         g = T.conv2d_dgrad(gh, self.head_wt, f.shape[3], 1, 1, 1, 0, f.shape[1:3], code)
@@ -253,7 +288,8 @@ class TrainPlan:
             g = b.backward(g, sb, nseg, code, grads)
         g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
         self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
-        return grads
+        grads.join(dev)
+        return dict(grads)
 
 
 class _PoseResNetTrainFn(torch.autograd.Function):
