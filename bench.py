@@ -73,8 +73,6 @@ def parse():
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
                          'after autotuning -- profile runs load it so traces hold no trial launches')
-    ap.add_argument('--streams', type=int, default=1,
-                    help='split each batch into this many parts, each forward on its own stream')
     ap.add_argument('--chunks', type=int, default=1,
                     help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
@@ -295,17 +293,14 @@ def compare_with_reference(out, ref, meta, dev):
 class Replayer:
     """Network and decode+geometry stages of one input batch, captured as two hipGraphs."""
 
-    def __init__(self, plan, views, meta, groups, chunks, use_graph, dev, side_streams=()):
+    def __init__(self, plan, views, meta, groups, chunks, use_graph, dev):
         from posu import ops
         self.plan, self.views, self.meta, self.groups, self.chunks = plan, views, meta, groups, chunks
-        self.side = list(side_streams)
         self.ops = ops
         self.use_graph = use_graph
         self.dev = dev
 
     def stage_net(self):
-        if self.side:
-            return self.plan.run_streams(self.plan.pack_input(self.views), self.side)
         return self.plan.run(self.plan.pack_input(self.views), chunks=self.chunks, keep_features=False)[0]
 
     def stage_geo(self, hm):
@@ -370,9 +365,8 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
     net = build_model(args.layers, args.size, precision, dev)
     meta, _ = synthetic_meta(args.groups, dev, image_size=args.size)
     plan = net.plan(dev)
-    side = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams) - 1)]
     reps = [Replayer(plan, input_views(args.groups, args.size, rank, b, dev), meta, args.groups, args.chunks,
-                     not args.no_graph, dev, side) for b in range(nbatch)]
+                     not args.no_graph, dev) for b in range(nbatch)]
     tuned = None
     with torch.no_grad():
         for r in reps:  # eager warmup (plan packing, allocator)
@@ -382,8 +376,7 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
             if args.tune_file and os.path.exists(args.tune_file):
                 tuned = 'loaded %d layer tiles from %s' % (load_tiles(args.tune_file), args.tune_file)
             else:
-                plan.autotune(plan.pack_input(reps[0].views), chunks=args.chunks, keep_features=False, reps=8,
-                              streams=side)
+                plan.autotune(plan.pack_input(reps[0].views), chunks=args.chunks, keep_features=False, reps=8)
                 torch.cuda.synchronize()
                 tuned = 'autotuned in-run'
                 if args.tune_file:
@@ -493,7 +486,7 @@ def infer_main(args):
                                % (args.groups, args.size, args.size, args.layers),
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
-                   'hipgraph': res['use_graph'], 'chunks': args.chunks, 'streams': args.streams, 'tiles': res['tuned'] or 'heuristic',
+                   'hipgraph': res['use_graph'], 'chunks': args.chunks, 'tiles': res['tuned'] or 'heuristic',
                    'input_batches_rotated': args.batches},
         'network_ms': round(res['net_ms'], 4), 'decode_geometry_ms': round(res['geo_ms'], 4),
         'groups_per_s': round(value / 4, 2), 'per_rank_frames': [int(p[0]) for p in per_rank],

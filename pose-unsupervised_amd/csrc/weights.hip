@@ -108,6 +108,24 @@ __device__ void pack_generic(const posu_pack_job& j, long long b) {
   }
 }
 
+// LDS staging: lds[dst(i)] = src[srcoff(i)] for i < n, 8 loads in flight per thread
+template <typename SrcOff, typename DstOff>
+__device__ __forceinline__ void stage(float* lds, const float* __restrict__ src, int n, SrcOff so, DstOff dof) {
+  for (int base = threadIdx.x; base < n; base += kThreads * 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * kThreads;
+      v[u] = i < n ? src[so(i)] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = base + u * kThreads;
+      if (i < n) lds[dof(i)] = v[u];
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_job* __restrict__ jobs, int njobs) {
   __shared__ float lds[kLdsFloats];
@@ -136,7 +154,8 @@ __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_
     const int per = j.cin * ntap;
     const int r0 = static_cast<int>(b) * R;
     const int rs = max(0, min(R, j.cout - r0));  // rows that have a source
-    for (int i = tid; i < rs * per; i += kThreads) lds[i] = src[static_cast<long long>(r0) * per + i];
+    const float* __restrict__ s0 = src + static_cast<long long>(r0) * per;
+    stage(lds, s0, rs * per, [](int i) { return static_cast<long long>(i); }, [](int i) { return i; });
     __syncthreads();
     const int rr = min(R, j.rows - r0);
     for (int g = tid; g < rr * kq; g += kThreads) {
@@ -157,9 +176,11 @@ __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_
     const int str = CI * ntap + 1;  // LDS row (one co) stride, padded against bank conflicts
     const int cin_n = max(0, min(CI, j.cin - c0)), co_n = max(0, min(kTileC, j.cout - o0));
     const int run = cin_n * ntap;   // contiguous source floats per co
-    for (int i = tid; i < co_n * run; i += kThreads) {
-      const int o = i / run, x = i - o * run;
-      lds[o * str + x] = src[(static_cast<long long>(o0 + o) * j.cin + c0) * ntap + x];
+    if (run > 0) {
+      const float* __restrict__ s0 = src + (static_cast<long long>(o0) * j.cin + c0) * ntap;
+      const long long cs = static_cast<long long>(j.cin) * ntap;  // source stride between co
+      stage(lds, s0, co_n * run, [=](int i) { return (i / run) * cs + i % run; },
+            [=](int i) { return (i / run) * str + i % run; });
     }
     __syncthreads();
     const int rr = min(CI, j.rows - c0);
@@ -192,9 +213,11 @@ __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_
     const int str = kDcCo * 16 + 1;
     const int ci_n = max(0, min(kTileC, j.cin - i0)), co_n = max(0, min(kDcCo, j.cout - o0));
     const int run = co_n * 16;
-    for (int i = tid; i < ci_n * run; i += kThreads) {
-      const int c = i / run, x = i - c * run;
-      lds[c * str + x] = src[(static_cast<long long>(i0 + c) * j.cout + o0) * 16 + x];
+    if (run > 0) {
+      const float* __restrict__ s0 = src + (static_cast<long long>(i0) * j.cout + o0) * 16;
+      const long long cs = static_cast<long long>(j.cout) * 16;  // source stride between ci
+      stage(lds, s0, ci_n * run, [=](int i) { return (i / run) * cs + i % run; },
+            [=](int i) { return (i / run) * str + i % run; });
     }
     __syncthreads();
     const long long per_cls = static_cast<long long>(j.rows) * j.kpad;

@@ -365,59 +365,17 @@ class PoseResNetPlan:
     def _block_cout(blk):
         return blk.cout
 
-    def autotune(self, x, chunks=1, keep_features=True, reps=3, streams=None):
+    def autotune(self, x, chunks=1, keep_features=True, reps=3):
         """Time every admissible tile configuration of every conv launch of this forward
-        (on the packed input x; split over `streams` as run_streams does) and keep the
-        fastest per layer geometry; later runs (and hipGraph captures) use the tuned tiles."""
+        (on the packed input x) and keep the fastest per layer geometry; later runs (and
+        hipGraph captures) use the tuned tiles."""
         _Tuner.active, _Tuner.reps = True, reps
         try:
             with torch.no_grad():
-                if streams:
-                    out = self.run_streams(x, streams)
-                else:
-                    out = self.run(x, chunks=chunks, keep_features=keep_features)
+                out = self.run(x, chunks=chunks, keep_features=keep_features)
         finally:
             _Tuner.active = False
         return out
-
-    def run_streams(self, x, streams):
-        """Heatmaps only, the batch split into len(streams) + 1 equal parts, each part's whole
-        forward enqueued on its own stream (the current stream and `streams`): the parts'
-        launches are independent, so one part's kernels fill the CUs the other part's
-        kernels leave idle (ramp-up / tail of every launch).  Joins back on the current
-        stream; hipGraph-capturable (fork / join by stream waits)."""
-        cur = torch.cuda.current_stream(x.device)
-        parts = [cur] + list(streams)
-        n = x.shape[0]
-        if n % len(parts):
-            raise ValueError('batch %d does not split into %d parts' % (n, len(parts)))
-        c = n // len(parts)
-        hm = torch.empty((n, self.njoints) + self._hm_hw(x), dtype=torch.float32, device=x.device)
-        for s in parts[1:]:
-            s.wait_stream(cur)
-        for k, s in enumerate(parts):
-            with torch.cuda.stream(s):
-                sl = slice(k * c, (k + 1) * c)
-                y = self.stem_pool(x[sl])
-                for layer in self.layers:
-                    for blk in layer:
-                        y = blk(y, self.code)
-                for dc in self.deconvs[:-1]:
-                    y = dc(y, self.code)
-                self._last_deconv_head(y, False, hm_out=hm[sl])
-        for s in parts[1:]:
-            cur.wait_stream(s)
-        return hm
-
-    def _hm_hw(self, x):
-        if isinstance(x, RawViews):
-            h, w = x.h, x.w
-        elif x.shape[3] == STEM_S2D_PAD:
-            h, w = 2 * x.shape[1], 2 * x.shape[2]
-        else:
-            h, w = x.shape[1], x.shape[2]
-        up = 2 ** len(self.deconvs)
-        return (h // 32 * up, w // 32 * up)
 
     def run(self, x, chunks=1, keep_features=True):
         """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC).

@@ -62,8 +62,18 @@ def main():
             cat[category(n)] += (e - s) / 1e3
             busy += (e - s) / 1e3
     k = len(steps)
-    print('%d steps: span %.1f us per step, kernel busy %.1f us, %d launches per step'
-          % (k, span / k, busy / k, len(steps[-1])))
+    union = 0.0  # time with at least one kernel running (streams overlap)
+    for st in steps:
+        end = None
+        for s, e, _ in sorted(st):
+            if end is None or s >= end:
+                union += (e - s) / 1e3
+                end = e
+            elif e > end:
+                union += (e - end) / 1e3
+                end = e
+    print('%d steps: span %.1f us per step, kernel busy %.1f us (summed), %.1f us (union over streams), '
+          '%d launches per step' % (k, span / k, busy / k, union / k, len(steps[-1])))
     for c, v in sorted(cat.items(), key=lambda x: -x[1]):
         print('  %-18s %9.1f us' % (c, v / k))
     if a.launches:
