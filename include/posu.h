@@ -197,6 +197,17 @@ int posu_bottleneck2_fwd(int dtype, const void* x, int N, int H, int W, int C, i
                          const float* b2, const void* w3, const float* s3, const float* b3, void* y,
                          void* stream);
 
+/* Tail of an identity Bottleneck of layer3 (lib/models/pose_resnet.py:79-99, eval BN folded),
+ * PoseResNet at 256x256: conv2 3x3 + BN2 + ReLU -> conv3 1x1 + BN3 + residual + ReLU in ONE
+ * launch (the 3x3's output tile stays in LDS); conv1 runs before it on posu_conv2d_fwd.
+ * t1 [N, H, 16, 256] (conv1 output), x [N, H, 16, 1024] (block input = residual),
+ * w2 [256][2304] / w3 [1024][256] as posu_conv2d_fwd packs them, s/b folded BN (f32),
+ * y [N, H, 16, 1024].  W = 16, C = 1024, P = 256, H a multiple of 8; BF16 / F16.
+ * Bit-identical to posu_conv2d_fwd(conv2) followed by posu_conv2d_fwd(conv3, residual). */
+int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                              const void* w2, const float* s2, const float* b2, const void* w3,
+                              const float* s3, const float* b3, void* y, void* stream);
+
 int posu_bottleneck_down_fwd(int dtype, const void* x, int N, int H, int W, int C, int P,
                              const void* w1, const float* s1, const float* b1, const void* w2,
                              const float* s2, const float* b2, const void* w3d, const float* shift3,

@@ -1,0 +1,274 @@
+// Tail of the identity Bottleneck of layer3 (lib/models/pose_resnet.py:61-99, eval mode, BN
+// folded) for PoseResNet at 256x256: t1 [N, H, 16, 256] (conv1's output, BN1 + ReLU applied,
+// from the conv kernel), x [N, H, 16, 1024] the block input,
+//
+//     y = relu( bn3(conv3( relu(bn2(conv2_3x3(t1))) )) + x )
+//
+// in ONE launch: the 3x3's output tile never leaves the CU (the two separate convolutions
+// wrote t2 to HBM and read it back, and each paid its own launch ramp and tail).
+//
+// One workgroup (8 waves, one per CU) owns 8 image rows x 16 px = 128 output pixels (two per
+// image at H = 16: 256 workgroups at batch 128).  LDS:
+//   * the t1 window of its rows -- rows y0-1 .. y0+8, columns -1 .. 16 (the 3x3's zero
+//     padding, out-of-image rows / columns load as zeros) x 256 channels, staged ONCE (90 KB);
+//   * a two-slot 32 KB ring through which ONE stream of stages flows:
+//       stages 0-35   conv2, K-tile kt = tap * 4 + c: w2 [256 co][64 ci]   (tap-major K,
+//                     exactly conv_igemm's K order: bit-identical accumulators)
+//       stages 36-51  conv3, output chunk n (256 co), K-tile c: w3 [256 co][64 ci]
+//   * t2 [128 px][256 ch] written over the window once conv2 is done.
+// One barrier per stage (its DMA has landed, the other slot is free), the next stage's DMA
+// issued right after it.  Waves: pm = w & 1 the pixel half (output rows 4 pm .. 4 pm + 3 =
+// m-tiles i), cn = w >> 1 the 64-channel quarter of the 256 outputs (n-tiles j).  MFMA
+// operands swapped (A = weights, B = pixels): lane (r16, q) accumulates channels 4q .. 4q+3 of
+// pixel r16; v_permlane16_swap pairs n-tiles into 8 consecutive channels for 16-B stores.
+// 512-B pixel rows (window, t2): 16-B chunk index XOR (pixel & 15); 128-B weight rows: swz().
+#include "gemm_common.h"
+
+namespace posu {
+namespace {
+
+struct Tail3Geom {
+  const void* t1;
+  const void* x;
+  void* y;
+  const void* w2;  // [256][2304]  k = (kh * 3 + kw) * 256 + ci
+  const float* s2;
+  const float* b2;
+  const void* w3;  // [1024][256]
+  const float* s3;
+  const float* b3;
+  int N, H;
+};
+
+constexpr int kW = 16, kP = 256, kC = 1024, kRows = 8, kPx = kRows * kW;
+constexpr int kWinRows = kRows + 2, kWinCols = kW + 2, kWinPix = kWinRows * kWinCols;  // 180
+constexpr int kSlotB = 32768;
+constexpr int kWin = 0;                              // window: 180 px x 512 B = 92160 B
+constexpr int kRing = kWinPix * 512;                 // two 32 KB slots
+constexpr int kBN = kRing + 2 * kSlotB;              // s2 b2 (256 each) f32
+constexpr int kLds = kBN + 2 * kP * 4;
+static_assert(kPx * 512 <= kRing, "t2 fits over the window");
+static_assert(kLds <= 160 * 1024, "LDS");
+constexpr int kConv2Stages = 36, kStages = kConv2Stages + 16;
+
+// 512-B row (256 bf16 channels) of pixel `pix`, 16-B chunk `chunk` (0..31)
+__device__ __forceinline__ int swz32(int pix, int chunk) { return pix * 512 + ((chunk ^ (pix & 15)) << 4); }
+
+template <typename T>
+__global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
+  using O = Op<T>;
+  constexpr int ES = 2;
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int pm = wid & 1, cn = wid >> 1;
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
+  const int H = g.H;
+  const int tiles_per_img = H / kRows;
+  const int n = blockIdx.x / tiles_per_img;
+  const int y0 = (blockIdx.x - n * tiles_per_img) * kRows;
+  float* bn = reinterpret_cast<float*>(smem + kBN);
+  if (tid < kP) {
+    bn[tid] = g.s2[tid];
+    bn[kP + tid] = g.b2[tid];
+  }
+
+  const u32x4 t1s = make_srd(g.t1, g.N * H * kW * kP * ES);
+  const u32x4 w2s = make_srd(g.w2, kP * 9 * kP * ES);
+  const u32x4 w3s = make_srd(g.w3, kC * kP * ES);
+
+  // ---- the t1 window: 90 wave-instructions of 1 KB (2 pixels each), instruction m by wave m & 7
+  {
+    const int half = lane >> 5, pc = lane & 31;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+      const int m = wid + 8 * k;
+      if (m < kWinPix / 2) {  // wave-uniform
+        const int pix = 2 * m + half;
+        const int wr = pix / kWinCols, wc = pix - wr * kWinCols;
+        const int yy = y0 + wr - 1, xx = wc - 1;
+        const int lc = pc ^ (pix & 15);
+        const bool ok = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < kW;
+        dma16(t1s, ok ? (((n * H + yy) * kW + xx) * kP + 8 * lc) * ES : kOOB,
+              lds0 + kWin + static_cast<unsigned>(m) * 1024u);
+      }
+    }
+  }
+  // ---- weight stages: [256 rows][128 B], 4 DMAs per thread (rows tid >> 3 + 64 i)
+  const int cL = (tid & 7) ^ ((tid >> 4) & 7);
+  const int drow = tid >> 3;
+  auto dma_stage = [&](int u, unsigned slot) {
+    const unsigned dst = lds0 + kRing + slot + wid_u * 1024;
+    if (u < kConv2Stages) {  // w2 K-tile u: columns 64 u .. 64 u + 63 of [256][2304]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dma16(w2s, ((drow + 64 * i) * (9 * kP) + 64 * u + 8 * cL) * ES, dst + i * 8192);
+    } else {  // w3 chunk nc = (u - 36) / 4, K-tile c = (u - 36) % 4
+      const int v = u - kConv2Stages, nc = v >> 2, c = v & 3;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        dma16(w3s, ((256 * nc + drow + 64 * i) * kP + 64 * c + 8 * cL) * ES, dst + i * 8192);
+    }
+  };
+  auto slot_of = [](int s) { return static_cast<unsigned>((s & 1) * kSlotB); };
+  dma_stage(0, slot_of(0));
+
+  f32x4 acc[4][4];  // [m-tile i: output row 4 pm + i][n-tile j: channels 64 cn + 16 j + 4 q ..]
+  auto zero = [&] {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto pair = [&](int i, int jp, float* v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                       __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+      v[e] = __uint_as_float(sw[0]);
+      v[4 + e] = __uint_as_float(sw[1]);
+    }
+  };
+  const int cpair = 16 * (q & 1) + 8 * (q >> 1);  // + 32 jp: a pair's channel offset
+
+  // one 64-channel K-tile: A = weight rows 64 cn + 16 j + r16 of the slot, B = pixel rows
+  // `bpix(i)` of the 512-B-row image at `img`, channel chunks 8 kc + 4 cb + q
+  auto mma_ktile = [&](unsigned slot, const char* img, int kc, auto bpix) {
+    const char* S = smem + kRing + slot;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      uint4 a[4], b[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const uint4*>(S + swz(64 * cn + 16 * j + r16, 4 * cb + q));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const uint4*>(img + swz32(bpix(i), 8 * kc + 4 * cb + q));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) O::mma(acc[i][j], a[j], b[i]);
+    }
+  };
+
+  const T* __restrict__ xg = reinterpret_cast<const T*>(g.x);
+  T* __restrict__ yg = reinterpret_cast<T*>(g.y);
+  uint4 rv[4][2];
+  // residual chunks of output chunk nc: pixel (row 4 pm + i, col r16), channels of pair jp
+  auto res_load = [&](int nc) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const T* xr = xg + (static_cast<size_t>(n * H + y0 + 4 * pm + i) * kW + r16) * kC + 256 * nc + 64 * cn + cpair;
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) rv[i][jp] = *reinterpret_cast<const uint4*>(xr + 32 * jp);
+    }
+  };
+
+  vm_wait<0>();  // window + stage 0
+#pragma unroll 1
+  for (int u = 0; u < kStages; ++u) {
+    // younger than this stage's DMA: the previous output chunk's 8 stores
+    if (u > kConv2Stages && ((u - kConv2Stages) & 3) == 0) vm_wait<8>();
+    else vm_wait<0>();
+    lds_barrier();
+    const unsigned cur = slot_of(u), nxt = slot_of(u + 1);
+    if (u < kConv2Stages) {
+      if (u + 1 < kStages) dma_stage(u + 1, nxt);
+      if (u == 0) zero();
+      const int tap = u >> 2, kc = u & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
+      mma_ktile(cur, smem + kWin, kc, [&](int i) { return (4 * pm + i + dy) * kWinCols + r16 + dx; });
+      if (u == kConv2Stages - 1) {
+        // BN2 + ReLU -> t2 over the window (every wave is done reading it first)
+        lds_barrier();
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int c0 = 64 * cn + 32 * jp + cpair;
+          float sc[8], sh[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            sc[e] = bn[c0 + e];
+            sh[e] = bn[kP + c0 + e];
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float v[8];
+            pair(i, jp, v);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+            *reinterpret_cast<uint4*>(smem + kWin + swz32(16 * (4 * pm + i) + r16, c0 >> 3)) = O::store_vals(v);
+          }
+        }
+      }
+    } else {
+      const int v = u - kConv2Stages, nc = v >> 2, kc = v & 3;
+      if (kc == 0) {
+        res_load(nc);
+        zero();
+      }
+      if (u + 1 < kStages) dma_stage(u + 1, nxt);
+      mma_ktile(cur, smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
+      if (kc == 3) {  // BN3 + residual + ReLU -> y
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int c0 = 256 * nc + 64 * cn + 32 * jp + cpair;
+          float sc[8], sh[8];
+          const float4 sa = *reinterpret_cast<const float4*>(g.s3 + c0);
+          const float4 sb = *reinterpret_cast<const float4*>(g.s3 + c0 + 4);
+          const float4 ha = *reinterpret_cast<const float4*>(g.b3 + c0);
+          const float4 hb = *reinterpret_cast<const float4*>(g.b3 + c0 + 4);
+          sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
+          sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float vv[8], r[8];
+            pair(i, jp, vv);
+            O::load_vals(rv[i][jp], r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[e] + sh[e] + r[e], 0.f);
+            *reinterpret_cast<uint4*>(yg + (static_cast<size_t>(n * H + y0 + 4 * pm + i) * kW + r16) * kC + c0) =
+                O::store_vals(vv);
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace posu
+
+using namespace posu;
+
+extern "C" int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                                         const void* w2, const float* s2, const float* b2, const void* w3,
+                                         const float* s3, const float* b3, void* y, void* stream) {
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_bottleneck3_tail_fwd: dtype must be BF16 or F16");
+  POSU_REQUIRE(t1 && x && w2 && s2 && b2 && w3 && s3 && b3 && y, "posu_bottleneck3_tail_fwd: null pointer");
+  POSU_REQUIRE(x != y && t1 != y, "posu_bottleneck3_tail_fwd: the output must not alias an input");
+  POSU_REQUIRE(W == kW && C == kC && P == kP,
+               "posu_bottleneck3_tail_fwd: built for W = 16, C = 1024, planes = 256 (layer3 of PoseResNet at 256x256)");
+  POSU_REQUIRE(N > 0 && H > 0 && H % kRows == 0, "posu_bottleneck3_tail_fwd: H must be a positive multiple of 8");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
+               "posu_bottleneck3_tail_fwd: activation exceeds the 2 GiB addressing range");
+  for (const void* p : {t1, x, static_cast<const void*>(y), w2, w3, static_cast<const void*>(s3),
+                        static_cast<const void*>(b3)})
+    POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, "posu_bottleneck3_tail_fwd: pointers must be 16-byte aligned");
+  Tail3Geom g{};
+  g.t1 = t1;
+  g.x = x;
+  g.y = y;
+  g.w2 = w2;
+  g.s2 = s2;
+  g.b2 = b2;
+  g.w3 = w3;
+  g.s3 = s3;
+  g.b3 = b3;
+  g.N = N;
+  g.H = H;
+  const dim3 grid(static_cast<unsigned>(N * (H / kRows)));
+  hipStream_t s = as_stream(stream);
+  if (dtype == POSU_BF16)
+    hipLaunchKernelGGL(bottleneck3_tail_kernel<uint16_t>, grid, dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL(bottleneck3_tail_kernel<f16_t>, grid, dim3(512), 0, s, g);
+  return check_launch("posu_bottleneck3_tail_fwd");
+}

@@ -155,13 +155,14 @@ class _DualTail:
 
 # Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch each in bf16 / fp16 plans
 # (posu_bottleneck_fwd; the first block, with its downsample, posu_bottleneck_down_fwd), and
-# the identity Bottlenecks of layer2 (planes 128, 32-wide maps; posu_bottleneck2_fwd);
+# the identity Bottlenecks of layer2 (planes 128, 32-wide maps; posu_bottleneck2_fwd), and the
+# conv2 + conv3 tail of layer3's identity Bottlenecks (posu_bottleneck3_tail_fwd);
 # False runs the convolutions
 FUSED_BOTTLENECK = True
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -171,6 +172,7 @@ class _Block:
         self.w1f = self.w3f = None   # conv1 / conv3 packed for the fused kernel (permuted K)
         self.w3d = None              # the fused first block's [w3*s3 | wd*sd] (permuted conv3 K)
         self.l2 = False              # a layer2 identity block (fused kernel, the convs' own packs)
+        self.l3 = False              # a layer3 identity block (conv1, then the fused conv2 + conv3 tail)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -193,12 +195,19 @@ class _Block:
             self.w3f = pack_bottleneck_conv3_weight(blk.conv3.weight, ops.torch_dtype(code))
         elif code in (ops.BF16, ops.F16) and len(names) == 3:
             self.l2 = self._layer2_shape()
+            self.l3 = self._layer3_shape()
 
     def _layer2_shape(self):
         c1, c2, c3 = self.convs
         return (c1.k == 1 and c1.stride == 1 and c1.w.shape == (128, 512) and
                 c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (128, 1152) and
                 c3.k == 1 and c3.stride == 1 and c3.w.shape == (512, 128))
+
+    def _layer3_shape(self):
+        c1, c2, c3 = self.convs
+        return (c1.k == 1 and c1.stride == 1 and c1.w.shape == (256, 1024) and
+                c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (256, 2304) and
+                c3.k == 1 and c3.stride == 1 and c3.w.shape == (1024, 256))
 
     def _fusable_shape(self):
         c1, c2, c3 = self.convs
@@ -228,6 +237,10 @@ class _Block:
             c1, c2, c3 = self.convs
             return ops.bottleneck2_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, c3.w, c3.scale,
                                         c3.shift, code, out=out)
+        if self.l3 and FUSED_BOTTLENECK and x.shape[2] == 16 and x.shape[1] % 8 == 0:
+            c1, c2, c3 = self.convs
+            return ops.bottleneck3_tail_nhwc(c1(x, code), x, c2.w, c2.scale, c2.shift, c3.w, c3.scale, c3.shift, code,
+                                             out=out)
         res = self.down(x, code) if self.down is not None else x
         for c in self.convs[:-1]:
             y = c(y, code)

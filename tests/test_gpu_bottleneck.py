@@ -139,6 +139,38 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
     assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(2, 16), (1, 8), (3, 24)])
+def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
+    """Layer3's identity block tail (16-wide maps, 1024 channels, planes 256): conv2 + conv3
+    (+ residual) in one launch, bit-identical to the two unfused launches (conv_igemm's K order
+    per accumulator, same epilogue arithmetic) and within the dtype's tolerance of torch fp32."""
+    g = torch.Generator().manual_seed(71 + h)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=1024, p=256)
+    x = torch.randn(n, 1024, h, 16, generator=g)
+    dt = ops.torch_dtype(code)
+    xq = x.to(dt).float()
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    bk = ops.conv_bk(code)
+    xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 1024, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 256, bk, dt)
+    p3 = packing.pack_conv_weight(w3.to(cuda), 256, bk, dt)
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, 256, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    fused = ops.bottleneck3_tail_nhwc(t1, xd, p2, s[2], s[3], p3, s[4], s[5], code)
+    t2 = ops.conv2d_nhwc(t1, p2, 256, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    two = ops.conv2d_nhwc(t2, p3, 1024, 1, 1, 1, 0, s[4], s[5], xd, True, code)
+    torch.cuda.synchronize()
+    d = (fused.float() - two.float()).abs()
+    print('layer3 tail fused vs two launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
+    assert torch.equal(fused, two)
+    got = fused.float().cpu().permute(0, 3, 1, 2)
+    err = (got - ref).abs()
+    tol = 0.05 if code == BF16 else 0.01
+    assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
+
+
 def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 32, 256, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 256, device=cuda, dtype=torch.bfloat16)
@@ -159,6 +191,15 @@ def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
         ops.bottleneck2_nhwc(x2, w1, s2, s2, w2, s2, s2, w3, s2, s2, BF16)
     with pytest.raises(RuntimeError, match='W = 32'):
         ops.bottleneck2_nhwc(x, w1, s2, s2, w2, s2, s2, w3, s2, s2, BF16)
+    x3 = torch.zeros(1, 12, 16, 1024, device=cuda, dtype=torch.bfloat16)
+    t3 = torch.zeros(1, 12, 16, 256, device=cuda, dtype=torch.bfloat16)
+    w32 = torch.zeros(256, 2304, device=cuda, dtype=torch.bfloat16)
+    w33 = torch.zeros(1024, 256, device=cuda, dtype=torch.bfloat16)
+    s3 = torch.ones(1024, device=cuda)
+    with pytest.raises(RuntimeError, match='multiple of 8'):
+        ops.bottleneck3_tail_nhwc(t3, x3, w32, s3, s3, w33, s3, s3, BF16)
+    with pytest.raises(RuntimeError, match='W = 16'):
+        ops.bottleneck3_tail_nhwc(t3[:, :8], x2[:, :4], w32, s3, s3, w33, s3, s3, BF16)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp16'])
@@ -172,6 +213,7 @@ def test_plan_with_fused_bottlenecks_matches_unfused_plan(cuda, precision):
     assert sum(b.w3f is not None for b in plan.layers[0]) == 2   # layer1 blocks 1 and 2
     assert plan.layers[0][0].w3d is not None                     # layer1 block 0
     assert [b.l2 for b in plan.layers[1]] == [False, True, True, True]   # layer2's identity blocks
+    assert [b.l3 for b in plan.layers[2]] == [False] + [True] * 5        # layer3's identity blocks
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=12)]
     saved = P.FUSED_BOTTLENECK
     try:
