@@ -391,7 +391,9 @@ int posu_reproject(const double* M, const double* intr, const double* xy, const 
  *   [round_up(Cin,64)][round_up(KH*KW*Cout, BK)] (K order (kh, kw, co)), i.e. the
  *   forward packing of W[:, :, ::-1, ::-1].transpose(0, 1);
  *   residual: NULL or [N,H,W,Cin] added to dx; dx: [N,H,W,Cin] dtype.
- *   Cout must be a power of two >= 8 (it is the GEMM's reduction channel count). */
+ *   Cout must be a power of two >= 8 (it is the GEMM's reduction channel count).
+ *   1x1 / stride 2 / pad 0 with residual == dx: accumulated in place, dx[2i][2j] += dy[i][j] W^T,
+ *   a GEMM over dy's pixels (the other pixels keep dx) instead of over the zero-upsampled grid. */
 int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
                       int Cin, int KH, int KW, int stride, int pad, const void* residual,
                       void* dx, int H, int W, void* stream);

@@ -58,6 +58,8 @@ struct ConvGeom {
   int up;            // 1: the input is read as its zero-upsampled image u[2i] = x[i], u[odd] = 0
                      //    (data gradient of a stride-2 convolution as a stride-1 one)
   int deconv;        // blockIdx.z = parity class
+  int ostride;       // > 1: output pixel (oy, ox) is written at (ostride oy, ostride ox) of out_H x out_W
+                     //      (data gradient of a 1x1 / stride-2 convolution, accumulated in place)
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out, 2: f32 rows blocked by vblk columns
   int vblk;          // mode 2: out[(co / vblk)][m][co % vblk] (view-major heatmaps of a GEMM)
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int mt = g.deconv ? rest >> 2 : rest;
   const int m0 = mt * BM, n0 = nt * BN;
 
-  int pad_h = g.pad_h, pad_w = g.pad_w, oy_off = 0, ox_off = 0, osc = 1;
+  int pad_h = g.pad_h, pad_w = g.pad_w, oy_off = 0, ox_off = 0, osc = g.ostride > 1 ? g.ostride : 1;
   const T* __restrict__ wp = reinterpret_cast<const T*>(g.w);
   if (g.deconv) {
     const int cls = rest & 3, py = cls >> 1, px = cls & 1;
@@ -1048,7 +1050,8 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     int mt, cls, nt;
     decode(k, mt, cls, nt);
     const int m0 = mt * BM, n0 = nt * BN;
-    const int osc = g.deconv ? 2 : 1, oy_off = g.deconv ? cls >> 1 : 0, ox_off = g.deconv ? cls & 1 : 0;
+    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : 0,
+              ox_off = g.deconv ? cls & 1 : 0;
     asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int i = 0; i < (ARES ? TM : 1); ++i) {
@@ -1072,7 +1075,8 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     int mt, cls, nt;
     decode(k, mt, cls, nt);
     const int m0 = mt * BM, n0 = nt * BN;
-    const int osc = g.deconv ? 2 : 1, oy_off = g.deconv ? cls >> 1 : 0, ox_off = g.deconv ? cls & 1 : 0;
+    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : 0,
+              ox_off = g.deconv ? cls & 1 : 0;
     int cop[TP];
     float sc[TP][8], sh[TP][8];
 #pragma unroll
@@ -1534,6 +1538,25 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
   ConvGeom g = base_geom(dy, N, Ho, Wo, Cout, wt, Cin, dtype);
   g.res = residual;
   g.y = dx;
+  if (KH == 1 && KW == 1 && pad == 0 && stride == 2 && residual == dx) {
+    // 1x1 / stride 2, accumulated in place: dx[2i][2j] += dy[i][j] W^T, the other pixels keep
+    // the residual -- a GEMM over dy's pixels instead of the zero-upsampled grid (4x fewer MACs)
+    g.Ho = Ho;
+    g.Wo = Wo;
+    g.M = N * Ho * Wo;
+    g.K = Cout;
+    g.Kpad = round_up(g.K, bk_of(dtype));
+    g.KH = 1;
+    g.KW = 1;
+    g.stride = 1;
+    g.pad_h = 0;
+    g.pad_w = 0;
+    g.up = 0;
+    g.out_H = H;
+    g.out_W = W;
+    g.ostride = 2;
+    return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
+  }
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;

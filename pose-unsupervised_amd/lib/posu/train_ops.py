@@ -27,6 +27,8 @@ def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=Non
     require_cuda(dy)
     n, ho, wo, cout = dy.shape
     h, w = hw
+    if out is None and residual is not None and kh == kw == 1 and stride == 2 and pad == 0:
+        out = residual  # accumulated in place over dy's pixels (posu_conv2d_dgrad)
     if out is None:
         out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)
     call('posu_conv2d_dgrad', code, ptr(dy), n, ho, wo, cout, ptr(wt_packed), cin, kh, kw, stride, pad,

@@ -36,7 +36,8 @@ DGRAD_CASES = [
     # n, cin, h, w, cout, k, stride, pad
     (2, 64, 16, 16, 64, 3, 1, 1),
     (2, 64, 17, 15, 128, 3, 2, 1),    # strided 3x3, odd input
-    (2, 128, 16, 16, 256, 1, 2, 0),   # downsample 1x1 / s2
+    (2, 128, 16, 16, 256, 1, 2, 0),   # downsample 1x1 / s2 (with residual: in place over dy's pixels)
+    (2, 64, 15, 17, 128, 1, 2, 0),    # the same, odd input
     (3, 256, 8, 8, 64, 1, 1, 0),
     (2, 128, 8, 8, 64, 4, 2, 1),      # the deconv's data gradient is this forward conv's shape
 ]
@@ -63,6 +64,7 @@ def test_conv_dgrad_matches_autograd(cuda, case, code):
         torch.testing.assert_close(_nchw(dx_r), dx_ref + res, **FP32_TOL)
     else:
         _close_lowp(_nchw(dx), dx_ref)
+        _close_lowp(_nchw(dx_r), dx_ref + res.to(dt).float())
 
 
 WGRAD_CASES = [
