@@ -24,6 +24,12 @@
 // 512-B pixel rows (window, t2): 16-B chunk index XOR (pixel & 15); 128-B weight rows: swz().
 #include "gemm_common.h"
 
+// timing ablations (tools/tail3_ablations.sh; never set in the product build):
+//   1: no MFMAs   2: no weight DMAs (stale slots)   3: no window DMA
+#ifndef POSU_TAIL3_ABLATE
+#define POSU_TAIL3_ABLATE 0
+#endif
+
 namespace posu {
 namespace {
 
@@ -85,7 +91,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
       const int m = wid + 8 * k;
-      if (m < kWinPix / 2) {  // wave-uniform
+      if (m < kWinPix / 2 && POSU_TAIL3_ABLATE != 3) {  // wave-uniform
         const int pix = 2 * m + half;
         const int wr = pix / kWinCols, wc = pix - wr * kWinCols;
         const int yy = y0 + wr - 1, xx = wc - 1;
@@ -100,6 +106,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
   const int drow = tid >> 3;
   auto dma_stage = [&](int u, unsigned slot) {
+    if (POSU_TAIL3_ABLATE == 2) return;
     const unsigned dst = lds0 + kRing + slot + wid_u * 1024;
     if (u < kConv2Stages) {  // w2 K-tile u: columns 64 u .. 64 u + 63 of [256][2304]
 #pragma unroll
@@ -146,21 +153,32 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) O::mma(acc[i][j], a[j], b[i]);
+        for (int j = 0; j < 4; ++j) {
+          if (POSU_TAIL3_ABLATE == 1) acc[i][j][0] += __uint_as_float(a[j].x ^ b[i].y);
+          else O::mma(acc[i][j], a[j], b[i]);
+        }
     }
   };
 
-  const T* __restrict__ xg = reinterpret_cast<const T*>(g.x);
-  T* __restrict__ yg = reinterpret_cast<T*>(g.y);
+  // x / y through buffer descriptors: a wave-uniform row offset + one lane offset (no 64-bit
+  // addresses live across the loop)
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g.x), 0, g.N * H * kW * kC * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(g.y, 0, g.N * H * kW * kC * ES, 0x00020000);
+  const int lane_off = (r16 * kC + cpair) * ES;
+  // byte offset of (output row 4 pm + i, column 0, channel 256 nc + 64 cn + 32 jp), wave-uniform
+  auto row_off = [&](int i, int nc, int jp) {
+    return __builtin_amdgcn_readfirstlane(((n * H + y0 + 4 * pm + i) * kW * kC + 256 * nc + 64 * cn + 32 * jp) * ES);
+  };
   uint4 rv[4][2];
-  // residual chunks of output chunk nc: pixel (row 4 pm + i, col r16), channels of pair jp
   auto res_load = [&](int nc) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const T* xr = xg + (static_cast<size_t>(n * H + y0 + 4 * pm + i) * kW + r16) * kC + 256 * nc + 64 * cn + cpair;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jp = 0; jp < 2; ++jp) rv[i][jp] = *reinterpret_cast<const uint4*>(xr + 32 * jp);
-    }
+      for (int jp = 0; jp < 2; ++jp) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_off, row_off(i, nc, jp), 0);
+        rv[i][jp] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
   };
 
   vm_wait<0>();  // window + stage 0
@@ -200,10 +218,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
       }
     } else {
       const int v = u - kConv2Stages, nc = v >> 2, kc = v & 3;
-      if (kc == 0) {
-        res_load(nc);
-        zero();
-      }
+      if (kc == 0) zero();
+      // the residual a stage ahead of its epilogue (loaded earlier, rv spills); the next
+      // stage's vm_wait<0> then retires it with this stage's DMA
+      if (kc == 2) res_load(nc);
       if (u + 1 < kStages) dma_stage(u + 1, nxt);
       mma_ktile(cur, smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
       if (kc == 3) {  // BN3 + residual + ReLU -> y
@@ -224,8 +242,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
             O::load_vals(rv[i][jp], r);
 #pragma unroll
             for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[e] + sh[e] + r[e], 0.f);
-            *reinterpret_cast<uint4*>(yg + (static_cast<size_t>(n * H + y0 + 4 * pm + i) * kW + r16) * kC + c0) =
-                O::store_vals(vv);
+            const uint4 u = O::store_vals(vv);
+            __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){u.x, u.y, u.z, u.w},
+                                                   yrs, lane_off, row_off(i, nc, jp), 0);
           }
         }
       }
