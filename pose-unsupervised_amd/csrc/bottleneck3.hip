@@ -25,7 +25,8 @@
 #include "gemm_common.h"
 
 // timing ablations (tools/tail3_ablations.sh; never set in the product build):
-//   1: no MFMAs   2: no weight DMAs (stale slots)   3: no window DMA
+//   1: no MFMAs   2: no weight DMAs (stale slots)   3: no window DMA   4: no fragment LDS reads
+//   5: no MFMAs and no weight DMAs   6: no epilogues (no t2 / y writes)
 #ifndef POSU_TAIL3_ABLATE
 #define POSU_TAIL3_ABLATE 0
 #endif
@@ -53,9 +54,17 @@ constexpr int kWin = 0;                              // window: 180 px x 512 B =
 constexpr int kRing = kWinPix * 512;                 // two 32 KB slots
 constexpr int kBN = kRing + 2 * kSlotB;              // s2 b2 (256 each) f32
 constexpr int kLds = kBN + 2 * kP * 4;
-static_assert(kPx * 512 <= kRing, "t2 fits over the window");
+constexpr int kS3 = kWin + kPx * 512;             // s3 b3 (1024 each) f32, over the window after conv2
+static_assert(kS3 + 2 * kC * 4 <= kRing, "t2 and BN3 fit over the window");
 static_assert(kLds <= 160 * 1024, "LDS");
 constexpr int kConv2Stages = 36, kStages = kConv2Stages + 16;
+
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
 // 512-B row (256 bf16 channels) of pixel `pix`, 16-B chunk `chunk` (0..31)
 __device__ __forceinline__ int swz32(int pix, int chunk) { return pix * 512 + ((chunk ^ (pix & 15)) << 4); }
@@ -106,7 +115,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
   const int drow = tid >> 3;
   auto dma_stage = [&](int u, unsigned slot) {
-    if (POSU_TAIL3_ABLATE == 2) return;
+    if (POSU_TAIL3_ABLATE == 2 || POSU_TAIL3_ABLATE == 5) return;
     const unsigned dst = lds0 + kRing + slot + wid_u * 1024;
     if (u < kConv2Stages) {  // w2 K-tile u: columns 64 u .. 64 u + 63 of [256][2304]
 #pragma unroll
@@ -147,24 +156,30 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
     for (int cb = 0; cb < 2; ++cb) {
       uint4 a[4], b[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = *reinterpret_cast<const uint4*>(S + swz(64 * cn + 16 * j + r16, 4 * cb + q));
+      for (int j = 0; j < 4; ++j)
+        a[j] = POSU_TAIL3_ABLATE == 4 ? make_uint4(lane, j, cb, kc)
+                                      : *reinterpret_cast<const uint4*>(S + swz(64 * cn + 16 * j + r16, 4 * cb + q));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) b[i] = *reinterpret_cast<const uint4*>(img + swz32(bpix(i), 8 * kc + 4 * cb + q));
+      for (int i = 0; i < 4; ++i)
+        b[i] = POSU_TAIL3_ABLATE == 4 ? make_uint4(i, lane, kc, cb)
+                                      : *reinterpret_cast<const uint4*>(img + swz32(bpix(i), 8 * kc + 4 * cb + q));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          if (POSU_TAIL3_ABLATE == 1) acc[i][j][0] += __uint_as_float(a[j].x ^ b[i].y);
+          if (POSU_TAIL3_ABLATE == 1 || POSU_TAIL3_ABLATE == 5) acc[i][j][0] += __uint_as_float(a[j].x ^ b[i].y);
           else O::mma(acc[i][j], a[j], b[i]);
         }
     }
   };
 
-  // x / y through buffer descriptors: a wave-uniform row offset + one lane offset (no 64-bit
+  // x through a buffer descriptor: a wave-uniform row offset + one lane offset (no 64-bit
   // addresses live across the loop)
   const __amdgpu_buffer_rsrc_t xrs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(g.x), 0, g.N * H * kW * kC * ES, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(g.y, 0, g.N * H * kW * kC * ES, 0x00020000);
+  // y: plain global stores at a 32-bit offset from this workgroup's first output row (a raw
+  // buffer store with the row in soffset corrupted a few elements per launch; not understood)
+  char* const ywg = static_cast<char*>(g.y) + static_cast<size_t>(n * H + y0) * kW * kC * ES;
   const int lane_off = (r16 * kC + cpair) * ES;
   // byte offset of (output row 4 pm + i, column 0, channel 256 nc + 64 cn + 32 jp), wave-uniform
   auto row_off = [&](int i, int nc, int jp) {
@@ -182,73 +197,80 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
   };
 
   vm_wait<0>();  // window + stage 0
+  // ---- conv2: stages 0 .. 35 (tap-major K-tiles over the window)
 #pragma unroll 1
-  for (int u = 0; u < kStages; ++u) {
-    // younger than this stage's DMA: the previous output chunk's 8 stores
-    if (u > kConv2Stages && ((u - kConv2Stages) & 3) == 0) vm_wait<8>();
-    else vm_wait<0>();
+  for (int u = 0; u < kConv2Stages; ++u) {
+    vm_wait<0>();
     lds_barrier();
-    const unsigned cur = slot_of(u), nxt = slot_of(u + 1);
-    if (u < kConv2Stages) {
-      if (u + 1 < kStages) dma_stage(u + 1, nxt);
-      if (u == 0) zero();
-      const int tap = u >> 2, kc = u & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
-      mma_ktile(cur, smem + kWin, kc, [&](int i) { return (4 * pm + i + dy) * kWinCols + r16 + dx; });
-      if (u == kConv2Stages - 1) {
-        // BN2 + ReLU -> t2 over the window (every wave is done reading it first)
-        lds_barrier();
+    dma_stage(u + 1, slot_of(u + 1));
+    if (u == 0) zero();
+    const int tap = u >> 2, kc = u & 3, dy = tap / 3, dx = tap - 3 * (tap / 3);
+    mma_ktile(slot_of(u), smem + kWin, kc, [&](int i) { return (4 * pm + i + dy) * kWinCols + r16 + dx; });
+  }
+  // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 parameters
+  // beside it
+  lds_barrier();
+  if (POSU_TAIL3_ABLATE != 6) {
+    float* b3l = reinterpret_cast<float*>(smem + kS3);
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const int c0 = 64 * cn + 32 * jp + cpair;
-          float sc[8], sh[8];
+    for (int e = 0; e < 2; ++e) {
+      b3l[2 * tid + e] = g.s3[2 * tid + e];
+      b3l[kC + 2 * tid + e] = g.b3[2 * tid + e];
+    }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            sc[e] = bn[c0 + e];
-            sh[e] = bn[kP + c0 + e];
-          }
+    for (int jp = 0; jp < 2; ++jp) {
+      const int c0 = 64 * cn + 32 * jp + cpair;
+      float sc[8], sh[8];
+      ld8(bn + c0, sc);
+      ld8(bn + kP + c0, sh);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float v[8];
-            pair(i, jp, v);
+      for (int i = 0; i < 4; ++i) {
+        float v[8];
+        pair(i, jp, v);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
-            *reinterpret_cast<uint4*>(smem + kWin + swz32(16 * (4 * pm + i) + r16, c0 >> 3)) = O::store_vals(v);
-          }
-        }
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+        *reinterpret_cast<uint4*>(smem + kWin + swz32(16 * (4 * pm + i) + r16, c0 >> 3)) = O::store_vals(v);
       }
-    } else {
-      const int v = u - kConv2Stages, nc = v >> 2, kc = v & 3;
+    }
+  }
+  // ---- conv3: output chunk nc (256 channels), K-tiles kc = 0 .. 3 of t2; stage u = 36 + 4 nc + kc
+#pragma unroll 1
+  for (int nc = 0; nc < 4; ++nc) {
+#pragma unroll 1
+    for (int kc = 0; kc < 4; ++kc) {
+      const int u = kConv2Stages + 4 * nc + kc;
+      // the chunk's residual loads (issued at kc == 1, after that stage's DMA) are the 8
+      // youngest vector-memory ops at kc == 2: its DMA is waited for without them
+      if (kc == 2) vm_wait<8>();
+      else vm_wait<0>();
+      lds_barrier();
       if (kc == 0) zero();
-      // the residual a stage ahead of its epilogue (loaded earlier, rv spills); the next
-      // stage's vm_wait<0> then retires it with this stage's DMA
-      if (kc == 2) res_load(nc);
-      if (u + 1 < kStages) dma_stage(u + 1, nxt);
-      mma_ktile(cur, smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
-      if (kc == 3) {  // BN3 + residual + ReLU -> y
+      // the last stage of a chunk issues the next stage's DMA after its y stores: the next
+      // stage's wait then covers both together instead of stalling a later stage behind them
+      if (kc != 3) dma_stage(u + 1, slot_of(u + 1));
+      if (kc == 1) res_load(nc);  // two stages ahead of the epilogue
+      mma_ktile(slot_of(u), smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
+    }
+    if (POSU_TAIL3_ABLATE != 6) {  // BN3 + residual + ReLU -> y
 #pragma unroll
-        for (int jp = 0; jp < 2; ++jp) {
-          const int c0 = 256 * nc + 64 * cn + 32 * jp + cpair;
-          float sc[8], sh[8];
-          const float4 sa = *reinterpret_cast<const float4*>(g.s3 + c0);
-          const float4 sb = *reinterpret_cast<const float4*>(g.s3 + c0 + 4);
-          const float4 ha = *reinterpret_cast<const float4*>(g.b3 + c0);
-          const float4 hb = *reinterpret_cast<const float4*>(g.b3 + c0 + 4);
-          sc[0] = sa.x; sc[1] = sa.y; sc[2] = sa.z; sc[3] = sa.w; sc[4] = sb.x; sc[5] = sb.y; sc[6] = sb.z; sc[7] = sb.w;
-          sh[0] = ha.x; sh[1] = ha.y; sh[2] = ha.z; sh[3] = ha.w; sh[4] = hb.x; sh[5] = hb.y; sh[6] = hb.z; sh[7] = hb.w;
+      for (int jp = 0; jp < 2; ++jp) {
+        const int c0 = 256 * nc + 64 * cn + 32 * jp + cpair;
+        float sc[8], sh[8];
+        const float* b3l = reinterpret_cast<const float*>(smem + kS3);
+        ld8(b3l + c0, sc);
+        ld8(b3l + kC + c0, sh);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float vv[8], r[8];
-            pair(i, jp, vv);
-            O::load_vals(rv[i][jp], r);
+        for (int i = 0; i < 4; ++i) {
+          float vv[8], r[8];
+          pair(i, jp, vv);
+          O::load_vals(rv[i][jp], r);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[e] + sh[e] + r[e], 0.f);
-            const uint4 u = O::store_vals(vv);
-            __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){u.x, u.y, u.z, u.w},
-                                                   yrs, lane_off, row_off(i, nc, jp), 0);
-          }
+          for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[e] + sh[e] + r[e], 0.f);
+          *reinterpret_cast<uint4*>(ywg + ((16 * (4 * pm + i) + r16) * kC + c0) * ES) = O::store_vals(vv);
         }
       }
     }
+    if (nc < 3) dma_stage(kConv2Stages + 4 * nc + 4, slot_of(kConv2Stages + 4 * nc + 4));
   }
 }
 
