@@ -159,6 +159,7 @@ class _DualTail:
 # conv2 + conv3 tail of layer3's identity Bottlenecks (posu_bottleneck3_tail_fwd);
 # False runs the convolutions
 FUSED_BOTTLENECK = True
+FUSED_LAYER3_TAIL = True
 
 
 class _Block:
@@ -237,7 +238,7 @@ class _Block:
             c1, c2, c3 = self.convs
             return ops.bottleneck2_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, c3.w, c3.scale,
                                         c3.shift, code, out=out)
-        if self.l3 and FUSED_BOTTLENECK and x.shape[2] == 16 and x.shape[1] % 8 == 0:
+        if self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and x.shape[2] == 16 and x.shape[1] % 8 == 0:
             c1, c2, c3 = self.convs
             return ops.bottleneck3_tail_nhwc(c1(x, code), x, c2.w, c2.scale, c2.shift, c3.w, c3.scale, c3.shift, code,
                                              out=out)
