@@ -252,23 +252,27 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
       mma_ktile(slot_of(u), smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
     }
     if (POSU_TAIL3_ABLATE != 6) {  // BN3 + residual + ReLU -> y
+      // pixel-major: the two 16-B stores of a pixel's two pairs (one 128-B line of y with the
+      // other q-lanes) are issued back to back, so L2 sees whole lines
+      float sc[2][8], sh[2][8];
+      const float* b3l = reinterpret_cast<const float*>(smem + kS3);
 #pragma unroll
       for (int jp = 0; jp < 2; ++jp) {
-        const int c0 = 256 * nc + 64 * cn + 32 * jp + cpair;
-        float sc[8], sh[8];
-        const float* b3l = reinterpret_cast<const float*>(smem + kS3);
-        ld8(b3l + c0, sc);
-        ld8(b3l + kC + c0, sh);
+        ld8(b3l + 256 * nc + 64 * cn + 32 * jp + cpair, sc[jp]);
+        ld8(b3l + kC + 256 * nc + 64 * cn + 32 * jp + cpair, sh[jp]);
+      }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jp = 0; jp < 2; ++jp) {
+          const int c0 = 256 * nc + 64 * cn + 32 * jp + cpair;
           float vv[8], r[8];
           pair(i, jp, vv);
           O::load_vals(rv[i][jp], r);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[e] + sh[e] + r[e], 0.f);
+          for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[jp][e] + sh[jp][e] + r[e], 0.f);
           *reinterpret_cast<uint4*>(ywg + ((16 * (4 * pm + i) + r16) * kC + c0) * ES) = O::store_vals(vv);
         }
-      }
     }
     if (nc < 3) dma_stage(kConv2Stages + 4 * nc + 4, slot_of(kConv2Stages + 4 * nc + 4));
   }
