@@ -69,6 +69,8 @@ def parse():
     ap.add_argument('--size', type=int, default=256)
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
+                    help="train mode: torch.optim.Adam's fused kernel (default) or its foreach launches")
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
@@ -534,7 +536,10 @@ def train_main(args):
     weight = torch.ones(nb, 16, 1, device=dev)
     mse = JointsMSELoss(use_target_weight=True)
     fund = FundamentalLoss(cfg, fundamental_matrix_dict=syn.fundamental_dict(), device=dev)
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3)
+    # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
+    # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
+    # launches (same math): 26.3 -> 22.8 ms per step measured A/B
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
     subj = meta.subj
 
     def step():
@@ -585,7 +590,8 @@ def train_main(args):
                                    'JointsMSE + FundamentalLoss, Adam) (BASELINE configs[3])'
                                    % (nb, args.size, args.size, args.layers),
                        'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
-                       'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce)' % world},
+                       'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce)' % world,
+                       'optimizer': 'Adam lr 1e-3 (%s)' % args.adam},
             'per_rank_frames': [int(p[0]) for p in per_rank],
             'loss': round(float(loss), 5), 'roofline': roof, 'cpu_baseline': None,
         }

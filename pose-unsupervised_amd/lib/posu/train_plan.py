@@ -257,9 +257,11 @@ class TrainPlan:
             saved['deconvs'].append(sd)
         saved['head_in'] = y
         hm = ops.head1x1_nchw(y, self.head_w, self.njoints, self.head_b, code)
-        for bn in self._bns():
-            if bn.num_batches_tracked is not None:
-                bn.num_batches_tracked.add_(nseg)
+        # num_batches_tracked += nseg for every BatchNorm (the reference's V backbone calls
+        # each add 1): one multi-tensor launch instead of one tiny kernel per layer
+        nbt = [bn.num_batches_tracked for bn in self._bns() if bn.num_batches_tracked is not None]
+        if nbt:
+            torch._foreach_add_(nbt, nseg)
         return hm, x1, y, saved
 
     def _bns(self):
