@@ -398,16 +398,6 @@ int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout
                       int Cin, int KH, int KW, int stride, int pad, const void* residual,
                       void* dx, int H, int W, void* stream);
 
-/* One parity class (py, px) of the data gradient of a 3x3 / stride-2 / pad-1 convolution
- * (pose_resnet.py:47-52 / 136-141 strided layers under autograd): dx[2a+py][2b+px] = sum over
- * the class's KHxKW taps (1x1, 1x2, 2x1 or 2x2) of dy[a+ty][b+tx] W_class[ty][tx]^T, as a
- * stride-1 convolution over dy without padding, written interleaved into dx [N,2Hd,2Wd,Cin].
- * The four classes cover dx exactly once: 9/4 taps per pixel instead of posu_conv2d_dgrad's 9
- * over the zero-upsampled grid.  wt: packed like posu_conv2d_dgrad's weight for the class's
- * taps (k = (ty*KW + tx)*Cout + co). */
-int posu_conv2d_dgrad_class(int dtype, const void* dy, int N, int Hd, int Wd, int Cout, const void* wt,
-                            int Cin, int KH, int KW, int py, int px, void* dx, int H, int W, void* stream);
-
 /* Weight gradient dW[Cout][Creal][KH][KW] (f32, the nn.Conv2d weight layout) of a
  * conv over x[N,H,W,C] (C >= Creal, padded channels ignored) with output gradient
  * dy[N,Ho,Wo,Cout].  Also ConvTranspose2d(4, s2, p1): pass x = the transposed

@@ -58,9 +58,8 @@ struct ConvGeom {
   int up;            // 1: the input is read as its zero-upsampled image u[2i] = x[i], u[odd] = 0
                      //    (data gradient of a stride-2 convolution as a stride-1 one)
   int deconv;        // blockIdx.z = parity class
-  int ostride;       // > 1: output pixel (oy, ox) is written at (ostride oy + oy0, ostride ox + ox0) of
-  int oy0, ox0;      //      out_H x out_W (data gradients of stride-2 convolutions: the 1x1 one
-                     //      accumulated in place, the 3x3 one as four parity-class convolutions)
+  int ostride;       // > 1: output pixel (oy, ox) is written at (ostride oy, ostride ox) of out_H x out_W
+                     //      (data gradient of a 1x1 / stride-2 convolution, accumulated in place)
   int out_H, out_W;  // output tensor spatial dims
   int mode;          // 0: NHWC out (dtype), 1: NCHW f32 out, 2: f32 rows blocked by vblk columns
   int vblk;          // mode 2: out[(co / vblk)][m][co % vblk] (view-major heatmaps of a GEMM)
@@ -133,7 +132,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int mt = g.deconv ? rest >> 2 : rest;
   const int m0 = mt * BM, n0 = nt * BN;
 
-  int pad_h = g.pad_h, pad_w = g.pad_w, oy_off = g.oy0, ox_off = g.ox0, osc = g.ostride > 1 ? g.ostride : 1;
+  int pad_h = g.pad_h, pad_w = g.pad_w, oy_off = 0, ox_off = 0, osc = g.ostride > 1 ? g.ostride : 1;
   const T* __restrict__ wp = reinterpret_cast<const T*>(g.w);
   if (g.deconv) {
     const int cls = rest & 3, py = cls >> 1, px = cls & 1;
@@ -1051,8 +1050,8 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     int mt, cls, nt;
     decode(k, mt, cls, nt);
     const int m0 = mt * BM, n0 = nt * BN;
-    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : g.oy0,
-              ox_off = g.deconv ? cls & 1 : g.ox0;
+    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : 0,
+              ox_off = g.deconv ? cls & 1 : 0;
     asm volatile("s_nop 4" ::: "memory");
 #pragma unroll
     for (int i = 0; i < (ARES ? TM : 1); ++i) {
@@ -1076,8 +1075,8 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
     int mt, cls, nt;
     decode(k, mt, cls, nt);
     const int m0 = mt * BM, n0 = nt * BN;
-    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : g.oy0,
-              ox_off = g.deconv ? cls & 1 : g.ox0;
+    const int osc = g.deconv ? 2 : (g.ostride > 1 ? g.ostride : 1), oy_off = g.deconv ? cls >> 1 : 0,
+              ox_off = g.deconv ? cls & 1 : 0;
     int cop[TP];
     float sc[TP][8], sh[TP][8];
 #pragma unroll
@@ -1572,39 +1571,6 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
   g.out_H = H;
   g.out_W = W;
   return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
-}
-
-// One parity class of the data gradient of a 3x3 / stride-2 / pad-1 convolution (or any
-// stride-1 window over dy whose outputs interleave): a KHxKW stride-1 convolution over
-// dy [N,Hd,Wd,Cout] with no padding (taps past the edge read zeros) whose output pixel (a, b)
-// is written at (2a + py, 2b + px) of dx [N,H,W,Cin].  wt: the class's taps packed as
-// posu_conv2d_dgrad's weight (k = (ty*KW + tx)*Cout + co).
-extern "C" int posu_conv2d_dgrad_class(int dtype, const void* dy, int N, int Hd, int Wd, int Cout, const void* wt,
-                                       int Cin, int KH, int KW, int py, int px, void* dx, int H, int W, void* stream) {
-  if (int st = common_checks(dtype, dy, wt, dx, N, Hd, Wd, Cout, Cin, "posu_conv2d_dgrad_class")) return st;
-  POSU_REQUIRE(Cin % (16 / esz_of(dtype)) == 0, "posu_conv2d_dgrad_class: Cin must be a multiple of 16 bytes");
-  POSU_REQUIRE(KH >= 1 && KH <= 2 && KW >= 1 && KW <= 2 && (py == 0 || py == 1) && (px == 0 || px == 1),
-               "posu_conv2d_dgrad_class: KH, KW in {1, 2}, parity (py, px) in {0, 1}");
-  POSU_REQUIRE(H == 2 * Hd && W == 2 * Wd, "posu_conv2d_dgrad_class: dx must be exactly twice dy's size");
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * Cin < (1LL << 31), "posu_conv2d_dgrad_class: output too large");
-  ConvGeom g = base_geom(dy, N, Hd, Wd, Cout, wt, Cin, dtype);
-  g.y = dx;
-  g.Ho = Hd;
-  g.Wo = Wd;
-  g.M = N * Hd * Wd;
-  g.K = KH * KW * Cout;
-  g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = KH;
-  g.KW = KW;
-  g.stride = 1;
-  g.pad_h = 0;
-  g.pad_w = 0;
-  g.out_H = H;
-  g.out_W = W;
-  g.ostride = 2;
-  g.oy0 = py;
-  g.ox0 = px;
-  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad_class");
 }
 
 // Plain GEMM on the conv kernel (1x1 window over M "pixels" of K channels):

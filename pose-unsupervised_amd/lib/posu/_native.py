@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 8
+ABI_VERSION = 7
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -68,7 +68,6 @@ _SIGNATURES = {
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
-    'posu_conv2d_dgrad_class': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_conv2d_wgrad_workspace': [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i],
     'posu_conv2d_wgrad': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _ll, _p],
     'posu_bn_workspace': [_i, _i],

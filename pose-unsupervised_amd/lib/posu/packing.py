@@ -158,26 +158,6 @@ def pack_conv_dgrad_weight(w, bk, dtype):
     return pack_conv_weight(wt, wt.shape[1], bk, dtype)
 
 
-# taps of a 3x3 / stride-2 / pad-1 kernel row (or column) that reach output parity 0 / 1, in the
-# order of the class window (dy rows a, a + 1): dx[2a] = dy[a] W[1]; dx[2a+1] = dy[a] W[2] + dy[a+1] W[0]
-S2_CLASS_TAPS = ([1], [2, 0])
-
-
-def pack_dgrad_s2_classes(w, bk, dtype):
-    """The four parity-class data-gradient weights of a 3x3 / stride-2 / pad-1 Conv2d
-    [Cout, Cin, 3, 3] (posu_conv2d_dgrad_class): [(wt, KH, KW, py, px)], wt packed like
-    pack_conv_dgrad_weight for the class's taps."""
-    wf = w.detach().float()
-    out = []
-    for py in (0, 1):
-        for px in (0, 1):
-            rows, cols = S2_CLASS_TAPS[py], S2_CLASS_TAPS[px]
-            sub = wf[:, :, rows][:, :, :, cols]                 # [Cout, Cin, KH, KW]
-            wt = sub.transpose(0, 1).contiguous()               # [Cin, Cout, KH, KW]
-            out.append((pack_conv_weight(wt, wt.shape[1], bk, dtype), len(rows), len(cols), py, px))
-    return out
-
-
 # ---- batched packing (posu_pack_weights): every weight of a training step in one launch
 PACK_CONV, PACK_DGRAD, PACK_DECONV = 0, 1, 2
 _JOB = np.dtype([('src', '<u8'), ('dst', '<u8'), ('block_start', '<i8'), ('mode', '<i4'), ('cout', '<i4'),

@@ -36,21 +36,6 @@ def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=Non
     return out
 
 
-def conv2d_dgrad_s2_classes(dy, classes, cin, hw, code, out=None):
-    """dx [N, H, W, cin] of a 3x3 / stride-2 / pad-1 conv x -> dy (H = 2 Hd, W = 2 Wd) as its four
-    parity-class convolutions over dy (packing.pack_dgrad_s2_classes), each writing its
-    interleaved quarter of dx."""
-    require_cuda(dy)
-    n, hd, wd, cout = dy.shape
-    h, w = hw
-    if out is None:
-        out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)
-    for wt, kh, kw, py, px in classes:
-        call('posu_conv2d_dgrad_class', code, ptr(dy), n, hd, wd, cout, ptr(wt), cin, kh, kw, py, px, ptr(out), h, w,
-             stream_of(dy.device))
-    return out
-
-
 def conv2d_wgrad(dy, x, creal, kh, kw, stride, pad, code, out=None):
     """dW [Cout, creal, kh, kw] f32 of a conv over x [N, H, W, C >= creal] with output grad dy."""
     require_cuda(dy, x)

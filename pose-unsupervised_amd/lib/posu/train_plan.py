@@ -25,7 +25,7 @@ once (packing.BatchedPacker) -- and their gradients come back f32 in the modules
 import torch
 
 from . import ops, train_ops as T
-from .packing import BatchedPacker, pack_dgrad_s2_classes
+from .packing import BatchedPacker
 
 STEM_CIN_PAD = 8
 # weight gradients on a side stream, overlapping the data-gradient chain (_Grads)
@@ -102,13 +102,7 @@ class _ConvBN:
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
         dx = None
-        if need_dx and dx_residual is None and self.k == 3 and self.stride == 2 and self.pad == 1 and \
-                x.shape[1] == 2 * dz.shape[1] and x.shape[2] == 2 * dz.shape[2]:
-            # four parity-class convolutions over dz (9/4 taps per dx pixel instead of 9 over the
-            # zero-upsampled grid); the class weights come from the parameter's current values
-            classes = pack_dgrad_s2_classes(self.conv.weight, ops.conv_bk(code), ops.torch_dtype(code))
-            dx = T.conv2d_dgrad_s2_classes(dz, classes, self.cin, x.shape[1:3], code)
-        elif need_dx:
+        if need_dx:
             dx = T.conv2d_dgrad(dz, self.wt, self.cin, self.k, self.k, self.stride, self.pad, x.shape[1:3], code,
                                 residual=dx_residual)
         return dx, gres

@@ -67,32 +67,6 @@ def test_conv_dgrad_matches_autograd(cuda, case, code):
         _close_lowp(_nchw(dx_r), dx_ref + res.to(dt).float())
 
 
-@pytest.mark.parametrize('n,cin,h,w,cout', [(2, 64, 16, 16, 128), (1, 128, 8, 12, 256)])
-@pytest.mark.parametrize('code', [F32, BF16])
-def test_conv_dgrad_s2_parity_classes_match_autograd(cuda, n, cin, h, w, cout, code):
-    """The 3x3 / stride-2 / pad-1 data gradient as four parity-class convolutions over dy
-    (posu_conv2d_dgrad_class) against torch autograd and against the zero-upsampled path."""
-    g = torch.Generator().manual_seed(13)
-    x = torch.randn(n, cin, h, w, generator=g, requires_grad=True)
-    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
-    y = F.conv2d(x, wt, stride=2, padding=1)
-    dy = torch.randn_like(y)
-    (dx_ref,) = torch.autograd.grad(y, x, dy)
-    dt, bk = ops.torch_dtype(code), ops.conv_bk(code)
-    classes = packing.pack_dgrad_s2_classes(wt.to(cuda), bk, dt)
-    dyd = _nhwc(dy, cuda, dt)
-    dx = T.conv2d_dgrad_s2_classes(dyd, classes, cin, (h, w), code)
-    wpk = packing.pack_conv_dgrad_weight(wt.to(cuda), bk, dt)
-    dx_up = T.conv2d_dgrad(dyd, wpk, cin, 3, 3, 2, 1, (h, w), code)
-    torch.cuda.synchronize()
-    if code == F32:
-        torch.testing.assert_close(_nchw(dx), dx_ref, **FP32_TOL)
-    else:
-        _close_lowp(_nchw(dx), dx_ref)
-    # the same taps in the same K order per output pixel as the upsampled grid minus its zero taps
-    torch.testing.assert_close(dx.float(), dx_up.float(), atol=1e-2 if code != F32 else 1e-5, rtol=1e-2)
-
-
 WGRAD_CASES = [
     # n, cin, cin_pad, h, w, cout, k, stride, pad
     (2, 3, 8, 32, 30, 64, 7, 2, 3),      # direct stem (channels padded to 8)
