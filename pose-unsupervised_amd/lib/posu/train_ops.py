@@ -10,6 +10,9 @@ from . import _native as nat
 from ._native import call, ptr, stream_of, require_cuda
 
 _WS = {}
+# 1x1 / stride-2 data gradients accumulated in place over dy's pixels (22.62 vs 23.02 ms per
+# training step A/B); False runs them over the zero-upsampled grid
+INPLACE_S2_DGRAD = True
 
 
 def workspace(device, nbytes, slot='default'):
@@ -27,7 +30,7 @@ def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=Non
     require_cuda(dy)
     n, ho, wo, cout = dy.shape
     h, w = hw
-    if out is None and residual is not None and kh == kw == 1 and stride == 2 and pad == 0:
+    if INPLACE_S2_DGRAD and out is None and residual is not None and kh == kw == 1 and stride == 2 and pad == 0:
         out = residual  # accumulated in place over dy's pixels (posu_conv2d_dgrad)
     if out is None:
         out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)
