@@ -310,6 +310,12 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// blocks per weight-gradient launch (tiles x pixel splits): one per CU.  Every block writes an
+// f32 partial tile, so more blocks cost partial traffic (2 x 67 MB at 1024 blocks); measured
+// per training step (weight gradients on the side stream): 128 blocks 23.06 ms, 192 22.21,
+// 256 21.97, 384 22.03, 512 22.12, 1024 22.76, 2048 23.69
+constexpr int kWgradBlocks = 256;
+
 template <typename T, int BM, int BN>
 void launch_wgrad(WgradGeom& g, hipStream_t s) {
   constexpr int ES = static_cast<int>(sizeof(T));
@@ -320,7 +326,7 @@ void launch_wgrad(WgradGeom& g, hipStream_t s) {
   g.Npad = g.ntiles * BN;
   const int tiles = g.mtiles * g.ntiles;
   const int pst = (g.P + BP - 1) / BP;
-  int splits = (1024 + tiles - 1) / tiles;
+  int splits = (kWgradBlocks + tiles - 1) / tiles;
   splits = std::max(1, std::min(splits, pst));
   const int stages_per_split = (pst + splits - 1) / splits;
   g.pps = stages_per_split * BP;
@@ -340,10 +346,10 @@ int wgrad_part_floats(int dtype, int M, int K, int P) {
   const int BM = M <= 64 ? 64 : 128;
   const long long mp = static_cast<long long>((M + BM - 1) / BM) * BM;
   const long long np = static_cast<long long>((K + 127) / 128) * 128;
-  // splits <= ceil(1024 / tiles) + 1: the partial buffer bound below is what the
+  // splits <= ceil(kWgradBlocks / tiles) + 1: the partial buffer bound below is what the
   // launcher can use
   const long long tiles = (mp / BM) * (np / 128);
-  const long long splits = (1024 + tiles - 1) / tiles + 1;
+  const long long splits = (kWgradBlocks + tiles - 1) / tiles + 1;
   const long long n = splits * mp * np;
   return n > (1LL << 31) - 1 ? -1 : static_cast<int>(n);
 }
