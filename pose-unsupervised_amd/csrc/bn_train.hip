@@ -29,7 +29,9 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
   r.CB = std::min(r.CPR, 64);  // one wave of channel chunks per pixel row: wide layers get more blocks
   r.PL = 256 / r.CB;
   r.CG = (r.CPR + r.CB - 1) / r.CB;
-  int nb = std::max(1, 512 / (r.CG * nseg));  // <= 128 partial blocks per view of 4: one load round per finalize lane
+  // <= 64 partial blocks per view of 4 (one load round per finalize lane); per training step
+  // measured 128 / 256 / 512 / 1024 total blocks: 22.61 / 21.93 / 22.09 / 22.43 ms
+  int nb = std::max(1, 256 / (r.CG * nseg));
   nb = std::min(nb, kMaxNB);
   nb = std::min(nb, std::max(1, Pseg / r.PL));
   // f64 partials of wide, short layers (layer4: 2048 channels x 2048 pixels per view) stay
