@@ -554,6 +554,13 @@ def train_main(args):
         opt.step()
         return loss
 
+    from posu import plan as pplan
+    if not args.no_autotune:  # the first warm-up step times every admissible tile per conv geometry
+        pplan._Tuner.active, pplan._Tuner.reps = True, 3
+        try:
+            step()
+        finally:
+            pplan._Tuner.active = False
     for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()

@@ -33,6 +33,23 @@ SIDE_STREAM_WGRAD = True
 HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
 
 
+def _conv_tuned(x, w, cout, k, stride, pad, code):
+    """A raw training convolution (no BN in the epilogue) on the tile the per-layer autotuner
+    picked for its geometry (posu.plan's table; every tile accumulates in the same K order, so
+    the choice changes speed, not results): tuned while `plan._Tuner.active` (bench.py tunes
+    during its first warm-up step), else the stored choice or the built-in heuristic.  The
+    stem (C = 8 direct gather) keeps the heuristic."""
+    from .plan import _tuned
+    n, h, wd, c = x.shape
+    ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
+    z = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
+    if c % 64:
+        return ops.conv2d_nhwc(x, w, cout, k, k, stride, pad, None, None, None, False, code, out=z)
+    key = ('train_conv', code, tuple(x.shape), cout, k, stride, pad)
+    return _tuned(key, cout, lambda t: ops.conv2d_nhwc(x, w, cout, k, k, stride, pad, None, None, None, False, code,
+                                                      out=z, tile=t))
+
+
 class _Grads(dict):
     """parameter -> gradient; weight gradients run on a side stream (`side`), off the
     backward's critical path: the data-gradient chain (BN backward -> dgrad -> next layer)
@@ -82,8 +99,7 @@ class _ConvBN:
         self.wt = packer.dgrad(self.conv.weight, bk) if need_dgrad else None
 
     def forward(self, x, nseg, code, residual=None):
-        z = ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, None, None, None, False,
-                            code)
+        z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
         bn = self.bn
         mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
                                             bn.running_var)
@@ -181,7 +197,7 @@ class _DeconvBN:
         grads.wgrad(self.dc.weight, lambda: T.deconv4x4s2_wgrad(x, dz, code), x, dz)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
-        return ops.conv2d_nhwc(dz, self.wd, self.cin, 4, 4, 2, 1, None, None, None, False, code)
+        return _conv_tuned(dz, self.wd, self.cin, 4, 2, 1, code)
 
 
 class TrainPlan:
