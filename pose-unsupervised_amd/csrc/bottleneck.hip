@@ -326,8 +326,12 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
       asm volatile("" ::"v"(u.x), "v"(u.y), "v"(u.z), "v"(u.w));
       return;
     }
+    // the row offset goes into the VGPR offset, soffset stays the constant 0: hipcc inserts the
+    // wait states of the store-data hazard (a VALU write of the data VGPRs right after a > 64-bit
+    // store) only for buffer stores WITHOUT an SGPR soffset, and on gfx950 a store with one
+    // stored corrupted values (tools/isa_hazards.py)
     __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){u.x, u.y, u.z, u.w}, yrs,
-                                           lane_off + 64 * k, pend_off, (kAbl & 64) ? 2 : 0);
+                                           lane_off + 64 * k + pend_off, 0, (kAbl & 64) ? 2 : 0);
   };
   auto conv3_row = [&](int y, const uint4(&tb)[2], const uint4(&res)[4]) {
     pend_off = __builtin_amdgcn_readfirstlane((n * H + y) * kRowBytes);

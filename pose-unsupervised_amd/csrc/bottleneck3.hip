@@ -30,6 +30,16 @@
 #ifndef POSU_TAIL3_ABLATE
 #define POSU_TAIL3_ABLATE 0
 #endif
+// store-ordering experiments (tools/store_order.sh; never set in the product build):
+//   RAWSTORE 1: y through a raw buffer store with the row offset in soffset
+//   EARLYDMA 1: the next chunk's first weight DMA issued BEFORE the chunk's y stores, and
+//               waited for with vmcnt(8) (the 8 stores younger than it left in flight)
+#ifndef POSU_TAIL3_RAWSTORE
+#define POSU_TAIL3_RAWSTORE 0
+#endif
+#ifndef POSU_TAIL3_EARLYDMA
+#define POSU_TAIL3_EARLYDMA 0
+#endif
 
 namespace posu {
 namespace {
@@ -180,6 +190,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
   // y: plain global stores at a 32-bit offset from this workgroup's first output row (a raw
   // buffer store with the row in soffset corrupted a few elements per launch; not understood)
   char* const ywg = static_cast<char*>(g.y) + static_cast<size_t>(n * H + y0) * kW * kC * ES;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(g.y, 0, g.N * H * kW * kC * ES, 0x00020000);
   const int lane_off = (r16 * kC + cpair) * ES;
   // byte offset of (output row 4 pm + i, column 0, channel 256 nc + 64 cn + 32 jp), wave-uniform
   auto row_off = [&](int i, int nc, int jp) {
@@ -241,13 +252,13 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
       const int u = kConv2Stages + 4 * nc + kc;
       // the chunk's residual loads (issued at kc == 1, after that stage's DMA) are the 8
       // youngest vector-memory ops at kc == 2: its DMA is waited for without them
-      if (kc == 2) vm_wait<8>();
+      if (kc == 2 || (POSU_TAIL3_EARLYDMA && kc == 0 && nc > 0)) vm_wait<8>();
       else vm_wait<0>();
       lds_barrier();
       if (kc == 0) zero();
       // the last stage of a chunk issues the next stage's DMA after its y stores: the next
       // stage's wait then covers both together instead of stalling a later stage behind them
-      if (kc != 3) dma_stage(u + 1, slot_of(u + 1));
+      if (kc != 3 || (POSU_TAIL3_EARLYDMA && nc < 3)) dma_stage(u + 1, slot_of(u + 1));
       if (kc == 1) res_load(nc);  // two stages ahead of the epilogue
       mma_ktile(slot_of(u), smem + kWin, kc, [&](int i) { return 16 * (4 * pm + i) + r16; });
     }
@@ -271,10 +282,16 @@ __global__ __launch_bounds__(512, 1) void bottleneck3_tail_kernel(Tail3Geom g) {
           O::load_vals(rv[i][jp], r);
 #pragma unroll
           for (int e = 0; e < 8; ++e) vv[e] = fmaxf(vv[e] * sc[jp][e] + sh[jp][e] + r[e], 0.f);
-          *reinterpret_cast<uint4*>(ywg + ((16 * (4 * pm + i) + r16) * kC + c0) * ES) = O::store_vals(vv);
+          if (POSU_TAIL3_RAWSTORE) {
+            const uint4 o = O::store_vals(vv);
+            __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w},
+                                                   yrs, lane_off, row_off(i, nc, jp), 0);
+          } else {
+            *reinterpret_cast<uint4*>(ywg + ((16 * (4 * pm + i) + r16) * kC + c0) * ES) = O::store_vals(vv);
+          }
         }
     }
-    if (nc < 3) dma_stage(kConv2Stages + 4 * nc + 4, slot_of(kConv2Stages + 4 * nc + 4));
+    if (!POSU_TAIL3_EARLYDMA && nc < 3) dma_stage(kConv2Stages + 4 * nc + 4, slot_of(kConv2Stages + 4 * nc + 4));
   }
 }
 

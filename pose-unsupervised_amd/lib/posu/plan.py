@@ -160,6 +160,15 @@ class _DualTail:
 # False runs the convolutions
 FUSED_BOTTLENECK = True
 FUSED_LAYER3_TAIL = True
+_FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
+
+
+def _fused_fits(x, cout):
+    """Input and output of a fused Bottleneck kernel inside its 32-bit addressing range (larger
+    batches run the convolutions, which use 64-bit addressing)."""
+    px = x.shape[0] * x.shape[1] * x.shape[2]
+    es = x.element_size()
+    return px * max(x.shape[3], cout) * es < _FUSED_MAX_BYTES
 
 
 class _Block:
@@ -222,7 +231,8 @@ class _Block:
 
     def __call__(self, x, code, out=None):
         y = x
-        if self.w3d is not None and FUSED_BOTTLENECK and x.shape[2] == 64 and x.shape[3] == 64:
+        fits = _fused_fits(x, self.cout)
+        if self.w3d is not None and FUSED_BOTTLENECK and fits and x.shape[2] == 64 and x.shape[3] == 64:
             c1, c2 = self.convs
             return ops.bottleneck_down_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3d,
                                             self.dual.shift, code, out=out)
@@ -230,15 +240,16 @@ class _Block:
             for c in self.convs:
                 y = c(y, code)
             return self.dual(y, x, code, out=out)
-        if self.w3f is not None and FUSED_BOTTLENECK and x.shape[2] == 64:
+        if self.w3f is not None and FUSED_BOTTLENECK and fits and x.shape[2] == 64:
             c1, c2, c3 = self.convs
             return ops.bottleneck_nhwc(x, self.w1f, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3f, c3.scale,
                                        c3.shift, code, out=out)
-        if self.l2 and FUSED_BOTTLENECK and x.shape[2] == 32 and x.shape[1] % 4 == 0:
+        if self.l2 and FUSED_BOTTLENECK and fits and x.shape[2] == 32 and x.shape[1] % 4 == 0:
             c1, c2, c3 = self.convs
             return ops.bottleneck2_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, c3.w, c3.scale,
                                         c3.shift, code, out=out)
-        if self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and x.shape[2] == 16 and x.shape[1] % 8 == 0:
+        if (self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and fits and x.shape[2] == 16 and
+                x.shape[1] % 8 == 0):
             c1, c2, c3 = self.convs
             return ops.bottleneck3_tail_nhwc(c1(x, code), x, c2.w, c2.scale, c2.shift, c3.w, c3.scale, c3.shift, code,
                                              out=out)

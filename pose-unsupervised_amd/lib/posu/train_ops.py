@@ -16,8 +16,11 @@ INPLACE_S2_DGRAD = True
 
 
 def workspace(device, nbytes, slot='default'):
-    """Grow-only scratch buffer per (device, slot), reused by consecutive launches on one stream."""
-    key = (str(device), slot)
+    """Grow-only scratch buffer per (device, slot, current stream), reused by consecutive
+    launches on that stream only: a buffer is allocated, used and (when it grows) released on
+    one stream, so the caching allocator orders its reuse behind every launch that used it (the
+    training step runs weight gradients on a side stream, train_plan._Grads)."""
+    key = (str(device), slot, torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
@@ -25,12 +28,15 @@ def workspace(device, nbytes, slot='default'):
     return buf
 
 
-def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=None, out=None):
-    """dx [N, H, W, cin] of a conv x -> dy; `hw` = (H, W) of x; optional residual added."""
+def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=None, out=None, inplace=False):
+    """dx [N, H, W, cin] of a conv x -> dy; `hw` = (H, W) of x; optional residual added.
+    inplace=True (1x1 / stride-2 convolutions with a residual only) accumulates into `residual`
+    itself and returns it -- the caller gives up that tensor; otherwise nothing is mutated."""
     require_cuda(dy)
     n, ho, wo, cout = dy.shape
     h, w = hw
-    if INPLACE_S2_DGRAD and out is None and residual is not None and kh == kw == 1 and stride == 2 and pad == 0:
+    if inplace and INPLACE_S2_DGRAD and out is None and residual is not None and kh == kw == 1 and stride == 2 \
+            and pad == 0:
         out = residual  # accumulated in place over dy's pixels (posu_conv2d_dgrad)
     if out is None:
         out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)

@@ -106,7 +106,8 @@ class _ConvBN:
         y = T.bn_apply(z, nseg, sc, sh, residual, self.relu)
         return y, (x, z, y, mean, rstd, sc, sh, residual is not None)
 
-    def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None):
+    def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None,
+                 inplace=False):
         x, z, y, mean, rstd, sc, sh, has_res = saved
         # ReLU mask: from y after a residual add, else recomputed from z (one tensor read less)
         mask_y = y if (self.relu and has_res) else None
@@ -120,7 +121,7 @@ class _ConvBN:
         dx = None
         if need_dx:
             dx = T.conv2d_dgrad(dz, self.wt, self.cin, self.k, self.k, self.stride, self.pad, x.shape[1:3], code,
-                                residual=dx_residual)
+                                residual=dx_residual, inplace=inplace)
         return dx, gres
 
 
@@ -162,7 +163,9 @@ class _Block:
             dx, _ = self.units[0].backward(g, su[0], nseg, code, grads, dx_residual=gres)
             return dx
         dx_main, _ = self.units[0].backward(g, su[0], nseg, code, grads)
-        dx, _ = self.down.backward(gres, sd, nseg, code, grads, dx_residual=dx_main)
+        # dx_main is this block's own temporary: the downsample's 1x1 / stride-2 data gradient
+        # accumulates into it in place
+        dx, _ = self.down.backward(gres, sd, nseg, code, grads, dx_residual=dx_main, inplace=True)
         return dx
 
 

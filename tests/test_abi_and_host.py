@@ -276,3 +276,15 @@ def test_bottleneck_conv3_order_is_the_accumulator_fragment_order():
     w1 = torch.randn(64, 256, 1, 1)
     x = torch.randn(256)
     torch.testing.assert_close(packing.pack_bottleneck_conv1_weight(w1, torch.float32) @ x[o1], w1.view(64, 256) @ x)
+
+
+def test_fused_bottleneck_byte_guard():
+    """Batches whose activations pass the fused kernels' 32-bit byte offsets take the
+    convolution path (plan._fused_fits) instead of a RuntimeError from the kernel's check."""
+    from posu import plan as P
+    ok = torch.empty((128, 64, 64, 64), dtype=torch.bfloat16, device='meta')
+    assert P._fused_fits(ok, 256)                        # layer1 block 0 at batch 128
+    big = torch.empty((1024, 64, 64, 256), dtype=torch.bfloat16, device='meta')
+    assert not P._fused_fits(big, 256)                   # 2 GiB of layer1 output
+    assert not P._fused_fits(torch.empty((1024, 64, 64, 64), dtype=torch.bfloat16, device='meta'), 256)
+    assert P._fused_fits(torch.empty((1023, 64, 64, 256), dtype=torch.bfloat16, device='meta'), 256)

@@ -22,6 +22,14 @@ def _block_params(g, c=256, p=64):
     return w1, bn(p), w2, bn(p), w3, bn(c)
 
 
+def _sentinel(like, shape=None):
+    """Output buffer pre-filled with a quiet-NaN pattern no kernel produces: a store that never
+    lands (or lands elsewhere) leaves it behind and fails the comparisons below."""
+    out = torch.empty(like.shape if shape is None else shape, dtype=like.dtype, device=like.device)
+    out.view(torch.int16).fill_(0x7fc1 if like.dtype == torch.bfloat16 else 0x7e01)
+    return out
+
+
 def _torch_block(x, w1, bn1, w2, bn2, w3, bn3):
     t = F.relu(F.conv2d(x, w1) * bn1[0].view(1, -1, 1, 1) + bn1[1].view(1, -1, 1, 1))
     t = F.relu(F.conv2d(t, w2, padding=1) * bn2[0].view(1, -1, 1, 1) + bn2[1].view(1, -1, 1, 1))
@@ -30,14 +38,15 @@ def _torch_block(x, w1, bn1, w2, bn2, w3, bn3):
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64)])
+@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64), (128, 64)])
 def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
+    """(128, 64) is the production grid (256 workgroups): against the unfused launches only."""
     g = torch.Generator().manual_seed(17 + h)
     w1, bn1, w2, bn2, w3, bn3 = _block_params(g)
     x = torch.randn(n, 256, h, 64, generator=g)
     dt = ops.torch_dtype(code)
     xq = x.to(dt).float()   # the input as the device sees it
-    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 128 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
@@ -46,7 +55,7 @@ def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
     p3f = packing.pack_bottleneck_conv3_weight(w3.to(cuda), dt)
     s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
     p1f = packing.pack_bottleneck_conv1_weight(w1.to(cuda), dt)
-    fused = ops.bottleneck_nhwc(xd, p1f, s[0], s[1], p2, s[2], s[3], p3f, s[4], s[5], code)
+    fused = ops.bottleneck_nhwc(xd, p1f, s[0], s[1], p2, s[2], s[3], p3f, s[4], s[5], code, out=_sentinel(xd))
     t1 = ops.conv2d_nhwc(xd, p1, 64, 1, 1, 1, 0, s[0], s[1], None, True, code)
     t2 = ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, code)
     three = ops.conv2d_nhwc(t2, p3, 256, 1, 1, 1, 0, s[4], s[5], xd, True, code)
@@ -59,6 +68,8 @@ def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
     ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * three.float().abs().clamp_min(2.0 ** -4)
     assert float(d.mean()) < 0.05 * float(ulp.mean()), float(d.mean())
     assert bool((d <= 16 * ulp).all()), float((d / ulp).max())
+    if ref is None:
+        return
     got = fused.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs()
     tol = 0.05 if code == BF16 else 0.01
@@ -66,7 +77,7 @@ def test_fused_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64)])
+@pytest.mark.parametrize('n,h', [(3, 10), (1, 2), (2, 64), (1, 7), (5, 64), (128, 64)])
 def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n, h):
     """Layer1 block 0: 64 input channels, downsample 1x1 + BN as the residual branch."""
     g = torch.Generator().manual_seed(29 + h)
@@ -81,7 +92,7 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
     t = F.relu(F.conv2d(xq, w1) * bn1[0].view(1, -1, 1, 1) + bn1[1].view(1, -1, 1, 1))
     t = F.relu(F.conv2d(t, w2, padding=1) * bn2[0].view(1, -1, 1, 1) + bn2[1].view(1, -1, 1, 1))
     ref = F.relu(F.conv2d(t, w3) * bn3[0].view(1, -1, 1, 1) + bn3[1].view(1, -1, 1, 1) +
-                 F.conv2d(xq, wd) * bnd[0].view(1, -1, 1, 1) + bnd[1].view(1, -1, 1, 1))
+                 F.conv2d(xq, wd) * bnd[0].view(1, -1, 1, 1) + bnd[1].view(1, -1, 1, 1)) if n < 128 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 64, bk, dt)
@@ -90,7 +101,8 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
     pdual = packing.pack_dual_1x1_weight(w3.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), dt)
     shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
     fused = ops.bottleneck_down_nhwc(xd, p1, s[0], s[1], p2, s[2], s[3],
-                                     packing.pack_bottleneck_down_weight(pdual, 64), shift, code)
+                                     packing.pack_bottleneck_down_weight(pdual, 64), shift, code,
+                                     out=_sentinel(xd, (n, h, 64, 256)))
     t1 = ops.conv2d_nhwc(xd, p1, 64, 1, 1, 1, 0, s[0], s[1], None, True, code)
     t2 = ops.conv2d_nhwc(t1, p2, 64, 3, 3, 1, 1, s[2], s[3], None, True, code)
     unfused = ops.conv1x1_dual_nhwc(t2, xd, 1, pdual, 256, shift, True, code)
@@ -101,6 +113,8 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
     ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * unfused.float().abs().clamp_min(2.0 ** -4)
     assert float(d.mean()) < 0.05 * float(ulp.mean()), float(d.mean())
     assert bool((d <= 16 * ulp).all()), float((d / ulp).max())
+    if ref is None:
+        return
     got = fused.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs()
     tol = 0.05 if code == BF16 else 0.01
@@ -108,7 +122,7 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12)])
+@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12), (128, 32)])
 def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
     """Layer2's identity block (32-wide maps, 512 channels, planes 128; weights streamed
     through LDS): bit-identical to the three unfused launches (same K order per accumulator,
@@ -118,14 +132,14 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
     x = torch.randn(n, 512, h, 32, generator=g)
     dt = ops.torch_dtype(code)
     xq = x.to(dt).float()
-    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 128 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 512, bk, dt)
     p2 = packing.pack_conv_weight(w2.to(cuda), 128, bk, dt)
     p3 = packing.pack_conv_weight(w3.to(cuda), 128, bk, dt)
     s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
-    fused = ops.bottleneck2_nhwc(xd, p1, s[0], s[1], p2, s[2], s[3], p3, s[4], s[5], code)
+    fused = ops.bottleneck2_nhwc(xd, p1, s[0], s[1], p2, s[2], s[3], p3, s[4], s[5], code, out=_sentinel(xd))
     t1 = ops.conv2d_nhwc(xd, p1, 128, 1, 1, 1, 0, s[0], s[1], None, True, code)
     t2 = ops.conv2d_nhwc(t1, p2, 128, 3, 3, 1, 1, s[2], s[3], None, True, code)
     three = ops.conv2d_nhwc(t2, p3, 512, 1, 1, 1, 0, s[4], s[5], xd, True, code)
@@ -133,6 +147,8 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
     d = (fused.float() - three.float()).abs()
     print('layer2 fused vs three launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
     assert torch.equal(fused, three)
+    if ref is None:
+        return
     got = fused.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs()
     tol = 0.05 if code == BF16 else 0.01
@@ -140,7 +156,7 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(2, 16), (1, 8), (3, 24)])
+@pytest.mark.parametrize('n,h', [(2, 16), (1, 8), (3, 24), (128, 16)])
 def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
     """Layer3's identity block tail (16-wide maps, 1024 channels, planes 256): conv2 + conv3
     (+ residual) in one launch, bit-identical to the two unfused launches (conv_igemm's K order
@@ -150,7 +166,7 @@ def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
     x = torch.randn(n, 1024, h, 16, generator=g)
     dt = ops.torch_dtype(code)
     xq = x.to(dt).float()
-    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3)
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 128 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 1024, bk, dt)
@@ -158,13 +174,15 @@ def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
     p3 = packing.pack_conv_weight(w3.to(cuda), 256, bk, dt)
     s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
     t1 = ops.conv2d_nhwc(xd, p1, 256, 1, 1, 1, 0, s[0], s[1], None, True, code)
-    fused = ops.bottleneck3_tail_nhwc(t1, xd, p2, s[2], s[3], p3, s[4], s[5], code)
+    fused = ops.bottleneck3_tail_nhwc(t1, xd, p2, s[2], s[3], p3, s[4], s[5], code, out=_sentinel(xd))
     t2 = ops.conv2d_nhwc(t1, p2, 256, 3, 3, 1, 1, s[2], s[3], None, True, code)
     two = ops.conv2d_nhwc(t2, p3, 1024, 1, 1, 1, 0, s[4], s[5], xd, True, code)
     torch.cuda.synchronize()
     d = (fused.float() - two.float()).abs()
     print('layer3 tail fused vs two launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
     assert torch.equal(fused, two)
+    if ref is None:
+        return
     got = fused.float().cpu().permute(0, 3, 1, 2)
     err = (got - ref).abs()
     tol = 0.05 if code == BF16 else 0.01
