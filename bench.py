@@ -13,10 +13,11 @@ on-die.
 Multi-GPU: `python bench.py --gpus N` starts N ranks itself (one process per GPU,
 torch.distributed.run, 127.0.0.1 rendezvous) before this process touches the GPU; the
 driver's `python -m torch.distributed.run ... bench.py --gpus N` lands directly in the
-rank code.  Every rank processes its own 32 groups per step (weak scaling, no data-path
-collective; the reference's DistributedSampler sharding, lib/utils/utils.py:134-141),
-`dist.get_world_size() == N` is asserted, time = max over ranks, value = all ranks'
-frames / that time.
+rank code.  The global batch of 32 x N groups is sharded over the ranks by
+posu.dist.shard_groups (the reference's DistributedSampler order, lib/utils/utils.py:134-141;
+every group's crops come from its own generator, so the global batch does not depend on N):
+32 groups per rank (weak scaling, no data-path collective), `dist.get_world_size() == N` is
+asserted, time = max over ranks, value = all ranks' frames / that time.
 
 Also reported, on the same JSON line (rank 0):
   roofline       -- the network (fused stem + implicit-GEMM MFMA conv stack + fused
@@ -26,7 +27,12 @@ Also reported, on the same JSON line (rank 0):
                     (fp32 reference network + soft-argmax + affine + fp64 triangulation)
                     on the same first input batch, as run/test/test_triangulate.py:98-102
                     computes MPJPE (mean / std / max per-joint error, mm);
+  triangulation_same_2d_mm_all_ranks -- every rank's device triangulation against the oracle's
+                    triangulation of the same device joints, reduced over ranks (posu.dist);
   fp32_mode      -- frames/s of the same pipeline with the exact-f32 kernels (parity mode);
+  configs1       -- BASELINE configs[1]: the R50 heatmap forward alone at batch 64, bf16;
+  train_mode     -- BASELINE configs[3]: the training step (fwd + bwd + Adam, DDP over RCCL
+                    when N > 1), time-bounded (--train-steps);
   cpu_baseline   -- that oracle chain timed on the host cores (rank 0 at N = 1): the full
                     32 x 4 batch (configs[2]) and batch 1 (configs[0]).
 `--dry-run` runs the launcher and the rank plumbing on CPU (gloo) without any GPU work.
@@ -81,6 +87,10 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-mpjpe', action='store_true', help='skip the oracle-chain MPJPE check')
     ap.add_argument('--fp32-steps', type=int, default=5, help='timed steps of the fp32 parity mode (0: skip)')
+    ap.add_argument('--train-steps', type=int, default=10,
+                    help='infer mode: timed steps of the configs[3] training step reported as train_mode (0: skip)')
+    ap.add_argument('--c1-steps', type=int, default=20,
+                    help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
     return ap.parse_args()
 
@@ -173,9 +183,12 @@ def build_model(layers, size, precision, device):
     return net.to(device).eval()
 
 
-def input_views(groups, size, rank, b, device):
+def input_views(shard, size, b, device):
+    """The 4 views of this rank's groups (`shard`, indices into the global batch) of input
+    batch b: every group's crops come from its own generator, so the global batch is the same
+    whatever the number of ranks."""
     from posu import synthetic as syn
-    return [v.to(device) for v in syn.synthetic_views(4, groups, size, seed=100 + 16 * rank + b)]
+    return [v.to(device) for v in syn.group_views(4, shard, size, seed=100 + b)]
 
 
 def pmc_traffic(layers, size, precision, groups):
@@ -226,7 +239,7 @@ def cpu_baseline(layers, size, groups, seconds):
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
                                   bn_stats=syn.load_bn_stats(layers, size))
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
-    views = syn.synthetic_views(4, groups, size, seed=100)
+    views = syn.group_views(4, range(groups), size, seed=100)   # the bench's input batch 0
     frames, ref, t0 = 0, None, time.perf_counter()
     while True:
         out = oracle_chain(sd, layers, size, views, host, full=ref is None)
@@ -361,13 +374,24 @@ def save_tiles(path):
         json.dump({'tiles': [{'key': list(k), 'tile': t} for k, t in pl.tuned_tiles().items()]}, f)
 
 
-def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, dist=None):
+def rank_meta(args, rank, world, dev):
+    """(shard, device metadata, host metadata) of this rank's groups of the global batch
+    (args.groups per rank, posu.dist.shard_groups: the reference's DistributedSampler order)."""
+    from posu import dist as pdist
+    from posu.pipeline import subset_meta, synthetic_meta
+    shard = pdist.shard_groups(args.groups * world, rank, world)
+    meta, host = synthetic_meta(args.groups * world, dev, image_size=args.size)
+    if world > 1:
+        meta, host = subset_meta(meta, host, shard)
+    return shard, meta, host
+
+
+def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, dist=None, world=1):
     """Build, (auto)tune, capture and time the pipeline in one precision; returns a dict."""
-    from posu.pipeline import synthetic_meta
     net = build_model(args.layers, args.size, precision, dev)
-    meta, _ = synthetic_meta(args.groups, dev, image_size=args.size)
+    shard, meta, host = rank_meta(args, rank, world, dev)
     plan = net.plan(dev)
-    reps = [Replayer(plan, input_views(args.groups, args.size, rank, b, dev), meta, args.groups, args.chunks,
+    reps = [Replayer(plan, input_views(shard, args.size, b, dev), meta, len(shard), args.chunks,
                      not args.no_graph, dev) for b in range(nbatch)]
     tuned = None
     with torch.no_grad():
@@ -424,7 +448,67 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
         torch.cuda.synchronize()
     return {'elapsed': elapsed, 'net_ms': net_ms, 'geo_ms': geo_ms, 'X0': X.detach().cpu().numpy().copy(),
             'coords0': coords.detach().cpu().numpy().copy(), 'hm0': r.hm.detach().cpu().clone(),
-            'use_graph': use_graph, 'tuned': tuned, 'loss0': float(loss), 'meta': r.meta}
+            'use_graph': use_graph, 'tuned': tuned, 'loss0': float(loss), 'meta': r.meta, 'host': host,
+            'shard': shard}
+
+
+def triangulation_parity_all_ranks(res, dev):
+    """Every rank: the device triangulation of its groups' device joints against the oracle's
+    triangulation of the SAME joints (the BASELINE 1e-2 mm gate, run/test/test_triangulate.py:98-102
+    arithmetic), reduced over ranks with posu.dist (error sums and counts, max)."""
+    from oracle import geometry_ref as G
+    from posu import dist as pdist
+    X0, c0 = res['X0'], res['coords0']
+    V, ng, J = c0.shape[0], c0.shape[1], c0.shape[2]
+    p2d = c0.transpose(1, 0, 2, 3).reshape(ng * V, J, 2).astype(np.float64)
+    err = np.linalg.norm(X0 - G.triangulate_poses(res['host']['cams'], p2d), axis=-1)
+    tot, cnt = pdist.sum_over_ranks([err.sum(), err.size], device=dev)
+    mx = pdist.max_over_ranks(err.max(), device=dev)
+    return {'mean': float('%.6g' % (tot / cnt)), 'max': float('%.6g' % mx), 'joints': int(cnt)}
+
+
+def time_configs1(args, dev, rank, world, dist):
+    """BASELINE configs[1]: the ResNet-50 heatmap forward alone on a synthetic 256x256 batch of 64
+    frames in bf16 (tiles autotuned for that batch, one hipGraph, HIP events on the launch
+    stream): frames/s and the fraction of the bf16 MFMA peak."""
+    from posu import synthetic as syn
+    if (args.layers, args.size) != (50, 256):
+        return None
+    net = build_model(50, 256, 'bf16', dev)
+    plan = net.plan(dev)
+    views = [v.to(dev) for v in syn.synthetic_views(1, 64, 256, seed=300 + rank)]
+    with torch.no_grad():
+        run = lambda: plan.run(plan.pack_input(views), keep_features=False)[0]  # noqa: E731
+        run()
+        if not args.no_autotune:
+            plan.autotune(plan.pack_input(views), keep_features=False, reps=8)
+        s = torch.cuda.Stream(dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            run()
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            run()
+        for _ in range(3):
+            g.replay()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(args.c1_steps):
+            g.replay()
+        b.record()
+        torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / args.c1_steps
+    from posu import dist as pdist
+    ms_max = pdist.max_over_ranks(ms, device=dev)
+    tf = GFLOP_PER_FRAME[(50, 256)] * 64 / (ms * 1e-3) / 1e3
+    return {'metric': 'ResNet-50 heatmap forward frames/s (BASELINE configs[1]: synthetic 256x256 batch 64, bf16)',
+            'value': round(64 * world / (ms_max * 1e-3), 2), 'unit': 'frames/s', 'network_ms': round(ms, 4),
+            'replays': args.c1_steps, 'n_gpus': world,
+            'roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(tf / PEAK_BF16_TFLOPS, 4)}}
 
 
 def infer_main(args):
@@ -435,7 +519,8 @@ def infer_main(args):
     rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
     frames = 4 * args.groups
     res = time_pipeline(args, args.precision, dev, rank, args.steps, args.warmup, args.batches,
-                        not args.no_autotune, dist)
+                        not args.no_autotune, dist, world)
+    tri_all = triangulation_parity_all_ranks(res, dev)
     elapsed = pdist.max_over_ranks(res['elapsed'], device=dev)
     value = pdist.throughput(frames, args.steps, world, elapsed)
     per_rank = gather_per_rank([frames * args.steps, res['elapsed']], dist, device=dev)
@@ -455,12 +540,20 @@ def infer_main(args):
             roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
     fp32 = None
     if args.fp32_steps > 0 and args.precision != 'fp32':
-        r32 = time_pipeline(args, 'fp32', dev, rank, args.fp32_steps, 2, args.batches, False, dist)
+        r32 = time_pipeline(args, 'fp32', dev, rank, args.fp32_steps, 2, args.batches, False, dist, world)
         el32 = pdist.max_over_ranks(r32['elapsed'], device=dev)
         fp32 = {'value': round(pdist.throughput(frames, args.fp32_steps, world, el32), 2), 'unit': 'frames/s',
                 'network_ms': round(r32['net_ms'], 3), 'steps': args.fp32_steps,
                 'roofline_frac_f32': (round(gf * frames / (r32['net_ms'] * 1e-3) / 1e3 / PEAK_F32_TFLOPS, 4)
                                       if gf else None)}
+    c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
+    train = None
+    if args.train_steps > 0:
+        t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
+        train = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
+        train.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
+                     parallelism=t['config']['parallelism'], workload=t['config']['workload'],
+                     optimizer=t['config']['optimizer'])
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -487,13 +580,15 @@ def infer_main(args):
                                '+ epipolar loss + fp64 DLT triangulation (BASELINE configs[2])'
                                % (args.groups, args.size, args.size, args.layers),
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
-                   'parallelism': 'dp%d (independent group shards, no data-path collective)' % world,
+                   'parallelism': 'dp%d (the global batch of %d groups sharded by posu.dist.shard_groups, '
+                                  'no data-path collective)' % (world, args.groups * world),
                    'hipgraph': res['use_graph'], 'chunks': args.chunks, 'tiles': res['tuned'] or 'heuristic',
                    'input_batches_rotated': args.batches},
         'network_ms': round(res['net_ms'], 4), 'decode_geometry_ms': round(res['geo_ms'], 4),
         'groups_per_s': round(value / 4, 2), 'per_rank_frames': [int(p[0]) for p in per_rank],
         'per_rank_seconds': [round(p[1], 5) for p in per_rank],
-        'mpjpe_vs_ref_mm': mpjpe, 'fp32_mode': fp32,
+        'mpjpe_vs_ref_mm': mpjpe, 'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32,
+        'configs1': c1, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }
     print(json.dumps(line))
@@ -502,31 +597,28 @@ def infer_main(args):
 
 
 # ------------------------------------------------------------------ training
-def train_main(args):
+def run_training(args, dev, rank, world, dist, steps, warmup):
     """configs[3]: one training step = 4-view batch (groups x 4 frames per GPU) through the
     reference's step (core/function.py:154-366): train-mode forward with per-view BN,
     JointsMSELoss per view + FundamentalLoss on soft-argmax coords, backward, Adam.
-    N > 1: DistributedDataParallel over RCCL (gradient all-reduce), weak scaling."""
+    world > 1: DistributedDataParallel over RCCL (gradient all-reduce overlapped with the staged
+    backward), weak scaling.  Returns the training line (a dict)."""
     from posu import dist as pdist
     from posu import synthetic as syn
-    from posu.pipeline import synthetic_meta
     from core.loss import JointsMSELoss, FundamentalLoss
     from models.multiview_pose_resnet import get_multiview_pose_net
     from utils.transforms import integral_preds_image_th
     from posu import ops
-    _, local, _ = pdist.env_rank()
-    dev = torch.device('cuda', local)
-    torch.cuda.set_device(dev)
-    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
     cfg = syn.make_cfg(num_layers=args.layers, image_size=args.size)
     net = build_model(args.layers, args.size, args.precision, dev).train()
     model = get_multiview_pose_net(net, cfg)
     if dist is not None:
+        local = dev.index
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local,
                                                           bucket_cap_mb=64)
     nb, nv, hs = args.groups, 4, args.size // 4
-    views = input_views(nb, args.size, rank, 0, dev)
-    meta, _ = synthetic_meta(nb, dev, image_size=args.size)
+    shard, meta, _ = rank_meta(args, rank, world, dev)
+    views = input_views(shard, args.size, 0, dev)
     g = torch.Generator().manual_seed(7 + rank)
     ys, xs = torch.meshgrid(torch.arange(hs, dtype=torch.float32), torch.arange(hs, dtype=torch.float32),
                             indexing='ij')
@@ -561,23 +653,23 @@ def train_main(args):
             step()
         finally:
             pplan._Tuner.active = False
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    per_rank = gather_per_rank([nv * nb * args.steps, elapsed], dist, device=dev)
+    per_rank = gather_per_rank([nv * nb * steps, elapsed], dist, device=dev)
     elapsed = pdist.max_over_ranks(elapsed, device=dev)
     frames = nv * nb
-    value = pdist.throughput(frames, args.steps, world, elapsed)
+    value = pdist.throughput(frames, steps, world, elapsed)
     gf = TRAIN_GFLOP_PER_FRAME.get((args.layers, args.size))
     roof = None
     if gf is not None:
@@ -587,21 +679,32 @@ def train_main(args):
                 'frac': round(achieved / peak, 4), 'traffic': None,
                 'kernel': 'whole training step per GPU (fwd + bwd convs, BN, Adam)',
                 'flop_per_launch': '%.1f GFLOP/frame x %d frames' % (gf, frames)}
+    return {
+        'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
+        'steps': steps, 'warmup': warmup, 'ms_per_step': round(elapsed / steps * 1e3, 4),
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision,
+        'data': 'synthetic',
+        'config': {'workload': '4-view batch %dx4 at %dx%d: PoseResNet-%d train step (per-view BN, '
+                               'JointsMSE + FundamentalLoss, Adam) (BASELINE configs[3])'
+                               % (nb, args.size, args.size, args.layers),
+                   'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
+                   'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce overlapped with the '
+                                  'staged backward)' % world,
+                   'optimizer': 'Adam lr 1e-3 (%s)' % args.adam},
+        'per_rank_frames': [int(p[0]) for p in per_rank],
+        'loss': round(float(loss.detach()), 5), 'roofline': roof, 'cpu_baseline': None,
+    }
+
+
+def train_main(args):
+    """`--mode train`: the configs[3] training step as the bench line."""
+    from posu import dist as pdist
+    _, local, _ = pdist.env_rank()
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
+    line = run_training(args, dev, rank, world, dist, args.steps, args.warmup)
     if rank == 0:
-        line = {
-            'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
-            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4),
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': args.precision,
-            'data': 'synthetic',
-            'config': {'workload': '4-view batch %dx4 at %dx%d: PoseResNet-%d train step (per-view BN, '
-                                   'JointsMSE + FundamentalLoss, Adam) (BASELINE configs[3])'
-                                   % (nb, args.size, args.size, args.layers),
-                       'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
-                       'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce)' % world,
-                       'optimizer': 'Adam lr 1e-3 (%s)' % args.adam},
-            'per_rank_frames': [int(p[0]) for p in per_rank],
-            'loss': round(float(loss), 5), 'roofline': roof, 'cpu_baseline': None,
-        }
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -21,8 +21,10 @@ NHWC activations in the compute dtype (zero-copy; fp32 in the default mode, like
 reference's).
 
 Training mode (``model.train()``) runs posu.train_plan: batch-statistics BN per view,
-differentiable through one autograd Function whose backward is the HIP kernel chain;
-parameter gradients land in ``.grad`` as usual (optimizers / DDP unchanged).
+differentiable through five stage Functions whose backward is the HIP kernel chain;
+parameter gradients land in ``.grad`` as usual, stage by stage (optimizers / DDP unchanged;
+DDP's bucketed all-reduce overlaps the rest of the backward).  ``layer1_out`` and
+``deconv_out`` are differentiable in training mode, as in the reference.
 """
 import logging
 import os
@@ -162,9 +164,9 @@ class PoseResNet(nn.Module):
             raise RuntimeError('model parameters are on %s but input is on %s'
                                % (self.conv1.weight.device, views[0].device))
         if self.training:
-            # batch-statistics BN per view (one segment per view), differentiable
-            x = views[0] if len(views) == 1 else torch.cat(views, 0)
-            return train_forward(self, self.train_plan(), x, len(views))
+            # batch-statistics BN per view (one segment per view), differentiable; the views
+            # are packed straight into one NHWC batch (no torch.cat)
+            return train_forward(self, self.train_plan(), list(views), len(views))
         plan = self.plan(views[0].device)
         hm, x1, f = plan.run(plan.pack_input(views))
         # NHWC -> NCHW-shaped channels-last views (no copy)

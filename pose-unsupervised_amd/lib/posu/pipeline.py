@@ -50,6 +50,28 @@ class MultiViewPipeline:
         return hm, coords, loss, X
 
 
+def subset_meta(meta, host, groups):
+    """The metadata of the listed groups of a batch (a rank's shard, posu.dist.shard_groups):
+    device tables indexed on their group axis, host camera / pose lists likewise."""
+    nv = meta.M.shape[1]
+    nb = meta.M.shape[0]
+    gi = torch.as_tensor(list(groups), dtype=torch.long, device=meta.M.device)
+    fi = (torch.arange(nv, device=gi.device)[:, None] * nb + gi[None, :]).reshape(-1)   # view-major frames
+    sub = MultiViewBatchMeta(
+        affines=meta.affines[fi].contiguous(), M=meta.M[gi].contiguous(), intr=meta.intr[gi].contiguous(),
+        F=meta.F, subj=meta.subj[gi].contiguous(),
+        weights=None if meta.weights is None else meta.weights[:, gi].contiguous(), undistort=meta.undistort)
+    g = list(groups)
+    hs = dict(host)
+    hs['cams'] = [c for k in g for c in host['cams'][k * nv:(k + 1) * nv]]
+    hs['poses3d'] = host['poses3d'][g]
+    hs['centers'] = host['centers'][:, g]
+    hs['scales'] = host['scales'][:, g]
+    hs['affines'] = host['affines'].reshape(nv, nb, 2, 3)[:, g].reshape(-1, 2, 3)
+    hs['subjects'] = host['subjects'][g]
+    return sub, hs
+
+
 def synthetic_meta(ngroups, device, image_size=256, njoints=16, distortion=True, nviews=4):
     """Crop affines / cameras / F table of a synthetic H36M-like batch (posu.synthetic)."""
     from utils.transforms import batch_inverse_affines

@@ -152,6 +152,18 @@ def synthetic_views(nviews, batch, image_size, seed=0, device='cpu'):
     return views
 
 
+def group_views(nviews, groups, image_size, seed=0, device='cpu'):
+    """V x [len(groups), 3, S, S] f32 N(0, 1) crops of the listed groups of a global batch:
+    group g's V crops are drawn from its own generator (seed, g), so a rank that holds a shard
+    of the groups (posu.dist.shard_groups) gets exactly those groups' crops of the batch that
+    one process would see."""
+    out = np.empty((nviews, len(groups), 3, image_size, image_size), dtype=np.float32)
+    for k, g in enumerate(groups):
+        r = np.random.default_rng([seed, int(g)])
+        out[:, k] = r.standard_normal((nviews, 3, image_size, image_size), dtype=np.float32)
+    return [torch.from_numpy(out[v]).to(device) for v in range(nviews)]
+
+
 # ---------------------------------------------------------------- geometry
 H36M_K = np.array([-0.207, 0.247, -0.003])
 H36M_P = np.array([-0.0009, -0.0016])

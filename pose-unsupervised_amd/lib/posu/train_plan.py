@@ -3,8 +3,10 @@
 The reference trains with torch autograd over nn.Conv2d / BatchNorm2d / ReLU /
 MaxPool2d / ConvTranspose2d (lib/models/pose_resnet.py:21-205, train mode, called once
 per camera view by multiview_pose_resnet.py:74-78) and Adam
-(core/function.py:364-366, utils/utils.py:79-83).  Here one autograd Function runs the
-whole network forward and backward as explicit kernel launches on NHWC activations:
+(core/function.py:364-366, utils/utils.py:79-83).  Here five autograd Functions (stem +
+layer1 | layer2 | layer3 | layer4 | deconvs + head, _StageFn) run the network forward and
+backward as explicit kernel launches on NHWC activations, so DDP's gradient all-reduce
+starts while the earlier stages are still in backward:
 
   forward   conv (raw, MFMA implicit GEMM) -> per-view batch statistics -> normalise
             (+ residual) + ReLU, for every conv / deconv; max-pool; 1x1 head
@@ -59,6 +61,7 @@ class _Grads(dict):
     def __init__(self, side):
         super().__init__()
         self.side = side
+        self.event = None
 
     def wgrad(self, param, fn, *inputs):
         if self.side is None:
@@ -76,6 +79,20 @@ class _Grads(dict):
     def join(self, device):
         if self.side is not None:
             torch.cuda.current_stream(device).wait_stream(self.side)
+
+    def close(self):
+        """Record the event after this set's last side-stream launch; returns self."""
+        self.event = None
+        if self.side is not None:
+            self.event = torch.cuda.Event()
+            self.event.record(self.side)
+        return self
+
+    def wait(self):
+        """Make the current stream wait for this set's side-stream launches (not for any
+        launched after it)."""
+        if self.event is not None:
+            torch.cuda.current_stream(self.side.device).wait_event(self.event)
 
 
 class _ConvBN:
@@ -254,85 +271,181 @@ class TrainPlan:
                        torch.zeros(self.njoints, device=fl.weight.device))
         self.packer.run()
 
-    def forward(self, x_nchw, nseg):
-        """x [nseg*B, 3, H, W] f32 -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC, saved)."""
+    # ------------------------------------------------------------------ stages
+    # The network runs as NSTAGES autograd Functions (stem + layer1 | layer2 | layer3 | layer4 |
+    # deconvs + head) so that parameter gradients reach autograd -- and DistributedDataParallel's
+    # bucketed all-reduce -- stage by stage during backward instead of all at once at its end
+    # (the reference's DDP overlaps its all-reduce with loss.backward(), run/pose2d/train.py:223,
+    # lib/core/function.py:366).
+    NSTAGES = 5
+
+    def stage_params(self, i):
+        """The parameters stage i computes gradients for (every parameter in exactly one stage,
+        in the modules' registration order)."""
+        if getattr(self, '_stage_params', None) is None:
+            net = self.net
+            mods = [[net.conv1, net.bn1, net.layer1], [net.layer2], [net.layer3], [net.layer4],
+                    [net.deconv_layers, net.final_layer]]
+            self._stage_params = [[p for m in ms for p in m.parameters()] for ms in mods]
+        return self._stage_params[i]
+
+    def forward_stage(self, i, x, nseg):
+        """Stage i's forward: stage 0 takes the list of V NCHW f32 views (stacked on N as nseg
+        BatchNorm segments, packed straight into one NHWC batch: no torch.cat), stages 1-3 the
+        previous stage's NHWC activation; returns (outputs, saved) -- stage 4's outputs are
+        (heatmaps NCHW f32, deconv output NHWC)."""
         code = self.code
-        self.pack()
-        x = ops.pack_nchw_to_nhwc(x_nchw, code, STEM_CIN_PAD)
-        a0, s0 = self.stem.forward(x, nseg, code)
-        p0 = ops.maxpool3x3s2_nhwc(a0, code)
-        saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
-        y = p0
-        x1 = None
-        for li, layer in enumerate(self.layers):
-            for b in layer:
+        if i == 0:
+            self.pack()
+            n, _, h, w = x[0].shape
+            xin = torch.empty((n * len(x), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(code), device=x[0].device)
+            for k, v in enumerate(x):
+                ops.pack_nchw_to_nhwc(v, code, STEM_CIN_PAD, out=xin[k * n:(k + 1) * n])
+            a0, s0 = self.stem.forward(xin, nseg, code)
+            y = ops.maxpool3x3s2_nhwc(a0, code)
+            saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
+            for b in self.layers[0]:
                 y, sb = b.forward(y, nseg, code)
                 saved['blocks'].append(sb)
-            if li == 0:
-                x1 = y
-        saved['deconvs'] = []
+            # num_batches_tracked += nseg for every BatchNorm (the reference's V backbone calls
+            # each add 1): one multi-tensor launch instead of one tiny kernel per layer
+            nbt = [bn.num_batches_tracked for bn in self._bns() if bn.num_batches_tracked is not None]
+            if nbt:
+                torch._foreach_add_(nbt, nseg)
+            return y, saved
+        if i < 4:
+            saved = []
+            y = x
+            for b in self.layers[i]:
+                y, sb = b.forward(y, nseg, code)
+                saved.append(sb)
+            return y, saved
+        saved = []
+        y = x
         for d in self.deconvs:
             y, sd = d.forward(y, nseg, code)
-            saved['deconvs'].append(sd)
-        saved['head_in'] = y
+            saved.append(sd)
         hm = ops.head1x1_nchw(y, self.head_w, self.njoints, self.head_b, code)
-        # num_batches_tracked += nseg for every BatchNorm (the reference's V backbone calls
-        # each add 1): one multi-tensor launch instead of one tiny kernel per layer
-        nbt = [bn.num_batches_tracked for bn in self._bns() if bn.num_batches_tracked is not None]
-        if nbt:
-            torch._foreach_add_(nbt, nseg)
-        return hm, x1, y, saved
+        return (hm, y), (saved, y)
+
+    def backward_stage(self, i, saved, gouts, nseg):
+        """Stage i's backward: gradient of its input activation (None for stage 0) and a _Grads
+        of its parameters, whose side-stream launches end with a recorded event."""
+        code = self.code
+        if SIDE_STREAM_WGRAD and self.side is None:
+            dev = self.head.weight.device
+            self.side = torch.cuda.Stream(dev)
+        grads = _Grads(self.side if SIDE_STREAM_WGRAD else None)
+        if i == 4:
+            dhm, df = gouts
+            dsaved, f = saved
+            g = None
+            if dhm is not None:
+                gh = ops.pack_nchw_to_nhwc(dhm.contiguous().float(), code, HEAD_CPAD)
+                fl = self.head
+                grads.wgrad(fl.weight, lambda: T.conv2d_wgrad(gh, f, f.shape[3], 1, 1, 1, 0, code)[:self.njoints]
+                            .contiguous(), gh, f)
+                if fl.bias is not None:
+                    grads[fl.bias] = T.channel_sum(gh)[:self.njoints].contiguous()
+                g = T.conv2d_dgrad(gh, self.head_wt, f.shape[3], 1, 1, 1, 0, f.shape[1:3], code)
+            if df is not None:   # the deconv features used by the caller's loss as well
+                df = df.contiguous()
+                g = df if g is None else g.add_(df)
+            if g is None:
+                return None, grads.close()
+            for d, sd in zip(reversed(self.deconvs), reversed(dsaved)):
+                g = d.backward(g, sd, nseg, code, grads)
+            return g, grads.close()
+        (g,) = gouts
+        if g is None:
+            return None, grads.close()
+        g = g.contiguous()
+        blocks = self.layers[i]
+        sblocks = saved['blocks'] if i == 0 else saved
+        for b, sb in zip(reversed(blocks), reversed(sblocks)):
+            g = b.backward(g, sb, nseg, code, grads)
+        if i == 0:
+            g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
+            self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
+            g = None
+        return g, grads.close()
 
     def _bns(self):
         out = [u.bn for u in self.units()] + [d.bn for d in self.deconvs]
         return out
 
-    def backward(self, dhm, saved, nseg):
-        """dL/dheatmaps (NCHW f32) -> {parameter: gradient (f32, parameter layout)}."""
-        code = self.code
-        dev = dhm.device
-        if SIDE_STREAM_WGRAD and self.side is None:
-            self.side = torch.cuda.Stream(dev)
-        grads = _Grads(self.side if SIDE_STREAM_WGRAD else None)
-        f = saved['head_in']
-        gh = ops.pack_nchw_to_nhwc(dhm, code, HEAD_CPAD)
-        fl = self.head
-        grads.wgrad(fl.weight, lambda: T.conv2d_wgrad(gh, f, f.shape[3], 1, 1, 1, 0, code)[:self.njoints].contiguous(),
-                    gh, f)
-        if fl.bias is not None:
-            grads[fl.bias] = T.channel_sum(gh)[:self.njoints].contiguous()
-        g = T.conv2d_dgrad(gh, self.head_wt, f.shape[3], 1, 1, 1, 0, f.shape[1:3], code)
-        for d, sd in zip(reversed(self.deconvs), reversed(saved['deconvs'])):
-            g = d.backward(g, sd, nseg, code, grads)
-        blocks = [b for layer in self.layers for b in layer]
-        for b, sb in zip(reversed(blocks), reversed(saved['blocks'])):
-            g = b.backward(g, sb, nseg, code, grads)
-        g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
-        self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
-        grads.join(dev)
-        return dict(grads)
+
+# Hand-off of a stage's parameter gradients to autograd: 'delayed' returns them from the NEXT
+# stage's backward (the earlier layers'), so the current stream waits for a stage's side-stream
+# weight gradients one stage later, when they have long finished; 'joined' returns them from
+# the stage itself (the current stream waits for the stage's last weight gradient right away)
+GRAD_HANDOFF = 'delayed'
 
 
-class _PoseResNetTrainFn(torch.autograd.Function):
+class _Stage:
+    """One stage of one training forward: the plan, the stage index, the BN segment count and
+    the stages' shared hand-off table {stage: (_Grads, its side-stream event)}."""
+
+    def __init__(self, plan, i, nseg, pending):
+        self.plan, self.i, self.nseg, self.pending = plan, i, nseg, pending
+
+    def take(self, j):
+        grads = self.pending.pop(j, None)
+        if grads is None:
+            return {}
+        grads.wait()
+        return grads
+
+
+def _handoff_stages(i, nstages):
+    """Stages whose gradients stage i's backward returns (GRAD_HANDOFF)."""
+    if GRAD_HANDOFF == 'joined':
+        return [i]
+    return ([i] if i == 0 else []) + ([i + 1] if i + 1 < nstages else [])
+
+
+class _StageFn(torch.autograd.Function):
+    """forward(x, stage, *params) -> the stage's outputs; backward returns the input activation's
+    gradient and the gradients of `params` (the parameters of the stages _handoff_stages names;
+    every other stage's parameters among them get None)."""
+
     @staticmethod
-    def forward(ctx, x, plan, nseg, *params):
-        hm, x1, f, saved = plan.forward(x, nseg)
-        ctx.plan, ctx.saved, ctx.nseg, ctx.params = plan, saved, nseg, params
-        ctx.mark_non_differentiable(x1, f)
-        return hm, x1, f
+    def forward(ctx, x, stage, *params):
+        ctx.set_materialize_grads(False)
+        outs, saved = stage.plan.forward_stage(stage.i, x, stage.nseg)
+        ctx.stage, ctx.saved, ctx.params = stage, saved, params
+        return outs
 
     @staticmethod
-    def backward(ctx, dhm, dx1, df):
-        if dhm is None:
-            return (None, None, None) + (None,) * len(ctx.params)
-        grads = ctx.plan.backward(dhm.contiguous().float(), ctx.saved, ctx.nseg)
+    def backward(ctx, *gouts):
+        st = ctx.stage
+        gx, grads = st.plan.backward_stage(st.i, ctx.saved, gouts, st.nseg)
         ctx.saved = None
-        return (None, None, None) + tuple(grads.get(p) for p in ctx.params)
+        st.pending[st.i] = grads
+        out = {}
+        for j in _handoff_stages(st.i, st.plan.NSTAGES):
+            out.update(st.take(j))
+        return (gx, None) + tuple(out.get(p) for p in ctx.params)
 
 
-def train_forward(net, plan, x, nseg):
-    """Differentiable training-mode forward: (heatmaps NCHW f32, layer1 out, deconv out);
-    the features are NCHW-shaped channels-last views, not differentiable."""
-    params = tuple(net.parameters())
-    hm, x1, f = _PoseResNetTrainFn.apply(x, plan, nseg, *params)
+def _stage_inputs(plan, i):
+    js = set(_handoff_stages(i, plan.NSTAGES)) | {i}
+    return tuple(p for j in sorted(js) for p in plan.stage_params(j))
+
+
+def train_forward(net, plan, views, nseg):
+    """Differentiable training-mode forward over a list of V views ([B, 3, H, W] each, V = nseg
+    BatchNorm segments): (heatmaps NCHW f32, layer1 out, deconv out) -- the features as
+    NCHW-shaped channels-last views, differentiable like the reference's (a loss on them adds
+    its gradient to the network's backward)."""
+    if torch.is_tensor(views):
+        views = [views]
+    pending = {}
+    y = views
+    for i in range(plan.NSTAGES - 1):
+        y = _StageFn.apply(y, _Stage(plan, i, nseg, pending), *_stage_inputs(plan, i))
+        if i == 0:
+            x1 = y
+    i = plan.NSTAGES - 1
+    hm, f = _StageFn.apply(y, _Stage(plan, i, nseg, pending), *_stage_inputs(plan, i))
     return hm, x1.permute(0, 3, 1, 2), f.permute(0, 3, 1, 2)
