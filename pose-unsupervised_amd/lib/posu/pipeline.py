@@ -72,19 +72,21 @@ def subset_meta(meta, host, groups):
     return sub, hs
 
 
-def synthetic_meta(ngroups, device, image_size=256, njoints=16, distortion=True, nviews=4):
-    """Crop affines / cameras / F table of a synthetic H36M-like batch (posu.synthetic)."""
+def synthetic_meta(ngroups, device, image_size=256, njoints=16, distortion=True, nviews=4, scale=5.0,
+                   pose_sigma=400.0):
+    """Crop affines / cameras / F table of a synthetic H36M-like batch (posu.synthetic): crops
+    centred on each group's projected root joint, `scale` x 200 px wide."""
     from utils.transforms import batch_inverse_affines
     from multiviews.triangulate import camera_tables
     from . import synthetic as syn
     cams = syn.group_cameras(ngroups, distortion=distortion)
-    poses = syn.synthetic_poses3d(ngroups, njoints)
+    poses = syn.synthetic_poses3d(ngroups, njoints, sigma=pose_sigma)
     from multiviews.cameras import project_pose
     centers = np.zeros((nviews, ngroups, 2))
     for g in range(ngroups):
         for v in range(nviews):
             centers[v, g] = project_pose(poses[g, :1], cams[g * nviews + v])[0]
-    scales = np.full((nviews, ngroups, 2), 5.0)
+    scales = np.full((nviews, ngroups, 2), float(scale))
     hm = image_size // 4
     aff = batch_inverse_affines(centers.reshape(-1, 2), scales.reshape(-1, 2), [hm, hm])
     M, intr = camera_tables(cams, nviews, no_distortion=not distortion)

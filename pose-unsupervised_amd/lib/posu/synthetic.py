@@ -200,10 +200,10 @@ def h36m_like_cameras(subject=9, distortion=True):
     return cams
 
 
-def synthetic_poses3d(ngroups, njoints=16, seed=0):
+def synthetic_poses3d(ngroups, njoints=16, seed=0, sigma=400.0):
     r = np.random.default_rng(seed)
     root = np.array([0.0, 0.0, 900.0])
-    return root + r.normal(0.0, 400.0, size=(ngroups, njoints, 3))
+    return root + r.normal(0.0, sigma, size=(ngroups, njoints, 3))
 
 
 def group_subjects(ngroups):

@@ -48,7 +48,7 @@ def oracle_run():
     net = get_pose_net(syn.make_cfg(num_layers=LAYERS, image_size=SIZE), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(LAYERS, SIZE))
     _, host = synthetic_meta(GROUPS, 'cpu', image_size=SIZE)
-    views = syn.synthetic_views(4, GROUPS, SIZE, seed=100)   # = bench.input_views(rank 0, batch 0)
+    views = syn.group_views(4, range(GROUPS), SIZE, seed=100)   # = bench.input_views(all groups, batch 0)
     ref = bench.oracle_chain(sd, LAYERS, SIZE, views, host, full=True)
     ref['host'] = host
     # the reference path's own fp32 error: the same forward in fp64 (the oracle is
@@ -67,7 +67,7 @@ def _bench_plan_outputs(cuda, precision, autotune, layers=LAYERS, size=SIZE, gro
     net = bench.build_model(layers, size, precision, cuda)
     meta, _ = synthetic_meta(groups, cuda, image_size=size)
     plan = net.plan(cuda)
-    rep = bench.Replayer(plan, bench.input_views(groups, size, 0, 0, cuda), meta, groups, 1, True, cuda)
+    rep = bench.Replayer(plan, bench.input_views(list(range(groups)), size, 0, cuda), meta, groups, 1, True, cuda)
     with torch.no_grad():
         rep.stage_geo(rep.stage_net())
         if autotune:
@@ -121,7 +121,7 @@ def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda):
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
                                   bn_stats=syn.load_bn_stats(layers, size))
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
-    views = syn.synthetic_views(4, groups, size, seed=100)
+    views = syn.group_views(4, range(groups), size, seed=100)
     ref = bench.oracle_chain(sd, layers, size, views, host, full=True)
     ref['host'] = host
     out = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=groups)

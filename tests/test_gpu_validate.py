@@ -142,3 +142,106 @@ def test_validate_batch_aggre_loss_terms(cuda):
     ref = ref + torch.nn.functional.mse_loss(torch.cat([r[sel] for r in raw]), torch.cat([a[sel] for a in agg]))
     ref = ref + sum(G.joints_mse(o, t, w) for o, t, w in zip(out, target, weight)) * 0.7
     np.testing.assert_allclose(res['loss'], float(ref), rtol=1e-5)
+
+
+class _FakeH5:
+    """Stands in for h5py (absent from this image): records what validate() writes."""
+
+    def __init__(self):
+        self.files = {}
+
+    def File(self, name, mode):   # noqa: N802 -- h5py's name
+        rec = self.files.setdefault(name, {'mode': mode})
+
+        class _F(dict):
+            def __enter__(self):
+                return self
+
+            def __exit__(self, *a):
+                rec.update(self)
+                return False
+
+            def close(self):
+                rec.update(self)
+        return _F()
+
+
+class _FakeDataset:
+    subset, dataset_type = 'validation', 'multiview_h36m'
+    flip_pairs = [[0, 5], [1, 4], [2, 3], [10, 15], [11, 14], [12, 13]]
+
+    def __init__(self, ngroups):
+        self.n = ngroups
+        # union-joint index -> dataset joint name ('*' = not annotated): 14 of 16 kept, out of order
+        names = ['j%d' % k for k in range(16)]
+        names[6] = names[9] = '*'
+        self.u2a_mapping = {k: names[k] for k in (3, 0, 1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 15, 14)}
+        self.evaluated = None
+
+    def __len__(self):
+        return self.n
+
+    def evaluate(self, preds, output_dir):
+        self.evaluated = preds.copy()
+        return {'mpjpe': 1.0}, 0.5
+
+
+@pytest.mark.parametrize('flip', [False, True])
+def test_validate_end_to_end_writes_the_reference_arrays(cuda, monkeypatch, tmp_path, flip):
+    """validate() over a two-batch loader (core/function.py:155-188, reference function.py:529-690):
+    the arrays handed to the h5 writer are the reference's -- heatmaps[:, u], locations[:, u]
+    (get_final_preds + maxvals, views interleaved view-minor per batch), joint_names_order = u
+    (the sorted annotated union joints) -- and dataset.evaluate gets all_preds[:, u]."""
+    import sys
+    from core import function as fn
+    from core.loss import JointsMSELoss
+    from models.multiview_pose_resnet import get_multiview_pose_net
+    from models.pose_resnet import get_pose_net
+    fake = _FakeH5()
+    monkeypatch.setitem(sys.modules, 'h5py', fake)
+    cfg = syn.make_cfg(num_layers=18, image_size=64, flip_test=flip, shift_heatmap=flip)
+    net = get_pose_net(cfg, is_train=False, precision='fp32')
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=4))
+    model = get_multiview_pose_net(net.to(cuda), cfg)
+    ds = _FakeDataset(ngroups=5)
+    rng = np.random.default_rng(0)
+    loader = []
+    for nb in (3, 2):
+        views = [torch.from_numpy(rng.standard_normal((nb, 3, 64, 64)).astype(np.float32)) for _ in range(4)]
+        target = [torch.from_numpy(rng.random((nb, 16, 16, 16)).astype(np.float32)) for _ in range(4)]
+        weight = [torch.ones(nb, 16, 1) for _ in range(4)]
+        meta = [{'center': torch.from_numpy(rng.uniform(100, 900, (nb, 2))),
+                 'scale': torch.from_numpy(rng.uniform(1, 3, (nb, 2))), 'source': ['h36m'] * nb} for _ in range(4)]
+        loader.append((views, target, weight, meta))
+    perf = fn.validate(cfg, loader, ds, {'base_model': model}, {'mse_weights': JointsMSELoss(True)}, str(tmp_path),
+                       None, 0)
+    assert perf == 0.5
+    (name, rec), = fake.files.items()
+    assert name.endswith('heatmaps_locations_validation_multiview_h36m.h5') and rec['mode'] == 'w'
+    u = np.array([0, 1, 2, 3, 4, 5, 7, 8, 10, 11, 12, 13, 14, 15])
+    np.testing.assert_array_equal(rec['joint_names_order'], u)
+    # expected: per batch, the views' heatmaps interleaved view-minor, decoded by the oracle
+    exp_hm, exp_loc = [], []
+    perm = torch.tensor(_perm(ds.flip_pairs), dtype=torch.int32, device=cuda)
+    for views, _, _, meta in loader:
+        nb = views[0].shape[0]
+        with torch.no_grad():
+            outs = [net(v.to(cuda))[0] for v in views]
+            if flip:
+                outf = [net(torch.flip(v, dims=[3]).to(cuda))[0] for v in views]
+                outs = [ops.flip_back(f, perm, hm=o, shift=True) for o, f in zip(outs, outf)]
+        hm = np.zeros((4 * nb, 16, 16, 16), np.float32)
+        loc = np.zeros((4 * nb, 16, 3), np.float32)
+        for k, (o, m) in enumerate(zip(outs, meta)):
+            o = o.cpu().numpy()
+            p, mv = G.get_final_preds(o, m['center'].numpy(), m['scale'].numpy())
+            hm[k::4] = o
+            loc[k::4, :, :2] = p
+            loc[k::4, :, 2:] = mv
+        exp_hm.append(hm)
+        exp_loc.append(loc)
+    exp_hm, exp_loc = np.concatenate(exp_hm), np.concatenate(exp_loc)
+    assert rec['heatmaps'].shape == (20, 14, 16, 16) and rec['locations'].shape == (20, 14, 3)
+    np.testing.assert_allclose(rec['heatmaps'], exp_hm[:, u], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(rec['locations'], exp_loc[:, u], rtol=0, atol=2e-3)
+    np.testing.assert_array_equal(ds.evaluated, rec['locations'])
