@@ -43,7 +43,9 @@ extern "C" {
 
 /* ---------------------------------------------------------------- runtime */
 const char* posu_last_error(void);
-/* 5: stateless conv knobs (4) + the fused layer1 Bottleneck kernels and batched weight packing */
+/* ABI revision: 4 stateless conv knobs; 5 the fused layer1 Bottleneck kernels and batched
+ * weight packing; 6 the LDS-tiled packing; 7 the layer3 Bottleneck tail; 8 the crop warp
+ * (posu_crop_warp).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -176,17 +178,6 @@ int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, in
                         const float* b2, const void* w3, const float* s3, const float* b3, void* y,
                         void* stream);
 
-/* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
- * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn
- * share one accumulator (as in posu_conv1x1_dual_fwd),
- *   y = relu( [w3*s3 | wd*sd] . [t2 ; x] + shift3 ),  t2 = conv2 output as above,
- * x read once (conv1 input and downsample input), y written once.  W = 64, C = P = 64,
- * 4P = 256 output channels; dtype BF16 / F16.
- *   x: [N, H, W, C]; y: [N, H, W, 4P] (must not alias x);
- *   w1: [P][C] (natural channel order), s1/b1 [P]; w2, s2, b2 as posu_bottleneck_fwd;
- *   w3d: [4P][2P]: columns 0..P-1 = conv3 weight * s3 with the posu_bottleneck_fwd column
- *        permutation of w3, columns P..2P-1 = downsample weight * sd (natural order);
- *   shift3: [4P] f32 = b3 + bd. */
 /* The identity Bottleneck of layer2 (lib/models/pose_resnet.py:61-99) as one launch, with the
  * weights streamed through LDS (they do not fit): W = 32, C = 512, P = 128, H % 4 == 0; dtype
  * BF16 / F16.  x, y: [N, H, W, C] (no alias); w1 [P][C], w2 [P][9P], w3 [C][P] in
@@ -208,6 +199,17 @@ int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, i
                               const void* w2, const float* s2, const float* b2, const void* w3,
                               const float* s3, const float* b3, void* y, void* stream);
 
+/* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
+ * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn
+ * share one accumulator (as in posu_conv1x1_dual_fwd),
+ *   y = relu( [w3*s3 | wd*sd] . [t2 ; x] + shift3 ),  t2 = conv2 output as above,
+ * x read once (conv1 input and downsample input), y written once.  W = 64, C = P = 64,
+ * 4P = 256 output channels; dtype BF16 / F16.
+ *   x: [N, H, W, C]; y: [N, H, W, 4P] (must not alias x);
+ *   w1: [P][C] (natural channel order), s1/b1 [P]; w2, s2, b2 as posu_bottleneck_fwd;
+ *   w3d: [4P][2P]: columns 0..P-1 = conv3 weight * s3 with the posu_bottleneck_fwd column
+ *        permutation of w3, columns P..2P-1 = downsample weight * sd (natural order);
+ *   shift3: [4P] f32 = b3 + bd. */
 int posu_bottleneck_down_fwd(int dtype, const void* x, int N, int H, int W, int C, int P,
                              const void* w1, const float* s1, const float* b1, const void* w2,
                              const float* s2, const float* b2, const void* w3d, const float* shift3,
@@ -310,6 +312,20 @@ int posu_flip_back(const float* hm_flipped, const int* perm, const float* hm, in
                    int H, int W, int shift, float* out, void* stream);
 
 /* ------------------------------------------------------------ data path */
+/* The crop of JointsDatasetCompatible.__getitem__ (lib/dataset/joints_dataset_compatible.py
+ * :161-172): per sample, cv2.warpAffine(img, trans, (dw, dh), flags=INTER_LINEAR) with the
+ * default constant-0 border, computed as OpenCV 3.4 does (the matrix inverted in double,
+ * coordinates in 1/1024-px fixed point rounded half to even, 1/32-px bilinear weights, 15-bit
+ * fixed-point sum); mode 1 fuses torchvision ToTensor + Normalize (the network input).
+ *   src: uint8 HWC images, sample n at byte offset src_off[n] with height / width
+ *        src_hw[2n], src_hw[2n + 1], C channels (all device arrays);
+ *   M:   [N][2][3] f64 src -> dst matrices (get_affine_transform, not inverted);
+ *   mode 0: out uint8 [N, dh, dw, C] (cv2.warpAffine's result);
+ *   mode 1: out f32 [N, C, dh, dw] = (v / 255 - mean[c]) / std[c] (mean, std: [C] f32). */
+int posu_crop_warp(const unsigned char* src, const long long* src_off, const int* src_hw, int C,
+                   const double* M, int N, int dh, int dw, int mode, const float* mean, const float* std,
+                   void* out, void* stream);
+
 /* Gaussian target heatmaps of a batch (JointsDatasetCompatible.generate_heatmap,
  * lib/dataset/joints_dataset_compatible.py:215-253): joints [N, J, 2] f32 in crop px,
  * vis [N, J] f32 (joints_vis[:, 0]); target [N, J, hm_h, hm_w] f32, weight [N, J] f32;

@@ -10,6 +10,12 @@ Sources (paths relative to the reference repo):
   fundamental_loss    lib/core/loss.py:101-133
   joints_mse          lib/core/loss.py:70-86
   project_point_radial lib/multiviews/cameras.py:25-49
+  warp_affine_linear  lib/dataset/joints_dataset_compatible.py:161-164 cv2.warpAffine(INTER_LINEAR,
+                      BORDER_CONSTANT 0) as OpenCV 3.4 (requirements.txt: opencv-python
+                      3.4.1.15) computes it: the affine inverted in double, coordinates in
+                      1/1024-px fixed point (cvRound), 1/32-px bilinear weight table, 15-bit
+                      fixed-point sum -- OpenCV is absent here: PARITY UNPINNED
+  to_tensor_normalize torchvision ToTensor + Normalize (run/pose2d/train.py:151-158)
   triangulate_poses   lib/multiviews/triangulate.py:17-99 with pymvg's
                       CameraModel.undistort (OpenCV fixed point, 5 iterations) and
                       MultiCameraSystem.find3d (DLT rows, numpy SVD) restated
@@ -20,6 +26,66 @@ import math
 
 import numpy as np
 import torch
+
+
+# ---------------------------------------------------------------- crop warp (data path)
+def _cv_round(x):
+    """cvRound on doubles: round half to even (lrint), as int64."""
+    return np.rint(x).astype(np.int64)
+
+
+def warp_affine_linear(src, M, dsize):
+    """cv2.warpAffine(src, M, dsize, flags=INTER_LINEAR) for uint8 [H, W, C] (border 0).
+    M: the 2x3 src -> dst matrix (get_affine_transform); dsize: (width, height)."""
+    src = np.asarray(src, dtype=np.uint8)
+    if src.ndim == 2:
+        src = src[:, :, None]
+    H, W, C = src.shape
+    dw, dh = int(dsize[0]), int(dsize[1])
+    m = np.asarray(M, dtype=np.float64).reshape(6).copy()
+    D = m[0] * m[4] - m[1] * m[3]                     # cv::warpAffine: invert (no WARP_INVERSE_MAP)
+    D = 1.0 / D if D != 0 else 0.0
+    a11, a22 = m[4] * D, m[0] * D
+    m[0], m[1], m[3], m[4] = a11, m[1] * -D, m[3] * -D, a22
+    b1 = -m[0] * m[2] - m[1] * m[5]
+    b2 = -m[3] * m[2] - m[4] * m[5]
+    m[2], m[5] = b1, b2
+    AB_BITS, INTER_BITS, TAB = 10, 5, 32
+    AB_SCALE = 1 << AB_BITS
+    round_delta = AB_SCALE // TAB // 2
+    xs = np.arange(dw, dtype=np.float64)
+    ys = np.arange(dh, dtype=np.float64)
+    adelta = _cv_round(m[0] * xs * AB_SCALE)
+    bdelta = _cv_round(m[3] * xs * AB_SCALE)
+    X0 = _cv_round((m[1] * ys + m[2]) * AB_SCALE) + round_delta
+    Y0 = _cv_round((m[4] * ys + m[5]) * AB_SCALE) + round_delta
+    X = (X0[:, None] + adelta[None, :]) >> (AB_BITS - INTER_BITS)
+    Y = (Y0[:, None] + bdelta[None, :]) >> (AB_BITS - INTER_BITS)
+    sx = np.clip(X >> INTER_BITS, -32768, 32767)
+    sy = np.clip(Y >> INTER_BITS, -32768, 32767)
+    fx, fy = X & (TAB - 1), Y & (TAB - 1)
+    # the bilinear table entries: (1 - fy/32, fy/32) x (1 - fx/32, fx/32) x 32768, exact integers
+    w = [(TAB - fy) * (TAB - fx) * 32, (TAB - fy) * fx * 32, fy * (TAB - fx) * 32, fy * fx * 32]
+    out = np.zeros((dh, dw, C), dtype=np.uint8)
+    outside = (sx >= W) | (sx + 1 < 0) | (sy >= H) | (sy + 1 < 0)   # whole pixel = the border value
+    acc = np.zeros((dh, dw, C), dtype=np.int64)
+    for k, (ox, oy) in enumerate(((0, 0), (1, 0), (0, 1), (1, 1))):
+        tx, ty = sx + ox, sy + oy
+        ok = (tx >= 0) & (tx < W) & (ty >= 0) & (ty < H)
+        v = src[np.clip(ty, 0, H - 1), np.clip(tx, 0, W - 1)].astype(np.int64)
+        acc += np.where(ok[..., None], v, 0) * w[k][..., None]
+    val = (acc + (1 << 14)) >> 15
+    out[:] = np.clip(val, 0, 255).astype(np.uint8)
+    out[outside] = 0
+    return out
+
+
+def to_tensor_normalize(img_u8, mean, std):
+    """torchvision ToTensor (HWC uint8 -> CHW float32 / 255) + Normalize ((x - mean) / std), f32."""
+    x = np.asarray(img_u8).transpose(2, 0, 1).astype(np.float32) / np.float32(255)
+    m = np.asarray(mean, dtype=np.float32)[:, None, None]
+    s = np.asarray(std, dtype=np.float32)[:, None, None]
+    return ((x - m) / s).astype(np.float32)
 
 
 # ---------------------------------------------------------------- heatmaps

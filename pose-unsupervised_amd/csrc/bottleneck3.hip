@@ -67,7 +67,7 @@ constexpr int kLds = kBN + 2 * kP * 4;
 constexpr int kS3 = kWin + kPx * 512;             // s3 b3 (1024 each) f32, over the window after conv2
 static_assert(kS3 + 2 * kC * 4 <= kRing, "t2 and BN3 fit over the window");
 static_assert(kLds <= 160 * 1024, "LDS");
-constexpr int kConv2Stages = 36, kStages = kConv2Stages + 16;
+constexpr int kConv2Stages = 36;
 
 __device__ __forceinline__ void ld8(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p);

@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -65,6 +65,7 @@ _SIGNATURES = {
     'posu_gemm_rows_f32': [_i, _p, _i, _i, _p, _i, _i, _p, _p],
     'posu_gaussian_targets': [_p, _p, _i, _i, _i, _i, _i, _i, _d, _p, _p, _p, _p],
     'posu_integral2d_fwd': [_p, _i, _i, _i, _i, _p, _p],
+    'posu_crop_warp': [_p, _p, _p, _i, _p, _i, _i, _i, _i, _p, _p, _p, _p],
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
