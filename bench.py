@@ -89,6 +89,8 @@ def parse():
     ap.add_argument('--fp32-steps', type=int, default=5, help='timed steps of the fp32 parity mode (0: skip)')
     ap.add_argument('--train-steps', type=int, default=10,
                     help='infer mode: timed steps of the configs[3] training step reported as train_mode (0: skip)')
+    ap.add_argument('--peaked-steps', type=int, default=1200,
+                    help='N = 1: fit steps of the peaked-heatmap network behind mpjpe_vs_ref_mm (0: skip)')
     ap.add_argument('--c1-steps', type=int, default=20,
                     help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
@@ -467,6 +469,25 @@ def triangulation_parity_all_ranks(res, dev):
     return {'mean': float('%.6g' % (tot / cnt)), 'max': float('%.6g' % mx), 'joints': int(cnt)}
 
 
+def peaked_parity(args, dev):
+    """tools/peaked.py: fit R50@256 to peaked targets through the training path, then the bf16 and
+    fp32 chains against the CPU oracle chain on those weights (the checker leg; N = 1)."""
+    sys.path.insert(0, os.path.join(REPO, 'tools'))
+    import peaked
+    t0 = time.perf_counter()
+    net, task = peaked.fit_peaked(dev, steps=args.peaked_steps)
+    torch.cuda.synchronize()
+    fit_s = time.perf_counter() - t0
+    out = {}
+    ref = None
+    for prec in ('fp32', args.precision):
+        out[prec], ref = peaked.parity(net, task, dev, prec, ref)
+    out['fit'] = {'steps': args.peaked_steps, 'seconds': round(fit_s, 2), 'groups': task['groups'],
+                  'heatmap_peak_mean': out['fp32']['heatmap_peak_mean'],
+                  'oracle_mpjpe_vs_gt_mm': out['fp32']['oracle_mpjpe_vs_gt_mm']}
+    return out
+
+
 def time_configs1(args, dev, rank, world, dist):
     """BASELINE configs[1]: the ResNet-50 heatmap forward alone on a synthetic 256x256 batch of 64
     frames in bf16 (tiles autotuned for that batch, one hipGraph, HIP events on the launch
@@ -558,20 +579,28 @@ def infer_main(args):
         if dist is not None:
             dist.destroy_process_group()
         return
-    cpu, mpjpe = None, None
+    cpu, mpjpe, random_w = None, None, None
     if world == 1 and not (args.no_cpu_baseline and args.no_mpjpe):
         cpu, ref = cpu_baseline(args.layers, args.size, args.groups,
                                 0.0 if args.no_cpu_baseline else args.cpu_baseline_seconds)
         if args.no_cpu_baseline:
             cpu = None
         if not args.no_mpjpe:
-            mpjpe = compare_with_reference(res, ref, res['meta'], dev)
-            mpjpe['what'] = ('%s pipeline vs the fp32 CPU oracle chain on the first input batch; mean/std/max: its '
-                             '2-D joint deviation laid on the synthetic poses\' projections and triangulated (mm, '
-                             'test_triangulate.py:98-102 arithmetic) -- see bench.compare_with_reference'
-                             % args.precision)
+            random_w = compare_with_reference(res, ref, res['meta'], dev)
+            random_w['what'] = ('%s pipeline vs the fp32 CPU oracle chain on the first input batch of the '
+                                'random-weight network (flat heatmaps); mean/std/max: its 2-D joint deviation laid on '
+                                'the synthetic poses\' projections and triangulated -- see bench.compare_with_reference'
+                                % args.precision)
             if fp32 is not None:
-                fp32['mpjpe_vs_ref_mm'] = compare_with_reference(r32, ref, r32['meta'], dev)
+                fp32['random_weight_chain_vs_ref'] = compare_with_reference(r32, ref, r32['meta'], dev)
+    peaked = None
+    if world == 1 and not args.no_mpjpe and args.peaked_steps > 0 and (args.layers, args.size) == (50, 256):
+        peaked = peaked_parity(args, dev)
+        mpjpe = dict(peaked[args.precision]['mpjpe_vs_ref_mm'])
+        mpjpe['what'] = ('%s chain (eval plan -> soft-argmax + crop affine -> fp64 DLT) vs the fp32 CPU oracle chain '
+                         'on a fitted R50@256 whose heatmaps peak (mean %.2f) where 8 synthetic 4-view poses project '
+                         '(tools/peaked.py); per-joint 3-D error in mm, test_triangulate.py:98-101 arithmetic; '
+                         'details in peaked_parity' % (args.precision, peaked['fit']['heatmap_peak_mean']))
     line = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
@@ -587,7 +616,9 @@ def infer_main(args):
         'network_ms': round(res['net_ms'], 4), 'decode_geometry_ms': round(res['geo_ms'], 4),
         'groups_per_s': round(value / 4, 2), 'per_rank_frames': [int(p[0]) for p in per_rank],
         'per_rank_seconds': [round(p[1], 5) for p in per_rank],
-        'mpjpe_vs_ref_mm': mpjpe, 'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32,
+        'mpjpe_vs_ref_mm': mpjpe, 'peaked_parity': peaked,
+        'random_weight_chain_vs_ref': random_w if world == 1 and not args.no_mpjpe else None,
+        'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32,
         'configs1': c1, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }

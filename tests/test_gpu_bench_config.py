@@ -31,12 +31,15 @@ pytestmark = pytest.mark.gpu
 
 GROUPS, LAYERS, SIZE = 32, 50, 256
 # measured on MI355X (round 2: fp32 hm 2.3e-5 / px 0.005 / mm 0.029; bf16 hm 0.19-0.21 / px 38-39).
-# bf16 has no mm gate: with random weights the heatmaps are flat noise and soft-argmax at
+# bf16 has no mm gate here: with random weights the heatmaps are flat noise and soft-argmax at
 # beta = 100 turns a 0.02 heatmap difference into a jump between noise maxima (tens of px),
 # which the DLT over four mutually inconsistent views turns into metres (472-3269 mm mean
-# between runs of the same code) -- the fp32 mode is the parity configuration.
+# between runs of the same code).  The mm gates of BASELINE.json (1e-2 mm, fp32) and of the
+# benched bf16 mode are in tests/test_gpu_peaked.py, on a fitted network's peaked heatmaps.
+# fp32 mm band: 0.05 (measured 0.029) -- on peakless maps the reference's OWN fp32 path sits
+# as far from its fp64 run (the 4x checks below), so 1e-2 mm is not reachable by any fp32 chain.
 BANDS = {
-    'fp32': {'hm_max': 1e-3, 'tri_max': 1e-2, 'loss_rel': 1e-5, 'px_mean': 0.02, 'mm_mean': 0.1},
+    'fp32': {'hm_max': 1e-3, 'tri_max': 1e-2, 'loss_rel': 1e-5, 'px_mean': 0.02, 'mm_mean': 0.05},
     'bf16': {'hm_max': 0.5, 'hm_mean': 0.05, 'tri_max': 1e-2, 'loss_rel': 1e-2, 'px_mean': 100.0, 'mm_mean': None},
 }
 

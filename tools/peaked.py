@@ -145,7 +145,8 @@ if __name__ == '__main__':
     dev = torch.device('cuda', 0)
     t0 = time.time()
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 300
-    net, task = fit_peaked(dev, steps=steps, log=print)
+    lr = float(sys.argv[2]) if len(sys.argv) > 2 else 1e-3
+    net, task = fit_peaked(dev, steps=steps, lr=lr, log=print)
     torch.cuda.synchronize()
     print('fitted in %.1f s' % (time.time() - t0))
     with torch.no_grad():
