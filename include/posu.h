@@ -199,6 +199,18 @@ int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, i
                               const void* w2, const float* s2, const float* b2, const void* w3,
                               const float* s3, const float* b3, void* y, void* stream);
 
+/* The tail of an identity Bottleneck of layer2 (W = 32, C = 512, P = 128) or layer3 (W = 16,
+ * C = 1024, P = 256) (lib/models/pose_resnet.py:79-99) with the weights streamed from L2
+ * straight into registers (each wave loads its own 2 n-tiles' MFMA fragments a few k-steps
+ * ahead; no LDS weight ring): conv2 3x3 + BN2 + ReLU -> conv3 1x1 + BN3 + residual + ReLU.
+ * t1 [N, H, W, P] (conv1 output), x [N, H, W, C], y [N, H, W, C], H a multiple of 8.
+ * wstream: packing.pack_tail_stream of the conv2 [P][9P] and conv3 [C][P] posu_conv2d_fwd packs,
+ * [P/32][9 P/32 + C/32][2][64][8] elements of dtype.  Bit-identical to posu_conv2d_fwd(conv2)
+ * followed by posu_conv2d_fwd(conv3, residual). */
+int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                    int P, const void* wstream, const float* s2, const float* b2,
+                                    const float* s3, const float* b3, void* y, void* stream);
+
 /* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
  * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn
  * share one accumulator (as in posu_conv1x1_dual_fwd),

@@ -1,0 +1,323 @@
+// Tail of an identity Bottleneck (lib/models/pose_resnet.py:79-99, eval mode, BN folded) of
+// PoseResNet at 256x256 with the weights streamed straight into registers, for layer2
+// (W = 32, planes 128, C = 512) and layer3 (W = 16, planes 256, C = 1024):
+//
+//     y = relu( bn3(conv3( relu(bn2(conv2_3x3(t1))) )) + x ),   t1 = conv1's output
+//
+// Why (csrc/bottleneck3.hip and bottleneck2.hip are the LDS-ring versions): those stream the
+// weights through a two-slot 32 KB LDS ring, so one 32 KB stage is in flight per CU and every
+// stage pays a full L2 round trip -- layer3's 52 stages x ~1.5 us = its 80 us (profiles/r02).
+// Here the LDS holds only activations; each wave loads its own weight fragments from L2 into
+// VGPRs kD k-steps ahead of their use (one contiguous 2 KB per k-step and wave, prepacked by
+// packing.pack_tail_stream), so 8 waves x kD x 2 KB are in flight and no barrier sits in the
+// weight stream.
+//
+// One workgroup (8 waves, one per CU) owns 8 image rows (128 px at W = 16, 256 px at W = 32).
+// Wave w: pixel group pg = w / NCQ (128 px = 8 m-tiles each, NPG = 8 / NCQ groups), channel
+// group cq = w % NCQ (32 output channels = 2 n-tiles of conv2, and of each conv3 chunk of
+// 32 NCQ channels).  The pixel operands come from LDS (8 x 1 KB ds_reads per 16 MFMAs).
+//   LDS: the t1 window (rows y0-1 .. y0+8, columns -1 .. W, zero padding; staged once by
+//        LDS-DMA), BN2; after conv2: t2 [8 W px][P ch] and BN3 over the window.
+//   weight stream of a wave: conv2 tap t, channel step c (p = KT t + c, KT = P / 32: the conv
+//        kernel's tap-major K order -- bit-identical accumulators), then conv3 chunk nc,
+//        channel step c (p = 9 KT + KT nc + c).
+// MFMA operands swapped (A = weights, B = pixels): lane (r16, q) accumulates channels
+// 4q .. 4q+3 of pixel r16; v_permlane16_swap pairs the 2 n-tiles into 8 consecutive channels.
+#include "gemm_common.h"
+
+namespace posu {
+namespace {
+
+struct TailSGeom {
+  const void* t1;
+  const void* x;
+  void* y;
+  const uint4* wst;  // [8 / NPG channel groups][steps][2 n-tiles][64 lanes] x 16 B
+  const float* s2;
+  const float* b2;
+  const float* s3;
+  const float* b3;
+  int N, H;
+};
+
+// timing ablations (tools/tail_ablations.sh; never set in the product build, wrong results):
+//   1 no MFMAs, 2 no weight loads in the loop, 4 no pixel-fragment LDS reads, 8 no conv3
+//   residual loads / y stores, 16 no window DMA
+#ifndef POSU_TS_ABLATE
+#define POSU_TS_ABLATE 0
+#endif
+constexpr int kAbl = POSU_TS_ABLATE;
+
+#ifndef POSU_TS_KD
+#define POSU_TS_KD 4
+#endif
+constexpr int kRows = 8;  // image rows per workgroup
+
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <int W, int P, int C>
+struct TailCfg {
+  static constexpr int kPx = kRows * W;            // tile pixels
+  static constexpr int kNPG = kPx / 128;           // pixel groups of 128 px
+  static constexpr int kNCQ = 8 / kNPG;            // channel groups of 32
+  static constexpr int kRowB = P * 2;              // LDS bytes per pixel (bf16 / fp16)
+  static constexpr int kWinCols = W + 2;
+  static constexpr int kWinPix = (kRows + 2) * kWinCols;
+  static constexpr int kBN2 = kWinPix * kRowB;     // s2 b2 f32 behind the window
+  static constexpr int kLds = kBN2 + 2 * P * 4;
+  static constexpr int kS3 = kPx * kRowB;          // s3 b3 f32 behind t2 (over the window)
+  static constexpr int kKT = P / 32;               // k-steps per tap / per conv3 chunk
+  static constexpr int kChunk = 32 * kNCQ;         // conv3 output channels per chunk
+  static constexpr int kNC = C / kChunk;           // conv3 chunks
+  static constexpr int kSteps = 9 * kKT + kNC * kKT;
+  static constexpr int kD = POSU_TS_KD < kKT ? POSU_TS_KD : kKT;  // weight prefetch depth (k-steps)
+  static_assert(kNPG * kNCQ == 8 && kNPG >= 1, "8 waves");
+  static_assert(kS3 + 2 * C * 4 <= kBN2, "t2 and BN3 fit over the window");
+  static_assert(kLds <= 160 * 1024, "LDS");
+  static_assert(kKT % kD == 0, "the ring slot of a k-step is static inside a block");
+};
+
+// P-channel LDS row of pixel `pix`, 16-B chunk `chunk`: the chunk index XOR `key` = the pixel's
+// column (in its LDS image) & 15.  Keyed by the column rather than the pixel index, the key of
+// an m-tile's lane is the same for every m-tile of a wave, so a k-step's fragment addresses are
+// four per-block base registers plus compile-time offsets (no address arithmetic in the loop).
+template <int RowB>
+__device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
+
+template <typename T, int W, int P, int C>
+__global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
+  using O = Op<T>;
+  using K = TailCfg<W, P, C>;
+  constexpr int ES = 2, kD = K::kD;
+  __shared__ __attribute__((aligned(16))) char smem[K::kLds];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const int pg = wu / K::kNCQ, cq = wu - pg * K::kNCQ;
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  const int H = g.H;
+  const int tiles_per_img = H / kRows;
+  const int n = blockIdx.x / tiles_per_img;
+  const int y0 = (blockIdx.x - n * tiles_per_img) * kRows;
+  float* bn2 = reinterpret_cast<float*>(smem + K::kBN2);
+  for (int c = tid; c < P; c += 512) {
+    bn2[c] = g.s2[c];
+    bn2[P + c] = g.b2[c];
+  }
+
+  // ---- the t1 window: 1 KB wave-instructions (1024 / kRowB pixels each), instruction m by wave m & 7
+  {
+    constexpr int kPixPerInst = 1024 / K::kRowB, kInst = K::kWinPix / kPixPerInst;
+    static_assert(K::kWinPix % kPixPerInst == 0, "whole instructions");
+    constexpr int kChunks = K::kRowB / 16;
+    const u32x4 t1s = make_srd(g.t1, g.N * H * W * P * ES);
+    const int sub = lane / kChunks, pc = lane % kChunks;
+#pragma unroll
+    for (int k = 0; k < (kInst + 7) / 8; ++k) {
+      const int m = wid + 8 * k;
+      if (m < kInst && !(kAbl & 16)) {  // wave-uniform
+        const int pix = kPixPerInst * m + sub;
+        const int wr = pix / K::kWinCols, wc = pix - wr * K::kWinCols;
+        const int yy = y0 + wr - 1, xx = wc - 1;
+        const int lc = pc ^ (wc & 15);
+        const bool ok = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < W;
+        dma16(t1s, ok ? (((n * H + yy) * W + xx) * P + 8 * lc) * ES : kOOB, lds0 + static_cast<unsigned>(m) * 1024u);
+      }
+    }
+  }
+
+  // ---- the weight stream: fragment j (n-tile 2 cq + j of the step's output group) of k-step p,
+  // one contiguous 2 KB per k-step and wave (prefetches past the end reload the last k-step)
+  const char* wst = reinterpret_cast<const char*>(g.wst) + cq * (K::kSteps * 2 * 1024);  // wave-uniform
+  const int wlane = lane * 16;
+  auto frag = [&](int p, int j) -> const uint4* {
+    return reinterpret_cast<const uint4*>(wst + (min(p, K::kSteps - 1) * 2 + j) * 1024 + wlane);
+  };
+  uint4 wa[kD][2];
+#pragma unroll
+  for (int d = 0; d < kD; ++d) {
+    wa[d][0] = *frag(d, 0);
+    wa[d][1] = *frag(d, 1);
+  }
+  vm_wait<0>();  // the window (LDS-DMA) and the first fragments
+  lds_barrier();
+
+  f32x4 acc[8][2];  // [m-tile i: tile pixels 128 pg + 16 i ..][n-tile j]
+  auto zero = [&] {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // the pair of n-tiles -> this lane's 8 consecutive channels cpair .. cpair + 7 of pixel r16
+  auto pair = [&](int i, float* v) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][0][e]), __float_as_uint(acc[i][1][e]),
+                                                       false, false);
+      v[e] = __uint_as_float(sw[0]);
+      v[4 + e] = __uint_as_float(sw[1]);
+    }
+  };
+  const int cpair = 16 * (q & 1) + 8 * (q >> 1);
+  // m-tile i's tile pixel (row-major in the tile) for this lane
+  auto tpix = [&](int i) { return 128 * pg + 16 * i + r16; };
+  // one block of kKT k-steps (one conv2 tap, or one conv3 output chunk over t2's P channels):
+  // k-step d reads, for m-tile i, the pixel lpix + coff(i) (coff compile-time) of an LDS image
+  // with `cols` pixels per row at 16-B chunk 4 d + q, swizzled by the lane's key (column & 15).
+  // The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run (two register
+  // sets); the scheduling barriers keep the compiler from hoisting more of them.
+  auto block = [&](int blk, int lpix, int key, auto coff) {
+    uint4 b[2][8];
+    // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3))
+    const char* lb = smem + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
+    const char* kb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kb[k] = lb + ((k ^ (key >> 2)) << 6);
+    auto rd = [&](int i, int d) -> uint4 {
+      if (kAbl & 4) return make_uint4(i, d, lane, blk);
+      return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d & 4) * 64);
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[0][i] = rd(i, 0);
+#pragma unroll
+    for (int d = 0; d < K::kKT; ++d) {
+      if (d + 1 < K::kKT) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) b[(d + 1) & 1][i] = rd(i, d + 1);
+      }
+      const int s = d % kD;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d & 1][i].y);
+          else O::mma(acc[i][j], wa[s][j], b[d & 1][i]);
+        }
+      const int p = K::kKT * blk + d + kD;
+      if (!(kAbl & 2)) {
+        wa[s][0] = *frag(p, 0);
+        wa[s][1] = *frag(p, 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- conv2: 9 taps x kKT channel steps over the window
+  zero();
+#pragma unroll 1
+  for (int t = 0; t < 9; ++t) {
+    const int dy = t / 3, dx = t - 3 * (t / 3);
+    // window pixel of m-tile i: tile row (128 pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
+    block(t, ((128 / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
+          [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
+  }
+  // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
+  lds_barrier();
+  {
+    float* b3l = reinterpret_cast<float*>(smem + K::kS3);
+    for (int c = tid; c < C; c += 512) {
+      b3l[c] = g.s3[c];
+      b3l[C + c] = g.b3[c];
+    }
+    const int c0 = 32 * cq + cpair;
+    float sc[8], sh[8];
+    ld8(bn2 + c0, sc);
+    ld8(bn2 + P + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8];
+      pair(i, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+      *reinterpret_cast<uint4*>(smem + swzp<K::kRowB>(tpix(i), r16, c0 >> 3)) = O::store_vals(v);
+    }
+  }
+  lds_barrier();
+
+  // ---- conv3: output chunk nc (kChunk channels; this wave's 32), kKT channel steps over t2
+  const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
+  T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C;
+  const float* b3l = reinterpret_cast<const float*>(smem + K::kS3);
+#pragma unroll 1
+  for (int nc = 0; nc < K::kNC; ++nc) {
+    const int c0 = K::kChunk * nc + 32 * cq + cpair;
+    // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
+    // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
+    uint4 rv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      rv[i] = (kAbl & 8) ? make_uint4(i, c0, 0, 0) : *reinterpret_cast<const uint4*>(xg + tpix(i) * C + c0);
+    zero();
+    block(9 + nc, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
+    float sc[8], sh[8];
+    ld8(b3l + c0, sc);
+    ld8(b3l + C + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8], r[8];
+      pair(i, v);
+      O::load_vals(rv[i], r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+      const uint4 o = O::store_vals(v);
+      if (kAbl & 8) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+      else *reinterpret_cast<uint4*>(yg + tpix(i) * C + c0) = o;
+    }
+  }
+}
+
+template <int W, int P, int C>
+void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
+  const dim3 grid(static_cast<unsigned>(g.N * (g.H / kRows)));
+  if (dtype == POSU_BF16)
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C>), grid, dim3(512), 0, s, g);
+  else
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C>), grid, dim3(512), 0, s, g);
+}
+
+}  // namespace
+}  // namespace posu
+
+using namespace posu;
+
+extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                               int P, const void* wstream, const float* s2, const float* b2,
+                                               const float* s3, const float* b3, void* y, void* stream) {
+  const std::string what = "posu_bottleneck_tail_stream_fwd";
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, what + ": dtype must be BF16 or F16");
+  POSU_REQUIRE(t1 && x && wstream && s2 && b2 && s3 && b3 && y, what + ": null pointer");
+  POSU_REQUIRE(x != y && t1 != y, what + ": the output must not alias an input");
+  const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
+  POSU_REQUIRE(l2 || l3, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16, C = 1024, "
+                                "planes = 256) of PoseResNet at 256x256");
+  POSU_REQUIRE(N > 0 && H > 0 && H % kRows == 0, what + ": H must be a positive multiple of 8");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
+               what + ": activation exceeds the 2 GiB addressing range");
+  for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(s3),
+                        static_cast<const void*>(b3)})
+    POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, what + ": pointers must be 16-byte aligned");
+  TailSGeom g{};
+  g.t1 = t1;
+  g.x = x;
+  g.y = y;
+  g.wst = static_cast<const uint4*>(wstream);
+  g.s2 = s2;
+  g.b2 = b2;
+  g.s3 = s3;
+  g.b3 = b3;
+  g.N = N;
+  g.H = H;
+  hipStream_t s = as_stream(stream);
+  if (l3)
+    launch_tail<16, 256, 1024>(dtype, g, s);
+  else
+    launch_tail<32, 128, 512>(dtype, g, s);
+  return check_launch(what.c_str());
+}

@@ -119,6 +119,18 @@ def bottleneck3_tail_nhwc(t1, x, w2, s2, b2, w3, s3, b3, code, out=None):
     return out
 
 
+def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
+    """conv2 + conv3 (+ residual) of a layer2 / layer3 identity Bottleneck with the weights
+    streamed into registers (posu_bottleneck_tail_stream_fwd, csrc/tail_stream.hip);
+    wstream = packing.pack_tail_stream(conv2 pack, conv3 pack)."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty_like(x)
+    call('posu_bottleneck_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream), ptr(s2),
+         ptr(b2), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
+    return out
+
+
 def bottleneck_down_nhwc(x, w1, s1, b1, w2, s2, b2, w3d, shift3, code, out=None):
     """Fused first Bottleneck of layer1 with its downsample (posu_bottleneck_down_fwd):
     x [N, H, W, C] -> y [N, H, W, w3d.shape[0]]."""

@@ -28,6 +28,29 @@ def pack_conv_weight(w, cin_pad, bk, dtype):
     return out.to(dtype).contiguous()
 
 
+def mfma_fragments(wpk):
+    """[Cout][K] (posu_conv2d_fwd packing) -> [Cout/16][K/32][64 lanes][8]: the MFMA A operand of
+    n-tile nt and k-step ks as one contiguous 1 KB block -- lane q * 16 + r holds row 16 nt + r,
+    columns 32 ks + 8 q .. + 7 (v_mfma_f32_16x16x32 operand layout)."""
+    co, k = wpk.shape
+    return wpk.reshape(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(co // 16, k // 32, 64, 8)
+
+
+def pack_tail_stream(w2pk, w3pk):
+    """The per-wave weight streams of posu_bottleneck_tail_stream_fwd (csrc/tail_stream.hip) from
+    the conv2 [P][9P] and conv3 [C][P] posu_conv2d_fwd packs: [NCQ][9 KT + NC KT][2][64][8] with
+    NCQ = P / 32 channel groups, KT = P / 32 k-steps per tap, NC = C / P conv3 chunks.  Group cq,
+    k-step p < 9 KT: conv2 n-tile 2 cq + j, k-step p; p = 9 KT + KT nc + c: conv3 n-tile
+    2 NCQ nc + 2 cq + j, k-step c."""
+    planes, c = w2pk.shape[0], w3pk.shape[0]
+    ncq, kt, nc = planes // 32, planes // 32, c // planes
+    f2 = mfma_fragments(w2pk)                                    # [2 ncq][9 kt][64][8]
+    f3 = mfma_fragments(w3pk)                                    # [2 ncq nc][kt][64][8]
+    s2 = f2.reshape(ncq, 2, 9 * kt, 64, 8).permute(0, 2, 1, 3, 4)
+    s3 = f3.reshape(nc, ncq, 2, kt, 64, 8).permute(1, 0, 3, 2, 4, 5).reshape(ncq, nc * kt, 2, 64, 8)
+    return torch.cat([s2, s3], dim=1).contiguous()
+
+
 def bottleneck_conv3_order(planes):
     """Input-channel order of the fused Bottleneck's conv3 K (csrc/bottleneck.hip): column
     32 b + 8 q + e reads channel 32 b + 16 (e >> 2) + 4 q + (e & 3) -- the order in which

@@ -19,7 +19,7 @@ import torch
 from . import ops
 from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
                       pack_conv_weight, pack_deconv4x4_weight,
-                      pack_dual_1x1_weight, pack_stem_fused_weight, pack_stem_s2d_weight)
+                      pack_dual_1x1_weight, pack_stem_fused_weight, pack_stem_s2d_weight, pack_tail_stream)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
@@ -160,6 +160,9 @@ class _DualTail:
 # False runs the convolutions
 FUSED_BOTTLENECK = True
 FUSED_LAYER3_TAIL = True
+# layer3's tail on the register-streamed kernel (posu_bottleneck_tail_stream_fwd: 59 vs 76 us per
+# block, tools/tail_micro.py); False: the LDS-ring kernel (posu_bottleneck3_tail_fwd)
+STREAMED_LAYER3_TAIL = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -172,7 +175,7 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -183,6 +186,7 @@ class _Block:
         self.w3d = None              # the fused first block's [w3*s3 | wd*sd] (permuted conv3 K)
         self.l2 = False              # a layer2 identity block (fused kernel, the convs' own packs)
         self.l3 = False              # a layer3 identity block (conv1, then the fused conv2 + conv3 tail)
+        self.wst = None              # layer3: the tail's per-wave weight streams (pack_tail_stream)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -206,6 +210,8 @@ class _Block:
         elif code in (ops.BF16, ops.F16) and len(names) == 3:
             self.l2 = self._layer2_shape()
             self.l3 = self._layer3_shape()
+            if self.l3:
+                self.wst = pack_tail_stream(self.convs[1].w, self.convs[2].w)
 
     def _layer2_shape(self):
         c1, c2, c3 = self.convs
@@ -251,6 +257,9 @@ class _Block:
         if (self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and fits and x.shape[2] == 16 and
                 x.shape[1] % 8 == 0):
             c1, c2, c3 = self.convs
+            if STREAMED_LAYER3_TAIL:
+                return ops.bottleneck_tail_stream_nhwc(c1(x, code), x, self.wst, c2.scale, c2.shift, c3.scale,
+                                                       c3.shift, code, out=out)
             return ops.bottleneck3_tail_nhwc(c1(x, code), x, c2.w, c2.scale, c2.shift, c3.w, c3.scale, c3.shift, code,
                                              out=out)
         res = self.down(x, code) if self.down is not None else x

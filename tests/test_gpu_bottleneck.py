@@ -123,7 +123,7 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12), (128, 32)])
+@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12), (128, 32), (1, 16)])
 def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
     """Layer2's identity block (32-wide maps, 512 channels, planes 128; weights streamed
     through LDS): bit-identical to the three unfused launches (same K order per accumulator,
@@ -144,10 +144,16 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
     t1 = ops.conv2d_nhwc(xd, p1, 128, 1, 1, 1, 0, s[0], s[1], None, True, code)
     t2 = ops.conv2d_nhwc(t1, p2, 128, 3, 3, 1, 1, s[2], s[3], None, True, code)
     three = ops.conv2d_nhwc(t2, p3, 512, 1, 1, 1, 0, s[4], s[5], xd, True, code)
+    streamed = None
+    if h % 8 == 0:   # the register-streamed tail (conv1 launch + conv2/conv3 tail), 8-row tiles
+        streamed = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5],
+                                                   code, out=_sentinel(xd))
     torch.cuda.synchronize()
     d = (fused.float() - three.float()).abs()
     print('layer2 fused vs three launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
     assert torch.equal(fused, three)
+    if streamed is not None:
+        assert torch.equal(streamed, three)
     if ref is None:
         return
     got = fused.float().cpu().permute(0, 3, 1, 2)
@@ -176,12 +182,18 @@ def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
     s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
     t1 = ops.conv2d_nhwc(xd, p1, 256, 1, 1, 1, 0, s[0], s[1], None, True, code)
     fused = ops.bottleneck3_tail_nhwc(t1, xd, p2, s[2], s[3], p3, s[4], s[5], code, out=_sentinel(xd))
+    streamed = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5],
+                                                code, out=_sentinel(xd))
     t2 = ops.conv2d_nhwc(t1, p2, 256, 3, 3, 1, 1, s[2], s[3], None, True, code)
     two = ops.conv2d_nhwc(t2, p3, 1024, 1, 1, 1, 0, s[4], s[5], xd, True, code)
     torch.cuda.synchronize()
     d = (fused.float() - two.float()).abs()
     print('layer3 tail fused vs two launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
+    d2 = (streamed.float() - two.float()).abs()
+    print('layer3 tail register-streamed vs two launches: max %.3g, differing elements %d'
+          % (float(d2.max()), int((d2 > 0).sum())))
     assert torch.equal(fused, two)
+    assert torch.equal(streamed, two)
     if ref is None:
         return
     got = fused.float().cpu().permute(0, 3, 1, 2)

@@ -17,7 +17,8 @@ import json
 import os
 import sys
 
-NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'stem_pool_kernel', 'maxpool_kernel',
+NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'tail_stream_kernel', 'stem_pool_kernel',
+               'maxpool_kernel',
                'pack_s2d_kernel', 'pack_kernel')
 
 

@@ -10,7 +10,7 @@ import csv
 import json
 import sys
 
-NET = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'stem_pool_kernel', 'maxpool_kernel',
+NET = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'tail_stream_kernel', 'stem_pool_kernel', 'maxpool_kernel',
        'pack_s2d_kernel', 'pack_kernel')
 
 

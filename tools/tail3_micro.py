@@ -61,18 +61,26 @@ def main():
     def fused():
         ops.bottleneck3_tail_nhwc(t1, x, p2, s[0], s[1], p3, s[2], s[3], BF16, out=y)
 
+    wst = packing.pack_tail_stream(p2, p3)
+    y3 = torch.empty_like(x)
+
+    def streamed():
+        ops.bottleneck_tail_stream_nhwc(t1, x, wst, s[0], s[1], s[2], s[3], BF16, out=y3)
+
     def two(t_2=-1, t_3=-1):
         ops.conv2d_nhwc(t1, p2, 256, 3, 3, 1, 1, s[0], s[1], None, True, BF16, out=t2, tile=t_2)
         ops.conv2d_nhwc(t2, p3, 1024, 1, 1, 1, 0, s[2], s[3], x, True, BF16, out=y2, tile=t_3)
 
     us_f = timeit(fused, a.reps, a.rounds)
+    us_s = timeit(streamed, a.reps, a.rounds)
     us_2 = timeit(two, a.reps, a.rounds)
     us_2t = timeit(lambda: two(31, 23), a.reps, a.rounds)
     us_c2 = timeit(lambda: ops.conv2d_nhwc(t1, p2, 256, 3, 3, 1, 1, s[0], s[1], None, True, BF16, out=t2, tile=31),
                    a.reps, a.rounds)
     gf = 2.0 * a.n * 256 * (2304 * 256 + 256 * 1024) / 1e9
-    print('layer3 tail, batch %d: fused %.1f us (%.0f TFLOP/s) | two launches %.1f us (heuristic tiles), '
-          '%.1f us (tiles 31 + 23; conv2 alone %.1f us)' % (a.n, us_f, gf / us_f * 1e3, us_2, us_2t, us_c2))
+    print('layer3 tail, batch %d: register-streamed %.1f us (%.0f TFLOP/s), equal %s | LDS-ring fused %.1f us '
+          '(%.0f TFLOP/s) | two launches %.1f us (heuristic tiles), %.1f us (tiles 31 + 23; conv2 alone %.1f us)'
+          % (a.n, us_s, gf / us_s * 1e3, bool(torch.equal(y3, y)), us_f, gf / us_f * 1e3, us_2, us_2t, us_c2))
 
 
 if __name__ == '__main__':
