@@ -51,7 +51,6 @@ constexpr int kAbl = POSU_TS_ABLATE;
 #ifndef POSU_TS_KD
 #define POSU_TS_KD 4
 #endif
-constexpr int kRows = 8;  // image rows per workgroup
 
 __device__ __forceinline__ void ld8(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -60,11 +59,13 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C>
+template <int W, int P, int C, int ROWS, int NW>
 struct TailCfg {
+  static constexpr int kRows = ROWS;               // image rows per workgroup
+  static constexpr int kNW = NW;                   // waves per workgroup
   static constexpr int kPx = kRows * W;            // tile pixels
   static constexpr int kNPG = kPx / 128;           // pixel groups of 128 px
-  static constexpr int kNCQ = 8 / kNPG;            // channel groups of 32
+  static constexpr int kNCQ = NW / kNPG;           // channel groups of 32
   static constexpr int kRowB = P * 2;              // LDS bytes per pixel (bf16 / fp16)
   static constexpr int kWinCols = W + 2;
   static constexpr int kWinPix = (kRows + 2) * kWinCols;
@@ -76,7 +77,7 @@ struct TailCfg {
   static constexpr int kNC = C / kChunk;           // conv3 chunks
   static constexpr int kSteps = 9 * kKT + kNC * kKT;
   static constexpr int kD = POSU_TS_KD < kKT ? POSU_TS_KD : kKT;  // weight prefetch depth (k-steps)
-  static_assert(kNPG * kNCQ == 8 && kNPG >= 1, "8 waves");
+  static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % 128 == 0, "every wave: 128 px x 32 channels");
   static_assert(kS3 + 2 * C * 4 <= kBN2, "t2 and BN3 fit over the window");
   static_assert(kLds <= 160 * 1024, "LDS");
   static_assert(kKT % kD == 0, "the ring slot of a k-step is static inside a block");
@@ -89,10 +90,11 @@ struct TailCfg {
 template <int RowB>
 __device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
 
-template <typename T, int W, int P, int C>
-__global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
+template <typename T, int W, int P, int C, int ROWS, int NW>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
-  using K = TailCfg<W, P, C>;
+  using K = TailCfg<W, P, C, ROWS, NW>;
+  constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
   __shared__ __attribute__((aligned(16))) char smem[K::kLds];
   const int tid = threadIdx.x;
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
   const int n = blockIdx.x / tiles_per_img;
   const int y0 = (blockIdx.x - n * tiles_per_img) * kRows;
   float* bn2 = reinterpret_cast<float*>(smem + K::kBN2);
-  for (int c = tid; c < P; c += 512) {
+  for (int c = tid; c < P; c += kThreads) {
     bn2[c] = g.s2[c];
     bn2[P + c] = g.b2[c];
   }
@@ -119,8 +121,8 @@ __global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
     const u32x4 t1s = make_srd(g.t1, g.N * H * W * P * ES);
     const int sub = lane / kChunks, pc = lane % kChunks;
 #pragma unroll
-    for (int k = 0; k < (kInst + 7) / 8; ++k) {
-      const int m = wid + 8 * k;
+    for (int k = 0; k < (kInst + NW - 1) / NW; ++k) {
+      const int m = wid + NW * k;
       if (m < kInst && !(kAbl & 16)) {  // wave-uniform
         const int pix = kPixPerInst * m + sub;
         const int wr = pix / K::kWinCols, wc = pix - wr * K::kWinCols;
@@ -222,7 +224,7 @@ __global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
   lds_barrier();
   {
     float* b3l = reinterpret_cast<float*>(smem + K::kS3);
-    for (int c = tid; c < C; c += 512) {
+    for (int c = tid; c < C; c += kThreads) {
       b3l[c] = g.s3[c];
       b3l[C + c] = g.b3[c];
     }
@@ -273,14 +275,22 @@ __global__ __launch_bounds__(512, 1) void tail_stream_kernel(TailSGeom g) {
   }
 }
 
-template <int W, int P, int C>
+template <int W, int P, int C, int ROWS, int NW>
 void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
-  const dim3 grid(static_cast<unsigned>(g.N * (g.H / kRows)));
+  const dim3 grid(static_cast<unsigned>(g.N * (g.H / ROWS)));
   if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C>), grid, dim3(512), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW>), grid, dim3(NW * 64), 0, s, g);
   else
-    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C>), grid, dim3(512), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW>), grid, dim3(NW * 64), 0, s, g);
 }
+
+// tiles: layer3 8 rows x 16 px with 8 waves (one workgroup per CU, 256 at batch 128); layer2
+// 4 rows x 32 px with 4 waves, two workgroups per CU, so one's conv3 epilogue (residual loads,
+// y stores) overlaps the other's MFMAs
+#ifndef POSU_TS_L2_ROWS
+#define POSU_TS_L2_ROWS 4
+#endif
+constexpr int kL2Rows = POSU_TS_L2_ROWS, kL2Waves = POSU_TS_L2_ROWS;
 
 }  // namespace
 }  // namespace posu
@@ -297,7 +307,9 @@ extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const 
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
   POSU_REQUIRE(l2 || l3, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16, C = 1024, "
                                 "planes = 256) of PoseResNet at 256x256");
-  POSU_REQUIRE(N > 0 && H > 0 && H % kRows == 0, what + ": H must be a positive multiple of 8");
+  const int rows = l3 ? 8 : kL2Rows;
+  POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
+               what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
   for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(s3),
@@ -316,8 +328,8 @@ extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const 
   g.H = H;
   hipStream_t s = as_stream(stream);
   if (l3)
-    launch_tail<16, 256, 1024>(dtype, g, s);
+    launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
   else
-    launch_tail<32, 128, 512>(dtype, g, s);
+    launch_tail<32, 128, 512, kL2Rows, kL2Waves>(dtype, g, s);
   return check_launch(what.c_str());
 }

@@ -145,7 +145,7 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
     t2 = ops.conv2d_nhwc(t1, p2, 128, 3, 3, 1, 1, s[2], s[3], None, True, code)
     three = ops.conv2d_nhwc(t2, p3, 512, 1, 1, 1, 0, s[4], s[5], xd, True, code)
     streamed = None
-    if h % 8 == 0:   # the register-streamed tail (conv1 launch + conv2/conv3 tail), 8-row tiles
+    if h % 4 == 0:   # the register-streamed tail (conv1 launch + conv2/conv3 tail), 4-row tiles
         streamed = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5],
                                                    code, out=_sentinel(xd))
     torch.cuda.synchronize()
