@@ -288,3 +288,24 @@ def test_fused_bottleneck_byte_guard():
     assert not P._fused_fits(big, 256)                   # 2 GiB of layer1 output
     assert not P._fused_fits(torch.empty((1024, 64, 64, 64), dtype=torch.bfloat16, device='meta'), 256)
     assert P._fused_fits(torch.empty((1023, 64, 64, 256), dtype=torch.bfloat16, device='meta'), 256)
+
+
+def test_u2a_indices_and_mpjpe_follow_test_triangulate():
+    """posu.metrics against run/test/test_triangulate.py:84-102 written out: the u2a mapping
+    (union index -> dataset index, '*' dropped, sorted by union index), pred3d[:, u] only for GT
+    2-D inputs, gt3d[:, a], per-joint Euclidean error mean / std / max."""
+    import numpy as np
+    from posu.metrics import mpjpe_stats, u2a_indices
+    u2a = {5: 2, 0: 0, 3: '*', 1: 4, 7: 1, 2: '*', 6: 3, 4: 5}
+    u, a = u2a_indices(u2a)
+    np.testing.assert_array_equal(u, [0, 1, 4, 5, 6, 7])
+    np.testing.assert_array_equal(a, [0, 4, 5, 2, 3, 1])
+    rng = np.random.default_rng(3)
+    pred_union = rng.normal(0, 500, (7, 8, 3))        # triangulated from GT 2-D: union order
+    gt = rng.normal(0, 500, (7, 6, 3))                # dataset order
+    st = mpjpe_stats(pred_union, gt, u, a, pred_in_union_order=False)
+    norm = np.linalg.norm(pred_union[:, u, :] - gt[:, a, :], axis=2)
+    assert st['mean'] == np.mean(norm) and st['std'] == np.std(norm) and st['max'] == np.amax(norm)
+    pred_sel = pred_union[:, u, :]                     # read from the validate() h5 (already u-selected)
+    st2 = mpjpe_stats(pred_sel, gt, u, a, pred_in_union_order=True)
+    assert st2['mean'] == st['mean'] and np.array_equal(st2['per_joint'], norm)
