@@ -380,22 +380,48 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) O::mma(acc[i][j], b[j], a[i]);
     };
-    POSU_DMA_TILE(0, 0);
+    // timing ablations (tools/igemm_ablations.sh; results wrong): POSU_IG_ABLATE bit 1 no
+    // MFMA, 2 no vmcnt wait, 4 no operand DMA, 8 no LDS fragment reads
+#ifndef POSU_IG_ABLATE
+#define POSU_IG_ABLATE 0
+#endif
+    constexpr int ABL = POSU_IG_ABLATE;
+    auto mmx = [&](const uint4 (&a)[TM], const uint4 (&b)[TN]) {
+      if constexpr (ABL & 1) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][0][0] += __builtin_bit_cast(float, a[i].x ^ b[i % TN].y);
+      } else {
+        mma(a, b);
+      }
+    };
+    auto rdx = [&](const char* As_, const char* Bs_, int cb, uint4 (&a)[TM], uint4 (&b)[TN]) {
+      if constexpr (ABL & 8) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) a[i] = make_uint4(cb, i, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) b[j] = make_uint4(j, cb, 0, 0);
+      } else {
+        read(As_, Bs_, cb, a, b);
+      }
+    };
+    if constexpr (!(ABL & 4)) POSU_DMA_TILE(0, 0);
     if (lag) __builtin_amdgcn_s_setprio(1);  // the lagging half wins issue arbitration (-2..-7 %)
     for (int kt = 0; kt < nk; ++kt) {
-      vm_wait<0>();
+      if constexpr (!(ABL & 2)) vm_wait<0>();
       __syncthreads();
-      if (kt + 1 < nk) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
+      if constexpr (!(ABL & 4))
+        if (kt + 1 < nk) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
       const char* As_ = smem + (kt & 1) * STAGE;
       const char* Bs_ = As_ + A_BYTES;
       uint4 af[TM], bfr[TN];
-      if (lag && kt > 0) mma(hA, hB);
-      read(As_, Bs_, 0, af, bfr);
-      mma(af, bfr);
-      read(As_, Bs_, 1, hA, hB);
-      if (!lag) mma(hA, hB);
+      if (lag && kt > 0) mmx(hA, hB);
+      rdx(As_, Bs_, 0, af, bfr);
+      mmx(af, bfr);
+      rdx(As_, Bs_, 1, hA, hB);
+      if (!lag) mmx(hA, hB);
     }
-    if (lag) mma(hA, hB);
+    if (lag) mmx(hA, hB);
+    if constexpr (ABL & 2) vm_wait<0>();
     __builtin_amdgcn_s_setprio(0);
   } else if constexpr (S == 1) {
     // single slot (short-K layers): a quarter of the LDS of a 2-slot ring, so more
