@@ -45,7 +45,7 @@ extern "C" {
 const char* posu_last_error(void);
 /* ABI revision: 4 stateless conv knobs; 5 the fused layer1 Bottleneck kernels and batched
  * weight packing; 6 the LDS-tiled packing; 7 the layer3 Bottleneck tail; 8 the crop warp
- * (posu_crop_warp); 9 the BN workspace's arrival counters (posu_bn_workspace).  The ctypes binding refuses a library of another revision. */
+ * (posu_crop_warp).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -442,10 +442,6 @@ int posu_conv2d_wgrad(int dtype, const void* dy, const void* x, int N, int H, in
  * views with separate statistics, torch.nn.functional.batch_norm(training=True)
  * per segment): mean/rstd/scale/shift [nseg, C] f32 out; running_mean/var
  * (optional) updated once per segment in order, unbiased variance. */
-/* workspace >= posu_bn_workspace(nseg, C) bytes; its first 256 bytes are arrival counters
- * (the statistics are finalized by the last block of each channel group, in the same
- * launch): zero them once when the workspace is allocated -- every call leaves them zero.
- * One workspace serves one stream at a time. */
 long long posu_bn_workspace(int nseg, int C);
 int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const float* gamma,
                       const float* beta, float eps, float momentum, float* running_mean,

@@ -47,117 +47,6 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
 //         mean is large against its spread keeps its variance in the f32 partials),
 //         else 0.  Block 0 of each segment stores K to kout [nseg][C].
 // MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0] (y optional)
-// What a finalize writes: MODE 0 the statistics (mean, rstd, the folded scale / shift, the
-// running statistics), MODE 1 the backward's coefficients and dgamma / dbeta.
-struct FinArgs {
-  const float* gamma;
-  const float* beta;
-  float eps, momentum;
-  const float* kshift;
-  float* running_mean;
-  float* running_var;
-  float* mean;
-  float* rstd;  // MODE 0: written; MODE 1: read
-  float* scale;
-  float* shift;
-  float* coef;
-  float* dgamma;
-  float* dbeta;
-};
-
-// one (segment, channel) of the forward statistics from the shifted sums
-__device__ __forceinline__ void stats_finalize_one(int seg, int c, int C, double n, double sum, double sq,
-                                                   const FinArgs& f, int Pseg) {
-  const double dm = sum / n;
-  const double mu = static_cast<double>(f.kshift[seg * C + c]) + dm;
-  const double var = fmax(sq / n - dm * dm, 0.0);
-  const double r = 1.0 / sqrt(var + static_cast<double>(f.eps));
-  const float gm = f.gamma ? f.gamma[c] : 1.f, bt = f.beta ? f.beta[c] : 0.f;
-  f.mean[seg * C + c] = static_cast<float>(mu);
-  f.rstd[seg * C + c] = static_cast<float>(r);
-  f.scale[seg * C + c] = static_cast<float>(gm * r);
-  f.shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
-  if (f.running_mean) f.running_mean[c] = (1.f - f.momentum) * f.running_mean[c] + f.momentum * static_cast<float>(mu);
-  if (f.running_var)
-    f.running_var[c] = (1.f - f.momentum) * f.running_var[c] +
-                       f.momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
-}
-
-// one (segment, channel) of the backward's coefficients
-__device__ __forceinline__ void bwd_finalize_one(int seg, int c, int C, double n, double sg, double sgx,
-                                                 const FinArgs& f) {
-  const float gm = f.gamma ? f.gamma[c] : 1.f;
-  f.coef[(seg * 3 + 0) * C + c] = gm * f.rstd[seg * C + c];
-  f.coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
-  f.coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
-}
-
-// The finalize of channels [c0, c0 + nch) (nch <= 512) by the block that wrote the last
-// partial of that channel group: L = 256 / nch lanes per channel (one channel pair per
-// thread at nch = 512) sum the group's partial blocks blk = ln, ln + L, ... of one
-// segment, the lanes combine in lane order, then lane 0 finalizes -- segments in order
-// per channel, so running statistics compose like the reference's per-view calls.
-template <int MODE>
-__device__ void finalize_group(const double* part, int nseg, int NB, int Pseg, int C, int c0, int nch,
-                               const FinArgs& f, double* red) {
-  const int tid = threadIdx.x;
-  const int L = nch >= 256 ? 1 : 256 / nch;
-  const int cpt = nch > 256 ? 2 : 1;  // channels per thread
-  const int cl = tid / L, ln = tid - cl * L;
-  const double n = static_cast<double>(Pseg);
-  double tg[2] = {0.0, 0.0}, tgx[2] = {0.0, 0.0};
-  for (int seg = 0; seg < nseg; ++seg) {
-    double a[2] = {0.0, 0.0}, b[2] = {0.0, 0.0};
-    const double* base = part + static_cast<size_t>(seg) * NB * 2 * C;
-#pragma unroll 4
-    for (int blk = ln; blk < NB; blk += L) {
-      const double* p = base + static_cast<size_t>(blk) * 2 * C + c0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        if (j < cpt && cl + 256 * j < nch) {
-          a[j] += p[cl + 256 * j];
-          b[j] += p[C + cl + 256 * j];
-        }
-    }
-    __syncthreads();  // red is free (the previous segment's combine has read it)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      red[(2 * j) * 256 + tid] = a[j];
-      red[(2 * j + 1) * 256 + tid] = b[j];
-    }
-    __syncthreads();
-    if (ln == 0) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = c0 + cl + 256 * j;
-        if (j >= cpt || cl + 256 * j >= nch) continue;
-        double s = 0.0, q = 0.0;
-        for (int l = 0; l < L; ++l) {
-          s += red[(2 * j) * 256 + tid + l];
-          q += red[(2 * j + 1) * 256 + tid + l];
-        }
-        if constexpr (MODE == 0) {
-          stats_finalize_one(seg, c, C, n, s, q, f, Pseg);
-        } else {
-          tg[j] += s;
-          tgx[j] += q;
-          bwd_finalize_one(seg, c, C, n, s, q, f);
-        }
-      }
-    }
-  }
-  if constexpr (MODE == 1) {
-    if (ln == 0)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int c = c0 + cl + 256 * j;
-        if (j >= cpt || cl + 256 * j >= nch) continue;
-        if (f.dgamma) f.dgamma[c] = static_cast<float>(tgx[j]);
-        if (f.dbeta) f.dbeta[c] = static_cast<float>(tg[j]);
-      }
-  }
-}
-
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z, const T* __restrict__ gy,
                                                          const T* __restrict__ y, const float* __restrict__ msc,
@@ -165,8 +54,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, int Pseg, int C,
                                                          RedShape rs, double* __restrict__ part,
-                                                         float* __restrict__ kout, int* __restrict__ arrivals,
-                                                         FinArgs fin) {
+                                                         float* __restrict__ kout) {
   constexpr int E = Vec<T>::E;
   __shared__ double red[2][256][E];
   const int tid = threadIdx.x;
@@ -285,27 +173,9 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       dst[C + ch * E + e] = red[1][tid][e];
     }
   }
-  if (!arrivals) return;
-  // Fused finalize: the last of the NB x nseg blocks of this channel group to arrive
-  // finalizes the group (release: partials (and kout) written back device-wide before the
-  // arrival; acquire: the last block's reads see every other block's partials).  The
-  // counter goes back to zero for the next launch on this workspace.
-  __shared__ int last;
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) {
-    const int old = atomicAdd(arrivals + blockIdx.y, 1);
-    last = old == rs.NB * static_cast<int>(gridDim.z) - 1;
-    if (last) atomicExch(arrivals + blockIdx.y, 0);
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  const int c0 = blockIdx.y * rs.CB * E;
-  finalize_group<MODE>(part, gridDim.z, rs.NB, Pseg, C, c0, min(rs.CB * E, C - c0), fin, &red[0][0][0]);
 }
 
-// ---- channel-sum finalize: one block per FCH channels, FLN lanes sum the partial blocks of up to
+// ---- finalize: one block per FCH channels, FLN lanes sum the partial blocks of up to
 // FSEG segments at once (every load of the pass in flight together: the partials are a few
 // hundred KiB, so this pass is latency-bound), fixed-order LDS combine.  Per segment the
 // summation order is the blocks' order, whatever the grouping.
@@ -347,6 +217,44 @@ __device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int
       }
     }
   __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                                int Pseg, int C, const float* __restrict__ gamma,
+                                                                const float* __restrict__ beta, float eps,
+                                                                float momentum, const float* __restrict__ kshift,
+                                                                float* running_mean,
+                                                                float* running_var, float* __restrict__ mean,
+                                                                float* __restrict__ rstd, float* __restrict__ scale,
+                                                                float* __restrict__ shift) {
+  __shared__ double red[2][FSEG][FLN][FCH];
+  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int c = blockIdx.x * FCH + cl;
+  const bool valid = c < C;
+  const double n = static_cast<double>(Pseg);
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    double sums[FSEG], sqs[FSEG];
+    const int ns = min(FSEG, nseg - seg0);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sums, sqs);
+    if (ln != 0 || !valid) continue;
+    for (int k = 0; k < ns; ++k) {  // in segment order: running stats compose like V calls
+      const int seg = seg0 + k;
+      const double sum = sums[k], sq = sqs[k];  // shifted by K = kshift[seg][c]
+      const double dm = sum / n;
+      const double mu = static_cast<double>(kshift[seg * C + c]) + dm;
+      const double var = fmax(sq / n - dm * dm, 0.0);
+      const double r = 1.0 / sqrt(var + static_cast<double>(eps));
+      const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+      mean[seg * C + c] = static_cast<float>(mu);
+      rstd[seg * C + c] = static_cast<float>(r);
+      scale[seg * C + c] = static_cast<float>(gm * r);
+      shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
+      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mu);
+      if (running_var)
+        running_var[c] = (1.f - momentum) * running_var[c] +
+                         momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+    }
+  }
 }
 
 // y = act(z * scale[seg] + shift[seg] (+ res)), one thread per 16-B chunk
@@ -530,6 +438,39 @@ inline bool seg_major(int C, int E, int nseg, int Pseg, std::initializer_list<co
   return cpr > 0 && 256 % cpr == 0 && nseg <= 65535 && n + static_cast<long long>(kSegU) * 1024 * 256 < (1LL << 31);
 }
 
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                              int Pseg, int C, const float* __restrict__ gamma,
+                                                              const float* __restrict__ rstd,
+                                                              float* __restrict__ coef, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  __shared__ double red[2][FSEG][FLN][FCH];
+  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int c = blockIdx.x * FCH + cl;
+  const bool valid = c < C;
+  const double n = static_cast<double>(Pseg);
+  double tg = 0.0, tgx = 0.0;
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    double sgs[FSEG], sgxs[FSEG];
+    const int ns = min(FSEG, nseg - seg0);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sgs, sgxs);
+    if (ln != 0 || !valid) continue;
+    for (int k = 0; k < ns; ++k) {
+      const int seg = seg0 + k;
+      const double sg = sgs[k], sgx = sgxs[k];
+      tg += sg;
+      tgx += sgx;
+      const float gm = gamma ? gamma[c] : 1.f;
+      coef[(seg * 3 + 0) * C + c] = gm * rstd[seg * C + c];
+      coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
+      coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
+    }
+  }
+  if (ln == 0 && valid) {
+    if (dgamma) dgamma[c] = static_cast<float>(tgx);
+    if (dbeta) dbeta[c] = static_cast<float>(tg);
+  }
+}
+
 // dz = gamma*rstd * (g' - mean(g') - xhat * mean(g' xhat)), g' = gy * [y > 0];
 // gres (optional) = g', the gradient of the residual branch
 template <typename T>
@@ -679,24 +620,13 @@ bool reducible(int C, int dtype) {
 
 long long partial_bytes(int nseg, int C) { return static_cast<long long>(nseg) * kMaxNB * 2 * C * 8; }
 
-// workspace = [arrival counters][f64 partials][nseg x 3 x C f32: shifts K / backward
-// coefficients]; the counters sit at a fixed offset, so calls of any shape share them
-constexpr int kArrivals = 64;  // one per channel group (CG <= C / E / 64 <= 64)
-constexpr long long kArrivalBytes = kArrivals * 4;
-long long coef_bytes(int nseg, int C) { return static_cast<long long>(nseg) * 3 * C * 4; }
-int* arrivals_of(void* ws) { return static_cast<int*>(ws); }
-double* partials_of(void* ws) { return reinterpret_cast<double*>(static_cast<char*>(ws) + kArrivalBytes); }
-float* coef_of(void* ws, int nseg, int C) {
-  return reinterpret_cast<float*>(static_cast<char*>(ws) + kArrivalBytes + partial_bytes(nseg, C));
-}
-
 }  // namespace
 }  // namespace posu
 
 using namespace posu;
 
 extern "C" long long posu_bn_workspace(int nseg, int C) {
-  return kArrivalBytes + partial_bytes(nseg, C) + coef_bytes(nseg, C);
+  return partial_bytes(nseg, C) + static_cast<long long>(nseg) * 3 * C * 4;
 }
 
 extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const float* gamma,
@@ -708,31 +638,19 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
                "posu_bn_train_fwd: bad shape (C / chunk must be a power of two or a multiple of 256)");
   POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_fwd: workspace too small");
   hipStream_t s = as_stream(stream);
-  double* part = partials_of(workspace);
+  double* part = static_cast<double*>(workspace);
   // the per-segment shifts K live where the backward keeps its coefficients
-  float* kshift = coef_of(workspace, nseg, C);
+  float* kshift = reinterpret_cast<float*>(static_cast<char*>(workspace) + partial_bytes(nseg, C));
   const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
-  POSU_REQUIRE(rs.CG <= kArrivals, "posu_bn_train_fwd: too many channel groups");
-  FinArgs f{};
-  f.gamma = gamma;
-  f.beta = beta;
-  f.eps = eps;
-  f.momentum = momentum;
-  f.kshift = kshift;
-  f.running_mean = running_mean;
-  f.running_var = running_var;
-  f.mean = mean;
-  f.rstd = rstd;
-  f.scale = scale;
-  f.shift = shift;
-  // statistics and their finalize in one launch (the last block of each channel group)
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
                        static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part,
-                       kshift, arrivals_of(workspace), f);
+                       kshift);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+                     gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
   return check_launch("posu_bn_train_fwd");
 }
 
@@ -768,24 +686,19 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
                "posu_bn_train_bwd: bad shape (C / chunk must be a power of two or a multiple of 256)");
   POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_bwd: workspace too small");
   hipStream_t s = as_stream(stream);
-  double* part = partials_of(workspace);
-  float* coef = coef_of(workspace, nseg, C);
+  double* part = static_cast<double*>(workspace);
+  float* coef = reinterpret_cast<float*>(static_cast<char*>(workspace) + partial_bytes(nseg, C));
   const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
   const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
-  POSU_REQUIRE(rs.CG <= kArrivals, "posu_bn_train_bwd: too many channel groups");
-  FinArgs f{};
-  f.gamma = gamma;
-  f.rstd = const_cast<float*>(rstd);
-  f.coef = coef;
-  f.dgamma = dgamma;
-  f.dbeta = dbeta;
   bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
                        static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale,
-                       relu_shift, mean, rstd, Pseg, C, rs, part, nullptr, arrivals_of(workspace), f);
+                       relu_shift, mean, rstd, Pseg, C, rs, part, nullptr);
   });
   POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
+                     rstd, coef, dgamma, dbeta);
   with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     const int E = chunk_elems(dtype);
@@ -810,12 +723,12 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
                "posu_channel_sum: bad shape (C / chunk must be a power of two or a multiple of 256)");
   POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(1, C), "posu_channel_sum: workspace too small");
   hipStream_t s = as_stream(stream);
-  double* part = partials_of(workspace);  // the counters stay untouched
+  double* part = static_cast<double*>(workspace);
   const RedShape rs = red_shape(P, C, chunk_elems(dtype), 1);
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, 1), dim3(256), 0, s, static_cast<const T*>(x),
-                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr, nullptr, FinArgs{});
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
   hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);

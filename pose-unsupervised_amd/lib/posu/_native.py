@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 9
+ABI_VERSION = 8
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()

@@ -15,17 +15,15 @@ _WS = {}
 INPLACE_S2_DGRAD = True
 
 
-def workspace(device, nbytes, slot='default', zeroed=False):
+def workspace(device, nbytes, slot='default'):
     """Grow-only scratch buffer per (device, slot, current stream), reused by consecutive
     launches on that stream only: a buffer is allocated, used and (when it grows) released on
     one stream, so the caching allocator orders its reuse behind every launch that used it (the
-    training step runs weight gradients on a side stream, train_plan._Grads).  zeroed: filled
-    with zeros when allocated (the BN workspace's arrival counters, which every launch leaves
-    zero)."""
+    training step runs weight gradients on a side stream, train_plan._Grads)."""
     key = (str(device), slot, torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
-        buf = (torch.zeros if zeroed else torch.empty)(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+        buf = torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
         _WS[key] = buf
     return buf
 
@@ -69,7 +67,7 @@ def deconv4x4s2_wgrad(x, dy, code, out=None):
 
 
 def _bn_ws(device, nseg, c):
-    return workspace(device, nat.load().posu_bn_workspace(nseg, c), 'bn', zeroed=True)
+    return workspace(device, nat.load().posu_bn_workspace(nseg, c), 'bn')
 
 
 def bn_train_fwd(z, nseg, gamma, beta, eps, momentum, running_mean=None, running_var=None):
