@@ -410,6 +410,28 @@ def test_staggered_tiles_bit_exact_vs_two_slot(cuda, code):
             assert torch.equal(a, b), (t, float((a.float() - b.float()).abs().max()))
 
 
+@pytest.mark.parametrize('code', [F32, BF16])
+def test_training_conv_tiles_bit_identical(cuda, code):
+    """The training convolutions (raw, no BN epilogue: train_plan._conv_tuned) run on whichever
+    tile the autotuner timed fastest; the claim that the choice changes speed, not results,
+    holds only if every candidate of plan._tile_candidates accumulates in the same K order.
+    One raw conv per geometry class (3x3 / 1x1, stride 1 / 2, ragged M) on every candidate
+    tile, outputs equal bit for bit."""
+    from posu.plan import _tile_candidates
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(11)
+    for cin, h, w, cout, k, stride, pad in [(64, 17, 15, 256, 3, 1, 1), (256, 13, 11, 64, 1, 1, 0),
+                                             (128, 18, 14, 128, 3, 2, 1), (256, 18, 14, 512, 1, 2, 0)]:
+        x = torch.randn(3, h, w, cin, device=cuda, generator=g).to(dt)
+        wt = (torch.randn(cout, k * k * cin, device=cuda, generator=g) * (k * k * cin) ** -0.5).to(dt)
+        outs = {t: ops.conv2d_nhwc(x, wt, cout, k, k, stride, pad, None, None, None, False, code, tile=t)
+                for t in _tile_candidates(cout)}
+        torch.cuda.synchronize()
+        t0 = _tile_candidates(cout)[0]
+        for t, o in outs.items():
+            assert torch.equal(o, outs[t0]), (cin, k, stride, cout, t)
+
+
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, None)])
 @pytest.mark.parametrize('cout', [256, 384])
 def test_conv2d_big_tiles_match_torch(cuda, code, tol, cout):
