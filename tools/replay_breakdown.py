@@ -32,9 +32,11 @@ def main():
     for s, e, n in rows:
         if 'stem_pool_kernel' in n:
             cur = [(s, e, n)]
-            replays.append(cur)
         elif cur is not None:
-            if 'softargmax' in n:
+            if s - cur[-1][1] > 20000:   # a graph replay runs back to back: a gap ends it (incomplete)
+                cur = None
+            elif 'softargmax' in n:   # only complete replays (the configs1 leg has no soft-argmax)
+                replays.append(cur)
                 cur = None
             else:
                 cur.append((s, e, n))
