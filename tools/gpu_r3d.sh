@@ -8,3 +8,8 @@ rc=$?; tail -4 $O/tests.log; [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -u bench.py --mode train --steps 10 --warmup 3 > $O/train.json 2> $O/train.err || exit 1
 tail -c 500 $O/train.json
 bash tools/profile_round.sh $O/prof $(cat COMMIT_STAMP 2>/dev/null || echo unknown)
+for v in l2r8 ts1 ts2 ts8; do
+  echo "== $v" >> $O/tail_var.txt
+  timeout -k 10 120 python tools/tail_micro.py --lib pose-unsupervised_amd/build/abl/libposeu_$v.so >> $O/tail_var.txt 2>&1 || exit 1
+done
+grep -v amdgpu.ids $O/tail_var.txt

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Builds a variant of libposeu.so with one source file compiled under extra defines:
+#     tools/variant_build.sh NAME SOURCE.hip -DFOO=1 [-DBAR=2 ...]
+# -> pose-unsupervised_amd/build/abl/libposeu_NAME.so (run here, on the CPU; the GPU tools take
+# it with --lib).  Timing ablations and tile experiments only; never the product library.
+set -euo pipefail
+cd "$(dirname "$0")/../pose-unsupervised_amd"
+name=$1; src=$2; shift 2
+make -s
+mkdir -p build/abl
+base=$(basename "$src" .hip)
+OTHERS=$(ls build/*.o | grep -v "/$base.o\$")
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c csrc/$base.hip -o build/abl/${base}_$name.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared $OTHERS build/abl/${base}_$name.o -o build/abl/libposeu_$name.so
+echo built build/abl/libposeu_$name.so
