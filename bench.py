@@ -94,7 +94,19 @@ def parse():
     ap.add_argument('--c1-steps', type=int, default=20,
                     help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
+    ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=0|1',
+                    help='A/B runs: set a boolean switch of posu.plan (e.g. STREAMED_LAYER2_TAIL=0) before '
+                         'the plans are built')
     return ap.parse_args()
+
+
+def apply_plan_flags(flags):
+    from posu import plan as pl
+    for f in flags:
+        name, _, val = f.partition('=')
+        if not hasattr(pl, name) or not isinstance(getattr(pl, name), bool) or val not in ('0', '1'):
+            raise SystemExit('--plan-flag %s: not a boolean switch of posu.plan' % f)
+        setattr(pl, name, val == '1')
 
 
 # ------------------------------------------------------------------ launcher
@@ -747,6 +759,7 @@ def main():
         sys.exit(spawn_ranks(args))   # before anything touches the GPU
     if args.dry_run:
         return dry_run_main(args)
+    apply_plan_flags(args.plan_flag)
     if args.mode == 'train':
         return train_main(args)
     return infer_main(args)

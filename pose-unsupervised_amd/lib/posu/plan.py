@@ -163,6 +163,9 @@ FUSED_LAYER3_TAIL = True
 # layer3's tail on the register-streamed kernel (posu_bottleneck_tail_stream_fwd: 59 vs 76 us per
 # block, tools/tail_micro.py); False: the LDS-ring kernel (posu_bottleneck3_tail_fwd)
 STREAMED_LAYER3_TAIL = True
+# layer2's identity Bottlenecks as conv1 (a conv launch) + the register-streamed tail instead of
+# the fused LDS-ring block (posu_bottleneck2_fwd)
+STREAMED_LAYER2_TAIL = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -186,7 +189,7 @@ class _Block:
         self.w3d = None              # the fused first block's [w3*s3 | wd*sd] (permuted conv3 K)
         self.l2 = False              # a layer2 identity block (fused kernel, the convs' own packs)
         self.l3 = False              # a layer3 identity block (conv1, then the fused conv2 + conv3 tail)
-        self.wst = None              # layer3: the tail's per-wave weight streams (pack_tail_stream)
+        self.wst = None              # layer2 / layer3: the tail's per-wave weight streams (pack_tail_stream)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -210,7 +213,7 @@ class _Block:
         elif code in (ops.BF16, ops.F16) and len(names) == 3:
             self.l2 = self._layer2_shape()
             self.l3 = self._layer3_shape()
-            if self.l3:
+            if self.l2 or self.l3:
                 self.wst = pack_tail_stream(self.convs[1].w, self.convs[2].w)
 
     def _layer2_shape(self):
@@ -252,6 +255,9 @@ class _Block:
                                        c3.shift, code, out=out)
         if self.l2 and FUSED_BOTTLENECK and fits and x.shape[2] == 32 and x.shape[1] % 4 == 0:
             c1, c2, c3 = self.convs
+            if STREAMED_LAYER2_TAIL:
+                return ops.bottleneck_tail_stream_nhwc(c1(x, code), x, self.wst, c2.scale, c2.shift, c3.scale,
+                                                       c3.shift, code, out=out)
             return ops.bottleneck2_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, c3.w, c3.scale,
                                         c3.shift, code, out=out)
         if (self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and fits and x.shape[2] == 16 and
