@@ -87,6 +87,34 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
+// s_waitcnt vmcnt(n), n wave-uniform in {0, D, 2D, ..} up to 3D (the ring's younger stages)
+template <int D>
+__device__ __forceinline__ void vm_wait_stages(int stages) {
+  if (stages >= 3) vm_wait<3 * D>();
+  else if (stages == 2) vm_wait<2 * D>();
+  else if (stages == 1) vm_wait<D>();
+  else vm_wait<0>();
+}
+
+// workgroup barrier that retires this wave's LDS reads (lgkmcnt(0)) and leaves the ring's
+// younger LDS-DMA stages in flight (__syncthreads() would wait for them too)
+__device__ __forceinline__ void wg_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// LDS ring slots of the weight-gradient kernel (S - 1 pixel stages in flight).  Measured on the
+// R50 training shapes (tools/wgrad_micro.py, profiles/r03/wgrad_slots_r3h.txt): S = 2 1644 us,
+// S = 3 2047 us, S = 4 1944 us summed -- the 3x3 layers lose 50-90 % with deeper rings, the
+// 1x1 ones gain up to 20 %; S = 2 kept
+#ifndef POSU_WG_SLOTS
+#define POSU_WG_SLOTS 2
+#endif
+constexpr int kWgSlots = POSU_WG_SLOTS;
+
 // chunk swizzle of LDS row `row` for rows of CG 16-byte chunks (see the header)
 template <int ES, int CG>
 __device__ __forceinline__ int swz_row(int row) {
@@ -146,8 +174,8 @@ __device__ __forceinline__ float frag_f32(const char* tile, int ks, int c0, int 
   return *reinterpret_cast<const float*>(tile + r * ROWB + ((chunk ^ swz_row<4, CG>(r)) << 4) + (col & 3) * 4);
 }
 
-// BM x BN tile of dW, 4 waves in a 2 x 2 grid, BP pixels per LDS stage, 2-slot ring
-template <typename T, int BM, int BN>
+// BM x BN tile of dW, 4 waves in a 2 x 2 grid, BP pixels per LDS stage, S-slot ring
+template <typename T, int BM, int BN, int S>
 __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
   constexpr int ES = static_cast<int>(sizeof(T));
   constexpr int E = 16 / ES;
@@ -159,8 +187,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
   constexpr int WTM = BM / 2, WTN = BN / 2, TM = WTM / 16, TN = WTN / 16;
   constexpr int KSTEP = WOp<T>::KSTEP;
   static_assert(DG >= 1 && DX >= 1 && DG * 4096 == G_BYTES && DX * 4096 == BP * RX, "tile / DMA split");
-  static_assert(DG + DX < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  static_assert(S >= 2 && S <= 4 && (DG + DX) * (S - 2) < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -244,12 +272,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  if (nst > 0) POSU_WG_DMA(0, 0);
+  // S-slot ring: stages st+1 .. st+S-2 stay in flight while stage st is consumed; the
+  // barrier publishes stage st and frees slot (st - 1) % S for stage st + S - 1
+  for (int s0 = 0; s0 < S - 1 && s0 < nst; ++s0) POSU_WG_DMA(s0, s0);
   for (int st = 0; st < nst; ++st) {
-    vm_wait<0>();
-    __syncthreads();  // stage st visible to all waves; slot (st+1)&1 no longer read
-    if (st + 1 < nst) POSU_WG_DMA(st + 1, (st + 1) & 1);
-    const char* Gs = smem + (st & 1) * STAGE;
+    vm_wait_stages<DG + DX>(min(S - 2, nst - 1 - st));
+    wg_barrier();
+    if (st + S - 1 < nst) POSU_WG_DMA(st + S - 1, (st + S - 1) % S);
+    const char* Gs = smem + (st % S) * STAGE;
     const char* Xs = Gs + G_BYTES;
 #pragma unroll
     for (int ks = 0; ks < BP; ks += KSTEP) {
@@ -291,22 +321,51 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
     }
 }
 
-// dW (parameter layout [M][Creal][KH][KW], f32) = sum over splits, fixed order
+// dW (parameter layout [M][Creal][KH][KW], f32) = sum over splits, fixed order.  A block owns
+// 64 consecutive k of one row m: thread (sl, c) sums the float4 column c over the splits
+// sl, sl + 16, .. (all of its loads in flight together: the partials were just written, so the
+// pass is latency-bound), then the 16 split lanes combine in lane order through LDS.
+constexpr int kRedCols = 16, kRedLanes = 16;
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int splits, int Mpad,
                                                            int Npad, int M, int K, int C, int Creal, int KH, int KW,
                                                            float* __restrict__ out) {
-  const long long total = static_cast<long long>(M) * K;
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
-    const int m = static_cast<int>(i / K), k = static_cast<int>(i - static_cast<long long>(m) * K);
-    const int tap = k / C, ci = k - tap * C;
-    if (ci >= Creal) continue;
-    float s = 0.f;
+  __shared__ float4 red[kRedLanes][kRedCols + 1];
+  const int kb = (K + 4 * kRedCols - 1) / (4 * kRedCols);  // 64-wide k blocks per row
+  const int m = blockIdx.x / kb;
+  const int k0 = (blockIdx.x - m * kb) * 4 * kRedCols;
+  const int c = threadIdx.x % kRedCols, sl = threadIdx.x / kRedCols;
+  const int k = k0 + 4 * c;
+  const size_t stride = static_cast<size_t>(Mpad) * Npad;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (m < M && k < Npad) {  // Npad is a multiple of 4: the float4 lies inside the padded row
     const float* src = part + static_cast<size_t>(m) * Npad + k;
-    const size_t stride = static_cast<size_t>(Mpad) * Npad;
-#pragma unroll 8
-    for (int sp = 0; sp < splits; ++sp) s += src[sp * stride];
-    const int kh = tap / KW, kw = tap - kh * KW;
-    out[((static_cast<size_t>(m) * Creal + ci) * KH + kh) * KW + kw] = s;
+#pragma unroll 4
+    for (int sp = sl; sp < splits; sp += kRedLanes) {
+      const float4 v = *reinterpret_cast<const float4*>(src + sp * stride);
+      a.x += v.x;
+      a.y += v.y;
+      a.z += v.z;
+      a.w += v.w;
+    }
+  }
+  red[sl][c] = a;
+  __syncthreads();
+  if (threadIdx.x < 4 * kRedCols) {
+    const int cc = threadIdx.x >> 2, e = threadIdx.x & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int l = 0; l < kRedLanes; ++l) {
+      const float4 v = red[l][cc];
+      s += e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;
+    }
+    const int kk = k0 + 4 * cc + e;
+    if (m < M && kk < K) {
+      const int tap = kk / C, ci = kk - tap * C;
+      if (ci < Creal) {
+        const int kh = tap / KW, kw = tap - kh * KW;
+        out[((static_cast<size_t>(m) * Creal + ci) * KH + kh) * KW + kw] = s;
+      }
+    }
   }
 }
 
@@ -331,7 +390,7 @@ void launch_wgrad(WgradGeom& g, hipStream_t s) {
   const int stages_per_split = (pst + splits - 1) / splits;
   g.pps = stages_per_split * BP;
   g.splits = (g.P + g.pps - 1) / g.pps;
-  hipLaunchKernelGGL((conv_wgrad_kernel<T, BM, BN>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+  hipLaunchKernelGGL((conv_wgrad_kernel<T, BM, BN, kWgSlots>), dim3(tiles * g.splits), dim3(256), 0, s, g);
 }
 
 template <typename T>
@@ -408,9 +467,8 @@ extern "C" int posu_conv2d_wgrad(int dtype, const void* dy, const void* x, int N
   else if (dtype == POSU_F16) launch_wgrad_t<f16_t>(g, s);
   else launch_wgrad_t<float>(g, s);
   if (int st = check_launch("posu_conv2d_wgrad")) return st;
-  const long long total = static_cast<long long>(Cout) * g.K;
-  const int blocks = static_cast<int>(std::min<long long>((total + 255) / 256, 4096));
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, s, g.part, g.splits, g.Mpad, g.Npad, Cout, g.K,
-                     C, Creal, KH, KW, dw);
+  const int kb = (g.K + 4 * kRedCols - 1) / (4 * kRedCols);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(static_cast<unsigned>(Cout * kb)), dim3(256), 0, s, g.part, g.splits,
+                     g.Mpad, g.Npad, Cout, g.K, C, Creal, KH, KW, dw);
   return check_launch("posu_conv2d_wgrad");
 }
