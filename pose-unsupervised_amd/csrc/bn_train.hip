@@ -6,7 +6,7 @@
 // backward, the bias-gradient channel sum and the stem max-pool backward.
 //
 // Reductions are deterministic: per-block partial sums in f64 written to a workspace,
-// then one thread per channel sums the blocks in a fixed order.  Running statistics
+// then a data-independent order (lanes over blocks, a fixed xor butterfly) per channel.  Running statistics
 // follow torch.nn.BatchNorm2d: biased variance for normalisation, unbiased variance in
 // running_var, running = (1 - momentum) * running + momentum * batch, updated once per
 // segment in segment (= view) order like the reference's four backbone calls.
@@ -177,13 +177,16 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
 
 // ---- finalize: one block per FCH channels, FLN lanes sum the partial blocks of up to
 // FSEG segments at once (every load of the pass in flight together: the partials are a few
-// hundred KiB, so this pass is latency-bound), fixed-order LDS combine.  Per segment the
-// summation order is the blocks' order, whatever the grouping.
+// hundred KiB, so this pass is latency-bound), then a fixed xor butterfly across the lanes
+// (round 2 combined the lanes serially through LDS in one thread: ~12 us per launch).
 constexpr int FCH = 8, FLN = 32, FSEG = 4;
 
+// thread t of a finalize block: channel blockIdx.x * FCH + t / FLN, lane t % FLN; the FLN lanes
+// of a channel are one half-wave.  Each lane sums the partial blocks ln, ln + FLN, .. of up to
+// FSEG segments (all loads in flight together), then a fixed xor butterfly over the half-wave;
+// lane 0's sums are the result (its association order does not depend on the data)
 __device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int seg0, int ns, int NB, int C, int c,
-                                            bool valid, int cl, int ln, double (*red)[FSEG][FLN][FCH], double* s,
-                                            double* q) {
+                                            bool valid, int ln, double* s, double* q) {
   double a[FSEG], b[FSEG];
 #pragma unroll
   for (int k = 0; k < FSEG; ++k) a[k] = b[k] = 0.0;
@@ -201,22 +204,17 @@ __device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int
     }
   }
 #pragma unroll
-  for (int k = 0; k < FSEG; ++k) {
-    red[0][k][ln][cl] = a[k];
-    red[1][k][ln][cl] = b[k];
-  }
-  __syncthreads();
-  if (ln == 0)
+  for (int off = FLN / 2; off > 0; off >>= 1)
 #pragma unroll
     for (int k = 0; k < FSEG; ++k) {
-      s[k] = 0.0;
-      q[k] = 0.0;
-      for (int l = 0; l < FLN; ++l) {
-        s[k] += red[0][k][l][cl];
-        q[k] += red[1][k][l][cl];
-      }
+      a[k] += __shfl_xor(a[k], off, FLN);
+      b[k] += __shfl_xor(b[k], off, FLN);
     }
-  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < FSEG; ++k) {
+    s[k] = a[k];
+    q[k] = b[k];
+  }
 }
 
 __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
@@ -227,15 +225,14 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
                                                                 float* running_var, float* __restrict__ mean,
                                                                 float* __restrict__ rstd, float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
-  __shared__ double red[2][FSEG][FLN][FCH];
-  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int cl = threadIdx.x / FLN, ln = threadIdx.x % FLN;
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
   for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
     double sums[FSEG], sqs[FSEG];
     const int ns = min(FSEG, nseg - seg0);
-    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sums, sqs);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, ln, sums, sqs);
     if (ln != 0 || !valid) continue;
     for (int k = 0; k < ns; ++k) {  // in segment order: running stats compose like V calls
       const int seg = seg0 + k;
@@ -443,8 +440,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
                                                               const float* __restrict__ rstd,
                                                               float* __restrict__ coef, float* __restrict__ dgamma,
                                                               float* __restrict__ dbeta) {
-  __shared__ double red[2][FSEG][FLN][FCH];
-  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int cl = threadIdx.x / FLN, ln = threadIdx.x % FLN;
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
@@ -452,7 +448,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
   for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
     double sgs[FSEG], sgxs[FSEG];
     const int ns = min(FSEG, nseg - seg0);
-    reduce_segs(part, seg0, ns, NB, C, c, valid, cl, ln, red, sgs, sgxs);
+    reduce_segs(part, seg0, ns, NB, C, c, valid, ln, sgs, sgxs);
     if (ln != 0 || !valid) continue;
     for (int k = 0; k < ns; ++k) {
       const int seg = seg0 + k;
@@ -515,11 +511,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
 
 __global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double* __restrict__ part, int NB, int C,
                                                                    float* __restrict__ out) {
-  __shared__ double red[2][FSEG][FLN][FCH];
-  const int cl = threadIdx.x % FCH, ln = threadIdx.x / FCH;
+  const int cl = threadIdx.x / FLN, ln = threadIdx.x % FLN;
   const int c = blockIdx.x * FCH + cl;
   double s[FSEG], q[FSEG];
-  reduce_segs(part, 0, 1, NB, C, c, c < C, cl, ln, red, s, q);
+  reduce_segs(part, 0, 1, NB, C, c, c < C, ln, s, q);
   if (ln == 0 && c < C) out[c] = static_cast<float>(s[0]);
 }
 
