@@ -94,6 +94,10 @@ def parse():
     ap.add_argument('--c1-steps', type=int, default=20,
                     help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
+    ap.add_argument('--train-stream', default='high', choices=['high', 'default'],
+                    help='train mode: run the step on a high-priority stream (the weight-gradient side '
+                         'stream keeps normal priority, so the data-gradient chain wins dispatch) or on '
+                         'the default stream')
     ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=0|1',
                     help='A/B runs: set a boolean switch of posu.plan (e.g. STREAMED_LAYER2_TAIL=0) before '
                          'the plans are built')
@@ -689,6 +693,15 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
         opt.step()
         return loss
 
+    from posu import plan as pplan
+    stream = torch.cuda.Stream(dev, priority=-1) if args.train_stream == 'high' else torch.cuda.current_stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))   # inputs / parameters made on the default stream
+    with torch.cuda.stream(stream):
+        return _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream)
+
+
+def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
+    from posu import dist as pdist
     from posu import plan as pplan
     if not args.no_autotune:  # the first warm-up step times every admissible tile per conv geometry
         pplan._Tuner.active, pplan._Tuner.reps = True, 3
