@@ -94,10 +94,10 @@ def parse():
     ap.add_argument('--c1-steps', type=int, default=20,
                     help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
-    ap.add_argument('--train-stream', default='high', choices=['high', 'default'],
+    ap.add_argument('--train-stream', default='default', choices=['high', 'default'],
                     help='train mode: run the step on a high-priority stream (the weight-gradient side '
                          'stream keeps normal priority, so the data-gradient chain wins dispatch) or on '
-                         'the default stream')
+                         'the default stream (default; measured equal: 21.82 vs 21.80 ms per step)')
     ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=0|1',
                     help='A/B runs: set a boolean switch of posu.plan (e.g. STREAMED_LAYER2_TAIL=0) before '
                          'the plans are built')
