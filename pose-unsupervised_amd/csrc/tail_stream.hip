@@ -42,7 +42,7 @@ struct TailSGeom {
 
 // timing ablations (tools/tail_ablations.sh; never set in the product build, wrong results):
 //   1 no MFMAs, 2 no weight loads in the loop, 4 no pixel-fragment LDS reads, 8 no conv3
-//   residual loads / y stores, 16 no window DMA
+//   residual loads / y stores, 16 no window DMA, 32 no y stores, 64 no residual loads
 #ifndef POSU_TS_ABLATE
 #define POSU_TS_ABLATE 0
 #endif
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-      rv[i] = (kAbl & 8) ? make_uint4(i, c0, 0, 0) : *reinterpret_cast<const uint4*>(xg + tpix(i) * C + c0);
+      rv[i] = (kAbl & 72) ? make_uint4(i, c0, 0, 0) : *reinterpret_cast<const uint4*>(xg + tpix(i) * C + c0);
   };
   // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
   lds_barrier();
@@ -269,7 +269,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
       const uint4 o = O::store_vals(v);
-      if (kAbl & 8) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
+      if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
       else *reinterpret_cast<uint4*>(yg + tpix(i) * C + c0) = o;
     }
   };
