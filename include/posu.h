@@ -45,7 +45,8 @@ extern "C" {
 const char* posu_last_error(void);
 /* ABI revision: 4 stateless conv knobs; 5 the fused layer1 Bottleneck kernels and batched
  * weight packing; 6 the LDS-tiled packing; 7 the layer3 Bottleneck tail; 8 the crop warp
- * (posu_crop_warp).  The ctypes binding refuses a library of another revision. */
+ * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd).  The
+ * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -210,6 +211,19 @@ int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, i
 int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
                                     int P, const void* wstream, const float* s2, const float* b2,
                                     const float* s3, const float* b3, void* y, void* stream);
+
+/* posu_bottleneck_tail_stream_fwd chained with the NEXT identity Bottleneck's conv1 (1x1, C -> P)
+ * + BN1 + ReLU over this block's output y (lib/models/pose_resnet.py:79-84 of block i+1; the
+ * reference runs it as a separate conv over y): each y chunk of P channels is staged in LDS as
+ * it is produced and multiplied into the next conv1's accumulators, so y is not re-read and the
+ * next block's conv1 launch disappears.  wstream: packing.pack_tail_stream(conv2, conv3, next
+ * conv1 [P][C] pack) -- [P/32][9 P/32 + 2 C/32][2][64][8]; s1n/b1n [P] the next conv1's folded
+ * BN; t1n [N, H, W, P] out (aliasing no other operand).  y and t1n are bit-identical to this
+ * tail followed by posu_conv2d_fwd(next conv1, ReLU) over y. */
+int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                         int P, const void* wstream, const float* s2, const float* b2,
+                                         const float* s3, const float* b3, void* y, const float* s1n,
+                                         const float* b1n, void* t1n, void* stream);
 
 /* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
  * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn

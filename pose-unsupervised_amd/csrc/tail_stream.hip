@@ -38,6 +38,11 @@ struct TailSGeom {
   const float* s3;
   const float* b3;
   int N, H;
+  // NEXT (chained tails): the next identity block's conv1 + BN1 + ReLU computed from this
+  // block's output y while it is produced (t1n = relu(y conv1n * s1n + b1n), [N][H][W][P])
+  const float* s1n;
+  const float* b1n;
+  void* t1n;
 };
 
 // timing ablations (tools/tail_ablations.sh; never set in the product build, wrong results):
@@ -51,6 +56,17 @@ constexpr int kAbl = POSU_TS_ABLATE;
 #ifndef POSU_TS_KD
 #define POSU_TS_KD 4
 #endif
+// NEXT (chained) variant: weight prefetch depth and pixel-fragment register sets.  The second
+// accumulator set leaves no room for the plain tail's 4-deep stream and two fragment sets; per
+// layer the fastest spill-free-ish point measured (tools/chain_micro.py, profiles/r03/chain_r3s.txt:
+// layer2 kD 1 / one set 105.0 us (no spills) vs 110.9 (2 / two) vs 116.8 (2 / one) vs 128.6
+// (4 / one); layer3 kD 2 / two sets 76.3 us vs 77.0 (2 / one), 78.6 (1 / one), 95.9 (4 / one))
+#ifndef POSU_TS_KD_NEXT
+#define POSU_TS_KD_NEXT 0  // 0: per layer, as measured
+#endif
+#ifndef POSU_TS_NB_NEXT
+#define POSU_TS_NB_NEXT 0
+#endif
 
 __device__ __forceinline__ void ld8(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -59,7 +75,7 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C, int ROWS, int NW>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false>
 struct TailCfg {
   static constexpr int kRows = ROWS;               // image rows per workgroup
   static constexpr int kNW = NW;                   // waves per workgroup
@@ -75,11 +91,19 @@ struct TailCfg {
   static constexpr int kKT = P / 32;               // k-steps per tap / per conv3 chunk
   static constexpr int kChunk = 32 * kNCQ;         // conv3 output channels per chunk
   static constexpr int kNC = C / kChunk;           // conv3 chunks
-  static constexpr int kSteps = 9 * kKT + kNC * kKT;
-  static constexpr int kD = POSU_TS_KD < kKT ? POSU_TS_KD : kKT;  // weight prefetch depth (k-steps)
+  static constexpr int kBlk3 = NEXT ? 2 : 1;       // stream blocks per conv3 chunk (+ the next conv1's K slice)
+  static constexpr int kSteps = 9 * kKT + kNC * kKT * kBlk3;
+  static constexpr int kYC = kS3 + 2 * C * 4;      // NEXT: the y chunk [kPx][P] behind BN3
+  static constexpr int kLdsAll = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
+  // weight prefetch depth (k-steps); NEXT keeps a second accumulator set live, so its stream
+  // runs POSU_TS_KD_NEXT deep
+  static constexpr int kDW = !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : W == 32 ? 1 : 2;
+  static constexpr int kNB = !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : W == 32 ? 1 : 2;
+  static constexpr int kD = kDW < kKT ? kDW : kKT;
   static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % 128 == 0, "every wave: 128 px x 32 channels");
   static_assert(kS3 + 2 * C * 4 <= kBN2, "t2 and BN3 fit over the window");
-  static_assert(kLds <= 160 * 1024, "LDS");
+  static_assert(kLdsAll <= 160 * 1024, "LDS");
+  static_assert(!NEXT || kChunk == P, "the next conv1 takes one y chunk per K slice of P channels");
   static_assert(kKT % kD == 0, "the ring slot of a k-step is static inside a block");
 };
 
@@ -90,13 +114,13 @@ struct TailCfg {
 template <int RowB>
 __device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
 
-template <typename T, int W, int P, int C, int ROWS, int NW>
+template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
-  using K = TailCfg<W, P, C, ROWS, NW>;
+  using K = TailCfg<W, P, C, ROWS, NW, NEXT>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
-  __shared__ __attribute__((aligned(16))) char smem[K::kLds];
+  __shared__ __attribute__((aligned(16))) char smem[K::kLdsAll];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
@@ -150,18 +174,19 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   vm_wait<0>();  // the window (LDS-DMA) and the first fragments
   lds_barrier();
 
-  f32x4 acc[8][2];  // [m-tile i: tile pixels 128 pg + 16 i ..][n-tile j]
-  auto zero = [&] {
+  f32x4 acc[8][2];   // [m-tile i: tile pixels 128 pg + 16 i ..][n-tile j]
+  f32x4 acc1[8][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
+  auto zero = [&](f32x4 (&a)[8][2]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j) a[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   // the pair of n-tiles -> this lane's 8 consecutive channels cpair .. cpair + 7 of pixel r16
-  auto pair = [&](int i, float* v) {
+  auto pair = [&](const f32x4 (&a)[8][2], int i, float* v) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][0][e]), __float_as_uint(acc[i][1][e]),
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i][0][e]), __float_as_uint(a[i][1][e]),
                                                        false, false);
       v[e] = __uint_as_float(sw[0]);
       v[4 + e] = __uint_as_float(sw[1]);
@@ -175,10 +200,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   // with `cols` pixels per row at 16-B chunk 4 d + q, swizzled by the lane's key (column & 15).
   // The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run (two register
   // sets); the scheduling barriers keep the compiler from hoisting more of them.
-  auto block = [&](int blk, int lpix, int key, auto coff) {
-    uint4 b[2][8];
+  auto block = [&](f32x4 (&acc)[8][2], int blk, int base, int lpix, int key, auto coff) {
+    constexpr int NB = K::kNB;  // pixel-fragment register sets
+    uint4 b[NB][8];
     // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3))
-    const char* lb = smem + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
+    const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
     const char* kb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) kb[k] = lb + ((k ^ (key >> 2)) << 6);
@@ -190,18 +216,21 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
     for (int i = 0; i < 8; ++i) b[0][i] = rd(i, 0);
 #pragma unroll
     for (int d = 0; d < K::kKT; ++d) {
-      if (d + 1 < K::kKT) {
+      if (NB == 2 && d + 1 < K::kKT) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) b[(d + 1) & 1][i] = rd(i, d + 1);
+        for (int i = 0; i < 8; ++i) b[(d + 1) % NB][i] = rd(i, d + 1);
       }
       const int s = d % kD;
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < 8; ++i) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d & 1][i].y);
-          else O::mma(acc[i][j], wa[s][j], b[d & 1][i]);
+          if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d % NB][i].y);
+          else O::mma(acc[i][j], wa[s][j], b[d % NB][i]);
         }
+        // one set: m-tile i's fragment of the next k-step once its MFMAs are issued
+        if (NB == 1 && d + 1 < K::kKT) b[0][i] = rd(i, d + 1);
+      }
       const int p = K::kKT * blk + d + kD;
       if (!(kAbl & 2)) {
         wa[s][0] = *frag(p, 0);
@@ -212,12 +241,12 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   };
 
   // ---- conv2: 9 taps x kKT channel steps over the window
-  zero();
+  zero(acc);
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
     const int dy = t / 3, dx = t - 3 * (t / 3);
     // window pixel of m-tile i: tile row (128 pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
-    block(t, ((128 / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
+    block(acc, t, 0, ((128 / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
           [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
   }
   const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
@@ -244,7 +273,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float v[8];
-      pair(i, v);
+      pair(acc, i, v);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
       *reinterpret_cast<uint4*>(smem + swzp<K::kRowB>(tpix(i), r16, c0 >> 3)) = O::store_vals(v);
@@ -254,44 +283,75 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
 
   // ---- conv3: output chunk nc (kChunk channels; this wave's 32), kKT channel steps over t2
   const float* b3l = reinterpret_cast<const float*>(smem + K::kS3);
-  auto chunk = [&](int nc, const uint4 (&rv)[8]) {
+  auto chunk = [&](int nc, uint4 (&rv)[8]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
-    zero();
-    block(9 + nc, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
+    zero(acc);
+    block(acc, 9 + K::kBlk3 * nc, 0, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
+    // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers)
+    if constexpr (NEXT) res_load(nc, rv);
     float sc[8], sh[8];
     ld8(b3l + c0, sc);
     ld8(b3l + C + c0, sh);
+    if constexpr (NEXT) {
+      if (nc > 0) lds_barrier();  // every wave is done reading the previous y chunk
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       float v[8], r[8];
-      pair(i, v);
+      pair(acc, i, v);
       O::load_vals(rv[i], r);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
       const uint4 o = O::store_vals(v);
       if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
       else *reinterpret_cast<uint4*>(yg + tpix(i) * C + c0) = o;
+      // NEXT: the chunk's y, laid out like t2 ([pixel][P] rows, column-keyed swizzle)
+      if constexpr (NEXT)
+        *reinterpret_cast<uint4*>(smem + K::kYC + swzp<K::kRowB>(tpix(i), r16, (32 * cq + cpair) >> 3)) = o;
+    }
+    if constexpr (NEXT) {
+      // the next block's conv1 over this K slice (y channels kChunk nc ..): same k order as a
+      // conv launch over y, so t1n is bit-identical to it
+      lds_barrier();
+      block(acc1, 9 + K::kBlk3 * nc + 1, K::kYC, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
     }
   };
   // unrolled: hipcc's wait counts at a loop head merge both paths and made every chunk's first
   // weight wait also wait for the previous chunk's y stores (layer2 tail 90.7 -> 86.7 us)
+  if constexpr (NEXT) zero(acc1);
 #pragma unroll
   for (int nc = 0; nc < K::kNC; ++nc) {
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
     // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
     uint4 rv[8];
-    res_load(nc, rv);
+    if constexpr (!NEXT) res_load(nc, rv);
     chunk(nc, rv);
+  }
+  if constexpr (NEXT) {
+    // t1n = relu(conv1n * s1n + b1n), this lane's 8 channels of each m-tile's pixel
+    T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * P;
+    const int c0 = 32 * cq + cpair;
+    float sc[8], sh[8];
+    ld8(g.s1n + c0, sc);
+    ld8(g.b1n + c0, sh);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      float v[8];
+      pair(acc1, i, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+      *reinterpret_cast<uint4*>(tg + tpix(i) * P + c0) = O::store_vals(v);
+    }
   }
 }
 
-template <int W, int P, int C, int ROWS, int NW>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false>
 void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(g.N * (g.H / ROWS)));
   if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT>), grid, dim3(NW * 64), 0, s, g);
   else
-    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // tiles: layer3 8 rows x 16 px with 8 waves (one workgroup per CU, 256 at batch 128); layer2
@@ -307,13 +367,17 @@ constexpr int kL2Rows = POSU_TS_L2_ROWS, kL2Waves = POSU_TS_L2_ROWS;
 
 using namespace posu;
 
-extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
-                                               int P, const void* wstream, const float* s2, const float* b2,
-                                               const float* s3, const float* b3, void* y, void* stream) {
-  const std::string what = "posu_bottleneck_tail_stream_fwd";
+namespace {
+int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                     const void* wstream, const float* s2, const float* b2, const float* s3, const float* b3, void* y,
+                     const float* s1n, const float* b1n, void* t1n, void* stream) {
+  const std::string what = name;
+  const bool next = t1n != nullptr;
   POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, what + ": dtype must be BF16 or F16");
   POSU_REQUIRE(t1 && x && wstream && s2 && b2 && s3 && b3 && y, what + ": null pointer");
   POSU_REQUIRE(x != y && t1 != y, what + ": the output must not alias an input");
+  POSU_REQUIRE(!next || (s1n && b1n && t1n != y && t1n != x && t1n != t1),
+               what + ": the next conv1 needs its BN and an output that aliases no other operand");
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
   POSU_REQUIRE(l2 || l3, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16, C = 1024, "
                                 "planes = 256) of PoseResNet at 256x256");
@@ -323,7 +387,8 @@ extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const 
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
   for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(s3),
-                        static_cast<const void*>(b3)})
+                        static_cast<const void*>(b3), next ? t1n : t1, static_cast<const void*>(next ? s1n : s3),
+                        static_cast<const void*>(next ? b1n : b3)})
     POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, what + ": pointers must be 16-byte aligned");
   TailSGeom g{};
   g.t1 = t1;
@@ -336,10 +401,40 @@ extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const 
   g.b3 = b3;
   g.N = N;
   g.H = H;
+  g.s1n = s1n;
+  g.b1n = b1n;
+  g.t1n = t1n;
   hipStream_t s = as_stream(stream);
-  if (l3)
-    launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
-  else
-    launch_tail<32, 128, 512, kL2Rows, kL2Waves>(dtype, g, s);
-  return check_launch(what.c_str());
+  if (l3) {
+    if (next) launch_tail<16, 256, 1024, 8, 8, true>(dtype, g, s);
+    else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
+  } else {
+    if (next) launch_tail<32, 128, 512, kL2Rows, kL2Waves, true>(dtype, g, s);
+    else launch_tail<32, 128, 512, kL2Rows, kL2Waves>(dtype, g, s);
+  }
+  return check_launch(name);
+}
+}  // namespace
+
+extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                               int P, const void* wstream, const float* s2, const float* b2,
+                                               const float* s3, const float* b3, void* y, void* stream) {
+  return tail_stream_impl("posu_bottleneck_tail_stream_fwd", dtype, t1, x, N, H, W, C, P, wstream, s2, b2, s3, b3, y,
+                          nullptr, nullptr, nullptr, stream);
+}
+
+// Chained identity Bottlenecks: the tail above, and the NEXT identity block's conv1 (+ BN1 +
+// ReLU) over this block's output y while its chunks are produced -- t1n, which the next
+// block's tail takes instead of a conv1 launch over y.  wstream = packing.pack_tail_stream
+// (conv2, conv3, next conv1).
+extern "C" int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W,
+                                                    int C, int P, const void* wstream, const float* s2,
+                                                    const float* b2, const float* s3, const float* b3, void* y,
+                                                    const float* s1n, const float* b1n, void* t1n, void* stream) {
+  if (!t1n) {
+    set_error("posu_bottleneck_tail_stream_next_fwd: null pointer (t1n)");
+    return POSU_ERR_ARG;
+  }
+  return tail_stream_impl("posu_bottleneck_tail_stream_next_fwd", dtype, t1, x, N, H, W, C, P, wstream, s2, b2, s3,
+                          b3, y, s1n, b1n, t1n, stream);
 }

@@ -131,6 +131,22 @@ def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
     return out
 
 
+def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, code, out=None, t1n=None):
+    """The tail above chained with the NEXT identity block's conv1 + BN1 + ReLU over its output
+    (posu_bottleneck_tail_stream_next_fwd); wstream = packing.pack_tail_stream(conv2 pack, conv3
+    pack, next conv1 pack).  Returns (y, t1n): t1n is what a conv launch of the next conv1 over y
+    would produce, bit for bit."""
+    n, h, w, c = x.shape
+    p = t1.shape[3]
+    if out is None:
+        out = torch.empty_like(x)
+    if t1n is None:
+        t1n = torch.empty((n, h, w, p), dtype=x.dtype, device=x.device)
+    call('posu_bottleneck_tail_stream_next_fwd', code, ptr(t1), ptr(x), n, h, w, c, p, ptr(wstream), ptr(s2),
+         ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n), ptr(t1n), stream_of(x.device))
+    return out, t1n
+
+
 def bottleneck_down_nhwc(x, w1, s1, b1, w2, s2, b2, w3d, shift3, code, out=None):
     """Fused first Bottleneck of layer1 with its downsample (posu_bottleneck_down_fwd):
     x [N, H, W, C] -> y [N, H, W, w3d.shape[0]]."""

@@ -36,19 +36,31 @@ def mfma_fragments(wpk):
     return wpk.reshape(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(co // 16, k // 32, 64, 8)
 
 
-def pack_tail_stream(w2pk, w3pk):
+def pack_tail_stream(w2pk, w3pk, w1n=None):
     """The per-wave weight streams of posu_bottleneck_tail_stream_fwd (csrc/tail_stream.hip) from
     the conv2 [P][9P] and conv3 [C][P] posu_conv2d_fwd packs: [NCQ][9 KT + NC KT][2][64][8] with
     NCQ = P / 32 channel groups, KT = P / 32 k-steps per tap, NC = C / P conv3 chunks.  Group cq,
     k-step p < 9 KT: conv2 n-tile 2 cq + j, k-step p; p = 9 KT + KT nc + c: conv3 n-tile
-    2 NCQ nc + 2 cq + j, k-step c."""
+    2 NCQ nc + 2 cq + j, k-step c.
+
+    w1n (the next identity block's conv1 pack [P][C], posu_bottleneck_tail_stream_next_fwd):
+    after conv3 chunk nc come the next conv1's KT k-steps over that chunk's channels -- p =
+    9 KT + 2 KT nc + c: conv3 as above; p = 9 KT + 2 KT nc + KT + c: conv1n n-tile 2 cq + j,
+    k-step KT nc + c."""
     planes, c = w2pk.shape[0], w3pk.shape[0]
     ncq, kt, nc = planes // 32, planes // 32, c // planes
     f2 = mfma_fragments(w2pk)                                    # [2 ncq][9 kt][64][8]
     f3 = mfma_fragments(w3pk)                                    # [2 ncq nc][kt][64][8]
     s2 = f2.reshape(ncq, 2, 9 * kt, 64, 8).permute(0, 2, 1, 3, 4)
-    s3 = f3.reshape(nc, ncq, 2, kt, 64, 8).permute(1, 0, 3, 2, 4, 5).reshape(ncq, nc * kt, 2, 64, 8)
-    return torch.cat([s2, s3], dim=1).contiguous()
+    s3 = f3.reshape(nc, ncq, 2, kt, 64, 8).permute(1, 0, 3, 2, 4, 5)              # [ncq][nc][kt][2][64][8]
+    if w1n is None:
+        return torch.cat([s2, s3.reshape(ncq, nc * kt, 2, 64, 8)], dim=1).contiguous()
+    if tuple(w1n.shape) != (planes, c):
+        raise ValueError('pack_tail_stream: the next conv1 pack must be [%d][%d]' % (planes, c))
+    f1 = mfma_fragments(w1n)                                     # [2 ncq][nc kt][64][8]
+    s1 = f1.reshape(ncq, 2, nc, kt, 64, 8).permute(0, 2, 3, 1, 4, 5)              # [ncq][nc][kt][2][64][8]
+    s31 = torch.stack([s3, s1], dim=2).reshape(ncq, nc * 2 * kt, 2, 64, 8)
+    return torch.cat([s2, s31], dim=1).contiguous()
 
 
 def bottleneck_conv3_order(planes):

@@ -166,6 +166,11 @@ STREAMED_LAYER3_TAIL = True
 # layer2's identity Bottlenecks as conv1 (a conv launch) + the register-streamed tail instead of
 # the fused LDS-ring block (posu_bottleneck2_fwd)
 STREAMED_LAYER2_TAIL = True
+# consecutive streamed identity tails chained: block i's tail also computes block i+1's conv1
+# over its output (posu_bottleneck_tail_stream_next_fwd), so block i+1 has no conv1 launch and y
+# is not re-read for it (tools/chain_micro.py: layer2 105.0 vs 130.0 us, layer3 76.3 vs 85.0 us
+# for a tail + the next conv1 launch; bit-identical)
+CHAINED_TAILS = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -178,7 +183,7 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -190,6 +195,8 @@ class _Block:
         self.l2 = False              # a layer2 identity block (fused kernel, the convs' own packs)
         self.l3 = False              # a layer3 identity block (conv1, then the fused conv2 + conv3 tail)
         self.wst = None              # layer2 / layer3: the tail's per-wave weight streams (pack_tail_stream)
+        self.chain = None            # the next identity block's conv1 (_Conv) when the tails chain
+        self.wsn = None              # the streams with that conv1 appended (pack_tail_stream(.., w1n))
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -215,6 +222,43 @@ class _Block:
             self.l3 = self._layer3_shape()
             if self.l2 or self.l3:
                 self.wst = pack_tail_stream(self.convs[1].w, self.convs[2].w)
+
+    def link_next(self, nxt):
+        """Chain this identity block's streamed tail with the next block's conv1 (same layer, same
+        kind of tail)."""
+        if (self.l2 and nxt.l2) or (self.l3 and nxt.l3):
+            self.chain = nxt.convs[0]
+            self.wsn = pack_tail_stream(self.convs[1].w, self.convs[2].w, self.chain.w)
+
+    def _tail_kind(self, x):
+        """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
+        if not FUSED_BOTTLENECK or not _fused_fits(x, self.cout):
+            return None
+        if self.l2 and STREAMED_LAYER2_TAIL and x.shape[2] == 32 and x.shape[1] % 4 == 0:
+            return 'l2'
+        if (self.l3 and FUSED_LAYER3_TAIL and STREAMED_LAYER3_TAIL and x.shape[2] == 16 and
+                x.shape[1] % 8 == 0):
+            return 'l3'
+        return None
+
+    def run(self, x, code, out=None, t1=None):
+        """-> (y, t1n): t1n = the next block's conv1 output when this block's tail is chained
+        (CHAINED_TAILS), else None; t1 = this block's conv1 output from the previous block's
+        chained tail (None: computed here)."""
+        kind = self._tail_kind(x)
+        if kind is None:
+            if t1 is not None:
+                raise RuntimeError('a chained conv1 output handed to a block without a streamed tail')
+            return self(x, code, out=out), None
+        c1, c2, c3 = self.convs
+        if t1 is None:
+            t1 = c1(x, code)
+        if self.chain is not None and CHAINED_TAILS:
+            n1 = self.chain
+            return ops.bottleneck_tail_stream_next_nhwc(t1, x, self.wsn, c2.scale, c2.shift, c3.scale, c3.shift,
+                                                        n1.scale, n1.shift, code, out=out)
+        return ops.bottleneck_tail_stream_nhwc(t1, x, self.wst, c2.scale, c2.shift, c3.scale, c3.shift, code,
+                                               out=out), None
 
     def _layer2_shape(self):
         c1, c2, c3 = self.convs
@@ -303,6 +347,9 @@ class PoseResNetPlan:
         self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, STEM_S2D_PAD, bk, ops.torch_dtype(code))
         self.layers = [[_Block(b, code, bk) for b in layer] for layer in
                        (net.layer1, net.layer2, net.layer3, net.layer4)]
+        for layer in self.layers:
+            for b0, b1 in zip(layer, layer[1:]):
+                b0.link_next(b1)
         mods = list(net.deconv_layers)
         self.deconvs = []
         for i in range(0, len(mods), 3):
@@ -370,19 +417,20 @@ class PoseResNetPlan:
         """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
         code = self.code
         x = self.stem_pool(x)
-        for li in (0, 1):
-            layer = self.layers[li]
-            for bi, blk in enumerate(layer):
-                last = bi == len(layer) - 1
-                if li == 0 and last and keep is not None:
-                    x = blk(x, code, out=keep)
-                elif li == 1 and last and out is not None:
-                    x = blk(x, code, out=out)
-                else:
-                    x = blk(x, code)
-            if li == 0:
-                x1 = x
+        x1 = x = self._run_layer(self.layers[0], x, code, out=keep)
+        x = self._run_layer(self.layers[1], x, code, out=out)
         return x, x1
+
+    @staticmethod
+    def _run_layer(layer, x, code, out=None):
+        """The blocks of one layer in order (out: the last block's output buffer); chained
+        streamed tails hand the next block its conv1 output."""
+        t1 = None
+        for bi, blk in enumerate(layer):
+            x, t1 = blk.run(x, code, out=out if bi == len(layer) - 1 else None, t1=t1)
+        if t1 is not None:
+            raise RuntimeError('the last block of a layer produced a chained conv1 output')
+        return x
 
     def _last_deconv_head(self, x, keep_f, hm_out=None, f_out=None):
         """Last deconv (+BN+ReLU) and the 1x1 head, fused into one launch when possible."""
@@ -431,8 +479,7 @@ class PoseResNetPlan:
             x = self.stem_pool(x)
             x1 = None
             for li, layer in enumerate(self.layers):
-                for blk in layer:
-                    x = blk(x, code)
+                x = self._run_layer(layer, x, code)
                 if li == 0:
                     x1 = x
             for dc in self.deconvs[:-1]:
@@ -456,8 +503,7 @@ class PoseResNetPlan:
             self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
         y = x2
         for layer in self.layers[2:]:
-            for blk in layer:
-                y = blk(y, code)
+            y = self._run_layer(layer, y, code)
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _native.exported_symbols()
-    assert lib.posu_abi_version() == _native.ABI_VERSION == 8
+    assert lib.posu_abi_version() == _native.ABI_VERSION == 9
     assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
 
 
@@ -276,6 +276,28 @@ def test_bottleneck_conv3_order_is_the_accumulator_fragment_order():
     w1 = torch.randn(64, 256, 1, 1)
     x = torch.randn(256)
     torch.testing.assert_close(packing.pack_bottleneck_conv1_weight(w1, torch.float32) @ x[o1], w1.view(64, 256) @ x)
+
+
+@pytest.mark.parametrize('planes,c', [(128, 512), (256, 1024)])
+def test_chained_tail_stream_interleaves_the_next_conv1(planes, c):
+    """pack_tail_stream(w2, w3, w1n): the plain tail's stream with, after conv3 chunk nc, the next
+    conv1's KT k-steps over that chunk's channels (wave cq: n-tiles 2 cq, 2 cq + 1), so the kernel
+    walks one linear stream of equal KT-step blocks (csrc/tail_stream.hip, NEXT)."""
+    w2, w3, w1n = torch.randn(planes, 9 * planes), torch.randn(c, planes), torch.randn(planes, c)
+    plain, chained = packing.pack_tail_stream(w2, w3), packing.pack_tail_stream(w2, w3, w1n)
+    ncq = kt = planes // 32
+    nc = c // planes
+    assert chained.shape == (ncq, 9 * kt + 2 * nc * kt, 2, 64, 8)
+    assert torch.equal(plain[:, :9 * kt], chained[:, :9 * kt])
+    f1 = packing.mfma_fragments(w1n)
+    for n in range(nc):
+        base = 9 * kt + 2 * n * kt
+        assert torch.equal(plain[:, 9 * kt + n * kt:9 * kt + (n + 1) * kt], chained[:, base:base + kt])
+        for q in range(ncq):
+            for j in range(2):
+                assert torch.equal(chained[q, base + kt:base + 2 * kt, j], f1[2 * q + j, n * kt:(n + 1) * kt])
+    with pytest.raises(ValueError):
+        packing.pack_tail_stream(w2, w3, torch.randn(planes, c // 2))
 
 
 def test_fused_bottleneck_byte_guard():

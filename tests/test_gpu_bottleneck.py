@@ -262,3 +262,75 @@ def test_plan_with_fused_bottlenecks_matches_unfused_plan(cuda, precision):
           % (precision, dx, dh.max(), dh.mean()))
     assert dx < (0.1 if precision == 'bf16' else 0.02)
     assert dh.mean() < (0.01 if precision == 'bf16' else 0.002)
+
+
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('layer,n,h', [('layer3', 2, 16), ('layer3', 1, 8), ('layer3', 3, 24), ('layer3', 128, 16),
+                                       ('layer2', 2, 32), ('layer2', 1, 4), ('layer2', 3, 12), ('layer2', 128, 32)])
+def test_chained_tail_matches_tail_and_next_conv1(cuda, code, layer, n, h):
+    """Chained streamed tail (posu_bottleneck_tail_stream_next_fwd): block i's tail computing block
+    i+1's conv1 + BN1 + ReLU over its output y.  y and t1n are bit-identical to the plain tail
+    followed by a conv launch of the next conv1 over y (the same K order per accumulator); both
+    outputs start as NaN sentinels, so a store that never lands fails."""
+    c, p, w = (1024, 256, 16) if layer == 'layer3' else (512, 128, 32)
+    g = torch.Generator().manual_seed(97 + h + n)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
+    w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1n = (torch.rand(p, generator=g) + 0.5, torch.randn(p, generator=g) * 0.1)
+    dt = ops.torch_dtype(code)
+    bk = ops.conv_bk(code)
+    xd = torch.randn(n, h, w, c, generator=g).to(cuda, dt)
+    p1, p2, p3, p1n = (packing.pack_conv_weight(t.to(cuda), t.shape[1], bk, dt) for t in (w1, w2, w3, w1n))
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1], bn1n[0], bn1n[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, p, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    y_ref = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5], code)
+    t1n_ref = ops.conv2d_nhwc(y_ref, p1n, p, 1, 1, 1, 0, s[6], s[7], None, True, code)
+    y, t1n = ops.bottleneck_tail_stream_next_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1n), s[2], s[3], s[4],
+                                                  s[5], s[6], s[7], code, out=_sentinel(xd),
+                                                  t1n=_sentinel(t1))
+    torch.cuda.synchronize()
+    dy = int((y.view(torch.int16) != y_ref.view(torch.int16)).sum())
+    dt1 = int((t1n.view(torch.int16) != t1n_ref.view(torch.int16)).sum())
+    print('%s chained tail n=%d h=%d: y differing %d, t1n differing %d' % (layer, n, h, dy, dt1))
+    assert dy == 0 and dt1 == 0
+
+
+def test_chained_tail_refuses_bad_operands(cuda):
+    x = torch.zeros(1, 4, 32, 512, device=cuda, dtype=torch.bfloat16)
+    t1 = torch.zeros(1, 4, 32, 128, device=cuda, dtype=torch.bfloat16)
+    ws = torch.zeros(4, 9 * 4 + 2 * 16, 2, 64, 8, device=cuda, dtype=torch.bfloat16)
+    s = torch.ones(512, device=cuda)
+    with pytest.raises(RuntimeError, match='alias'):
+        ops.bottleneck_tail_stream_next_nhwc(t1, x, ws, s, s, s, s, s, s, BF16, t1n=t1)
+    with pytest.raises(RuntimeError, match='multiple of 4'):
+        ops.bottleneck_tail_stream_next_nhwc(t1[:, :3], x[:, :3], ws, s, s, s, s, s, s, BF16)
+    with pytest.raises(ValueError, match='next conv1 pack'):
+        packing.pack_tail_stream(torch.zeros(128, 1152, device=cuda, dtype=torch.bfloat16),
+                                 torch.zeros(512, 128, device=cuda, dtype=torch.bfloat16),
+                                 torch.zeros(128, 256, device=cuda, dtype=torch.bfloat16))
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp16'])
+def test_plan_with_chained_tails_matches_unchained_plan(cuda, precision):
+    """The R50 plan with the chained layer2 / layer3 tails (plan.CHAINED_TAILS) gives exactly the
+    heatmaps of the plan that runs every conv1 as its own launch."""
+    import posu.plan as P
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
+    net = net.to(cuda).eval()
+    plan = net.plan(cuda)
+    assert [b.chain is not None for b in plan.layers[1]] == [False, True, True, False]
+    assert [b.chain is not None for b in plan.layers[2]] == [False, True, True, True, True, False]
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=13)]
+    saved = P.CHAINED_TAILS
+    try:
+        with torch.no_grad():
+            P.CHAINED_TAILS = True
+            hm1, _, f1 = plan.run(plan.pack_input(views))
+            P.CHAINED_TAILS = False
+            hm0, _, f0 = plan.run(plan.pack_input(views))
+    finally:
+        P.CHAINED_TAILS = saved
+    torch.cuda.synchronize()
+    assert torch.equal(hm1, hm0) and torch.equal(f1, f0)
