@@ -221,36 +221,46 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
                                                                 int Pseg, int C, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
                                                                 float momentum, const float* __restrict__ kshift,
-                                                                float* running_mean,
-                                                                float* running_var, float* __restrict__ mean,
-                                                                float* __restrict__ rstd, float* __restrict__ scale,
+                                                                float* __restrict__ running_mean,
+                                                                float* __restrict__ running_var,
+                                                                float* __restrict__ mean, float* __restrict__ rstd,
+                                                                float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
   const int cl = threadIdx.x / FLN, ln = threadIdx.x % FLN;
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
+  // the per-channel parameters first: their loads overlap the partials' (one round trip, not
+  // one per segment behind the running-statistics stores)
+  const int cc = valid ? c : 0;
+  const float gm = gamma ? gamma[cc] : 1.f, bt = beta ? beta[cc] : 0.f;
+  float rm = running_mean ? running_mean[cc] : 0.f, rv = running_var ? running_var[cc] : 0.f;
   for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
-    double sums[FSEG], sqs[FSEG];
     const int ns = min(FSEG, nseg - seg0);
+    float ks[FSEG];
+#pragma unroll
+    for (int k = 0; k < FSEG; ++k) ks[k] = k < ns ? kshift[(seg0 + k) * C + cc] : 0.f;
+    double sums[FSEG], sqs[FSEG];
     reduce_segs(part, seg0, ns, NB, C, c, valid, ln, sums, sqs);
     if (ln != 0 || !valid) continue;
     for (int k = 0; k < ns; ++k) {  // in segment order: running stats compose like V calls
       const int seg = seg0 + k;
       const double sum = sums[k], sq = sqs[k];  // shifted by K = kshift[seg][c]
       const double dm = sum / n;
-      const double mu = static_cast<double>(kshift[seg * C + c]) + dm;
+      const double mu = static_cast<double>(ks[k]) + dm;
       const double var = fmax(sq / n - dm * dm, 0.0);
       const double r = 1.0 / sqrt(var + static_cast<double>(eps));
-      const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
       mean[seg * C + c] = static_cast<float>(mu);
       rstd[seg * C + c] = static_cast<float>(r);
       scale[seg * C + c] = static_cast<float>(gm * r);
       shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
-      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * static_cast<float>(mu);
-      if (running_var)
-        running_var[c] = (1.f - momentum) * running_var[c] +
-                         momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+      rm = (1.f - momentum) * rm + momentum * static_cast<float>(mu);
+      rv = (1.f - momentum) * rv + momentum * static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
     }
+  }
+  if (ln == 0 && valid) {
+    if (running_mean) running_mean[c] = rm;
+    if (running_var) running_var[c] = rv;
   }
 }
 
@@ -444,10 +454,15 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
   const int c = blockIdx.x * FCH + cl;
   const bool valid = c < C;
   const double n = static_cast<double>(Pseg);
+  const int cc = valid ? c : 0;
+  const float gm = gamma ? gamma[cc] : 1.f;
   double tg = 0.0, tgx = 0.0;
   for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
-    double sgs[FSEG], sgxs[FSEG];
     const int ns = min(FSEG, nseg - seg0);
+    float rs[FSEG];  // loaded beside the partials
+#pragma unroll
+    for (int k = 0; k < FSEG; ++k) rs[k] = k < ns ? rstd[(seg0 + k) * C + cc] : 0.f;
+    double sgs[FSEG], sgxs[FSEG];
     reduce_segs(part, seg0, ns, NB, C, c, valid, ln, sgs, sgxs);
     if (ln != 0 || !valid) continue;
     for (int k = 0; k < ns; ++k) {
@@ -455,8 +470,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const double* __re
       const double sg = sgs[k], sgx = sgxs[k];
       tg += sg;
       tgx += sgx;
-      const float gm = gamma ? gamma[c] : 1.f;
-      coef[(seg * 3 + 0) * C + c] = gm * rstd[seg * C + c];
+      coef[(seg * 3 + 0) * C + c] = gm * rs[k];
       coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
       coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
     }

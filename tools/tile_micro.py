@@ -49,6 +49,7 @@ def main():
     ap.add_argument('--lib', default=None, help='another build of libposeu.so (experiments)')
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--only', default='', help='comma-separated substrings of the shape names to run')
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(',')]
     if a.lib:
@@ -58,6 +59,8 @@ def main():
     dt = torch.bfloat16
     bk = ops.conv_bk(BF16)
     for name, kind, (n, h, w, cin), cout, k in SHAPES:
+        if a.only and not any(o in name for o in a.only.split(',')):
+            continue
         x = torch.randn(n, h, w, cin, device=dev, generator=g).to(dt)
         sc = torch.rand(cout, device=dev, generator=g) + 0.5
         sh = torch.randn(cout, device=dev, generator=g) * 0.1
