@@ -109,7 +109,8 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *   x: [N, H, W, C] dtype, C % 8 == 0.
  *   w: packed [CoutPad][Kpad] dtype, k = (kh*KW + kw)*C + ci, zero padded;
  *      CoutPad = round_up(Cout, 64), Kpad = round_up(KH*KW*C, posu_conv_bk(dtype)).
- *   scale/shift: [Cout] f32 (may be NULL: scale 1, shift 0).
+ *   scale/shift: [Cout] f32 (may be NULL: scale 1, shift 0), 16-byte aligned (here and
+ *   in posu_conv1x1_dual_fwd / posu_deconv4x4s2_fwd / posu_deconv4x4s2_head_fwd).
  *   residual: NULL or [N, Ho, Wo, Cout] dtype.
  *   y: [N, Ho, Wo, Cout] dtype.  `pad` is the top/left padding; Ho/Wo may be
  *   smaller than (H + 2 pad - KH) / stride + 1 (bottom/right padding implied).

@@ -458,6 +458,13 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // pixel per lane), so its partial heatmaps over its 64 channels are 2 MFMAs per m-tile;
   // the four column waves' partials are summed in LDS in a fixed order.
   constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && E == 8;
+  if constexpr (SG && (POSU_IG_ABLATE & 16)) {  // timing ablation: no epilogue (results wrong)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+    return;
+  }
   if (E == 8 && TN % 2 == 0 && g.mode == 0 && (!g.hm || HEAD256)) {
     // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
     // holds 8 consecutive channels (16-B stores, half the store instructions):
@@ -483,23 +490,33 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     float sc[TP][8], sh[TP][8];
 #pragma unroll
     for (int jp = 0; jp < TP; ++jp) {
+      // 8 consecutive channels, all inside Cout or all past it (Cout is a multiple of 8): two
+      // 16-B loads per parameter instead of eight 4-B ones
       cop[jp] = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int co = cop[jp] + e;
-        sc[jp][e] = (co < g.Cout && g.scale) ? g.scale[co] : 1.f;
-        sh[jp][e] = (co < g.Cout && g.shift) ? g.shift[co] : 0.f;
-      }
+      const bool in = cop[jp] < g.Cout;
+      const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 s0 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp]) : one;
+      const float4 s1 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp] + 4) : one;
+      const float4 h0 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp]) : zero;
+      const float4 h1 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp] + 4) : zero;
+      sc[jp][0] = s0.x; sc[jp][1] = s0.y; sc[jp][2] = s0.z; sc[jp][3] = s0.w;
+      sc[jp][4] = s1.x; sc[jp][5] = s1.y; sc[jp][6] = s1.z; sc[jp][7] = s1.w;
+      sh[jp][0] = h0.x; sh[jp][1] = h0.y; sh[jp][2] = h0.z; sh[jp][3] = h0.w;
+      sh[jp][4] = h1.x; sh[jp][5] = h1.y; sh[jp][6] = h1.z; sh[jp][7] = h1.w;
     }
+    // the fused head without the deconv output stored reads no pixel address: skip the decode
+    const bool no_pix = head && yp == nullptr && rp == nullptr;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + rowA(i) + r16;
       const bool mok = m < g.M;
-      const int mm = mok ? m : 0;
-      const int n = mm / HoWo, rem = mm - n * HoWo;
-      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-      const size_t pix =
-          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      size_t pix = 0;
+      if (!no_pix) {
+        const int mm = mok ? m : 0;
+        const int n = mm / HoWo, rem = mm - n * HoWo;
+        const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+        pix = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      }
       uint4 rv[TP];
 #pragma unroll
       for (int jp = 0; jp < TP; ++jp) {
@@ -542,6 +559,11 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
     if constexpr (HEAD256) {
       if (head) {
+        if constexpr (SG && (POSU_IG_ABLATE & 32)) {  // timing ablation: no head reduction / stores
+#pragma unroll
+          for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(hacc[i]));
+          return;
+        }
         __syncthreads();  // the ring is no longer read: partial heatmaps [wn][joint][256 px]
         float* Hs = reinterpret_cast<float*>(smem);
 #pragma unroll
@@ -1370,6 +1392,11 @@ int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what,
   return POSU_ERR_ARG;
 }
 
+// the direct epilogue reads the per-channel BN parameters as 16-B vectors
+bool params_aligned(const float* scale, const float* shift) {
+  return (reinterpret_cast<size_t>(scale) & 15) == 0 && (reinterpret_cast<size_t>(shift) & 15) == 0;
+}
+
 int bk_of(int dtype) { return dtype == POSU_F32 ? 32 : 64; }
 int esz_of(int dtype) { return dtype == POSU_F32 ? 4 : 2; }
 
@@ -1420,6 +1447,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
                "posu_conv2d_fwd: Ho/Wo larger than the window allows");
   POSU_REQUIRE(static_cast<long long>(N) * Ho * Wo * Cout < (1LL << 31), "posu_conv2d_fwd: output too large");
+  POSU_REQUIRE(params_aligned(scale, shift), "posu_conv2d_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
   g.shift = shift;
@@ -1452,6 +1480,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
   POSU_REQUIRE(stride2 > 0 && (H - 1) * stride2 < H2 && (W - 1) * stride2 < W2,
                "posu_conv1x1_dual_fwd: source-2 grid too small for the output grid");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * Cout < (1LL << 31), "posu_conv1x1_dual_fwd: output too large");
+  POSU_REQUIRE(params_aligned(scale, shift), "posu_conv1x1_dual_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.x2 = x2;
   g.H2 = H2;
@@ -1482,6 +1511,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
                "posu_deconv4x4s2_fwd: output too large");
+  POSU_REQUIRE(params_aligned(scale, shift), "posu_deconv4x4s2_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
   g.shift = shift;
@@ -1506,6 +1536,7 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   if (int st = common_checks(dtype, x, w, hm, N, H, W, C, Cout, "posu_deconv4x4s2_head_fwd")) return st;
   POSU_REQUIRE(hw && Cout == 256 && J > 0 && J <= 16,
                "posu_deconv4x4s2_head_fwd: needs Cout == 256, 0 < J <= 16 and head weights");
+  POSU_REQUIRE(params_aligned(scale, shift), "posu_deconv4x4s2_head_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
   g.shift = shift;
