@@ -75,6 +75,9 @@ def parse():
     ap.add_argument('--size', type=int, default=256)
     ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
     ap.add_argument('--no-graph', action='store_true')
+    ap.add_argument('--serial-geo', action='store_true',
+                    help='run each batch\'s decode + geometry after its network on one stream (default: on a '
+                         'second stream, overlapping the next batch\'s network)')
     ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
                     help="train mode: torch.optim.Adam's fused kernel (default) or its foreach launches")
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
@@ -441,18 +444,34 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
         stream = torch.cuda.current_stream(dev)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        # decode + geometry of batch i on a second stream, overlapping the network of batch i + 1
+        # (a two-stage pipeline over the rotated batches): batch i's geometry waits for its own
+        # network; a batch's next network replay waits for its previous geometry (its graphs
+        # share one memory pool and the heatmap buffer).  --serial-geo: one stream, in order.
+        geo_stream = None if args.serial_geo or nbatch < 2 else torch.cuda.Stream(dev)
+        geo_done = [None] * nbatch
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(steps):
-            r = reps[i % nbatch]
+            b = i % nbatch
+            r = reps[b]
+            if geo_done[b] is not None:
+                stream.wait_event(geo_done[b])
             ev[i][0].record(stream)
             hm = r.run_net()
             ev[i][1].record(stream)
-            r.run_geo(hm)
-            ev[i][2].record(stream)
+            if geo_stream is None:
+                r.run_geo(hm)
+                ev[i][2].record(stream)
+                continue
+            geo_stream.wait_event(ev[i][1])
+            with torch.cuda.stream(geo_stream):
+                r.run_geo(hm)
+            ev[i][2].record(geo_stream)
+            geo_done[b] = ev[i][2]
         torch.cuda.synchronize()
         if dist is not None:
             dist.barrier()
@@ -628,7 +647,10 @@ def infer_main(args):
                    'parallelism': 'dp%d (the global batch of %d groups sharded by posu.dist.shard_groups, '
                                   'no data-path collective)' % (world, args.groups * world),
                    'hipgraph': res['use_graph'], 'chunks': args.chunks, 'tiles': res['tuned'] or 'heuristic',
-                   'input_batches_rotated': args.batches},
+                   'input_batches_rotated': args.batches,
+                   'stages': ('network and decode+geometry in order on one stream' if args.serial_geo or args.batches < 2
+                              else 'network on the main stream, decode+geometry of the same batch on a second '
+                                   'stream overlapping the next batch\'s network')},
         'network_ms': round(res['net_ms'], 4), 'decode_geometry_ms': round(res['geo_ms'], 4),
         'groups_per_s': round(value / 4, 2), 'per_rank_frames': [int(p[0]) for p in per_rank],
         'per_rank_seconds': [round(p[1], 5) for p in per_rank],
