@@ -212,6 +212,21 @@ def input_views(shard, size, b, device):
     return [v.to(device) for v in syn.group_views(4, shard, size, seed=100 + b)]
 
 
+def pmc_traffic_train(layers, size, precision, groups):
+    """HBM bytes of one training step from the newest committed PMC reduction
+    (profiles/<round>/pmc_traffic_train.txt, tools/pmc_train_traffic.py), for the default
+    training workload; (None, None) otherwise."""
+    if (layers, size, precision, groups) != (50, 256, 'bf16', 32):
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*', 'pmc_traffic_train.txt')))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.loads(next(ln for ln in f if ln.startswith('{')))
+    return d['traffic_bytes'], {'file': os.path.relpath(files[-1], REPO), 'commit': d.get('commit')}
+
+
 def pmc_traffic(layers, size, precision, groups):
     """HBM bytes of one network forward from the newest committed PMC reduction
     (profiles/<round>/pmc_traffic_network.txt, written by tools/profile_round.sh with the
@@ -608,6 +623,7 @@ def infer_main(args):
         t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
         train = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
         train.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
+                     traffic=t['roofline']['traffic'] if t['roofline'] else None,
                      parallelism=t['config']['parallelism'], workload=t['config']['workload'],
                      optimizer=t['config']['optimizer'])
     if rank != 0:
@@ -753,10 +769,14 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
     if gf is not None:
         achieved = gf * value / world / 1e3
         peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS
+        traffic, src = pmc_traffic_train(args.layers, args.size, args.precision, nb)
         roof = {'bound': 'mfma', 'achieved': round(achieved, 2), 'peak': peak, 'unit': 'TFLOP/s',
-                'frac': round(achieved / peak, 4), 'traffic': None,
+                'frac': round(achieved / peak, 4), 'traffic': traffic,
                 'kernel': 'whole training step per GPU (fwd + bwd convs, BN, Adam)',
                 'flop_per_launch': '%.1f GFLOP/frame x %d frames' % (gf, frames)}
+        if traffic:
+            roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per training step')
+            roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
     return {
         'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
         'steps': steps, 'warmup': warmup, 'ms_per_step': round(elapsed / steps * 1e3, 4),
