@@ -102,18 +102,19 @@ def parse():
                          'stream keeps normal priority, so the data-gradient chain wins dispatch) or on '
                          'the default stream (default; measured equal: 21.82 vs 21.80 ms per step)')
     ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=0|1',
-                    help='A/B runs: set a boolean switch of posu.plan (e.g. STREAMED_LAYER2_TAIL=0) before '
-                         'the plans are built')
+                    help='A/B runs: set a boolean switch of posu.plan / posu.train_plan (e.g. '
+                         'STREAMED_LAYER2_TAIL=0, FUSED_BN_STATS=0) before the plans are built')
     return ap.parse_args()
 
 
 def apply_plan_flags(flags):
-    from posu import plan as pl
+    from posu import plan as pl, train_plan as tpl
     for f in flags:
         name, _, val = f.partition('=')
-        if not hasattr(pl, name) or not isinstance(getattr(pl, name), bool) or val not in ('0', '1'):
-            raise SystemExit('--plan-flag %s: not a boolean switch of posu.plan' % f)
-        setattr(pl, name, val == '1')
+        mod = next((m for m in (pl, tpl) if isinstance(getattr(m, name, None), bool)), None)
+        if mod is None or val not in ('0', '1'):
+            raise SystemExit('--plan-flag %s: not a boolean switch of posu.plan / posu.train_plan' % f)
+        setattr(mod, name, val == '1')
 
 
 # ------------------------------------------------------------------ launcher

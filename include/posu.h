@@ -45,7 +45,8 @@ extern "C" {
 const char* posu_last_error(void);
 /* ABI revision: 4 stateless conv knobs; 5 the fused layer1 Bottleneck kernels and batched
  * weight packing; 6 the LDS-tiled packing; 7 the layer3 Bottleneck tail; 8 the crop warp
- * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd).  The
+ * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd); 10 the
+ * BatchNorm statistics in the conv epilogue (posu_conv2d_fwd_stats, posu_bn_stats_finalize).  The
  * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
@@ -462,6 +463,31 @@ int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const
                       const float* beta, float eps, float momentum, float* running_mean,
                       float* running_var, float* mean, float* rstd, float* scale, float* shift,
                       void* workspace, long long workspace_bytes, void* stream);
+/* The same forward with its statistics taken in the producing convolution's epilogue instead of
+ * a pass over z (training forward, lib/models/pose_resnet.py:79-84 with train-mode BN):
+ * posu_conv2d_fwd_stats is the raw conv (no BN / residual / ReLU; y bit-identical to
+ * posu_conv2d_fwd with scale/shift NULL) that also writes per-output-tile channel sums and
+ * sums of squares of the stored values, part [nseg][ntiles][2][Cout] f32 (*ntiles_out = tiles
+ * per segment), taken about a per-channel shift kshift [Cout] (NULL: 0; the running mean keeps the
+ * variance of channels whose mean is large against their spread); BF16 / F16, N*Ho*Wo/nseg a
+ * multiple of 256, part_bytes >= nseg * (N*Ho*Wo/nseg / 64) * 2 * Cout * 4.  posu_bn_stats_finalize
+ * (same kshift, which may be running_mean itself: it is read before the update) turns them into
+ * mean/rstd/scale/shift and the running statistics like posu_bn_train_fwd (tiles summed in order,
+ * f64). */
+int posu_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
+                          int KH, int KW, int stride, int pad, void* y, int Ho, int Wo, int tile, int nseg,
+                          const float* kshift, float* part, long long part_bytes, int* ntiles_out, void* stream);
+/* The same for the deconvolution (posu_deconv4x4s2_fwd raw: no BN / ReLU): segments of
+ * N*H*W/nseg INPUT pixels (a multiple of 256), part [nseg][4 ntiles][2][Cout] (*ntiles_out counts
+ * the four parity classes' tiles; the finalize's Pseg is the output pixels, 4 N*H*W/nseg),
+ * part_bytes >= nseg * 4 * (N*H*W/nseg / 64) * 2 * Cout * 4. */
+int posu_deconv4x4s2_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
+                               void* y, int tile, int nseg, const float* kshift, float* part,
+                               long long part_bytes, int* ntiles_out, void* stream);
+int posu_bn_stats_finalize(int nseg, int Pseg, int C, int ntiles, const float* part, const float* kshift,
+                           const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
+                           float* running_var, float* mean, float* rstd, float* scale, float* shift,
+                           void* stream);
 /* y = act(z * scale[seg] + shift[seg] (+ residual)) */
 int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
                   const float* shift, const void* residual, int relu, void* y, void* stream);
