@@ -1,7 +1,12 @@
 set -o pipefail
 O=gpurun_out/r3ae
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_train_kernels.py tests/test_gpu_train.py -q -x --timeout 120 --timeout-method thread > $O/tests.log 2>&1; rc=$?
+# the training tests with the fused BN statistics switched on (train_plan.FUSED_BN_STATS)
+timeout -k 10 400 python -u -c "
+import sys; sys.path[:0] = ['pose-unsupervised_amd/lib', '.']
+import posu.train_plan as t; t.FUSED_BN_STATS = True
+import pytest; sys.exit(pytest.main(['tests/test_gpu_train_kernels.py', 'tests/test_gpu_train.py', '-q', '-x', '--timeout', '120', '--timeout-method', 'thread']))
+" > $O/tests.log 2>&1; rc=$?
 tail -15 $O/tests.log; [ $rc -eq 0 ] || exit $rc
 T="bench.py --mode train --steps 10 --warmup 3"
 timeout -k 10 300 python -u $T --plan-flag FUSED_BN_STATS=1 > $O/t_on.json 2>/dev/null || exit 1
