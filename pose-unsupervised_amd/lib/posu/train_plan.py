@@ -54,8 +54,9 @@ def _conv_tuned(x, w, cout, k, stride, pad, code):
 
 # BatchNorm statistics of the training forward taken in the producing conv's epilogue
 # (posu_conv2d_fwd_stats + posu_bn_stats_finalize) instead of a pass over z, where it applies
-# (bf16 / fp16, segments of a multiple of 256 output pixels); False: bn_train_fwd's pass
-FUSED_BN_STATS = False  # set True once validated on the GPU (tools/gpu_r3ae.sh)
+# (bf16 / fp16, segments of a multiple of 256 output pixels); False (default): bn_train_fwd's pass
+# -- measured faster: 21.54 vs 21.91 / 21.99 ms per step (profiles/r03/fused_bn_stats_ab_r3ae.txt)
+FUSED_BN_STATS = False
 
 
 def _conv_stats_tuned(x, w, cout, k, stride, pad, nseg, code, kshift):
