@@ -531,7 +531,8 @@ def peaked_parity(args, dev):
     fit_s = time.perf_counter() - t0
     out = {}
     ref = None
-    for prec in ('fp32', args.precision):
+    # fp32 (the parity mode) first, then both 2-byte modes (same MFMA rate), the benched one included
+    for prec in dict.fromkeys(('fp32', args.precision, 'bf16', 'fp16')):
         out[prec], ref = peaked.parity(net, task, dev, prec, ref)
     out['fit'] = {'steps': args.peaked_steps, 'seconds': round(fit_s, 2), 'groups': task['groups'],
                   'heatmap_peak_mean': out['fp32']['heatmap_peak_mean'],
@@ -809,6 +810,16 @@ def train_main(args):
         dist.destroy_process_group()
 
 
+def dump_tiles():
+    """POSU_DUMP_TILES=path: the process's autotuned tile table (every leg) as JSON, for diffing
+    the tile choices of two runs."""
+    path = os.environ.get('POSU_DUMP_TILES')
+    if path:
+        from posu import plan as pl
+        with open(path, 'w') as f:
+            json.dump(sorted([[repr(k), t] for k, t in pl.tuned_tiles().items()]), f, indent=0)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
@@ -816,9 +827,12 @@ def main():
     if args.dry_run:
         return dry_run_main(args)
     apply_plan_flags(args.plan_flag)
-    if args.mode == 'train':
-        return train_main(args)
-    return infer_main(args)
+    try:
+        if args.mode == 'train':
+            return train_main(args)
+        return infer_main(args)
+    finally:
+        dump_tiles()
 
 
 if __name__ == '__main__':

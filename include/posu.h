@@ -46,8 +46,9 @@ const char* posu_last_error(void);
 /* ABI revision: 4 stateless conv knobs; 5 the fused layer1 Bottleneck kernels and batched
  * weight packing; 6 the LDS-tiled packing; 7 the layer3 Bottleneck tail; 8 the crop warp
  * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd); 10 the
- * BatchNorm statistics in the conv epilogue (posu_conv2d_fwd_stats, posu_bn_stats_finalize).  The
- * ctypes binding refuses a library of another revision. */
+ * BatchNorm statistics in the conv epilogue (measured slower, removed in 11); 11 the streamed
+ * tails take their weight stream's byte size, the round-2 LDS-ring layer2 block / layer3 tail
+ * kernels removed.  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -181,38 +182,19 @@ int posu_bottleneck_fwd(int dtype, const void* x, int N, int H, int W, int C, in
                         const float* b2, const void* w3, const float* s3, const float* b3, void* y,
                         void* stream);
 
-/* The identity Bottleneck of layer2 (lib/models/pose_resnet.py:61-99) as one launch, with the
- * weights streamed through LDS (they do not fit): W = 32, C = 512, P = 128, H % 4 == 0; dtype
- * BF16 / F16.  x, y: [N, H, W, C] (no alias); w1 [P][C], w2 [P][9P], w3 [C][P] in
- * posu_conv2d_fwd's packing (natural channel order); s/b as posu_bottleneck_fwd.  Same K
- * order per accumulator as the three convolutions. */
-int posu_bottleneck2_fwd(int dtype, const void* x, int N, int H, int W, int C, int P, const void* w1,
-                         const float* s1, const float* b1, const void* w2, const float* s2,
-                         const float* b2, const void* w3, const float* s3, const float* b3, void* y,
-                         void* stream);
-
-/* Tail of an identity Bottleneck of layer3 (lib/models/pose_resnet.py:79-99, eval BN folded),
- * PoseResNet at 256x256: conv2 3x3 + BN2 + ReLU -> conv3 1x1 + BN3 + residual + ReLU in ONE
- * launch (the 3x3's output tile stays in LDS); conv1 runs before it on posu_conv2d_fwd.
- * t1 [N, H, 16, 256] (conv1 output), x [N, H, 16, 1024] (block input = residual),
- * w2 [256][2304] / w3 [1024][256] as posu_conv2d_fwd packs them, s/b folded BN (f32),
- * y [N, H, 16, 1024].  W = 16, C = 1024, P = 256, H a multiple of 8; BF16 / F16.
- * Bit-identical to posu_conv2d_fwd(conv2) followed by posu_conv2d_fwd(conv3, residual). */
-int posu_bottleneck3_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
-                              const void* w2, const float* s2, const float* b2, const void* w3,
-                              const float* s3, const float* b3, void* y, void* stream);
-
 /* The tail of an identity Bottleneck of layer2 (W = 32, C = 512, P = 128) or layer3 (W = 16,
  * C = 1024, P = 256) (lib/models/pose_resnet.py:79-99) with the weights streamed from L2
  * straight into registers (each wave loads its own 2 n-tiles' MFMA fragments a few k-steps
  * ahead; no LDS weight ring): conv2 3x3 + BN2 + ReLU -> conv3 1x1 + BN3 + residual + ReLU.
  * t1 [N, H, W, P] (conv1 output), x [N, H, W, C], y [N, H, W, C], H a multiple of 8.
  * wstream: packing.pack_tail_stream of the conv2 [P][9P] and conv3 [C][P] posu_conv2d_fwd packs,
- * [P/32][9 P/32 + C/32][2][64][8] elements of dtype.  Bit-identical to posu_conv2d_fwd(conv2)
- * followed by posu_conv2d_fwd(conv3, residual). */
+ * [P/32][9 P/32 + C/32][2][64][8] elements of dtype; wstream_bytes = its size in bytes (checked
+ * against what the kernel reads: a pack for another layer or the chained variant's pack is
+ * refused, never read past).  Bit-identical to posu_conv2d_fwd(conv2) followed by
+ * posu_conv2d_fwd(conv3, residual). */
 int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
-                                    int P, const void* wstream, const float* s2, const float* b2,
-                                    const float* s3, const float* b3, void* y, void* stream);
+                                    int P, const void* wstream, long long wstream_bytes, const float* s2,
+                                    const float* b2, const float* s3, const float* b3, void* y, void* stream);
 
 /* posu_bottleneck_tail_stream_fwd chained with the NEXT identity Bottleneck's conv1 (1x1, C -> P)
  * + BN1 + ReLU over this block's output y (lib/models/pose_resnet.py:79-84 of block i+1; the
@@ -223,9 +205,9 @@ int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, in
  * BN; t1n [N, H, W, P] out (aliasing no other operand).  y and t1n are bit-identical to this
  * tail followed by posu_conv2d_fwd(next conv1, ReLU) over y. */
 int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
-                                         int P, const void* wstream, const float* s2, const float* b2,
-                                         const float* s3, const float* b3, void* y, const float* s1n,
-                                         const float* b1n, void* t1n, void* stream);
+                                         int P, const void* wstream, long long wstream_bytes, const float* s2,
+                                         const float* b2, const float* s3, const float* b3, void* y,
+                                         const float* s1n, const float* b1n, void* t1n, void* stream);
 
 /* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
  * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn
@@ -463,31 +445,6 @@ int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, int C, const
                       const float* beta, float eps, float momentum, float* running_mean,
                       float* running_var, float* mean, float* rstd, float* scale, float* shift,
                       void* workspace, long long workspace_bytes, void* stream);
-/* The same forward with its statistics taken in the producing convolution's epilogue instead of
- * a pass over z (training forward, lib/models/pose_resnet.py:79-84 with train-mode BN):
- * posu_conv2d_fwd_stats is the raw conv (no BN / residual / ReLU; y bit-identical to
- * posu_conv2d_fwd with scale/shift NULL) that also writes per-output-tile channel sums and
- * sums of squares of the stored values, part [nseg][ntiles][2][Cout] f32 (*ntiles_out = tiles
- * per segment), taken about a per-channel shift kshift [Cout] (NULL: 0; the running mean keeps the
- * variance of channels whose mean is large against their spread); BF16 / F16, N*Ho*Wo/nseg a
- * multiple of 256, part_bytes >= nseg * (N*Ho*Wo/nseg / 64) * 2 * Cout * 4.  posu_bn_stats_finalize
- * (same kshift, which may be running_mean itself: it is read before the update) turns them into
- * mean/rstd/scale/shift and the running statistics like posu_bn_train_fwd (tiles summed in order,
- * f64). */
-int posu_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
-                          int KH, int KW, int stride, int pad, void* y, int Ho, int Wo, int tile, int nseg,
-                          const float* kshift, float* part, long long part_bytes, int* ntiles_out, void* stream);
-/* The same for the deconvolution (posu_deconv4x4s2_fwd raw: no BN / ReLU): segments of
- * N*H*W/nseg INPUT pixels (a multiple of 256), part [nseg][4 ntiles][2][Cout] (*ntiles_out counts
- * the four parity classes' tiles; the finalize's Pseg is the output pixels, 4 N*H*W/nseg),
- * part_bytes >= nseg * 4 * (N*H*W/nseg / 64) * 2 * Cout * 4. */
-int posu_deconv4x4s2_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
-                               void* y, int tile, int nseg, const float* kshift, float* part,
-                               long long part_bytes, int* ntiles_out, void* stream);
-int posu_bn_stats_finalize(int nseg, int Pseg, int C, int ntiles, const float* part, const float* kshift,
-                           const float* gamma, const float* beta, float eps, float momentum, float* running_mean,
-                           float* running_var, float* mean, float* rstd, float* scale, float* shift,
-                           void* stream);
 /* y = act(z * scale[seg] + shift[seg] (+ residual)) */
 int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
                   const float* shift, const void* residual, int relu, void* y, void* stream);

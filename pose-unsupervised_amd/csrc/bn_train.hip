@@ -185,22 +185,21 @@ constexpr int FCH = 8, FLN = 32, FSEG = 4;
 // of a channel are one half-wave.  Each lane sums the partial blocks ln, ln + FLN, .. of up to
 // FSEG segments (all loads in flight together), then a fixed xor butterfly over the half-wave;
 // lane 0's sums are the result (its association order does not depend on the data)
-template <typename PT>
-__device__ __forceinline__ void reduce_segs(const PT* __restrict__ part, int seg0, int ns, int NB, int C, int c,
+__device__ __forceinline__ void reduce_segs(const double* __restrict__ part, int seg0, int ns, int NB, int C, int c,
                                             bool valid, int ln, double* s, double* q) {
   double a[FSEG], b[FSEG];
 #pragma unroll
   for (int k = 0; k < FSEG; ++k) a[k] = b[k] = 0.0;
   if (valid) {
-    const PT* base = part + static_cast<size_t>(seg0) * NB * 2 * C + c;
+    const double* base = part + static_cast<size_t>(seg0) * NB * 2 * C + c;
 #pragma unroll 4
     for (int blk = ln; blk < NB; blk += FLN) {
 #pragma unroll
       for (int k = 0; k < FSEG; ++k)
         if (k < ns) {
-          const PT* p = base + (static_cast<size_t>(k) * NB + blk) * 2 * C;
-          a[k] += static_cast<double>(p[0]);
-          b[k] += static_cast<double>(p[C]);
+          const double* p = base + (static_cast<size_t>(k) * NB + blk) * 2 * C;
+          a[k] += p[0];
+          b[k] += p[C];
         }
     }
   }
@@ -218,15 +217,12 @@ __device__ __forceinline__ void reduce_segs(const PT* __restrict__ part, int seg
   }
 }
 
-// PT = double: bn_partial_kernel's shifted partials; float: the per-tile sums of a conv epilogue
-// (posu_conv2d_fwd_stats: one per-channel shift for every segment, kss = 0)
-template <typename PT>
-__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const PT* __restrict__ part, int nseg, int NB,
+__global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __restrict__ part, int nseg, int NB,
                                                                 int Pseg, int C, const float* __restrict__ gamma,
                                                                 const float* __restrict__ beta, float eps,
-                                                                float momentum, const float* kshift, int kss,
-                                                                float* running_mean,  // may be kshift itself
-                                                                float* running_var,
+                                                                float momentum, const float* __restrict__ kshift,
+                                                                float* __restrict__ running_mean,
+                                                                float* __restrict__ running_var,
                                                                 float* __restrict__ mean, float* __restrict__ rstd,
                                                                 float* __restrict__ scale,
                                                                 float* __restrict__ shift) {
@@ -243,7 +239,7 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const PT* __rest
     const int ns = min(FSEG, nseg - seg0);
     float ks[FSEG];
 #pragma unroll
-    for (int k = 0; k < FSEG; ++k) ks[k] = k < ns && kshift ? kshift[(seg0 + k) * kss + cc] : 0.f;
+    for (int k = 0; k < FSEG; ++k) ks[k] = k < ns ? kshift[(seg0 + k) * C + cc] : 0.f;
     double sums[FSEG], sqs[FSEG];
     reduce_segs(part, seg0, ns, NB, C, c, valid, ln, sums, sqs);
     if (ln != 0 || !valid) continue;
@@ -662,27 +658,9 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
                        kshift);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
-  hipLaunchKernelGGL(bn_stats_finalize_kernel<double>, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB,
-                     Pseg, C, gamma, beta, eps, momentum, kshift, C, running_mean, running_var, mean, rstd, scale,
-                     shift);
+  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+                     gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
   return check_launch("posu_bn_train_fwd");
-}
-
-// The statistics half of posu_bn_train_fwd from the per-tile sums a conv epilogue wrote
-// (posu_conv2d_fwd_stats: part [nseg][ntiles][2][C] f32 about kshift [C], the same pointer the
-// conv took -- read here before running_mean is updated): mean / rstd / scale / shift per segment
-// and the running statistics, exactly as posu_bn_train_fwd's finalize (tiles added in order, f64).
-extern "C" int posu_bn_stats_finalize(int nseg, int Pseg, int C, int ntiles, const float* part, const float* kshift,
-                                      const float* gamma, const float* beta, float eps, float momentum,
-                                      float* running_mean,
-                                      float* running_var, float* mean, float* rstd, float* scale, float* shift,
-                                      void* stream) {
-  POSU_REQUIRE(part && mean && rstd && scale && shift, "posu_bn_stats_finalize: null pointer");
-  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && ntiles > 0, "posu_bn_stats_finalize: bad shape");
-  hipLaunchKernelGGL(bn_stats_finalize_kernel<float>, dim3((C + FCH - 1) / FCH), dim3(256), 0, as_stream(stream),
-                     part, nseg, ntiles, Pseg, C, gamma, beta, eps, momentum, kshift, 0, running_mean, running_var,
-                     mean, rstd, scale, shift);
-  return check_launch("posu_bn_stats_finalize");
 }
 
 extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,

@@ -69,12 +69,6 @@ struct ConvGeom {
   float* hm;
   int J, hkp;
   int mtiles, ntiles;
-  // ST kernels (training forward): per-channel sums of the stored outputs for the BatchNorm that
-  // follows -- part[((seg * (spseg / BM) + tile) * 2 + {0: sum, 1: sum of squares}) * Cout + c]
-  // f32, one row pair per output tile of a segment of spseg pixels
-  float* part;
-  int spseg;
-  const float* kshift;  // ST: per-channel shift K (NULL: 0) -- the sums are of (value - K)
 };
 
 template <int BM, int BN, int S>
@@ -95,7 +89,7 @@ constexpr int kEarlyNK = 8;
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
 // SG: eight-wave tiles with waves 4-7 staggered by half a K-tile (two-slot ring).
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false, bool ST = false>
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int NT = NW * 64;
@@ -512,21 +506,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
     // the fused head without the deconv output stored reads no pixel address: skip the decode
     const bool no_pix = head && yp == nullptr && rp == nullptr;
-    // ST: this lane's channel sums over its pixels of (stored, rounded value - K[c]): a shift
-    // near the channel mean (the caller passes the running mean) keeps the variance in f32
-    float ssum[ST ? TP : 1][8], ssq[ST ? TP : 1][8], kk[ST ? TP : 1][8];
-    if constexpr (ST) {
-#pragma unroll
-      for (int jp = 0; jp < TP; ++jp) {
-        const bool in = cop[jp] < g.Cout && g.kshift;
-        const float4 k0 = in ? *reinterpret_cast<const float4*>(g.kshift + cop[jp]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4 k1 = in ? *reinterpret_cast<const float4*>(g.kshift + cop[jp] + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        kk[jp][0] = k0.x; kk[jp][1] = k0.y; kk[jp][2] = k0.z; kk[jp][3] = k0.w;
-        kk[jp][4] = k1.x; kk[jp][5] = k1.y; kk[jp][6] = k1.z; kk[jp][7] = k1.w;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) ssum[jp][e] = ssq[jp][e] = 0.f;
-      }
-    }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = m0 + rowA(i) + r16;
@@ -575,57 +554,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
             continue;
           }
         }
-        const uint4 ov = O::store_vals(v);
-        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = ov;
-        if constexpr (ST) {
-          float rr[8];
-          O::load_vals(ov, rr);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float t = mok ? rr[e] - kk[jp][e] : 0.f;
-            ssum[jp][e] += t;
-            ssq[jp][e] += t * t;
-          }
-        }
-      }
-    }
-    if constexpr (ST) {
-      // the 16 pixel lanes of a channel group (fixed xor order), the WGM wave rows through LDS
-      // (row order), one f32 row pair per tile; the finalize adds the tiles in order
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-        for (int jp = 0; jp < TP; ++jp)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            ssum[jp][e] += __shfl_xor(ssum[jp][e], off);
-            ssq[jp][e] += __shfl_xor(ssq[jp][e], off);
-          }
-      __syncthreads();  // every wave is done with the ring
-      float* Ls = reinterpret_cast<float*>(smem);  // [WGM][2][BN]
-      if (r16 == 0) {
-#pragma unroll
-        for (int jp = 0; jp < TP; ++jp)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const int lc = cop[jp] - n0 + e;
-            Ls[(wm * 2 + 0) * BN + lc] = ssum[jp][e];
-            Ls[(wm * 2 + 1) * BN + lc] = ssq[jp][e];
-          }
-      }
-      __syncthreads();
-      // row (segment, deconv parity class, tile of the segment's class grid)
-      const int seg = m0 / g.spseg;
-      const int tl = (m0 - seg * g.spseg) / BM;
-      const int ncl = g.deconv ? 4 : 1, cls = g.deconv ? (rest & 3) : 0;
-      float* dst = g.part + static_cast<size_t>((seg * ncl + cls) * (g.spseg / BM) + tl) * 2 * g.Cout;
-      for (int idx = tid; idx < 2 * BN; idx += NT) {
-        const int st = idx / BN, lc = idx - st * BN;
-        if (n0 + lc >= g.Cout) continue;
-        float a = 0.f;
-#pragma unroll
-        for (int w = 0; w < WGM; ++w) a += Ls[(w * 2 + st) * BN + lc];
-        dst[st * g.Cout + n0 + lc] = a;
+        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
       }
     }
     if constexpr (HEAD256) {
@@ -1326,45 +1255,21 @@ void launch_persist(const ConvGeom& g, int ntile, hipStream_t s) {
   hipLaunchKernelGGL((conv_persist_kernel<T, BM, BN, NW, WGM, S, DUAL>), dim3(grid), dim3(NW * 64), 0, s, g);
 }
 
-template <typename T, int BM, int BN, int NW, int WGM, bool DUAL, bool ST = false>
+template <typename T, int BM, int BN, int NW, int WGM, bool DUAL>
 void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
   if constexpr (NW == 4) {
     if (stages == 1) {
-      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 1, DUAL, false, ST>), dim3(blocks), dim3(NW * 64), 0,
-                         s, g);
+      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 1, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
       return;
     }
   }
   if constexpr (ring_bytes<BM, BN, 3>() <= 160 * 1024) {
     if (stages >= 3) {
-      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 3, DUAL, false, ST>), dim3(blocks), dim3(NW * 64), 0,
-                         s, g);
+      hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 3, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
       return;
     }
   }
-  hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 2, DUAL, false, ST>), dim3(blocks), dim3(NW * 64), 0, s,
-                     g);
-}
-
-// a one-source conv launch with its BatchNorm statistics (ST kernels, 2-byte dtypes)
-template <typename T>
-void launch_stats(const ConvGeom& g, int cfg, int nb, int st, bool sg, hipStream_t s) {
-  if (sg) {
-    if (cfg == 5)
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, false, true, true>), dim3(nb), dim3(512), 0, s, g);
-    else
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, false, true, true>), dim3(nb), dim3(512), 0, s, g);
-    return;
-  }
-  switch (cfg) {
-    case 0: launch_cfg<T, 256, 64, 4, 4, false, true>(g, nb, st, s); break;
-    case 1: launch_cfg<T, 128, 64, 4, 2, false, true>(g, nb, st, s); break;
-    case 2: launch_cfg<T, 64, 64, 4, 2, false, true>(g, nb, st, s); break;
-    case 3: launch_cfg<T, 128, 128, 4, 2, false, true>(g, nb, st, s); break;
-    case 4: launch_cfg<T, 64, 128, 4, 2, false, true>(g, nb, st, s); break;
-    case 5: launch_cfg<T, 256, 256, 8, 2, false, true>(g, nb, 2, s); break;
-    default: launch_cfg<T, 256, 128, 8, 4, false, true>(g, nb, st == 3 ? 3 : 2, s); break;
-  }
+  hipLaunchKernelGGL((conv_igemm_kernel<T, BM, BN, NW, WGM, 2, DUAL>), dim3(blocks), dim3(NW * 64), 0, s, g);
 }
 
 
@@ -1383,9 +1288,6 @@ bool tile_ok(int tile) {
   const int c = tile & 7, v = (tile >> 3) & 3;
   return c <= 6 && v <= 2 && !(v == 1 && c > 4) && !(v == 2 && c == 5);
 }
-
-// tiles per segment of the last ST launch on this thread (posu_conv2d_fwd_stats reports it)
-thread_local int stats_tiles = 0;
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
@@ -1436,7 +1338,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
       // persistent K-tile stream: 2-byte dtypes, direct NHWC epilogue, outputs addressable
       // by a 32-bit buffer offset
-      persist = (tile & 32) != 0 && sizeof(T) == 2 && g.mode == 0 && g.part == nullptr &&
+      persist = (tile & 32) != 0 && sizeof(T) == 2 && g.mode == 0 &&
                 static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
     }
   } else if (sizeof(T) == 2 && (cfg == 5 || cfg == 6)) {
@@ -1447,13 +1349,6 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
-  if constexpr (sizeof(T) == 2 && !DUAL) {
-    if (g.part) {
-      stats_tiles = g.spseg / kBM[cfg] * nclass;
-      launch_stats<T>(g, cfg, nb, st, sg, s);
-      return check_launch(what);
-    }
-  }
   if constexpr (sizeof(T) == 2) {
     if (persist) {
       switch (cfg) {
@@ -1574,54 +1469,6 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd", tile);
 }
 
-// Training forward of a conv followed by BatchNorm (lib/models/pose_resnet.py:79-84 in train mode,
-// the reference's per-view BN statistics): the raw conv (no BN / residual / ReLU) and, in its
-// epilogue, per-channel sums and sums of squares of the stored outputs per output tile of each of
-// nseg segments, taken about a per-channel shift kshift [Cout] (NULL: 0; the running mean keeps
-// the variance of channels whose mean is large against their spread) (part: [nseg][ntiles][2]
-// [Cout] f32; *ntiles_out = tiles per segment, for posu_bn_stats_finalize).  BF16 / F16; (N Ho Wo) / nseg a multiple of 256; part_bytes >=
-// nseg * ((N Ho Wo / nseg) / 64) * 2 * Cout * 4.  y is bit-identical to posu_conv2d_fwd.
-extern "C" int posu_conv2d_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
-                                     int KH, int KW, int stride, int pad, void* y, int Ho, int Wo, int tile, int nseg,
-                                     const float* kshift, float* part, long long part_bytes, int* ntiles_out,
-                                     void* stream) {
-  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd_stats")) return st;
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_conv2d_fwd_stats: dtype must be BF16 or F16");
-  POSU_REQUIRE(tile_ok(tile), "posu_conv2d_fwd_stats: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
-  POSU_REQUIRE(Cout % 8 == 0, "posu_conv2d_fwd_stats: Cout must be a multiple of 8");
-  POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd_stats: bad window");
-  POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
-               "posu_conv2d_fwd_stats: Ho/Wo larger than the window allows");
-  POSU_REQUIRE(static_cast<long long>(N) * Ho * Wo * Cout < (1LL << 31), "posu_conv2d_fwd_stats: output too large");
-  const long long M = static_cast<long long>(N) * Ho * Wo;
-  POSU_REQUIRE(nseg > 0 && M % nseg == 0 && (M / nseg) % 256 == 0,
-               "posu_conv2d_fwd_stats: the output pixels must split into nseg segments of a multiple of 256");
-  POSU_REQUIRE(part && ntiles_out && part_bytes >= static_cast<long long>(nseg) * (M / nseg / 64) * 2 * Cout * 4,
-               "posu_conv2d_fwd_stats: partial buffer too small (or null)");
-  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
-  g.y = y;
-  g.Ho = Ho;
-  g.Wo = Wo;
-  g.M = static_cast<int>(M);
-  g.K = KH * KW * C;
-  g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = KH;
-  g.KW = KW;
-  g.stride = stride;
-  g.pad_h = pad;
-  g.pad_w = pad;
-  g.out_H = Ho;
-  g.out_W = Wo;
-  POSU_REQUIRE((reinterpret_cast<size_t>(kshift) & 15) == 0, "posu_conv2d_fwd_stats: kshift must be 16-byte aligned");
-  g.part = part;
-  g.spseg = static_cast<int>(M / nseg);
-  g.kshift = kshift;
-  stats_tiles = 0;
-  const int rc = dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd_stats", tile);
-  *ntiles_out = stats_tiles;
-  return rc;
-}
-
 extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2, int H2,
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
@@ -1711,45 +1558,6 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   g.J = J;
   g.hkp = round_up(Cout, bk_of(dtype));
   return dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_head_fwd");
-}
-
-// posu_deconv4x4s2_fwd's raw form (no BN / ReLU) with the following BatchNorm's sums in its
-// epilogue, as posu_conv2d_fwd_stats: segments of (N H W / nseg) input pixels (a multiple of 256),
-// part [nseg][4 ntiles][2][Cout] f32 (*ntiles_out counts the four parity classes' tiles),
-// part_bytes >= nseg * 4 * (N H W / nseg / 64) * 2 * Cout * 4.
-extern "C" int posu_deconv4x4s2_fwd_stats(int dtype, const void* x, int N, int H, int W, int C, const void* w,
-                                          int Cout, void* y, int tile, int nseg, const float* kshift, float* part,
-                                          long long part_bytes, int* ntiles_out, void* stream) {
-  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd_stats")) return st;
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_deconv4x4s2_fwd_stats: dtype must be BF16 or F16");
-  POSU_REQUIRE(tile_ok(tile), "posu_deconv4x4s2_fwd_stats: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
-  POSU_REQUIRE(Cout % 8 == 0, "posu_deconv4x4s2_fwd_stats: Cout must be a multiple of 8");
-  POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31), "posu_deconv4x4s2_fwd_stats: output too large");
-  const long long M = static_cast<long long>(N) * H * W;
-  POSU_REQUIRE(nseg > 0 && M % nseg == 0 && (M / nseg) % 256 == 0,
-               "posu_deconv4x4s2_fwd_stats: the input pixels must split into nseg segments of a multiple of 256");
-  POSU_REQUIRE(part && ntiles_out && part_bytes >= static_cast<long long>(nseg) * 4 * (M / nseg / 64) * 2 * Cout * 4,
-               "posu_deconv4x4s2_fwd_stats: partial buffer too small (or null)");
-  POSU_REQUIRE((reinterpret_cast<size_t>(kshift) & 15) == 0, "posu_deconv4x4s2_fwd_stats: kshift must be 16-byte aligned");
-  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
-  g.y = y;
-  g.Ho = H;
-  g.Wo = W;
-  g.M = static_cast<int>(M);
-  g.K = 4 * C;
-  g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = 2;
-  g.KW = 2;
-  g.deconv = 1;
-  g.out_H = 2 * H;
-  g.out_W = 2 * W;
-  g.part = part;
-  g.spseg = static_cast<int>(M / nseg);
-  g.kshift = kshift;
-  stats_tiles = 0;
-  const int rc = dispatch<false>(dtype, g, 4, stream, "posu_deconv4x4s2_fwd_stats", tile);
-  *ntiles_out = stats_tiles;
-  return rc;
 }
 
 extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,

@@ -4,8 +4,8 @@
 //
 //     y = relu( bn3(conv3( relu(bn2(conv2_3x3(t1))) )) + x ),   t1 = conv1's output
 //
-// Why (csrc/bottleneck3.hip and bottleneck2.hip are the LDS-ring versions): those stream the
-// weights through a two-slot 32 KB LDS ring, so one 32 KB stage is in flight per CU and every
+// Why (the round-2 LDS-ring versions, removed in round 4, streamed the weights through a
+// two-slot 32 KB LDS ring): so one 32 KB stage is in flight per CU and every
 // stage pays a full L2 round trip -- layer3's 52 stages x ~1.5 us = its 80 us (profiles/r02).
 // Here the LDS holds only activations; each wave loads its own weight fragments from L2 into
 // VGPRs kD k-steps ahead of their use (one contiguous 2 KB per k-step and wave, prepacked by
@@ -369,8 +369,9 @@ using namespace posu;
 
 namespace {
 int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
-                     const void* wstream, const float* s2, const float* b2, const float* s3, const float* b3, void* y,
-                     const float* s1n, const float* b1n, void* t1n, void* stream) {
+                     const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
+                     const float* s3, const float* b3, void* y, const float* s1n, const float* b1n, void* t1n,
+                     void* stream) {
   const std::string what = name;
   const bool next = t1n != nullptr;
   POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, what + ": dtype must be BF16 or F16");
@@ -381,6 +382,14 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
   POSU_REQUIRE(l2 || l3, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16, C = 1024, "
                                 "planes = 256) of PoseResNet at 256x256");
+  {
+    // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
+    // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream)
+    const long long kt = P / 32, nc = C / P;
+    const long long need = (P / 32) * (9 * kt + (next ? 2 : 1) * nc * kt) * 2 * 64 * 8 * 2;
+    POSU_REQUIRE(wstream_bytes >= need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
+                                            (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
+  }
   const int rows = l3 ? 8 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
@@ -417,10 +426,11 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
 }  // namespace
 
 extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
-                                               int P, const void* wstream, const float* s2, const float* b2,
-                                               const float* s3, const float* b3, void* y, void* stream) {
-  return tail_stream_impl("posu_bottleneck_tail_stream_fwd", dtype, t1, x, N, H, W, C, P, wstream, s2, b2, s3, b3, y,
-                          nullptr, nullptr, nullptr, stream);
+                                               int P, const void* wstream, long long wstream_bytes,
+                                               const float* s2, const float* b2, const float* s3, const float* b3,
+                                               void* y, void* stream) {
+  return tail_stream_impl("posu_bottleneck_tail_stream_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes, s2,
+                          b2, s3, b3, y, nullptr, nullptr, nullptr, stream);
 }
 
 // Chained identity Bottlenecks: the tail above, and the NEXT identity block's conv1 (+ BN1 +
@@ -428,13 +438,14 @@ extern "C" int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const 
 // block's tail takes instead of a conv1 launch over y.  wstream = packing.pack_tail_stream
 // (conv2, conv3, next conv1).
 extern "C" int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W,
-                                                    int C, int P, const void* wstream, const float* s2,
-                                                    const float* b2, const float* s3, const float* b3, void* y,
-                                                    const float* s1n, const float* b1n, void* t1n, void* stream) {
+                                                    int C, int P, const void* wstream, long long wstream_bytes,
+                                                    const float* s2, const float* b2, const float* s3,
+                                                    const float* b3, void* y, const float* s1n, const float* b1n,
+                                                    void* t1n, void* stream) {
   if (!t1n) {
     set_error("posu_bottleneck_tail_stream_next_fwd: null pointer (t1n)");
     return POSU_ERR_ARG;
   }
-  return tail_stream_impl("posu_bottleneck_tail_stream_next_fwd", dtype, t1, x, N, H, W, C, P, wstream, s2, b2, s3,
-                          b3, y, s1n, b1n, t1n, stream);
+  return tail_stream_impl("posu_bottleneck_tail_stream_next_fwd", dtype, t1, x, N, H, W, C, P, wstream,
+                          wstream_bytes, s2, b2, s3, b3, y, s1n, b1n, t1n, stream);
 }

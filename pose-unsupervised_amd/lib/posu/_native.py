@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -42,11 +42,9 @@ _SIGNATURES = {
     'posu_conv_bk': [_i],
     'posu_stem_pool_fwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p],
     'posu_bottleneck_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
-    'posu_bottleneck2_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
-    'posu_bottleneck3_tail_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p],
-    'posu_bottleneck_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
-    'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p,
-                                             _p],
+    'posu_bottleneck_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p],
+    'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
+                                             _p, _p],
     'posu_bottleneck_down_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
@@ -75,10 +73,6 @@ _SIGNATURES = {
     'posu_conv2d_wgrad_workspace': [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i],
     'posu_conv2d_wgrad': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _ll, _p],
     'posu_bn_workspace': [_i, _i],
-    'posu_conv2d_fwd_stats': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _p, _ll, _p,
-                              _p],
-    'posu_deconv4x4s2_fwd_stats': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _i, _i, _p, _p, _ll, _p, _p],
-    'posu_bn_stats_finalize': [_i, _i, _i, _i, _p, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p],
     'posu_bn_train_fwd': [_i, _p, _i, _i, _i, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_bn_apply': [_i, _p, _i, _i, _i, _p, _p, _p, _i, _p, _p],
     'posu_bn_train_bwd': [_i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],

@@ -98,27 +98,6 @@ def bottleneck_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
     return out
 
 
-def bottleneck2_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
-    """Fused identity Bottleneck of layer2 (posu_bottleneck2_fwd): x [N, H, 32, 512] -> y."""
-    n, h, w, c = x.shape
-    if out is None:
-        out = torch.empty_like(x)
-    call('posu_bottleneck2_fwd', code, ptr(x), n, h, w, c, w1.shape[0], ptr(w1), ptr(s1), ptr(b1), ptr(w2),
-         ptr(s2), ptr(b2), ptr(w3), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
-    return out
-
-
-def bottleneck3_tail_nhwc(t1, x, w2, s2, b2, w3, s3, b3, code, out=None):
-    """conv2 + conv3 (+ residual) of a layer3 identity Bottleneck (posu_bottleneck3_tail_fwd):
-    t1 [N, H, 16, 256], x [N, H, 16, 1024] -> y [N, H, 16, 1024]."""
-    n, h, w, c = x.shape
-    if out is None:
-        out = torch.empty_like(x)
-    call('posu_bottleneck3_tail_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(w2), ptr(s2), ptr(b2),
-         ptr(w3), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
-    return out
-
-
 def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
     """conv2 + conv3 (+ residual) of a layer2 / layer3 identity Bottleneck with the weights
     streamed into registers (posu_bottleneck_tail_stream_fwd, csrc/tail_stream.hip);
@@ -126,8 +105,8 @@ def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty_like(x)
-    call('posu_bottleneck_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream), ptr(s2),
-         ptr(b2), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
+    call('posu_bottleneck_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
     return out
 
 
@@ -142,8 +121,9 @@ def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, c
         out = torch.empty_like(x)
     if t1n is None:
         t1n = torch.empty((n, h, w, p), dtype=x.dtype, device=x.device)
-    call('posu_bottleneck_tail_stream_next_fwd', code, ptr(t1), ptr(x), n, h, w, c, p, ptr(wstream), ptr(s2),
-         ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n), ptr(t1n), stream_of(x.device))
+    call('posu_bottleneck_tail_stream_next_fwd', code, ptr(t1), ptr(x), n, h, w, c, p, ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n),
+         ptr(t1n), stream_of(x.device))
     return out, t1n
 
 

@@ -154,18 +154,12 @@ class _DualTail:
 
 
 # Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch each in bf16 / fp16 plans
-# (posu_bottleneck_fwd; the first block, with its downsample, posu_bottleneck_down_fwd), and
-# the identity Bottlenecks of layer2 (planes 128, 32-wide maps; posu_bottleneck2_fwd), and the
-# conv2 + conv3 tail of layer3's identity Bottlenecks (posu_bottleneck3_tail_fwd);
-# False runs the convolutions
+# (posu_bottleneck_fwd; the first block, with its downsample, posu_bottleneck_down_fwd), and the
+# identity Bottlenecks of layer2 / layer3 as conv1 (a conv launch) + the register-streamed
+# conv2 + conv3 + residual tail (posu_bottleneck_tail_stream_fwd); False runs the convolutions.
+# (The round-2 LDS-ring layer2 block / layer3 tail kernels, slower than the streamed tail, were
+# removed from the library in round 4.)
 FUSED_BOTTLENECK = True
-FUSED_LAYER3_TAIL = True
-# layer3's tail on the register-streamed kernel (posu_bottleneck_tail_stream_fwd: 59 vs 76 us per
-# block, tools/tail_micro.py); False: the LDS-ring kernel (posu_bottleneck3_tail_fwd)
-STREAMED_LAYER3_TAIL = True
-# layer2's identity Bottlenecks as conv1 (a conv launch) + the register-streamed tail instead of
-# the fused LDS-ring block (posu_bottleneck2_fwd)
-STREAMED_LAYER2_TAIL = True
 # consecutive streamed identity tails chained: block i's tail also computes block i+1's conv1
 # over its output (posu_bottleneck_tail_stream_next_fwd), so block i+1 has no conv1 launch and y
 # is not re-read for it (tools/chain_micro.py: layer2 105.0 vs 130.0 us, layer3 76.3 vs 85.0 us
@@ -234,10 +228,9 @@ class _Block:
         """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
         if not FUSED_BOTTLENECK or not _fused_fits(x, self.cout):
             return None
-        if self.l2 and STREAMED_LAYER2_TAIL and x.shape[2] == 32 and x.shape[1] % 4 == 0:
+        if self.l2 and x.shape[2] == 32 and x.shape[1] % 4 == 0:
             return 'l2'
-        if (self.l3 and FUSED_LAYER3_TAIL and STREAMED_LAYER3_TAIL and x.shape[2] == 16 and
-                x.shape[1] % 8 == 0):
+        if self.l3 and x.shape[2] == 16 and x.shape[1] % 8 == 0:
             return 'l3'
         return None
 
@@ -297,21 +290,10 @@ class _Block:
             c1, c2, c3 = self.convs
             return ops.bottleneck_nhwc(x, self.w1f, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3f, c3.scale,
                                        c3.shift, code, out=out)
-        if self.l2 and FUSED_BOTTLENECK and fits and x.shape[2] == 32 and x.shape[1] % 4 == 0:
+        if self._tail_kind(x) is not None:
             c1, c2, c3 = self.convs
-            if STREAMED_LAYER2_TAIL:
-                return ops.bottleneck_tail_stream_nhwc(c1(x, code), x, self.wst, c2.scale, c2.shift, c3.scale,
-                                                       c3.shift, code, out=out)
-            return ops.bottleneck2_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, c3.w, c3.scale,
-                                        c3.shift, code, out=out)
-        if (self.l3 and FUSED_BOTTLENECK and FUSED_LAYER3_TAIL and fits and x.shape[2] == 16 and
-                x.shape[1] % 8 == 0):
-            c1, c2, c3 = self.convs
-            if STREAMED_LAYER3_TAIL:
-                return ops.bottleneck_tail_stream_nhwc(c1(x, code), x, self.wst, c2.scale, c2.shift, c3.scale,
-                                                       c3.shift, code, out=out)
-            return ops.bottleneck3_tail_nhwc(c1(x, code), x, c2.w, c2.scale, c2.shift, c3.w, c3.scale, c3.shift, code,
-                                             out=out)
+            return ops.bottleneck_tail_stream_nhwc(c1(x, code), x, self.wst, c2.scale, c2.shift, c3.scale, c3.shift,
+                                                   code, out=out)
         res = self.down(x, code) if self.down is not None else x
         for c in self.convs[:-1]:
             y = c(y, code)

@@ -85,52 +85,6 @@ def bn_train_fwd(z, nseg, gamma, beta, eps, momentum, running_mean=None, running
     return st[0], st[1], st[2], st[3]
 
 
-def conv2d_fwd_stats(x, w_packed, cout, k, stride, pad, nseg, code, tile=-1, kshift=None):
-    """Raw training conv (no BN) with the following BatchNorm's per-tile channel sums taken in
-    its epilogue (posu_conv2d_fwd_stats): -> (z [N, Ho, Wo, cout], partials, tiles per segment).
-    The partials live in a per-stream workspace until the next call on that stream."""
-    import ctypes
-    require_cuda(x)
-    n, h, w, c = x.shape
-    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    m = n * ho * wo
-    z = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
-    need = nseg * (m // nseg // 64) * 2 * cout * 4
-    ws = workspace(x.device, need, 'bnstats')
-    nt = ctypes.c_int(0)
-    call('posu_conv2d_fwd_stats', code, ptr(x), n, h, w, c, ptr(w_packed), cout, k, k, stride, pad, ptr(z), ho, wo,
-         int(tile), nseg, ptr(kshift), ptr(ws), ws.numel(), ctypes.addressof(nt), stream_of(x.device))
-    return z, ws, nt.value
-
-
-def deconv4x4s2_fwd_stats(x, w_packed, cout, nseg, code, tile=-1, kshift=None):
-    """Raw ConvTranspose2d(4, s2, p1) (no BN) with the following BatchNorm's per-tile channel sums
-    in its epilogue (posu_deconv4x4s2_fwd_stats): -> (z [N, 2H, 2W, cout], partials, tiles per
-    segment, all four parity classes)."""
-    import ctypes
-    require_cuda(x)
-    n, h, w, c = x.shape
-    m = n * h * w
-    z = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
-    need = nseg * 4 * (m // nseg // 64) * 2 * cout * 4
-    ws = workspace(x.device, need, 'bnstats')
-    nt = ctypes.c_int(0)
-    call('posu_deconv4x4s2_fwd_stats', code, ptr(x), n, h, w, c, ptr(w_packed), cout, ptr(z), int(tile), nseg,
-         ptr(kshift), ptr(ws), ws.numel(), ctypes.addressof(nt), stream_of(x.device))
-    return z, ws, nt.value
-
-
-def bn_stats_finalize(part, ntiles, nseg, pseg, c, gamma, beta, eps, momentum, running_mean=None, running_var=None,
-                      kshift=None):
-    """mean, rstd, scale, shift ([nseg, c] f32 each) from conv2d_fwd_stats' partials (taken about
-    kshift, the same tensor the conv got), the running statistics updated like bn_train_fwd."""
-    st = torch.empty((4, nseg, c), dtype=torch.float32, device=part.device)
-    call('posu_bn_stats_finalize', nseg, pseg, c, ntiles, ptr(part), ptr(kshift), ptr(gamma), ptr(beta), float(eps),
-         float(momentum), ptr(running_mean), ptr(running_var), ptr(st[0]), ptr(st[1]), ptr(st[2]), ptr(st[3]),
-         stream_of(part.device))
-    return st[0], st[1], st[2], st[3]
-
-
 def bn_apply(z, nseg, scale, shift, residual=None, relu=True, out=None):
     require_cuda(z)
     c = z.shape[-1]

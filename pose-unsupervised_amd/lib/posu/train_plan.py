@@ -52,34 +52,6 @@ def _conv_tuned(x, w, cout, k, stride, pad, code):
                                                       out=z, tile=t))
 
 
-# BatchNorm statistics of the training forward taken in the producing conv's epilogue
-# (posu_conv2d_fwd_stats + posu_bn_stats_finalize) instead of a pass over z, where it applies
-# (bf16 / fp16, segments of a multiple of 256 output pixels); False (default): bn_train_fwd's pass
-# -- measured faster: 21.54 vs 21.91 / 21.99 ms per step (profiles/r03/fused_bn_stats_ab_r3ae.txt)
-FUSED_BN_STATS = False
-
-
-def _conv_stats_tuned(x, w, cout, k, stride, pad, nseg, code, kshift):
-    """_conv_tuned with the BatchNorm statistics in the epilogue: -> (z, partials, tiles per
-    segment), or None where the fused statistics do not apply."""
-    from .plan import _tuned
-    n, h, wd, c = x.shape
-    ho, wo = (h + 2 * pad - k) // stride + 1, (wd + 2 * pad - k) // stride + 1
-    m = n * ho * wo
-    if not FUSED_BN_STATS or code not in (ops.BF16, ops.F16) or cout % 8 or m % nseg or (m // nseg) % 256:
-        return None
-    if c % 64:
-        return T.conv2d_fwd_stats(x, w, cout, k, stride, pad, nseg, code, kshift=kshift)
-    key = ('train_conv_stats', code, tuple(x.shape), cout, k, stride, pad, nseg)
-    res = {}
-
-    def launch(t):
-        res['r'] = T.conv2d_fwd_stats(x, w, cout, k, stride, pad, nseg, code, tile=t, kshift=kshift)
-        return res['r'][0]
-    _tuned(key, cout, launch)
-    return res['r']
-
-
 class _Grads(dict):
     """parameter -> gradient; weight gradients run on a side stream (`side`), off the
     backward's critical path: the data-gradient chain (BN backward -> dgrad -> next layer)
@@ -144,19 +116,10 @@ class _ConvBN:
         self.wt = packer.dgrad(self.conv.weight, bk) if need_dgrad else None
 
     def forward(self, x, nseg, code, residual=None):
+        z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
         bn = self.bn
-        # the running mean as the statistics' shift (read by the conv and the finalize before the
-        # finalize updates it)
-        fused = _conv_stats_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, nseg, code, bn.running_mean)
-        if fused is not None:
-            z, part, nt = fused
-            mean, rstd, sc, sh = T.bn_stats_finalize(part, nt, nseg, z.numel() // self.cout // nseg, self.cout,
-                                                     bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
-                                                     bn.running_var, kshift=bn.running_mean)
-        else:
-            z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
-            mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
-                                                bn.running_var)
+        mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                            bn.running_var)
         y = T.bn_apply(z, nseg, sc, sh, residual, self.relu)
         return y, (x, z, y, mean, rstd, sc, sh, residual is not None)
 
@@ -241,18 +204,10 @@ class _DeconvBN:
         self.wd = packer.conv(self.dc.weight, self.cout, bk)
 
     def forward(self, x, nseg, code):
+        z = ops.deconv4x4s2_nhwc(x, self.w, self.cout, None, None, False, code)
         bn = self.bn
-        m = x.numel() // x.shape[3]
-        if (FUSED_BN_STATS and code in (ops.BF16, ops.F16) and self.cout % 8 == 0 and m % nseg == 0 and
-                (m // nseg) % 256 == 0):
-            z, part, nt = T.deconv4x4s2_fwd_stats(x, self.w, self.cout, nseg, code, kshift=bn.running_mean)
-            mean, rstd, sc, sh = T.bn_stats_finalize(part, nt, nseg, 4 * m // nseg, self.cout, bn.weight, bn.bias,
-                                                     bn.eps, bn.momentum, bn.running_mean, bn.running_var,
-                                                     kshift=bn.running_mean)
-        else:
-            z = ops.deconv4x4s2_nhwc(x, self.w, self.cout, None, None, False, code)
-            mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
-                                                bn.running_var)
+        mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                            bn.running_var)
         y = T.bn_apply(z, nseg, sc, sh, None, True)
         return y, (x, z, mean, rstd, sc, sh)
 

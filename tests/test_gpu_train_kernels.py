@@ -286,95 +286,3 @@ def test_batched_weight_packing_network_sizes(cuda, code):
     for i, (got, ref) in enumerate(outs):
         assert got.shape == ref.shape, (i, got.shape, ref.shape)
         assert torch.equal(got, ref), (i, float((got.float() - ref.float()).abs().max()))
-
-
-STATS_CASES = [
-    # nseg, b, cin, h, w, cout, k, stride, pad, tile
-    (4, 2, 64, 16, 16, 64, 3, 1, 1, -1),
-    (4, 2, 64, 16, 16, 128, 1, 1, 0, 3),
-    (2, 4, 128, 16, 16, 256, 3, 2, 1, 23),     # staggered eight-wave tile, strided
-    (4, 1, 256, 16, 16, 256, 1, 1, 0, 31),
-    (4, 2, 64, 32, 32, 64, 3, 1, 1, 8),        # single-slot 256x64
-    (4, 2, 64, 32, 32, 256, 1, 1, 0, 37),      # a persistent tile id: runs its non-persistent loop
-    (2, 2, 8, 32, 32, 64, 7, 2, 3, -1),        # stem-like direct gather (C = 8)
-]
-
-
-@pytest.mark.parametrize('case', STATS_CASES)
-@pytest.mark.parametrize('code', [BF16, F16])
-def test_conv_stats_epilogue_matches_conv_and_bn_pass(cuda, case, code):
-    """posu_conv2d_fwd_stats: z bit-identical to the plain conv; its per-tile sums (about the
-    running mean) finalized into mean / rstd / scale / shift and the running statistics that match
-    posu_bn_train_fwd's pass over z (same f64 combination, different f32 partial grouping)."""
-    nseg, b, cin, h, w, cout, k, stride, pad, tile = case
-    g = torch.Generator().manual_seed(hash(case) % 1000)
-    dt = ops.torch_dtype(code)
-    x = torch.randn(nseg * b, h, w, cin, generator=g).to(cuda, dt)
-    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
-    wp = packing.pack_conv_weight(wt.to(cuda), cin, ops.conv_bk(code), dt)
-    z_ref = ops.conv2d_nhwc(x, wp, cout, k, k, stride, pad, None, None, None, False, code, tile=tile)
-    gamma = (torch.rand(cout, generator=g) + 0.5).to(cuda)
-    beta = torch.randn(cout, generator=g).to(cuda)
-    rm0 = (torch.randn(cout, generator=g) * 0.2).to(cuda)
-    rv0 = (torch.rand(cout, generator=g) + 0.5).to(cuda)
-    rm_a, rv_a, rm_b, rv_b = rm0.clone(), rv0.clone(), rm0.clone(), rv0.clone()
-    ref = T.bn_train_fwd(z_ref, nseg, gamma, beta, 1e-5, 0.1, rm_a, rv_a)
-    z, part, nt = T.conv2d_fwd_stats(x, wp, cout, k, stride, pad, nseg, code, tile=tile, kshift=rm_b)
-    pseg = z.numel() // cout // nseg
-    got = T.bn_stats_finalize(part, nt, nseg, pseg, cout, gamma, beta, 1e-5, 0.1, rm_b, rv_b, kshift=rm_b)
-    torch.cuda.synchronize()
-    assert torch.equal(z.view(torch.int16), z_ref.view(torch.int16))
-    assert nt in (pseg // 64, pseg // 128, pseg // 256)
-    for a, r in zip(got, ref):
-        torch.testing.assert_close(a, r, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(rm_b, rm_a, atol=1e-6, rtol=1e-6)
-    torch.testing.assert_close(rv_b, rv_a, atol=1e-5, rtol=1e-5)
-
-
-@pytest.mark.parametrize('code', [BF16])
-def test_conv_stats_with_a_large_mean_offset(cuda, code):
-    """Channels whose mean is large against their spread: with the running mean near the batch mean
-    as the shift, the epilogue's f32 sums keep the variance (as the shifted pass does)."""
-    g = torch.Generator().manual_seed(5)
-    nseg, b, c, h, w = 2, 4, 64, 16, 16
-    dt = ops.torch_dtype(code)
-    # a 1x1 identity conv of an input with large per-channel offsets
-    off = torch.linspace(-60, 60, c)
-    x = (off.view(1, 1, 1, c) + 0.5 * torch.randn(nseg * b, h, w, c, generator=g)).to(cuda, dt)
-    wp = packing.pack_conv_weight(torch.eye(c).view(c, c, 1, 1).to(cuda), c, ops.conv_bk(code), dt)
-    gamma, beta = torch.ones(c, device=cuda), torch.zeros(c, device=cuda)
-    rm = off.to(cuda) + 0.05
-    z, part, nt = T.conv2d_fwd_stats(x, wp, c, 1, 1, 0, nseg, code, kshift=rm)
-    mean, rstd, _, _ = T.bn_stats_finalize(part, nt, nseg, h * w * b, c, gamma, beta, 1e-5, 0.1, rm, None, kshift=rm)
-    torch.cuda.synchronize()
-    zs = z.double().cpu().view(nseg, b * h * w, c)
-    torch.testing.assert_close(mean.cpu().double(), zs.mean(dim=1), atol=1e-4, rtol=1e-6)
-    torch.testing.assert_close(rstd.cpu().double(), 1 / torch.sqrt(zs.var(dim=1, unbiased=False) + 1e-5), atol=0,
-                               rtol=1e-3)
-
-
-@pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('nseg,b,h,w', [(4, 4, 8, 8), (2, 1, 16, 16), (4, 1, 32, 32)])
-def test_deconv_stats_epilogue_matches_deconv_and_bn_pass(cuda, code, nseg, b, h, w):
-    """posu_deconv4x4s2_fwd_stats: z bit-identical to the raw deconv, statistics of all four parity
-    classes finalized like posu_bn_train_fwd's pass over z."""
-    g = torch.Generator().manual_seed(nseg * 100 + h)
-    dt = ops.torch_dtype(code)
-    cin, cout = 128, 64
-    x = torch.randn(nseg * b, h, w, cin, generator=g).to(cuda, dt)
-    wt = torch.randn(cin, cout, 4, 4, generator=g) * (1.0 / (cin * 4)) ** 0.5
-    wp = packing.pack_deconv4x4_weight(wt.to(cuda), ops.conv_bk(code), dt)
-    z_ref = ops.deconv4x4s2_nhwc(x, wp, cout, None, None, False, code)
-    gamma, beta = (torch.rand(cout, generator=g) + 0.5).to(cuda), torch.randn(cout, generator=g).to(cuda)
-    rm_a = (torch.randn(cout, generator=g) * 0.1).to(cuda)
-    rv_a = torch.ones(cout, device=cuda)
-    rm_b, rv_b = rm_a.clone(), rv_a.clone()
-    ref = T.bn_train_fwd(z_ref, nseg, gamma, beta, 1e-5, 0.1, rm_a, rv_a)
-    z, part, nt = T.deconv4x4s2_fwd_stats(x, wp, cout, nseg, code, kshift=rm_b)
-    got = T.bn_stats_finalize(part, nt, nseg, 4 * b * h * w, cout, gamma, beta, 1e-5, 0.1, rm_b, rv_b, kshift=rm_b)
-    torch.cuda.synchronize()
-    assert torch.equal(z.view(torch.int16), z_ref.view(torch.int16))
-    for a, r in zip(got, ref):
-        torch.testing.assert_close(a, r, atol=1e-5, rtol=1e-5)
-    torch.testing.assert_close(rm_b, rm_a, atol=1e-6, rtol=1e-6)
-    torch.testing.assert_close(rv_b, rv_a, atol=1e-5, rtol=1e-5)

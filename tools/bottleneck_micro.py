@@ -103,8 +103,11 @@ def main():
     u2 = torch.empty_like(u1)
     yl23 = torch.empty_like(xl2)
 
-    def fused_l2():
-        ops.bottleneck2_nhwc(xl2, q1, sl[0], bl[0], q2, sl[1], bl[1], q3, sl[2], bl[2], BF16, out=yl2)
+    wst2 = packing.pack_tail_stream(q2, q3)
+
+    def fused_l2():   # conv1 launch + the register-streamed tail (the plan's layer2 identity block)
+        ops.conv2d_nhwc(xl2, q1, 128, 1, 1, 1, 0, sl[0], bl[0], None, True, BF16, out=u1)
+        ops.bottleneck_tail_stream_nhwc(u1, xl2, wst2, sl[1], bl[1], sl[2], bl[2], BF16, out=yl2)
 
     def three_l2():
         ops.conv2d_nhwc(xl2, q1, 128, 1, 1, 1, 0, sl[0], bl[0], None, True, BF16, out=u1)

@@ -7,7 +7,7 @@ states for global stores and for buffer stores with an immediate soffset, but tr
 store whose soffset is an SGPR as hazard-free -- on gfx950 it is not: the round-2 layer3 tail
 kernel with `__builtin_amdgcn_raw_buffer_store_b128(..., soffset = row offset)` stored wrong
 values into a few hundred 16-B chunks per launch (pixel columns 12-15 of the first rows of
-a tile; tools/store_check.py, profiles/r03/store_order.txt).  This scanner disassembles the
+a tile; profiles/r03/store_order.txt, measured by tools removed in round 4 with the kernel).  This scanner disassembles the
 built library and reports every store whose data VGPRs a VALU instruction overwrites within
 WAIT_STATES instructions (s_nop n counts n + 1).
 
@@ -54,20 +54,46 @@ def _written(mn, ops):
     return w
 
 
+_ADDR = re.compile(r'//\s*([0-9A-Fa-f]+):')
+_END = ('s_endpgm', 's_setpc_b64', 's_trap', 's_rfe_b64')
+
+
+def _branch_target(addr, ops):
+    """Target address of an s_branch / s_cbranch_* at addr: PC + 4 + 4 * simm16."""
+    imm = int(ops[0], 0) & 0xFFFF
+    if imm & 0x8000:
+        imm -= 0x10000
+    return addr[0], addr[1] + 4 + 4 * imm
+
+
 def scan(text):
-    """-> list of (function, store instruction, offending instruction)."""
-    out, fn = [], '?'
-    insts = []
+    """-> list of (function, store instruction, offending instruction).
+
+    From every > 64-bit store, every control-flow path is followed for WAIT_STATES wait states:
+    s_nop n counts n + 1, any other instruction 1 (a branch too: it issues, as LLVM's hazard
+    recognizer counts it); s_branch continues at its target, s_cbranch_* at its target AND its
+    fall-through, so a VALU at a branch target or at a loop head reached through a back-edge is
+    checked too, not only the straight-line successors."""
+    out, fn, obj = [], '?', 0
+    insts, at = [], {}
     for line in text.splitlines():
         s = line.strip()
+        if 'file format' in s:   # a new code object: addresses restart
+            obj += 1
+            continue
         if s.endswith('>:'):
             fn = s
-            insts.append((fn, None, [], s))
+            insts.append((fn, None, [], s, None))
             continue
         mn, ops = _split(line)
         if mn is not None:
-            insts.append((fn, mn, ops, s))
-    for i, (f, mn, ops, s) in enumerate(insts):
+            m = _ADDR.search(line)
+            addr = int(m.group(1), 16) if m else None
+            if addr is not None:
+                addr = (obj, addr)
+                at[addr] = len(insts)
+            insts.append((fn, mn, ops, s, addr))
+    for i, (f, mn, ops, s, _) in enumerate(insts):
         if mn is None:
             continue
         m = _STORE.match(mn)
@@ -75,17 +101,37 @@ def scan(text):
             continue
         # operands: global_store v[addr], v[data], ... ; buffer_store v[data], voffset, ...
         data = _regs(ops[1] if m.group(1) in ('global', 'flat', 'scratch') else ops[0])
-        waits = 0
-        for f2, mn2, ops2, s2 in insts[i + 1:]:
-            if mn2 is None or waits >= WAIT_STATES:
-                break
-            if mn2 == 's_nop':
-                waits += int(ops2[0], 0) + 1 if ops2 else 1
-                continue
-            if _written(mn2, ops2) & data:
-                out.append((f, s, s2))
-                break
-            waits += 1
+        hit, seen, todo = None, set(), [(i + 1, 0)]
+        while todo and hit is None:
+            j, waits = todo.pop()
+            while j < len(insts) and waits < WAIT_STATES and (j, waits) not in seen:
+                seen.add((j, waits))
+                f2, mn2, ops2, s2, a2 = insts[j]
+                if mn2 is None or mn2 in _END:
+                    break
+                if mn2 == 's_nop':
+                    waits += int(ops2[0], 0) + 1 if ops2 else 1
+                    j += 1
+                    continue
+                if mn2 == 's_branch' or mn2.startswith('s_cbranch'):
+                    tgt = at.get(_branch_target(a2, ops2)) if a2 is not None and ops2 else None
+                    if tgt is None:            # unresolved target: a hazard unless waited out
+                        hit = s2 + '  (unresolved branch target inside the window)'
+                        break
+                    waits += 1
+                    if mn2 == 's_branch':
+                        j = tgt
+                        continue
+                    todo.append((tgt, waits))
+                    j += 1
+                    continue
+                if _written(mn2, ops2) & data:
+                    hit = s2
+                    break
+                waits += 1
+                j += 1
+        if hit is not None:
+            out.append((f, s, hit))
     return out
 
 
