@@ -262,15 +262,34 @@ def oracle_chain(sd, layers, size, views_cpu, host, full=False):
     return X
 
 
+def host_cores():
+    """(cores this process may run on, the host's CPU count): the scheduler affinity, capped by a
+    cgroup CPU quota when one is set (a GPU box gives each GPU's job a share of a larger host)."""
+    host = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = host
+    try:
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            quota, period = f.read().split()[:2]
+        if quota != 'max':
+            usable = min(usable, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return usable, host
+
+
 def cpu_baseline(layers, size, groups, seconds):
     """The oracle chain on the host cores: the full configs[2] batch (groups x 4 frames,
     repeated until `seconds` have passed, at least once) and configs[0] (batch 1,
-    forward only).  Returns (cpu_baseline dict, the first full batch's oracle outputs)."""
+    forward only), on every core this process may use (host_cores).  Returns (cpu_baseline dict,
+    the first full batch's oracle outputs)."""
     from models.pose_resnet import get_pose_net
     from oracle import pose_resnet_ref as PR
     from posu import synthetic as syn
     from posu.pipeline import synthetic_meta
-    threads = min(16, os.cpu_count() or 1)
+    threads, host = host_cores()
     torch.set_num_threads(threads)
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
@@ -293,7 +312,8 @@ def cpu_baseline(layers, size, groups, seconds):
         n1 += 1
     c1_ms = (time.perf_counter() - t1) / n1 * 1e3
     ref['host'] = host
-    return ({'value': round(frames / el, 3), 'unit': 'frames/s', 'cores': threads, 'kind': 'port',
+    return ({'value': round(frames / el, 3), 'unit': 'frames/s', 'cores': threads, 'host_cpus': host,
+             'kind': 'port',
              'sample': '%d frames = %d pass(es) of the full %dx4 batch (R%d@%d) through the CPU oracle chain: '
                        'torch-CPU fp32 forward + soft-argmax + transform_back + FundamentalLoss + numpy DLT/SVD '
                        'triangulation, %.1f s' % (frames, frames // (4 * groups), groups, layers, size, el),
@@ -459,7 +479,7 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
             r.run_geo(r.run_net())
         stream = torch.cuda.current_stream(dev)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-               torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+               torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
         # decode + geometry of batch i on a second stream, overlapping the network of batch i + 1
         # (a two-stage pipeline over the rotated batches): batch i's geometry waits for its own
         # network; a batch's next network replay waits for its previous geometry (its graphs
@@ -480,10 +500,12 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
             hm = r.run_net()
             ev[i][1].record(stream)
             if geo_stream is None:
+                ev[i][3].record(stream)
                 r.run_geo(hm)
                 ev[i][2].record(stream)
                 continue
             geo_stream.wait_event(ev[i][1])
+            ev[i][3].record(geo_stream)   # geometry starts: its own network done, the previous geometry too
             with torch.cuda.stream(geo_stream):
                 r.run_geo(hm)
             ev[i][2].record(geo_stream)
@@ -493,8 +515,8 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        net_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
-        geo_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+        net_ms = float(np.mean([a.elapsed_time(b) for a, b, _, _ in ev]))
+        geo_ms = float(np.mean([d.elapsed_time(c) for _, _, c, d in ev]))
         # the first batch's outputs, for the MPJPE check
         r = reps[0]
         coords, loss, X = r.run_geo(r.run_net())

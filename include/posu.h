@@ -48,7 +48,7 @@ const char* posu_last_error(void);
  * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd); 10 the
  * BatchNorm statistics in the conv epilogue (measured slower, removed in 11); 11 the streamed
  * tails take their weight stream's byte size, the round-2 LDS-ring layer2 block / layer3 tail
- * kernels removed.  The ctypes binding refuses a library of another revision. */
+ * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) added.  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -208,6 +208,20 @@ int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* 
                                          int P, const void* wstream, long long wstream_bytes, const float* s2,
                                          const float* b2, const float* s3, const float* b3, void* y,
                                          const float* s1n, const float* b1n, void* t1n, void* stream);
+
+/* The tail of the FIRST Bottleneck of layer2 (lib/models/pose_resnet.py:61-99 with the downsample
+ * branch, pose_resnet.py:136-141; eval BN folded) of PoseResNet at 256x256, in one launch:
+ *   y = relu( [w3*s3 | wd*sd] . [ relu(bn2(conv2_3x3_stride2(t1))) ; x(2 oy, 2 ox) ] + shift ),
+ * i.e. posu_conv2d_fwd(conv2, stride 2) followed by posu_conv1x1_dual_fwd(t2, x, stride 2) with t2
+ * kept on chip.  t1 [N, H, 64, 128] (conv1's output), x [N, H, 64, 256] (the block input),
+ * y [N, H/2, 32, 512]; H a multiple of 8; BF16 / F16.  s2 / b2: conv2's folded BN [128] f32;
+ * shift = b3 + bd [512] f32 (16-B aligned).  wstream: packing.pack_s2_tail_stream of the conv2
+ * [128][1152] and dual [512][384] posu_conv2d_fwd / posu_conv1x1_dual_fwd packs,
+ * [4][84][2][64][8] elements of dtype; wstream_bytes its size (checked).  Bit-identical to the two
+ * launches (same MFMA sequence per accumulator). */
+int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                                const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
+                                const float* shift, int Cout, void* y, void* stream);
 
 /* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
  * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn

@@ -20,7 +20,6 @@ def project_point_radial(x, R, T, f, c, k, p):
     """World points [N, 3] -> pixels [N, 2] with the H36M radial + tangential model
     (reference cameras.py:25-49): y = xcam[:2] / xcam[2];
     y_d = y * (1 + k1 r^2 + k2 r^4 + k3 r^6 + p0 y1 + p1 y0) + [p1, p0] r^2; px = f y_d + c."""
-    n = x.shape[0]
     xcam = R.dot(x.T - T)
     y = xcam[:2] / xcam[2]
     r2 = np.sum(y ** 2, axis=0)
@@ -29,7 +28,6 @@ def project_point_radial(x, R, T, f, c, k, p):
     radial = 1 + (kk[0] * r2 + kk[1] * r2 ** 2 + kk[2] * r2 ** 3)
     tan = pp[0] * y[1] + pp[1] * y[0]
     y = y * np.tile(radial + tan, (2, 1)) + np.outer(np.array([pp[1], pp[0]]), r2)
-    del n
     return ((f * y) + np.asarray(c, dtype=np.float64).reshape(2, 1)).T
 
 

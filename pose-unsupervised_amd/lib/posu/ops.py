@@ -110,6 +110,19 @@ def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
     return out
 
 
+def bottleneck_s2_tail_nhwc(t1, x, wstream, s2, b2, shift, code, out=None):
+    """conv2 (3x3 / stride 2) + the conv3 | downsample dual GEMM of layer2's first Bottleneck in one
+    launch (posu_bottleneck_s2_tail_fwd, csrc/tail_s2.hip): t1 [N, H, 64, 128], x [N, H, 64, 256] ->
+    y [N, H/2, 32, 512]; wstream = packing.pack_s2_tail_stream(conv2 pack, dual pack)."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, h // 2, w // 2, shift.numel()), dtype=x.dtype, device=x.device)
+    call('posu_bottleneck_s2_tail_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(shift), shift.numel(), ptr(out),
+         stream_of(x.device))
+    return out
+
+
 def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, code, out=None, t1n=None):
     """The tail above chained with the NEXT identity block's conv1 + BN1 + ReLU over its output
     (posu_bottleneck_tail_stream_next_fwd); wstream = packing.pack_tail_stream(conv2 pack, conv3

@@ -36,6 +36,22 @@ def mfma_fragments(wpk):
     return wpk.reshape(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(co // 16, k // 32, 64, 8)
 
 
+def pack_s2_tail_stream(w2pk, wdual):
+    """The per-wave weight streams of posu_bottleneck_s2_tail_fwd (csrc/tail_s2.hip) from the conv2
+    [128][1152] (posu_conv2d_fwd) and dual [512][384] (pack_dual_1x1_weight) packs:
+    [4 channel groups][84 k-steps][2 n-tiles][64 lanes][8].  Group cq, k-step p < 36: conv2 n-tile
+    2 cq + j, k-step p (tap-major K); p = 36 + 12 nc + c: dual n-tile 8 nc + 2 cq + j, k-step c
+    (t2's 4 k-steps, then x's 8)."""
+    if tuple(w2pk.shape) != (128, 1152) or tuple(wdual.shape) != (512, 384):
+        raise ValueError('pack_s2_tail_stream: conv2 pack [128][1152] and dual pack [512][384] expected, got %s / %s'
+                         % (tuple(w2pk.shape), tuple(wdual.shape)))
+    f2 = mfma_fragments(w2pk)                                     # [8][36][64][8]
+    s2 = f2.reshape(4, 2, 36, 64, 8).permute(0, 2, 1, 3, 4)       # [cq][36][j][64][8]
+    fd = mfma_fragments(wdual)                                    # [32][12][64][8]
+    sd = fd.reshape(4, 4, 2, 12, 64, 8).permute(1, 0, 3, 2, 4, 5)  # [cq][nc][12][j][64][8]
+    return torch.cat([s2, sd.reshape(4, 48, 2, 64, 8)], dim=1).contiguous()
+
+
 def pack_tail_stream(w2pk, w3pk, w1n=None):
     """The per-wave weight streams of posu_bottleneck_tail_stream_fwd (csrc/tail_stream.hip) from
     the conv2 [P][9P] and conv3 [C][P] posu_conv2d_fwd packs: [NCQ][9 KT + NC KT][2][64][8] with

@@ -19,7 +19,8 @@ import torch
 from . import ops
 from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
                       pack_conv_weight, pack_deconv4x4_weight,
-                      pack_dual_1x1_weight, pack_stem_fused_weight, pack_stem_s2d_weight, pack_tail_stream)
+                      pack_dual_1x1_weight, pack_s2_tail_stream, pack_stem_fused_weight, pack_stem_s2d_weight,
+                      pack_tail_stream)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
@@ -160,6 +161,9 @@ class _DualTail:
 # (The round-2 LDS-ring layer2 block / layer3 tail kernels, slower than the streamed tail, were
 # removed from the library in round 4.)
 FUSED_BOTTLENECK = True
+# layer2's first Bottleneck: conv2 (3x3 / stride 2) and the conv3 | downsample dual GEMM as ONE
+# launch (posu_bottleneck_s2_tail_fwd) after the conv1 launch; False: two launches
+S2_TAIL = True
 # consecutive streamed identity tails chained: block i's tail also computes block i+1's conv1
 # over its output (posu_bottleneck_tail_stream_next_fwd), so block i+1 has no conv1 launch and y
 # is not re-read for it (tools/chain_micro.py: layer2 105.0 vs 130.0 us, layer3 76.3 vs 85.0 us
@@ -177,7 +181,7 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -191,6 +195,7 @@ class _Block:
         self.wst = None              # layer2 / layer3: the tail's per-wave weight streams (pack_tail_stream)
         self.chain = None            # the next identity block's conv1 (_Conv) when the tails chain
         self.wsn = None              # the streams with that conv1 appended (pack_tail_stream(.., w1n))
+        self.ws2 = None              # layer2 block 0: the strided tail's weight streams (pack_s2_tail_stream)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -203,6 +208,11 @@ class _Block:
                     c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (64, 576) and \
                     self.dual.w.shape[1] >= 128:
                 self.w3d = pack_bottleneck_down_weight(self.dual.w, 64)
+            if code in (ops.BF16, ops.F16) and self.dual.stride2 == 2 and self.dual.cout == 512 and \
+                    c1.k == 1 and c1.stride == 1 and c1.w.shape == (128, 256) and \
+                    c2.k == 3 and c2.stride == 2 and c2.pad == 1 and c2.w.shape == (128, 1152) and \
+                    tuple(self.dual.w.shape) == (512, 384):
+                self.ws2 = pack_s2_tail_stream(c2.w, self.dual.w)
             return
         for nm in names:
             self.convs.append(_Conv(getattr(blk, nm), getattr(blk, 'bn' + nm[-1]), True, code, bk))
@@ -282,6 +292,11 @@ class _Block:
             c1, c2 = self.convs
             return ops.bottleneck_down_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3d,
                                             self.dual.shift, code, out=out)
+        if (self.ws2 is not None and S2_TAIL and FUSED_BOTTLENECK and fits and x.shape[2] == 64 and
+                x.shape[1] % 8 == 0):
+            c1, c2 = self.convs
+            return ops.bottleneck_s2_tail_nhwc(c1(x, code), x, self.ws2, c2.scale, c2.shift, self.dual.shift, code,
+                                               out=out)
         if self.dual is not None:
             for c in self.convs:
                 y = c(y, code)

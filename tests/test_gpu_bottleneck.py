@@ -195,6 +195,66 @@ def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
     assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(1, 8), (2, 16), (3, 24), (1, 64), (128, 64)])
+def test_layer2_first_block_strided_tail_matches_two_launches_and_torch(cuda, code, n, h):
+    """Layer2's first block after its conv1 launch: conv2 (3x3 / stride 2) + the conv3 | downsample
+    dual GEMM in one launch (posu_bottleneck_s2_tail_fwd), bit-identical to the two launches it
+    replaces (same MFMA sequence per accumulator) with every output written (NaN sentinel), and
+    within the dtype's tolerance of torch fp32.  (128, 64) is the production grid (2048
+    workgroups)."""
+    g = torch.Generator().manual_seed(91 + h)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=512, p=128)
+    w1 = w1[:, :256].contiguous() * 2 ** 0.5          # conv1 256 -> 128
+    wd = torch.randn(512, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5 * 0.3
+    bnd = (torch.rand(512, generator=g) + 0.5, torch.randn(512, generator=g) * 0.1)
+    x = torch.randn(n, 256, h, 64, generator=g).abs()
+    dt = ops.torch_dtype(code)
+    xq = x.to(dt).float()
+    bk = ops.conv_bk(code)
+    xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 128, bk, dt)
+    pdual = packing.pack_dual_1x1_weight(w3.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), dt)
+    shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, 128, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    fused = ops.bottleneck_s2_tail_nhwc(t1, xd, packing.pack_s2_tail_stream(p2, pdual), s[2], s[3], shift, code,
+                                        out=_sentinel(xd, (n, h // 2, 32, 512)))
+    t2 = ops.conv2d_nhwc(t1, p2, 128, 3, 3, 2, 1, s[2], s[3], None, True, code)
+    two = ops.conv1x1_dual_nhwc(t2, xd, 2, pdual, 512, shift, True, code)
+    torch.cuda.synchronize()
+    d = (fused.float() - two.float()).abs()
+    print('layer2 strided tail vs two launches: max %.3g, differing elements %d' % (float(d.max()), int((d > 0).sum())))
+    assert torch.equal(fused, two)
+    if n >= 128:
+        return
+    t1r = F.relu(F.conv2d(xq, w1) * bn1[0].view(1, -1, 1, 1) + bn1[1].view(1, -1, 1, 1))
+    t2r = F.relu(F.conv2d(t1r, w2, stride=2, padding=1) * bn2[0].view(1, -1, 1, 1) + bn2[1].view(1, -1, 1, 1))
+    ref = F.relu(F.conv2d(t2r, w3) * bn3[0].view(1, -1, 1, 1) + bn3[1].view(1, -1, 1, 1) +
+                 F.conv2d(xq, wd, stride=2) * bnd[0].view(1, -1, 1, 1) + bnd[1].view(1, -1, 1, 1))
+    err = (fused.float().cpu().permute(0, 3, 1, 2) - ref).abs()
+    tol = 0.05 if code == BF16 else 0.01
+    assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
+
+
+def test_strided_tail_refuses_unsupported_shapes(cuda):
+    x = torch.zeros(1, 8, 64, 256, device=cuda, dtype=torch.bfloat16)
+    t1 = torch.zeros(1, 8, 64, 128, device=cuda, dtype=torch.bfloat16)
+    w2 = torch.zeros(128, 1152, device=cuda, dtype=torch.bfloat16)
+    wdual = torch.zeros(512, 384, device=cuda, dtype=torch.bfloat16)
+    ws = packing.pack_s2_tail_stream(w2, wdual)
+    s = torch.ones(512, device=cuda)
+    with pytest.raises(RuntimeError, match='multiple of 8'):
+        ops.bottleneck_s2_tail_nhwc(t1[:, :4], x[:, :4], ws, s, s, s, BF16)
+    with pytest.raises(RuntimeError, match='first Bottleneck of layer2'):
+        ops.bottleneck_s2_tail_nhwc(t1[:, :, :32], x[:, :, :32], ws, s, s, s, BF16)
+    with pytest.raises(RuntimeError, match='wstream holds'):
+        ops.bottleneck_s2_tail_nhwc(t1, x, ws[:3], s, s, s, BF16)
+    with pytest.raises(ValueError, match='pack_s2_tail_stream'):
+        packing.pack_s2_tail_stream(w2[:64], wdual)
+
+
 def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 32, 256, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 256, device=cuda, dtype=torch.bfloat16)
@@ -257,6 +317,31 @@ def test_plan_with_fused_bottlenecks_matches_unfused_plan(cuda, precision):
           % (precision, dx, dh.max(), dh.mean()))
     assert dx < (0.1 if precision == 'bf16' else 0.02)
     assert dh.mean() < (0.01 if precision == 'bf16' else 0.002)
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp16'])
+def test_plan_strided_tail_is_bit_identical_to_two_launches(cuda, precision):
+    """The R50@256 plan with layer2's first block on the strided tail (S2_TAIL) gives the same heatmaps
+    and layer1 features, bit for bit, as with conv2 + the dual GEMM as two launches."""
+    import posu.plan as P
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision=precision)
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
+    net = net.to(cuda).eval()
+    plan = net.plan(cuda)
+    assert plan.layers[1][0].ws2 is not None and all(b.ws2 is None for b in plan.layers[2] + plan.layers[3])
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=13)]
+    saved = P.S2_TAIL
+    try:
+        with torch.no_grad():
+            P.S2_TAIL = True
+            hm1, _, f1 = plan.run(plan.pack_input(views))
+            P.S2_TAIL = False
+            hm0, _, f0 = plan.run(plan.pack_input(views))
+    finally:
+        P.S2_TAIL = saved
+    torch.cuda.synchronize()
+    assert torch.equal(hm1, hm0) and torch.equal(f1, f0)
 
 
 @pytest.mark.parametrize('code', [BF16, F16])

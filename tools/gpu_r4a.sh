@@ -4,6 +4,8 @@
 set -o pipefail
 O=gpurun_out/r4a
 mkdir -p $O
+
+
 timeout -k 10 240 python -u tools/precision_attribution.py 1200 > $O/attribution.json 2> $O/attribution.err || exit 1
 echo attribution done
 C="--no-cpu-baseline --no-mpjpe"
