@@ -96,6 +96,12 @@ def parse():
                     help='N = 1: fit steps of the peaked-heatmap network behind mpjpe_vs_ref_mm (0: skip)')
     ap.add_argument('--c1-steps', type=int, default=20,
                     help='infer mode: timed replays of the configs[1] forward (batch 64) reported as configs1 (0: skip)')
+    ap.add_argument('--c4-steps', type=int, default=10,
+                    help='infer mode: timed steps of configs[4]\'s per-GPU pipeline (R152@384 fp16, 16 groups x 4 '
+                         'views) reported as configs4 (0: skip)')
+    ap.add_argument('--control-steps', type=int, default=10,
+                    help='infer mode: timed steps of the same pipeline with this round\'s plan switches off '
+                         '(CONTROL_FLAGS: the previous round\'s plan), reported as control (0: skip)')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
     ap.add_argument('--train-stream', default='default', choices=['high', 'default'],
                     help='train mode: run the step on a high-priority stream (the weight-gradient side '
@@ -105,6 +111,11 @@ def parse():
                     help='A/B runs: set a boolean switch of posu.plan / posu.train_plan (e.g. '
                          'STREAMED_LAYER2_TAIL=0, FUSED_BN_STATS=0) before the plans are built')
     return ap.parse_args()
+
+
+# the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
+# line's `control` leg times it in the same process, so a gain shows on the driver's own box
+CONTROL_FLAGS = ('S2_TAIL', 'STEM_VIEWS')
 
 
 def apply_plan_flags(flags):
@@ -606,6 +617,44 @@ def time_configs1(args, dev, rank, world, dist):
                          'frac': round(tf / PEAK_BF16_TFLOPS, 4)}}
 
 
+def time_control(args, dev, rank, world, dist):
+    """The benched pipeline with CONTROL_FLAGS off (the previous round's plan), same process and
+    box: its network_ms beside the line's."""
+    from posu import plan as pl
+    saved = {f: getattr(pl, f) for f in CONTROL_FLAGS}
+    try:
+        for f in CONTROL_FLAGS:
+            setattr(pl, f, False)
+        r = time_pipeline(args, args.precision, dev, rank, args.control_steps, 3, args.batches,
+                          not args.no_autotune, dist, world)
+    finally:
+        for f, v in saved.items():
+            setattr(pl, f, v)
+    return {'flags_off': list(CONTROL_FLAGS), 'network_ms': round(r['net_ms'], 4), 'steps': args.control_steps,
+            'ms_per_step': round(r['elapsed'] / args.control_steps * 1e3, 4)}
+
+
+def time_configs4(args, dev, rank, world, dist):
+    """BASELINE configs[4]'s per-GPU pipeline: R152 backbone at 384x384, fp16 compute, fp64
+    triangulation, 16 groups x 4 views per GPU (the 8-GPU job's shard), tiles autotuned, the same
+    two-stage replay as the line: frames/s and the fraction of the fp16 (= bf16) MFMA peak."""
+    import argparse as _ap
+    a4 = _ap.Namespace(**vars(args))
+    a4.layers, a4.size, a4.groups, a4.precision, a4.tune_file = 152, 384, 16, 'fp16', ''
+    r = time_pipeline(a4, 'fp16', dev, rank, args.c4_steps, 3, 2, not args.no_autotune, dist, world)
+    from posu import dist as pdist
+    el = pdist.max_over_ranks(r['elapsed'], device=dev)
+    frames = 4 * a4.groups
+    tf = GFLOP_PER_FRAME[(152, 384)] * frames / (r['net_ms'] * 1e-3) / 1e3
+    return {'metric': '4-view 384x384 frames/sec (fwd+triangulate), R152 fp16 (BASELINE configs[4], per-GPU shard '
+                      'of 16 groups x 4 views)', 'value': round(pdist.throughput(frames, args.c4_steps, world, el), 2),
+            'unit': 'frames/s', 'n_gpus': world, 'steps': args.c4_steps, 'network_ms': round(r['net_ms'], 4),
+            'ms_per_step': round(el / args.c4_steps * 1e3, 4), 'dtype': 'fp16',
+            'roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': round(tf / PEAK_BF16_TFLOPS, 4),
+                         'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (GFLOP_PER_FRAME[(152, 384)], frames)}}
+
+
 def infer_main(args):
     from posu import dist as pdist
     _, local, world = pdist.env_rank()
@@ -633,6 +682,16 @@ def infer_main(args):
         if traffic:
             roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward')
             roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
+    # the training leg right after the headline leg, before the other legs (see DESIGN.md section 6:
+    # behind the fp32 / configs1 legs the same step read 23.98 instead of 21.6 ms)
+    train = None
+    if args.train_steps > 0:
+        t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
+        train = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
+        train.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
+                     traffic=t['roofline']['traffic'] if t['roofline'] else None,
+                     parallelism=t['config']['parallelism'], workload=t['config']['workload'],
+                     optimizer=t['config']['optimizer'])
     fp32 = None
     if args.fp32_steps > 0 and args.precision != 'fp32':
         r32 = time_pipeline(args, 'fp32', dev, rank, args.fp32_steps, 2, args.batches, False, dist, world)
@@ -642,14 +701,8 @@ def infer_main(args):
                 'roofline_frac_f32': (round(gf * frames / (r32['net_ms'] * 1e-3) / 1e3 / PEAK_F32_TFLOPS, 4)
                                       if gf else None)}
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
-    train = None
-    if args.train_steps > 0:
-        t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
-        train = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
-        train.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
-                     traffic=t['roofline']['traffic'] if t['roofline'] else None,
-                     parallelism=t['config']['parallelism'], workload=t['config']['workload'],
-                     optimizer=t['config']['optimizer'])
+    control = time_control(args, dev, rank, world, dist) if args.control_steps > 0 else None
+    c4 = time_configs4(args, dev, rank, world, dist) if args.c4_steps > 0 else None
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -697,7 +750,7 @@ def infer_main(args):
         'mpjpe_vs_ref_mm': mpjpe, 'peaked_parity': peaked,
         'random_weight_chain_vs_ref': random_w if world == 1 and not args.no_mpjpe else None,
         'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32,
-        'configs1': c1, 'train_mode': train,
+        'configs1': c1, 'configs4': c4, 'control': control, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }
     print(json.dumps(line))

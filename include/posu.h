@@ -48,7 +48,8 @@ const char* posu_last_error(void);
  * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd); 10 the
  * BatchNorm statistics in the conv epilogue (measured slower, removed in 11); 11 the streamed
  * tails take their weight stream's byte size, the round-2 LDS-ring layer2 block / layer3 tail
- * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) added.  The ctypes binding refuses a library of another revision. */
+ * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) and the
+ * one-launch multi-view stem (posu_stem_pool_views_fwd) added.  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -135,6 +136,12 @@ int posu_conv_bk(int dtype);
  * y NHWC [N, H/4, W/4, 64] dtype.  BF16 / F16, H % 8 == 0, W in {256, 384}. */
 int posu_stem_pool_fwd(int dtype, const float* x, int N, int H, int W, int hflip, const void* w,
                        const float* scale, const float* shift, void* y, void* stream);
+/* posu_stem_pool_fwd over the views of one forward in ONE launch (lib/models/multiview_pose_resnet.py
+ * runs the backbone per view; the stem needs no per-view statistics in eval mode): views = host
+ * array of nviews (1..8) device pointers to [Nv, 3, H, W] f32, y = [nviews * Nv, H/4, W/4, 64]
+ * view-major.  Same values as nviews posu_stem_pool_fwd launches. */
+int posu_stem_pool_views_fwd(int dtype, const float* const* views, int nviews, int Nv, int H, int W, int hflip,
+                             const void* w, const float* scale, const float* shift, void* y, void* stream);
 int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,

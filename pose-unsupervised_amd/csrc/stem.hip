@@ -21,6 +21,9 @@
 // Pool padding (-inf in MaxPool2d) and ReLU >= 0 make "ignore" and "0" the same, so rows /
 // columns outside the stem image enter the max as 0.  The stem values are rounded to the
 // compute dtype before the max exactly like the two-launch path (rounding is monotonic).
+#include <string>
+#include <type_traits>
+
 #include "posu_common.h"
 
 namespace posu {
@@ -28,7 +31,6 @@ namespace {
 
 constexpr int kStemK = 224;       // 7 kernel rows x 8 taps x 4 channels
 constexpr int kStemPitch = 232;   // weight row pitch in LDS (elements): conflict-free B reads
-constexpr int kWinRows = 15;      // input rows under two pool rows
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
@@ -58,158 +60,226 @@ struct StemOp<f16_t> {
   static __device__ __forceinline__ float round(float a) { return static_cast<float>(static_cast<_Float16>(a)); }
 };
 
-// NW waves; wave w owns stem columns 16w .. 16w + 15 (one m-tile column group) of the 5
-// stem rows -> 5 m-tiles x 4 n-tiles (64 channels) of accumulators.
+// The views of one forward (the caller's NCHW f32 tensors, each [Nv, 3, H, W]) in one launch.
+constexpr int kMaxViews = 8;
+struct StemViews {
+  const float* x[kMaxViews];
+};
+
+// NW waves; wave w owns stem columns 16w .. 16w + 15 (one m-tile column group).  A block walks a
+// strip of consecutive pool-row pairs of one image (item k = pool rows 2k, 2k+1 = stem rows
+// 4k-1 .. 4k+3):
+//   * the input rows live in a 16-row LDS ring (slot = input row & 15, [col][4 ch] as above);
+//     item k reads input rows 8k-3 .. 8k+9, of which 8k+2 .. 8k+9 are new: they are loaded into
+//     registers while item k-1 computes and written to the ring behind it;
+//   * stem row 4k-1 (the first row of pool row 2k's window) is item k-1's last stem row, carried
+//     in registers: an item computes 4 stem rows (the strip's first item 5), not 5.
 template <typename T, int NW>
-__global__ __launch_bounds__(NW * 64) void stem_pool_kernel(const float* __restrict__ x, int N, int H, int W,
-                                                            int hflip, const T* __restrict__ w,
-                                                            const float* __restrict__ scale,
-                                                            const float* __restrict__ shift, T* __restrict__ y) {
+__global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int Nv, int N, int H, int W, int hflip,
+                                                               int strips, const T* __restrict__ w,
+                                                               const float* __restrict__ scale,
+                                                               const float* __restrict__ shift, T* __restrict__ y) {
   using O = StemOp<T>;
   constexpr int NT = NW * 64;
   constexpr int WP = NW * 32 + 8;            // window columns: input cols -3 .. W + 4
-  constexpr int WIN_BYTES = kWinRows * WP * 8;
+  constexpr int RB = WP * 8;                 // bytes per ring row
+  constexpr int RING = 16;
   constexpr int W_BYTES = 64 * kStemPitch * 2;
-  __shared__ __attribute__((aligned(16))) char smem[WIN_BYTES + W_BYTES + NW * 2 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[RING * RB + W_BYTES + NW * 2 * 64 * 4];
   char* win = smem;
-  char* wl = smem + WIN_BYTES;
-  float* edge = reinterpret_cast<float*>(smem + WIN_BYTES + W_BYTES);  // [wave][pool row][64 ch]
+  char* wl = smem + RING * RB;
+  float* edge = reinterpret_cast<float*>(smem + RING * RB + W_BYTES);  // [wave][pool row][64 ch]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
   const int Hp = H / 4, Wp = W / 4;
-  const int pairs = Hp / 2;
-  const int n = blockIdx.x / pairs, p0 = 2 * (blockIdx.x - n * pairs);  // pool rows p0, p0 + 1
-  const int r0 = 4 * p0 - 5;                                           // first window input row
-
-  // ---- global -> registers first (the block's loads all in flight at once), then LDS
-  constexpr int WCH = 64 * (kStemK / 8);                 // 16-B weight chunks
-  constexpr int WIT = (WCH + NT - 1) / NT;
-  u32x4 wv[WIT];
-#pragma unroll
-  for (int it = 0; it < WIT; ++it) {
-    const int i = min(tid + it * NT, WCH - 1);  // clamped: duplicate chunks store the same bytes
-    wv[it] = *reinterpret_cast<const u32x4*>(w + i * 8);
-  }
-  // input window pixel (r, c) = input (r0 + r, c - 3), 3 channels + 0, read as 16-B groups
-  // of 4 input columns (4 gk - 4 .. 4 gk - 1) per plane: window columns 4 gk - 1 .. 4 gk + 2
+  const int pairs = Hp / 2, per = pairs / strips;
+  const int n = blockIdx.x / strips;
+  const int k0 = (blockIdx.x - n * strips) * per, k1 = k0 + per;
+  const float* __restrict__ xn = xs.x[n / Nv] + static_cast<size_t>(n % Nv) * 3 * H * W;
   const size_t plane = static_cast<size_t>(H) * W;
-  const float* __restrict__ xn = x + static_cast<size_t>(n) * 3 * plane;
-  constexpr int GPR = NW * 8 + 2;                          // groups per window row (W / 4 + 2)
-  constexpr int XG = (kWinRows * GPR + NT - 1) / NT;       // groups per thread
-  float4 xv[XG][3];
+
+  // ---- weights -> LDS (once per block)
+  {
+    constexpr int WCH = 64 * (kStemK / 8);
 #pragma unroll
-  for (int it = 0; it < XG; ++it) {
-    const int i = tid + it * NT;
-    const int r = i / GPR, gk = i - r * GPR;
-    const int iy = r0 + r, c0 = 4 * (gk - 1);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) xv[it][p] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < kWinRows * GPR && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
-        static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
-      const size_t o = static_cast<size_t>(iy) * W + (hflip ? W - 4 - c0 : c0);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        float4 v = *reinterpret_cast<const float4*>(xn + p * plane + o);
-        if (hflip) v = make_float4(v.w, v.z, v.y, v.x);
-        xv[it][p] = v;
+    for (int it = 0; it < (WCH + NT - 1) / NT; ++it) {
+      const int i = tid + it * NT;
+      if (i < WCH) {
+        const int co = i / (kStemK / 8), ck = i - co * (kStemK / 8);
+        *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = *reinterpret_cast<const u32x4*>(w + i * 8);
       }
     }
   }
-#pragma unroll
-  for (int it = 0; it < WIT; ++it) {
-    const int i = min(tid + it * NT, WCH - 1);
-    const int co = i / (kStemK / 8), ck = i - co * (kStemK / 8);
-    *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = wv[it];
-  }
-#pragma unroll
-  for (int it = 0; it < XG; ++it) {
-    const int i = tid + it * NT;
-    if (i >= kWinRows * GPR) continue;
-    const int r = i / GPR, gk = i - r * GPR;
-    const float a0[4] = {xv[it][0].x, xv[it][0].y, xv[it][0].z, xv[it][0].w};
-    const float a1[4] = {xv[it][1].x, xv[it][1].y, xv[it][1].z, xv[it][1].w};
-    const float a2[4] = {xv[it][2].x, xv[it][2].y, xv[it][2].z, xv[it][2].w};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int wc = 4 * gk - 1 + e;
-      if (wc >= 0 && wc < WP)
-        *reinterpret_cast<uint2*>(win + (r * WP + wc) * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
-    }
-  }
-  __syncthreads();
 
-  // ---- stem GEMM: m-tile rl = local stem row, pixel column sc = 16 wid + r16
-  f32x4 acc[5][4];
+  // input rows -> registers: row i0 + r (r < NR), group gk = 4 input columns 4 (gk - 1) .. + 3 of
+  // each plane (window columns 4 gk - 1 .. 4 gk + 2)
+  constexpr int GPR = NW * 8 + 2;
+  constexpr int XG8 = (8 * GPR + NT - 1) / NT;
+  auto load_rows = [&](int i0, auto nr, float4 (*xv)[3]) {
+    constexpr int NR = decltype(nr)::value, XG = (NR * GPR + NT - 1) / NT;
 #pragma unroll
-  for (int i = 0; i < 5; ++i)
+    for (int it = 0; it < XG; ++it) {
+      const int i = tid + it * NT;
+      const int r = i / GPR, gk = i - r * GPR;
+      const int iy = i0 + r, c0 = 4 * (gk - 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int p = 0; p < 3; ++p) xv[it][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < NR * GPR && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
+          static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
+        const size_t o = static_cast<size_t>(iy) * W + (hflip ? W - 4 - c0 : c0);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          float4 v = *reinterpret_cast<const float4*>(xn + p * plane + o);
+          if (hflip) v = make_float4(v.w, v.z, v.y, v.x);
+          xv[it][p] = v;
+        }
+      }
+    }
+  };
+  auto store_rows = [&](int i0, auto nr, float4 (*xv)[3]) {
+    constexpr int NR = decltype(nr)::value, XG = (NR * GPR + NT - 1) / NT;
+#pragma unroll
+    for (int it = 0; it < XG; ++it) {
+      const int i = tid + it * NT;
+      if (i >= NR * GPR) continue;
+      const int r = i / GPR, gk = i - r * GPR;
+      char* row = win + ((i0 + r) & (RING - 1)) * RB;
+      const float a0[4] = {xv[it][0].x, xv[it][0].y, xv[it][0].z, xv[it][0].w};
+      const float a1[4] = {xv[it][1].x, xv[it][1].y, xv[it][1].z, xv[it][1].w};
+      const float a2[4] = {xv[it][2].x, xv[it][2].y, xv[it][2].z, xv[it][2].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int wc = 4 * gk - 1 + e;
+        if (wc >= 0 && wc < WP)
+          *reinterpret_cast<uint2*>(row + wc * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
+      }
+    }
+  };
+
   const int sc = 16 * wid + r16;
+  // stem rows r0 .. r0 + M - 1 (m-tile rl = stem row r0 + rl; pixel column sc), BN + ReLU, rounded
+  // (zeros for rows outside the image), folded straight into the two pool rows' vertical maxima:
+  // M = 5: rows 4k-1 .. 4k+3; M = 4: rows 4k .. 4k+3 with row 4k-1 = carry.  carry <- row 4k+3.
+  // (channel 16 j + 4 q + e)
+  auto stem_rows = [&](int r0, auto mrows, float (*carry)[4], float (*vm)[4][4]) {
+    constexpr int M = decltype(mrows)::value;
+    f32x4 acc[M][4];
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-  for (int kh = 0; kh < 7; ++kh) {
-    uint4 bfr[4], af[5];
+    for (int kh = 0; kh < 7; ++kh) {
+      uint4 bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(wl + ((16 * j + r16) * kStemPitch + kh * 32 + 8 * q) * 2);
+      // input row 2 (r0 + rl) - 3 + kh, window column 2 sc + 2 q (= input col 2 sc - 3 + 2 q)
+      auto rd = [&](int rl) {
+        return *reinterpret_cast<const uint4*>(win + ((2 * (r0 + rl) - 3 + kh) & (RING - 1)) * RB +
+                                               (2 * sc + 2 * q) * 8);
+      };
+      if constexpr (NW <= 8) {
+        uint4 af[M];
+#pragma unroll
+        for (int rl = 0; rl < M; ++rl) af[rl] = rd(rl);
+#pragma unroll
+        for (int rl = 0; rl < M; ++rl)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O::mma(acc[rl][j], bfr[j], af[rl]);
+      } else {  // twelve waves: fewer registers in flight
+#pragma unroll
+        for (int rl = 0; rl < M; ++rl) {
+          const uint4 af = rd(rl);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) O::mma(acc[rl][j], bfr[j], af);
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      bfr[j] = *reinterpret_cast<const uint4*>(wl + ((16 * j + r16) * kStemPitch + kh * 32 + 8 * q) * 2);
-    // window row 2 rl + kh, window column 2 sc + 2 q (= input col 2 sc - 3 + 2 q)
 #pragma unroll
-    for (int rl = 0; rl < 5; ++rl)
-      af[rl] = *reinterpret_cast<const uint4*>(win + ((2 * rl + kh) * WP + 2 * sc + 2 * q) * 8);
+      for (int e = 0; e < 4; ++e) {
+        const int co = 16 * j + 4 * q + e;
+        const float s_ = scale[co], b_ = shift[co];
+        float v[M];
 #pragma unroll
-    for (int rl = 0; rl < 5; ++rl)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) O::mma(acc[rl][j], bfr[j], af[rl]);
-  }
+        for (int rl = 0; rl < M; ++rl)
+          v[rl] = (r0 + rl >= 0) ? O::round(fmaxf(acc[rl][j][e] * s_ + b_, 0.f)) : 0.f;
+        const float first = M == 5 ? v[0] : carry[j][e];
+        const float* u = v + (M == 5 ? 1 : 0);   // stem rows 4k .. 4k+3
+        vm[0][j][e] = fmaxf(fmaxf(first, u[0]), u[1]);
+        vm[1][j][e] = fmaxf(fmaxf(u[1], u[2]), u[3]);
+        carry[j][e] = u[3];
+      }
+  };
 
-  // ---- BN + ReLU (+ rounding to T), vertical max over local stem rows 2p .. 2p + 2
-  const bool row0_valid = p0 > 0;  // local stem row 0 = stem row 2 p0 - 1
-  float vm[2][4][4];               // [pool row][n-tile][ch]
+  T* __restrict__ yn = y + static_cast<size_t>(n) * Hp * Wp * 64;
+  // pool rows 2k, 2k+1 from their vertical maxima: horizontal max with lane shuffles (a wave's
+  // left neighbour column through LDS), 8-byte NHWC stores
+  auto pool = [&](int k, const float (*vm)[4][4]) {
+    if (r16 == 15) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+      for (int p = 0; p < 2; ++p)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int co = 16 * j + 4 * q + e;
-      const float s_ = scale[co], b_ = shift[co];
-      float v[5];
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int rl = 0; rl < 5; ++rl) v[rl] = O::round(fmaxf(acc[rl][j][e] * s_ + b_, 0.f));
-      if (!row0_valid) v[0] = 0.f;
-      vm[0][j][e] = fmaxf(fmaxf(v[0], v[1]), v[2]);
-      vm[1][j][e] = fmaxf(fmaxf(v[2], v[3]), v[4]);
+          for (int e = 0; e < 4; ++e) edge[(wid * 2 + p) * 64 + 16 * j + 4 * q + e] = vm[p][j][e];
     }
-  // the band's last column (r16 = 15) is the next wave's left neighbour
-  if (r16 == 15) {
+    __syncthreads();
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) {
+        float o[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) edge[(wid * 2 + p) * 64 + 16 * j + 4 * q + e] = vm[p][j][e];
-  }
-  __syncthreads();
+        for (int e = 0; e < 4; ++e) {
+          const float self = vm[p][j][e];
+          const float right = __shfl_down(self, 1, 16);  // column sc + 1 (r16 even < 15)
+          float left = __shfl_up(self, 1, 16);           // column sc - 1
+          if (r16 == 0) left = wid > 0 ? edge[((wid - 1) * 2 + p) * 64 + 16 * j + 4 * q + e] : 0.f;
+          o[e] = fmaxf(fmaxf(left, self), right);
+        }
+        if ((r16 & 1) == 0) {
+          const int pc = 8 * wid + (r16 >> 1);
+          T* dst = yn + (static_cast<size_t>(2 * k + p) * Wp + pc) * 64 + 16 * j + 4 * q;
+          *reinterpret_cast<uint2*>(dst) = make_uint2(O::pack2(o[0], o[1]), O::pack2(o[2], o[3]));
+        }
+      }
+  };
 
-  // ---- horizontal max: pool col pc <- stem cols 2 pc - 1, 2 pc, 2 pc + 1 (even lanes)
-  T* __restrict__ yn = y + static_cast<size_t>(n) * Hp * Wp * 64;
-#pragma unroll
-  for (int p = 0; p < 2; ++p)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      float o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float self = vm[p][j][e];
-        const float right = __shfl_down(self, 1, 16);  // column sc + 1 (r16 even < 15)
-        float left = __shfl_up(self, 1, 16);           // column sc - 1
-        if (r16 == 0) left = wid > 0 ? edge[((wid - 1) * 2 + p) * 64 + 16 * j + 4 * q + e] : 0.f;
-        o[e] = fmaxf(fmaxf(left, self), right);
-      }
-      if ((r16 & 1) == 0) {
-        const int pc = 8 * wid + (r16 >> 1);
-        T* dst = yn + (static_cast<size_t>(p0 + p) * Wp + pc) * 64 + 16 * j + 4 * q;
-        *reinterpret_cast<uint2*>(dst) = make_uint2(O::pack2(o[0], o[1]), O::pack2(o[2], o[3]));
-      }
-    }
+  // ---- the strip's first item: input rows 8 k0 - 5 .. 8 k0 + 9, stem rows 4 k0 - 1 .. 4 k0 + 3
+  using I4 = std::integral_constant<int, 4>;
+  using I5 = std::integral_constant<int, 5>;
+  using I8 = std::integral_constant<int, 8>;
+  float carry[4][4], vm[2][4][4];
+  float4 xv[XG8][3];
+  // (16 rows 8 k0 - 5 .. 8 k0 + 10: two 8-row loads through the prefetch registers; the last row
+  // is not read by this item and is rewritten before item k0 + 1 reads it)
+  load_rows(8 * k0 - 5, I8{}, xv);
+  store_rows(8 * k0 - 5, I8{}, xv);
+  load_rows(8 * k0 + 3, I8{}, xv);
+  store_rows(8 * k0 + 3, I8{}, xv);
+  __syncthreads();
+  // PF: the next item's new input rows are loaded into registers while this item computes, and
+  // stem row 4k-1 is carried (eight waves); twelve waves per block (W = 384) have no registers
+  // left for either: rows loaded in turn, every item computes its 5 stem rows
+  constexpr bool PF = NW <= 8;
+  stem_rows(4 * k0 - 1, I5{}, carry, vm);
+  if (PF && k0 + 1 < k1) load_rows(8 * k0 + 10, I8{}, xv);   // item k0 + 1's new rows, during item k0's pool
+  pool(k0, vm);
+  for (int k = k0 + 1; k < k1; ++k) {
+    if (!PF) load_rows(8 * k + 2, I8{}, xv);
+    // every wave is past item k-1's window reads (the pool barrier): its dead rows take item k's
+    __syncthreads();
+    store_rows(8 * k + 2, I8{}, xv);
+    __syncthreads();
+    if (PF && k + 1 < k1) load_rows(8 * k + 10, I8{}, xv);   // item k + 1's, during item k
+    if constexpr (PF) stem_rows(4 * k, I4{}, carry, vm);
+    else stem_rows(4 * k - 1, I5{}, carry, vm);
+    pool(k, vm);
+  }
 }
 
 }  // namespace
@@ -217,29 +287,53 @@ __global__ __launch_bounds__(NW * 64) void stem_pool_kernel(const float* __restr
 
 using namespace posu;
 
-extern "C" int posu_stem_pool_fwd(int dtype, const float* x, int N, int H, int W, int hflip, const void* w,
-                                  const float* scale, const float* shift, void* y, void* stream) {
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_stem_pool_fwd: dtype must be BF16 or F16");
-  POSU_REQUIRE(x && w && scale && shift && y, "posu_stem_pool_fwd: null pointer");
-  POSU_REQUIRE(N > 0 && H > 0 && H % 8 == 0 && (W == 256 || W == 384),
-               "posu_stem_pool_fwd: needs H % 8 == 0 and W in {256, 384}");
-  POSU_REQUIRE(static_cast<long long>(N) * 3 * H * W < (1LL << 40), "posu_stem_pool_fwd: input too large");
+namespace {
+int stem_launch(int dtype, const float* const* views, int nviews, int Nv, int H, int W, int hflip, const void* w,
+                const float* scale, const float* shift, void* y, void* stream, const char* what) {
+  const std::string wh(what);
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, wh + ": dtype must be BF16 or F16");
+  POSU_REQUIRE(views && nviews >= 1 && nviews <= kMaxViews, wh + ": 1 .. 8 views");
+  for (int v = 0; v < nviews; ++v) POSU_REQUIRE(views[v], wh + ": null view pointer");
+  POSU_REQUIRE(w && scale && shift && y, wh + ": null pointer");
+  POSU_REQUIRE(Nv > 0 && H > 0 && H % 8 == 0 && (W == 256 || W == 384),
+               wh + ": needs H % 8 == 0 and W in {256, 384}");
+  POSU_REQUIRE(static_cast<long long>(Nv) * 3 * H * W < (1LL << 40), wh + ": input too large");
+  StemViews xs{};
+  for (int v = 0; v < nviews; ++v) xs.x[v] = views[v];
+  const int N = Nv * nviews, pairs = H / 8;
+  // strips per image: about one block per CU (a strip of `pairs / strips` consecutive items)
+  int strips = 1;
+  while (N * strips * 2 <= 256 && pairs % (strips * 2) == 0) strips *= 2;
   hipStream_t s = as_stream(stream);
-  const int blocks = N * (H / 8);
+  const dim3 grid(static_cast<unsigned>(N * strips));
   if (dtype == POSU_BF16) {
     if (W == 256)
-      hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 8>), dim3(blocks), dim3(512), 0, s, x, N, H, W, hflip,
+      hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 8>), grid, dim3(512), 0, s, xs, Nv, N, H, W, hflip, strips,
                          static_cast<const uint16_t*>(w), scale, shift, static_cast<uint16_t*>(y));
     else
-      hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 12>), dim3(blocks), dim3(768), 0, s, x, N, H, W, hflip,
+      hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 12>), grid, dim3(768), 0, s, xs, Nv, N, H, W, hflip, strips,
                          static_cast<const uint16_t*>(w), scale, shift, static_cast<uint16_t*>(y));
   } else {
     if (W == 256)
-      hipLaunchKernelGGL((stem_pool_kernel<f16_t, 8>), dim3(blocks), dim3(512), 0, s, x, N, H, W, hflip,
+      hipLaunchKernelGGL((stem_pool_kernel<f16_t, 8>), grid, dim3(512), 0, s, xs, Nv, N, H, W, hflip, strips,
                          static_cast<const f16_t*>(w), scale, shift, static_cast<f16_t*>(y));
     else
-      hipLaunchKernelGGL((stem_pool_kernel<f16_t, 12>), dim3(blocks), dim3(768), 0, s, x, N, H, W, hflip,
+      hipLaunchKernelGGL((stem_pool_kernel<f16_t, 12>), grid, dim3(768), 0, s, xs, Nv, N, H, W, hflip, strips,
                          static_cast<const f16_t*>(w), scale, shift, static_cast<f16_t*>(y));
   }
-  return check_launch("posu_stem_pool_fwd");
+  return check_launch(what);
+}
+}  // namespace
+
+extern "C" int posu_stem_pool_fwd(int dtype, const float* x, int N, int H, int W, int hflip, const void* w,
+                                  const float* scale, const float* shift, void* y, void* stream) {
+  return stem_launch(dtype, &x, 1, N, H, W, hflip, w, scale, shift, y, stream, "posu_stem_pool_fwd");
+}
+
+// The same over the views of one forward in one launch: views[v] = [Nv, 3, H, W] f32 (host array
+// of device pointers), y = the views' pooled outputs stacked view-major [nviews * Nv, H/4, W/4, 64].
+extern "C" int posu_stem_pool_views_fwd(int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                                        int hflip, const void* w, const float* scale, const float* shift, void* y,
+                                        void* stream) {
+  return stem_launch(dtype, views, nviews, Nv, H, W, hflip, w, scale, shift, y, stream, "posu_stem_pool_views_fwd");
 }

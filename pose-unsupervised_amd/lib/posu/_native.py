@@ -41,6 +41,7 @@ _SIGNATURES = {
     'posu_conv1x1_dual_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_conv_bk': [_i],
     'posu_stem_pool_fwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p],
+    'posu_stem_pool_views_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
     'posu_bottleneck_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_bottleneck_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p],
     'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,

@@ -182,6 +182,24 @@ def head1x1_nchw(x, wpk, cout, bias, code, out=None):
     return out
 
 
+def stem_pool_views(views, wpk, scale, shift, code, out=None, hflip=False):
+    """stem_pool over the views of one forward in ONE launch (posu_stem_pool_views_fwd): a list of
+    NCHW f32 [Nv, 3, H, W] tensors (same shape) -> NHWC [V * Nv, H/4, W/4, 64], view-major."""
+    import ctypes
+    if not views or not all(v.is_cuda for v in views):
+        raise RuntimeError('stem_pool_views: HIP op needs GPU tensors')
+    n, c, h, w = views[0].shape
+    if c != 3 or any(tuple(v.shape) != (n, c, h, w) for v in views):
+        raise ValueError('stem_pool_views: views of one shape [N, 3, H, W] expected')
+    views = [v.contiguous().float() for v in views]
+    if out is None:
+        out = torch.empty((n * len(views), h // 4, w // 4, 64), dtype=torch_dtype(code), device=views[0].device)
+    arr = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
+    call('posu_stem_pool_views_fwd', code, ctypes.cast(arr, ctypes.c_void_p), len(views), n, h, w, int(bool(hflip)),
+         ptr(wpk), ptr(scale), ptr(shift), ptr(out), stream_of(views[0].device))
+    return out
+
+
 def stem_pool(x, wpk, scale, shift, code, out=None, hflip=False):
     """Fused input pack + 7x7/s2 stem + BN + ReLU + 3x3/s2 max-pool: NCHW f32 [N, 3, H, W]
     -> NHWC [N, H/4, W/4, 64] (compute dtype)."""

@@ -27,6 +27,9 @@ STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
 # fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
 FUSED_STEM = True
+# the fused stem over all views of a forward in one launch (posu_stem_pool_views_fwd); False: one
+# launch per view
+STEM_VIEWS = True
 
 
 class RawViews:
@@ -384,9 +387,12 @@ class PoseResNetPlan:
         return x
 
     def stem_pool(self, x):
-        """stem + max-pool: one fused launch per view for RawViews, else two launches."""
+        """stem + max-pool: one fused launch over the views for RawViews, else two launches."""
         code = self.code
         if isinstance(x, RawViews):
+            if STEM_VIEWS and len({tuple(v.shape) for v in x.views}) == 1 and len(x.views) <= 8:
+                return ops.stem_pool_views(x.views, self.stem_fused_w, self.stem.scale, self.stem.shift, code,
+                                           hflip=x.hflip)
             out = torch.empty((x.shape[0], x.h // 4, x.w // 4, self.stem.cout), dtype=ops.torch_dtype(code),
                               device=x.device)
             base = 0

@@ -114,23 +114,45 @@ def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precisio
 
 
 def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda):
-    """configs[4]'s per-GPU pipeline (R152 backbone at 384x384, fp16 compute, fp64
-    triangulation) on one 4-view group, through bench's replay path (hipGraph, fused stem;
-    layer1 stays unfused at 96x96 maps), against the fp32 CPU oracle chain."""
-    layers, size, groups = 152, 384, 1
+    """configs[4]'s per-GPU pipeline at its per-GPU shape: R152 backbone at 384x384, fp16 compute,
+    fp64 triangulation, 16 groups x 4 views, per-layer AUTOTUNED tiles, bench's replay path
+    (hipGraph, fused stem; layer1 unfused at 96x96 maps).
+      * oracle subset (CPU-feasible): groups 0-1 against the fp32 CPU oracle chain;
+      * full size, property checks: every output finite; the device triangulation of all 16
+        groups against the oracle's DLT on the same device joints (BASELINE's 1e-2 mm); the
+        device epipolar loss against the oracle FundamentalLoss of the device joints; batch
+        invariance -- groups 0-1 of the 16-group autotuned run equal, bit for bit, a 2-group run
+        with the heuristic tiles (every tile sums K in the same order)."""
+    layers, size, groups, sub = 152, 384, 16, 2
     from models.pose_resnet import get_pose_net
+    from oracle import geometry_ref as G
     torch.set_num_threads(16)
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
                                   bn_stats=syn.load_bn_stats(layers, size))
+    full = _bench_plan_outputs(cuda, 'fp16', True, layers=layers, size=size, groups=groups)
+    small = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=sub)
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
-    views = syn.group_views(4, range(groups), size, seed=100)
-    ref = bench.oracle_chain(sd, layers, size, views, host, full=True)
-    ref['host'] = host
-    out = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=groups)
-    c = bench.compare_with_reference(out, ref, out['meta'], cuda)
-    print('R152@384 fp16 pipeline vs oracle: %s' % c)
-    assert np.isfinite(out['X0']).all()
+    # full size: triangulation and loss consistency of every group
+    V, J = 4, full['coords0'].shape[2]
+    assert np.isfinite(full['X0']).all() and np.isfinite(full['coords0']).all() and torch.isfinite(full['hm0']).all()
+    p2d = full['coords0'].transpose(1, 0, 2, 3).reshape(groups * V, J, 2).astype(np.float64)
+    tri = np.linalg.norm(full['X0'] - G.triangulate_poses(host['cams'], p2d), axis=-1)
+    lref = G.fundamental_loss([torch.from_numpy(full['coords0'][v]) for v in range(V)], [torch.ones(groups, J, 1)] * V,
+                              host['subjects'], host['F_dict'])
+    print('R152@384 fp16, 16 groups: triangulation vs oracle DLT on the device joints max %.3g mm; epipolar loss '
+          'rel %.3g' % (tri.max(), abs(full['loss0'] / float(lref) - 1)))
+    assert tri.max() < 1e-2
+    assert abs(full['loss0'] / float(lref) - 1) < 1e-4
+    # batch invariance (autotuned 16-group plan vs heuristic-tile 2-group plan)
+    rows = [v * groups + g for v in range(V) for g in range(sub)]
+    assert torch.equal(full['hm0'][rows], small['hm0'])
+    # the oracle subset: groups 0-1 against the fp32 CPU oracle chain
+    _, hsub = synthetic_meta(sub, 'cpu', image_size=size)
+    ref = bench.oracle_chain(sd, layers, size, syn.group_views(4, range(sub), size, seed=100), hsub, full=True)
+    ref['host'] = hsub
+    c = bench.compare_with_reference(small, ref, small['meta'], cuda)
+    print('R152@384 fp16 pipeline (groups 0-1) vs oracle: %s' % c)
     assert c['heatmap_abs_err']['mean'] < 0.05 and c['heatmap_abs_err']['max'] < 0.5
     assert c['triangulation_same_2d_mm']['max'] < 1e-2      # the DLT itself: BASELINE's 1e-2 mm
     assert c['epipolar_loss_rel_err'] < 0.1

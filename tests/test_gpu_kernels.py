@@ -511,3 +511,37 @@ def test_fused_stem_pool_matches_two_launch_path(cuda, size, code, hflip):
     ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * ref.float().abs()
     assert bool((d <= 2 * ulp + 1e-3).all()), float(d.max())
     assert float((d > 0).float().mean()) < 0.05
+
+
+@pytest.mark.parametrize('size,nv', [(256, 32), (384, 16)])
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('hflip', [False, True])
+def test_stem_pool_views_one_launch(cuda, size, nv, code, hflip):
+    """posu_stem_pool_views_fwd at the bench shapes (4 views x 32 frames at 256, x 16 at 384: strips
+    of 16 / 24 consecutive pool-row pairs per block, the rolling input ring and the carried stem
+    row): against the two-launch path per view (one rounding step at most), and bit-identical to
+    one posu_stem_pool_fwd launch per view (every stem value is the same MFMA sequence)."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(23)
+    views = [torch.randn(nv, 3, size, size, device=cuda, generator=g) for _ in range(4)]
+    wt = torch.randn(64, 3, 7, 7, device=cuda, generator=g) * (2.0 / 147) ** 0.5
+    sc = torch.rand(64, device=cuda, generator=g) + 0.5
+    sh = torch.randn(64, device=cuda, generator=g) * 0.1
+    wpk = packing.pack_stem_fused_weight(wt, dt)
+    out = torch.empty(4 * nv, size // 4, size // 4, 64, device=cuda, dtype=dt)
+    out.view(torch.int16).fill_(0x7fc1 if code == BF16 else 0x7e01)   # NaN sentinel: every pixel written
+    got = ops.stem_pool_views(views, wpk, sc, sh, code, out=out, hflip=hflip)
+    per_view = torch.cat([ops.stem_pool(v, wpk, sc, sh, code, hflip=hflip) for v in views])
+    ws = packing.pack_stem_s2d_weight(wt, 16, ops.conv_bk(code), dt)
+    refs = []
+    for v in views:
+        stem = ops.conv2d_nhwc(ops.pack_s2d_nchw(v, code, 16, hflip=hflip), ws, 64, 4, 4, 1, 2, sc, sh, None, True,
+                               code, out_hw=(size // 2, size // 2))
+        refs.append(ops.maxpool3x3s2_nhwc(stem, code))
+    ref = torch.cat(refs)
+    torch.cuda.synchronize()
+    assert torch.equal(got, per_view)
+    d = (got.float() - ref.float()).abs()
+    ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * ref.float().abs()
+    assert bool((d <= 2 * ulp + 1e-3).all()), float(d.max())
+    assert float((d > 0).float().mean()) < 0.05

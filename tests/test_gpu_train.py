@@ -174,3 +174,69 @@ def test_adam_trajectory_matches_reference(cuda, golden, precision):
     assert rel.max() < b['loss'], rel
     assert np.median(nrel, axis=1).max() < b['norm_median']
     assert nrel.max() < b['norm_max']
+
+
+def _inputs_r50_256(groups=2, seed=3):
+    """A configs[3]-shaped training batch (R50@256, 4 views x `groups`): Gaussian targets (sigma 2) at
+    seeded positions, target weights with a few zeros, the synthetic crops' centers / scales /
+    subjects -- in the layout of the reference train-step golden, for _step and the oracle."""
+    from posu.pipeline import synthetic_meta
+    _, host = synthetic_meta(groups, 'cpu', image_size=256)
+    r = np.random.default_rng(seed)
+    c = r.uniform(4, 60, size=(4, groups, 16, 2))
+    ys, xs = np.meshgrid(np.arange(64), np.arange(64), indexing='ij')
+    tgt = np.exp(-((xs - c[..., 0, None, None]) ** 2 + (ys - c[..., 1, None, None]) ** 2) / 8.0).astype(np.float32)
+    tw = (r.uniform(size=(4, groups, 16, 1)) > 0.1).astype(np.float32)
+    return {'num_layers': 50, 'image_size': 256, 'nviews': 4, 'batch': groups, 'seed': seed, 'fund_weight': 10.0,
+            'targets': tgt, 'target_weight': tw, 'centers': host['centers'], 'scales': host['scales'],
+            'subjects': host['subjects']}
+
+
+# measured-deviation bands of the bf16 step (fp32: the reference golden's gates)
+TRAIN_256_BANDS = {'fp32': {'hm': 1e-3, 'loss': 1e-4, 'norm_rel_max': 2e-3},
+                   'bf16': {'hm': 0.1, 'loss': 2e-2, 'norm_rel_median': 3e-2}}
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_train_step_r50_256_matches_oracle_autograd(cuda, precision):
+    """configs[3]'s training step at its image size: R50@256, 4 views x 2 groups, per-view batch
+    statistics, JointsMSE + 10 x FundamentalLoss, through the staged training plan with the
+    training conv tiles AUTOTUNED as bench.py tunes them (a throwaway first step), against the
+    oracle's train-mode forward + losses + autograd on CPU (tests/test_oracle_golden.py pins that
+    oracle to the reference's own training step): heatmaps, both losses, every parameter
+    gradient's norm, the running statistics."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_oracle_golden import train_step_oracle
+    from posu import plan as pplan
+    torch.set_num_threads(16)
+    g = _inputs_r50_256()
+    pplan._Tuner.active, pplan._Tuner.reps = True, 2
+    try:
+        _step(cuda, g, precision)   # tunes the raw training convolutions at these geometries
+    finally:
+        pplan._Tuner.active = False
+    net, hm, joints, mse, fund = _step(cuda, g, precision)
+    params, bufs, hm_r, joints_r, mse_r, fund_r = train_step_oracle(g)
+    named = dict(net.named_parameters())
+    names = list(named)
+    norms = np.array([named[n].grad.norm().item() for n in names])
+    norms_r = np.array([params[n].grad.norm().item() for n in names])
+    rel = np.abs(norms / norms_r - 1)
+    hm_err = float((torch.stack(hm).detach().cpu() - hm_r.detach()).abs().max())
+    b = TRAIN_256_BANDS[precision]
+    print('%s R50@256 4x2 train step vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs %.6g, grad-norm '
+          'rel median %.3g max %.3g (%s)' % (precision, hm_err, mse.item(), mse_r.item(), fund.item(), fund_r.item(),
+                                             np.median(rel), rel.max(), names[int(rel.argmax())]))
+    assert hm_err < b['hm']
+    np.testing.assert_allclose(mse.item(), mse_r.item(), rtol=b['loss'])
+    np.testing.assert_allclose(fund.item(), fund_r.item(), rtol=b['loss'] * 10)
+    if 'norm_rel_max' in b:
+        assert rel.max() < b['norm_rel_max'], names[int(rel.argmax())]
+    else:
+        assert np.median(rel) < b['norm_rel_median']
+    sd = net.state_dict()
+    for k, v in bufs.items():
+        np.testing.assert_allclose(sd[k].cpu().numpy(), v.numpy(), atol=1e-4 if precision == 'fp32' else 2e-2,
+                                   rtol=1e-4 if precision == 'fp32' else 2e-2, err_msg=k)

@@ -157,3 +157,49 @@ def test_ransac_oracle_known_answers():
     proj, rv = G.reproject_poses(p2d, cams, vis, no_distortion=True)
     np.testing.assert_allclose(proj[0], p2d[0], atol=1e-6)
     assert rv[2 * 4:2 * 4 + 4, 7].sum() == 0
+
+
+def train_step_oracle(g, num_layers=None, size=None):
+    """The reference's training step (core/function.py:154-366, train mode, per-view BatchNorm)
+    restated on the oracle: -> (params, buffers, heatmaps [V, B, J, h, w], joints [V, B, J, 2],
+    mse, fund); the loss is back-propagated into params[k].grad."""
+    nl = int(g['num_layers']) if num_layers is None else num_layers
+    size = int(g['image_size']) if size is None else size
+    nv, b, seed = int(g['nviews']), int(g['batch']), int(g['seed'])
+    sd = syn.synthetic_state_dict(_reference_shaped_state(nl, size), seed=seed)
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()
+              if not ('running_' in k or 'num_batches' in k)}
+    bufs = {k: v.clone() for k, v in sd.items() if 'running_' in k}
+    views = syn.synthetic_views(nv, b, size, seed=seed + 1)
+    hms, joints, mse = [], [], 0
+    for v in range(nv):
+        hm, _, _ = PR.pose_resnet_train_forward(views[v], params, bufs, nl)
+        hms.append(hm)
+        mse = mse + G.joints_mse(hm, torch.from_numpy(g['targets'][v]), torch.from_numpy(g['target_weight'][v]))
+        sa = G.softargmax2d(hm)
+        joints.append(G.transform_back(sa, g['centers'][v], g['scales'][v], [size // 4] * 2))
+    fund = G.fundamental_loss(joints, [torch.from_numpy(w) for w in g['target_weight']], g['subjects'],
+                              syn.fundamental_dict()) * float(g['fund_weight'])
+    (mse + fund).backward()
+    return params, bufs, torch.stack(hms), torch.stack(joints), mse, fund
+
+
+def test_oracle_train_step_matches_reference(golden):
+    """The oracle's train-mode forward (pose_resnet_train_forward) + losses + autograd against the
+    reference's own training step (tests/golden/train_step_r50_128.npz): heatmaps, joints, losses,
+    every parameter gradient's norm, the full gradients held in the golden, running statistics."""
+    torch.set_num_threads(8)
+    g = golden('train_step_r50_128.npz')
+    params, bufs, hm, joints, mse, fund = train_step_oracle(g)
+    np.testing.assert_allclose(hm.detach().numpy(), g['heatmaps'], atol=1e-5, rtol=0)
+    np.testing.assert_allclose(joints.detach().numpy(), g['joints'], atol=1e-3, rtol=0)
+    np.testing.assert_allclose(mse.item(), g['loss_mse'], rtol=1e-5)
+    np.testing.assert_allclose(fund.item(), g['loss_fund'], rtol=1e-5)
+    norms = np.array([params[n].grad.norm().item() for n in g['grad_names']])
+    np.testing.assert_allclose(norms, g['grad_norms'], rtol=1e-4)
+    for k in g:
+        if k.startswith('grad__'):
+            np.testing.assert_allclose(params[k[6:]].grad.numpy(), g[k], atol=1e-4 * np.abs(g[k]).max(), rtol=1e-3,
+                                       err_msg=k)
+        if k.startswith('buf__') and 'num_batches' not in k:   # F.batch_norm keeps no counter
+            np.testing.assert_allclose(bufs[k[5:]].numpy(), g[k], atol=1e-6, rtol=1e-5, err_msg=k)
