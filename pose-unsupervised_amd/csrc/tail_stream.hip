@@ -75,12 +75,13 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
 struct TailCfg {
   static constexpr int kRows = ROWS;               // image rows per workgroup
   static constexpr int kNW = NW;                   // waves per workgroup
+  static constexpr int kMT = MT;                   // m-tiles (16 px) per wave
   static constexpr int kPx = kRows * W;            // tile pixels
-  static constexpr int kNPG = kPx / 128;           // pixel groups of 128 px
+  static constexpr int kNPG = kPx / (16 * MT);     // pixel groups of 16 MT px
   static constexpr int kNCQ = NW / kNPG;           // channel groups of 32
   static constexpr int kRowB = P * 2;              // LDS bytes per pixel (bf16 / fp16)
   static constexpr int kWinCols = W + 2;
@@ -97,10 +98,11 @@ struct TailCfg {
   static constexpr int kLdsAll = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
   // weight prefetch depth (k-steps); NEXT keeps a second accumulator set live, so its stream
   // runs POSU_TS_KD_NEXT deep
-  static constexpr int kDW = !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : W == 32 ? 1 : 2;
-  static constexpr int kNB = !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : W == 32 ? 1 : 2;
+  static constexpr int kDW = !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : (W == 32 && MT == 8) ? 1 : 2;
+  static constexpr int kNB = !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : (W == 32 && MT == 8) ? 1 : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
-  static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % 128 == 0, "every wave: 128 px x 32 channels");
+  static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % (16 * MT) == 0 && (16 * MT) % W == 0,
+                "every wave: 16 MT px (whole image rows) x 32 channels");
   static_assert(kS3 + 2 * C * 4 <= kBN2, "t2 and BN3 fit over the window");
   static_assert(kLdsAll <= 160 * 1024, "LDS");
   static_assert(!NEXT || kChunk == P, "the next conv1 takes one y chunk per K slice of P channels");
@@ -114,10 +116,10 @@ struct TailCfg {
 template <int RowB>
 __device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
 
-template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false>
-__global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom g) {
+template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
+__global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
-  using K = TailCfg<W, P, C, ROWS, NW, NEXT>;
+  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
   __shared__ __attribute__((aligned(16))) char smem[K::kLdsAll];
@@ -174,16 +176,16 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   vm_wait<0>();  // the window (LDS-DMA) and the first fragments
   lds_barrier();
 
-  f32x4 acc[8][2];   // [m-tile i: tile pixels 128 pg + 16 i ..][n-tile j]
-  f32x4 acc1[8][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
-  auto zero = [&](f32x4 (&a)[8][2]) {
+  f32x4 acc[MT][2];   // [m-tile i: tile pixels 16 MT pg + 16 i ..][n-tile j]
+  f32x4 acc1[MT][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
+  auto zero = [&](f32x4 (&a)[MT][2]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) a[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   // the pair of n-tiles -> this lane's 8 consecutive channels cpair .. cpair + 7 of pixel r16
-  auto pair = [&](const f32x4 (&a)[8][2], int i, float* v) {
+  auto pair = [&](const f32x4 (&a)[MT][2], int i, float* v) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i][0][e]), __float_as_uint(a[i][1][e]),
@@ -194,15 +196,15 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   };
   const int cpair = 16 * (q & 1) + 8 * (q >> 1);
   // m-tile i's tile pixel (row-major in the tile) for this lane
-  auto tpix = [&](int i) { return 128 * pg + 16 * i + r16; };
+  auto tpix = [&](int i) { return 16 * MT * pg + 16 * i + r16; };
   // one block of kKT k-steps (one conv2 tap, or one conv3 output chunk over t2's P channels):
   // k-step d reads, for m-tile i, the pixel lpix + coff(i) (coff compile-time) of an LDS image
   // with `cols` pixels per row at 16-B chunk 4 d + q, swizzled by the lane's key (column & 15).
   // The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run (two register
   // sets); the scheduling barriers keep the compiler from hoisting more of them.
-  auto block = [&](f32x4 (&acc)[8][2], int blk, int base, int lpix, int key, auto coff) {
+  auto block = [&](f32x4 (&acc)[MT][2], int blk, int base, int lpix, int key, auto coff) {
     constexpr int NB = K::kNB;  // pixel-fragment register sets
-    uint4 b[NB][8];
+    uint4 b[NB][MT];
     // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3))
     const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
     const char* kb[4];
@@ -213,16 +215,16 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
       return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d & 4) * 64);
     };
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[0][i] = rd(i, 0);
+    for (int i = 0; i < MT; ++i) b[0][i] = rd(i, 0);
 #pragma unroll
     for (int d = 0; d < K::kKT; ++d) {
       if (NB == 2 && d + 1 < K::kKT) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) b[(d + 1) % NB][i] = rd(i, d + 1);
+        for (int i = 0; i < MT; ++i) b[(d + 1) % NB][i] = rd(i, d + 1);
       }
       const int s = d % kD;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < MT; ++i) {
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d % NB][i].y);
@@ -245,17 +247,17 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
     const int dy = t / 3, dx = t - 3 * (t / 3);
-    // window pixel of m-tile i: tile row (128 pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
-    block(acc, t, 0, ((128 / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
+    // window pixel of m-tile i: tile row (16 MT pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
+    block(acc, t, 0, ((16 * MT / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
           [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
   }
   const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
   T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C;
   // conv3 chunk nc's residual in the epilogue's lane layout
-  auto res_load = [&](int nc, uint4 (&rv)[8]) {
+  auto res_load = [&](int nc, uint4 (&rv)[MT]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < MT; ++i)
       rv[i] = (kAbl & 72) ? make_uint4(i, c0, 0, 0) : *reinterpret_cast<const uint4*>(xg + tpix(i) * C + c0);
   };
   // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
     ld8(bn2 + c0, sc);
     ld8(bn2 + P + c0, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc, i, v);
 #pragma unroll
@@ -283,10 +285,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
 
   // ---- conv3: output chunk nc (kChunk channels; this wave's 32), kKT channel steps over t2
   const float* b3l = reinterpret_cast<const float*>(smem + K::kS3);
-  auto chunk = [&](int nc, uint4 (&rv)[8]) {
+  auto chunk = [&](int nc, uint4 (&rv)[MT]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
     zero(acc);
-    block(acc, 9 + K::kBlk3 * nc, 0, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
+    block(acc, 9 + K::kBlk3 * nc, 0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers)
     if constexpr (NEXT) res_load(nc, rv);
     float sc[8], sh[8];
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
       if (nc > 0) lds_barrier();  // every wave is done reading the previous y chunk
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < MT; ++i) {
       float v[8], r[8];
       pair(acc, i, v);
       O::load_vals(rv[i], r);
@@ -313,7 +315,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
       // the next block's conv1 over this K slice (y channels kChunk nc ..): same k order as a
       // conv launch over y, so t1n is bit-identical to it
       lds_barrier();
-      block(acc1, 9 + K::kBlk3 * nc + 1, K::kYC, 128 * pg + r16, r16, [&](int i) { return 16 * i; });
+      block(acc1, 9 + K::kBlk3 * nc + 1, K::kYC, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     }
   };
   // unrolled: hipcc's wait counts at a loop head merge both paths and made every chunk's first
@@ -323,7 +325,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   for (int nc = 0; nc < K::kNC; ++nc) {
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
     // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
-    uint4 rv[8];
+    uint4 rv[MT];
     if constexpr (!NEXT) res_load(nc, rv);
     chunk(nc, rv);
   }
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
     ld8(g.s1n + c0, sc);
     ld8(g.b1n + c0, sh);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc1, i, v);
 #pragma unroll
@@ -345,13 +347,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void tail_stream_kernel(TailSGeom 
   }
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
 void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(g.N * (g.H / ROWS)));
   if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT, MT>), grid, dim3(NW * 64), 0, s, g);
   else
-    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // tiles: layer3 8 rows x 16 px with 8 waves (one workgroup per CU, 256 at batch 128); layer2
@@ -360,7 +362,13 @@ void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
 #ifndef POSU_TS_L2_ROWS
 #define POSU_TS_L2_ROWS 4
 #endif
-constexpr int kL2Rows = POSU_TS_L2_ROWS, kL2Waves = POSU_TS_L2_ROWS;
+// layer2 m-tiles per wave: 8 (4-row tiles of 128 px, 4 waves) or 4 (2-row tiles of 64 px, 4 waves,
+// up to three workgroups per CU)
+#ifndef POSU_TS_L2_MT
+#define POSU_TS_L2_MT 8
+#endif
+constexpr int kL2MT = POSU_TS_L2_MT;
+constexpr int kL2Rows = POSU_TS_L2_ROWS * kL2MT / 8, kL2Waves = POSU_TS_L2_ROWS;
 
 }  // namespace
 }  // namespace posu
@@ -418,8 +426,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     if (next) launch_tail<16, 256, 1024, 8, 8, true>(dtype, g, s);
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
   } else {
-    if (next) launch_tail<32, 128, 512, kL2Rows, kL2Waves, true>(dtype, g, s);
-    else launch_tail<32, 128, 512, kL2Rows, kL2Waves>(dtype, g, s);
+    if (next) launch_tail<32, 128, 512, kL2Rows, kL2Waves, true, kL2MT>(dtype, g, s);
+    else launch_tail<32, 128, 512, kL2Rows, kL2Waves, false, kL2MT>(dtype, g, s);
   }
   return check_launch(name);
 }

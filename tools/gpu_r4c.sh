@@ -16,4 +16,18 @@ for f in "S2_TAIL=1 --plan-flag STEM_VIEWS=1" "S2_TAIL=0 --plan-flag STEM_VIEWS=
   timeout -k 10 200 python -u bench.py $C --plan-flag $f > $O/ab.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
   python -c "import json;d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1]);print('$f',d['value'],d['network_ms'])"
 done
+# layer2 tails with 2-row tiles (4 m-tiles per wave, three workgroups per CU) vs the default
+if [ -f pose-unsupervised_amd/build/ab/libposeu_l2mt4.so ]; then
+  timeout -k 10 120 python -u tools/chain_micro.py --only layer2 > $O/chain_default.txt 2>&1 || { cat $O/chain_default.txt; exit 1; }
+  timeout -k 10 120 python -u tools/chain_micro.py --only layer2 --lib pose-unsupervised_amd/build/ab/libposeu_l2mt4.so > $O/chain_l2mt4.txt 2>&1 || { cat $O/chain_l2mt4.txt; exit 1; }
+  cat $O/chain_default.txt $O/chain_l2mt4.txt
+  for lib in default l2mt4 default l2mt4; do
+    if [ $lib = default ]; then
+      timeout -k 10 200 python -u bench.py $C > $O/ab.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
+    else
+      timeout -k 10 200 python -u tools/with_lib.py pose-unsupervised_amd/build/ab/libposeu_$lib.so bench.py $C > $O/ab.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
+    fi
+    python -c "import json;d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1]);print('lib $lib',d['value'],d['network_ms'])"
+  done
+fi
 bash tools/gpu_r4a.sh

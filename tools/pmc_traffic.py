@@ -1,7 +1,9 @@
 """HBM traffic of one network forward from rocprofv3 PMC passes.
 
-    rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D1 -o run --output-format csv -- python3 bench.py --no-graph ...
-    rocprofv3 --pmc WRITE_SIZE --kernel-trace -d D2 -o run --output-format csv -- python3 bench.py --no-graph ...
+    rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D1 -o run --output-format csv -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --kernel-trace -d D2 -o run --output-format csv -- python3 bench.py ...
+(the benched hipGraph replays themselves since round 4; the round-3 reductions came from eager
+--no-graph runs whose launch list differed from the graph's)
     python tools/pmc_traffic.py D1/run_counter_collection.csv D2/run_counter_collection.csv [launches_per_forward]
 
 Per MI355X_MICROARCH.md (HBM section): FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
@@ -17,7 +19,8 @@ import json
 import os
 import sys
 
-NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'tail_stream_kernel', 'stem_pool_kernel',
+NET_KERNELS = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'tail_stream_kernel', 'tail_s2_kernel',
+               'stem_pool_kernel',
                'maxpool_kernel',
                'pack_s2d_kernel', 'pack_kernel')
 

@@ -2,8 +2,10 @@
 
     python tools/replay_breakdown.py gpurun_out/prof/run_kernel_trace.csv [--last 5]
 
-A replay = the dispatches from one stem_pool_kernel up to (not including) the next
-soft-argmax kernel.  Prints, for the chosen replays, each launch's median duration (us)
+A replay = the dispatches from the first of a run of stem_pool_kernel launches (one per view in
+the round-3 plan, one for all views since round 4) up to (not including) the next soft-argmax
+kernel.  (The round-3 version restarted a replay at EVERY stem launch, so its breakdowns counted
+one of the four per-view stem launches of that plan.)  Prints, for the chosen replays, each launch's median duration (us)
 with its kernel name, and the replay's launch-time sum and wall span (first start to last
 end: the sum plus the gaps between launches)."""
 import argparse
@@ -31,7 +33,10 @@ def main():
     replays, cur = [], None
     for s, e, n in rows:
         if 'stem_pool_kernel' in n:
-            cur = [(s, e, n)]
+            if cur is not None and len(cur) and all('stem_pool_kernel' in c[2] for c in cur) and s - cur[-1][1] <= 20000:
+                cur.append((s, e, n))   # the next view's stem launch of the same replay
+            else:
+                cur = [(s, e, n)]
         elif cur is not None:
             if s - cur[-1][1] > 20000:   # a graph replay runs back to back: a gap ends it (incomplete)
                 cur = None

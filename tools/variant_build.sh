@@ -7,9 +7,9 @@ set -euo pipefail
 cd "$(dirname "$0")/../pose-unsupervised_amd"
 name=$1; src=$2; shift 2
 make -s
-mkdir -p build/abl
+mkdir -p build/${POSU_AB_DIR:-abl}
 base=$(basename "$src" .hip)
 OTHERS=$(ls build/*.o | grep -v "/$base.o\$")
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c csrc/$base.hip -o build/abl/${base}_$name.o
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared $OTHERS build/abl/${base}_$name.o -o build/abl/libposeu_$name.so
-echo built build/abl/libposeu_$name.so
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c csrc/$base.hip -o build/${POSU_AB_DIR:-abl}/${base}_$name.o
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -shared $OTHERS build/${POSU_AB_DIR:-abl}/${base}_$name.o -o build/${POSU_AB_DIR:-abl}/libposeu_$name.so
+echo built build/${POSU_AB_DIR:-abl}/libposeu_$name.so
