@@ -123,7 +123,8 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *         5: 256x256, 6: 256x128 (eight waves);
  *     variant 1: single-slot LDS ring (cfg 0-4), 2: three-slot ring (cfg != 5);
  *     + 32 (bf16 / f16): the persistent K-tile stream;
- *     23 / 31 (bf16 / f16): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile.
+ *     23 / 31 (bf16 / f16): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile;
+ *     7 / 15 (bf16 / f16, ABI 11): 128x128 with eight staggered waves (2x4 / 4x2 wave grids).
  *   The tile only changes speed (every configuration computes the same sums in the same
  *   K order); the Python plan picks it per layer by timing every admissible
  *   configuration once (PoseResNetPlan.autotune).  The library keeps no mutable state:

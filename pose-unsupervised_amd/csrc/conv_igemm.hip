@@ -1281,9 +1281,12 @@ void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
 //   +32 (2-byte dtypes): the persistent K-tile stream (conv_persist_kernel);
 //   23 / 31 (2-byte dtypes): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile
 //   (also what the heuristic runs for those shapes);
+//   7 / 15 (2-byte dtypes, round 4): 128x128 with eight waves, staggered, as 2x4 waves of
+//   64x32 / 4x2 waves of 32x64 (M = 8192-pixel layers: 256 tiles of 128x128 give every CU one
+//   block, and eight waves two per SIMD);
 //   -1: the built-in heuristic.
 bool tile_ok(int tile) {
-  if (tile == -1 || tile == 23 || tile == 31) return true;
+  if (tile == -1 || tile == 23 || tile == 31 || tile == 7 || tile == 15) return true;
   if (tile < 0 || tile >= 64) return false;
   const int c = tile & 7, v = (tile >> 3) & 3;
   return c <= 6 && v <= 2 && !(v == 1 && c > 4) && !(v == 2 && c == 5);
@@ -1324,11 +1327,18 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   }
   int st = 2;
   bool sg = false, persist = false;
+  bool wg4 = false;  // tile 15: the 4 x 2 wave grid of the 128x128 eight-wave tile
   if (tile == 23 || tile == 31) {
     const int c = tile == 23 ? 5 : 6;
     if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
       cfg = c;
       sg = true;
+    }
+  } else if (tile == 7 || tile == 15) {
+    if (sizeof(T) == 2 && g.CoutPad % 128 == 0) {
+      cfg = 7;
+      sg = true;
+      wg4 = tile == 15;
     }
   } else if (tile >= 0) {
     const int c = tile & 7, v = (tile >> 3) & 3;
@@ -1344,8 +1354,8 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   } else if (sizeof(T) == 2 && (cfg == 5 || cfg == 6)) {
     sg = true;  // untuned eight-wave launches take the staggered loop (bit-exact with the plain one)
   }
-  static const int kBM[] = {256, 128, 64, 128, 64, 256, 256};
-  static const int kBN[] = {64, 64, 64, 128, 128, 256, 128};
+  static const int kBM[] = {256, 128, 64, 128, 64, 256, 256, 128};
+  static const int kBN[] = {64, 64, 64, 128, 128, 256, 128, 128};
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
@@ -1365,6 +1375,10 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     if (sg) {
       if (cfg == 5)
         hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
+      else if (cfg == 7 && wg4)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
+      else if (cfg == 7)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       else
         hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
@@ -1440,7 +1454,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
                                int KH, int KW, int stride, int pad, const float* scale, const float* shift,
                                const void* residual, int relu, void* y, int Ho, int Wo, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd")) return st;
-  POSU_REQUIRE(tile_ok(tile), "posu_conv2d_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
+  POSU_REQUIRE(tile_ok(tile), "posu_conv2d_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 7, 15, 23 or 31");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_conv2d_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
@@ -1473,7 +1487,7 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
                                      int W2, int C2, int stride2, const void* w, int Cout, const float* scale,
                                      const float* shift, int relu, void* y, int tile, void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv1x1_dual_fwd")) return st;
-  POSU_REQUIRE(tile_ok(tile), "posu_conv1x1_dual_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
+  POSU_REQUIRE(tile_ok(tile), "posu_conv1x1_dual_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 7, 15, 23 or 31");
   if (int st = common_checks(dtype, x2, w, y, N, H2, W2, C2, Cout, "posu_conv1x1_dual_fwd")) return st;
   const int BK = bk_of(dtype);
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
@@ -1506,7 +1520,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
                                     int Cout, const float* scale, const float* shift, int relu, void* y, int tile,
                                     void* stream) {
   if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_deconv4x4s2_fwd")) return st;
-  POSU_REQUIRE(tile_ok(tile), "posu_deconv4x4s2_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 23 or 31");
+  POSU_REQUIRE(tile_ok(tile), "posu_deconv4x4s2_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 7, 15, 23 or 31");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
   POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),

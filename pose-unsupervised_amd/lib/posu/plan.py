@@ -73,7 +73,8 @@ def _tile_candidates(cout):
     """Tile ids (include/posu.h): cfg 0..6, cfg + 8 = single-slot ring (four-wave tiles;
     short-K layers: more blocks per CU), cfg + 16 = three-slot ring (two K-tiles in flight),
     cfg + 32 = persistent K-tile stream (epilogue stores overlap the next tile's fetch),
-    23 / 31 = 256x256 / 256x128 with waves 4-7 staggered by half a K-tile."""
+    23 / 31 = 256x256 / 256x128 with waves 4-7 staggered by half a K-tile, 7 / 15 = 128x128 with
+    eight staggered waves."""
     cpad = (cout + 63) // 64 * 64
     c = [0, 1, 2]
     if cpad % 128 == 0:
@@ -81,8 +82,9 @@ def _tile_candidates(cout):
     if cpad % 256 == 0:
         c.append(5)
     # + 32: the persistent K-tile stream (2-byte dtypes; others ignore the bit);
-    # 23 / 31: the eight-wave tiles with waves 4-7 staggered by half a K-tile
-    sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)]
+    # 23 / 31: the eight-wave tiles with waves 4-7 staggered by half a K-tile; 7 / 15: 128x128 with
+    # eight staggered waves (2x4 / 4x2 wave grids)
+    sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 else [])
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c] + sg
 
 

@@ -397,7 +397,7 @@ def test_staggered_tiles_bit_exact_vs_two_slot(cuda, code):
     wdc = (rnd(4, 256, 4 * 128).float() * 0.03).to(dt)
     assert (9 * 128) % bk == 0
     outs = {}
-    for t in (5, 23, 6, 31):
+    for t in (5, 23, 6, 31, 3, 7, 15):
         outs[t] = [
             ops.conv2d_nhwc(x, w3, 256, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
             ops.conv2d_nhwc(x, w3[:, :128].contiguous(), 256, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
@@ -405,7 +405,7 @@ def test_staggered_tiles_bit_exact_vs_two_slot(cuda, code):
             ops.conv1x1_dual_nhwc(x, x2, 2, wd, 256, sh, True, code, tile=t),
         ]
     torch.cuda.synchronize()
-    for t, base in ((23, 5), (31, 6)):
+    for t, base in ((23, 5), (31, 6), (7, 3), (15, 3)):   # 7 / 15: 128x128 eight-wave staggered (round 4)
         for a, b in zip(outs[base], outs[t]):
             assert torch.equal(a, b), (t, float((a.float() - b.float()).abs().max()))
 
