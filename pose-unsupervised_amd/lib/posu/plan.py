@@ -59,6 +59,9 @@ class RawViews:
             base += v.shape[0]
         return RawViews(self.plan, out, self.hflip)
 
+# the 128x128 eight-wave staggered conv tiles (7 / 15, round 4) among the autotuner's candidates
+TILES_128X8 = True
+
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
 _TUNE_CACHE = {}
@@ -84,16 +87,19 @@ def _tile_candidates(cout):
     # + 32: the persistent K-tile stream (2-byte dtypes; others ignore the bit);
     # 23 / 31: the eight-wave tiles with waves 4-7 staggered by half a K-tile; 7 / 15: 128x128 with
     # eight staggered waves (2x4 / 4x2 wave grids)
-    sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 else [])
+    sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 and TILES_128X8 else [])
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c] + sg
 
 
 def _tuned(key, cout, launch):
     """launch(tile) -> output.  While tuning, time every admissible tile once on the real
     operands (HIP events) and keep the fastest for this geometry."""
-    if _Tuner.active and key not in _TUNE_CACHE:
+    cands = _tile_candidates(cout)
+    # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan
+    # switch such as TILES_128X8 turned off for a control run)
+    if _Tuner.active and (key not in _TUNE_CACHE or _TUNE_CACHE[key] not in cands):
         best = None
-        for t in _tile_candidates(cout):
+        for t in cands:
             launch(t)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
@@ -105,7 +111,8 @@ def _tuned(key, cout, launch):
             if best is None or ms < best[0]:
                 best = (ms, t)
         _TUNE_CACHE[key] = best[1]
-    return launch(_TUNE_CACHE.get(key, -1))
+    t = _TUNE_CACHE.get(key, -1)
+    return launch(t if t in cands else -1)
 
 
 def tuned_tiles():

@@ -12,7 +12,7 @@ tail -2 $O/bneck_tests.log
 timeout -k 10 120 python -u tools/s2tail_micro.py > $O/s2tail_micro.txt 2>&1 || { cat $O/s2tail_micro.txt; exit 1; }
 cat $O/s2tail_micro.txt
 C="--no-cpu-baseline --no-mpjpe --fp32-steps 0 --train-steps 0 --c1-steps 0 --peaked-steps 0 --c4-steps 0 --control-steps 0"
-for f in "S2_TAIL=1 --plan-flag STEM_VIEWS=1" "S2_TAIL=0 --plan-flag STEM_VIEWS=0" "S2_TAIL=1 --plan-flag STEM_VIEWS=0" "S2_TAIL=0 --plan-flag STEM_VIEWS=1" "S2_TAIL=1 --plan-flag STEM_VIEWS=1"; do
+for f in "S2_TAIL=1" "S2_TAIL=0 --plan-flag STEM_VIEWS=0 --plan-flag TILES_128X8=0" "S2_TAIL=0" "STEM_VIEWS=0" "TILES_128X8=0" "S2_TAIL=1"; do
   timeout -k 10 200 python -u bench.py $C --plan-flag $f > $O/ab.json 2> $O/ab.err || { tail -5 $O/ab.err; exit 1; }
   python -c "import json;d=json.loads(open('$O/ab.json').read().strip().splitlines()[-1]);print('$f',d['value'],d['network_ms'])"
 done
