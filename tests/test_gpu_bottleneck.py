@@ -284,8 +284,10 @@ def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
     s3 = torch.ones(1024, device=cuda)
     with pytest.raises(RuntimeError, match='wstream holds'):
         ops.bottleneck_tail_stream_nhwc(t3, x3, p2, s3, s3, s3, s3, BF16)
+    p3 = packing.pack_tail_stream(torch.zeros(256, 2304, device=cuda, dtype=torch.bfloat16),
+                                  torch.zeros(1024, 256, device=cuda, dtype=torch.bfloat16))
     with pytest.raises(RuntimeError, match='multiple of 8'):
-        ops.bottleneck_tail_stream_nhwc(t3[:, :4], x3[:, :4], p2, s3, s3, s3, s3, BF16)
+        ops.bottleneck_tail_stream_nhwc(t3[:, :4], x3[:, :4], p3, s3, s3, s3, s3, BF16)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp16'])
