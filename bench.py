@@ -809,6 +809,10 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
         return loss
 
     from posu import plan as pplan
+    # POSU_STREAM_SKIP=k (diagnostic): take k streams from torch's pool first, as earlier legs of a
+    # process do -- the training plan's weight-gradient side stream is the next pool stream
+    for _ in range(int(os.environ.get('POSU_STREAM_SKIP', '0'))):
+        torch.cuda.Stream(dev)
     stream = torch.cuda.Stream(dev, priority=-1) if args.train_stream == 'high' else torch.cuda.current_stream(dev)
     stream.wait_stream(torch.cuda.current_stream(dev))   # inputs / parameters made on the default stream
     with torch.cuda.stream(stream):
