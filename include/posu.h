@@ -48,8 +48,9 @@ const char* posu_last_error(void);
  * (posu_crop_warp); 9 the chained streamed tail (posu_bottleneck_tail_stream_next_fwd); 10 the
  * BatchNorm statistics in the conv epilogue (measured slower, removed in 11); 11 the streamed
  * tails take their weight stream's byte size, the round-2 LDS-ring layer2 block / layer3 tail
- * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) and the
- * one-launch multi-view stem (posu_stem_pool_views_fwd) added.  The ctypes binding refuses a library of another revision. */
+ * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) the
+ * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
+ * optional split-precision head (hw_lo).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -264,11 +265,17 @@ int posu_gemm_rows_f32(int dtype, const void* x, int M, int K, const void* wt, i
  * so the 256-channel deconv output need not round-trip through HBM.
  *   y: NULL (do not store f) or [N, 2H, 2W, Cout] dtype; Cout == 256;
  *   hw: packed head weight [>= 16][round_up(Cout, posu_conv_bk)] dtype (rows >= J zero);
+ *   hw_lo (ABI 11): NULL, or (BF16 / F16) the head weight's rounding residual w - hw rounded to
+ *   the dtype, same layout: the split-precision head -- the deconv output f enters as
+ *   round(f) + round(f - round(f)) and the head sums hi.hi + lo.hi + hi.lo products (three MFMAs
+ *   per fragment), so the heatmaps carry about twice the dtype's mantissa instead of f's
+ *   rounding to the dtype (the largest single source of the 2-byte chains' joint error,
+ *   DESIGN.md section 5); f itself is still stored rounded;
  *   hbias: [J] f32; hm: [N, J, 2H, 2W] f32; J <= 16. */
 int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H, int W, int C,
                               const void* w, int Cout, const float* scale, const float* shift,
-                              void* y, const void* hw, int J, const float* hbias, float* hm,
-                              void* stream);
+                              void* y, const void* hw, const void* hw_lo, int J, const float* hbias,
+                              float* hm, void* stream);
 
 /* 1x1 convolution (+bias) writing NCHW fp32 heatmaps: PoseResNet.final_layer
  * (lib/models/pose_resnet.py:126-132, 203).

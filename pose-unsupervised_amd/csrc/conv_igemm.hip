@@ -65,6 +65,8 @@ struct ConvGeom {
   int vblk;          // mode 2: out[(co / vblk)][m][co % vblk] (view-major heatmaps of a GEMM)
   // fused 1x1 head (mode 0, Cout == 256): hm[n][j][pix] = bias[j] + sum_c hw[j][c] relu(out[c])
   const void* hw;    // packed head weight [>= 16 rows][hkp] (dtype)
+  const void* hw_lo;  // NULL, or the head weight's rounding residual (w - hw, rounded, same layout):
+                      // the split-precision head (hi + lo operands on both sides, three MFMAs)
   const float* hbias;
   float* hm;
   int J, hkp;
@@ -473,15 +475,19 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     constexpr int TP = TN / 2;
     const bool head = HEAD256 && g.hm != nullptr;
-    uint4 hwf[HEAD256 ? TP : 1];
+    uint4 hwf[HEAD256 ? TP : 1], hwl[HEAD256 ? TP : 1];
     f32x4 hacc[HEAD256 ? TM : 1];
+    const bool split = HEAD256 && head && g.hw_lo != nullptr;
     if constexpr (HEAD256) {
       if (head) {
         const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
+        const T* __restrict__ hwq = reinterpret_cast<const T*>(split ? g.hw_lo : g.hw);
 #pragma unroll
-        for (int jp = 0; jp < TP; ++jp)  // joint r16, this lane's 8 channels of pair jp
-          hwf[jp] = *reinterpret_cast<const uint4*>(hwp + static_cast<size_t>(r16) * g.hkp + n0 + colB(2 * jp) +
-                                                    16 * (q & 1) + 8 * (q >> 1));
+        for (int jp = 0; jp < TP; ++jp) {  // joint r16, this lane's 8 channels of pair jp
+          const size_t o = static_cast<size_t>(r16) * g.hkp + n0 + colB(2 * jp) + 16 * (q & 1) + 8 * (q >> 1);
+          hwf[jp] = *reinterpret_cast<const uint4*>(hwp + o);
+          hwl[jp] = *reinterpret_cast<const uint4*>(hwq + o);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) hacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -550,6 +556,17 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           if (head) {
             const uint4 pk = O::store_vals(v);
             O::mma(hacc[i], hwf[jp], pk);  // rows = joints, cols = pixels
+            if (split) {
+              // the deconv output's rounding residual v - round(v) (exact in f32) rounded again: the
+              // head sees v to 2 x the dtype's mantissa, its weights likewise (hi.hi + lo.hi + hi.lo)
+              float vr[8], vl[8];
+              O::load_vals(pk, vr);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) vl[e] = v[e] - vr[e];
+              const uint4 pl = O::store_vals(vl);
+              O::mma(hacc[i], hwl[jp], pk);
+              O::mma(hacc[i], hwf[jp], pl);
+            }
             if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
             continue;
           }
@@ -1546,7 +1563,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
 
 extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* w,
                                          int Cout, const float* scale, const float* shift, void* y, const void* hw,
-                                         int J, const float* hbias, float* hm, void* stream) {
+                                         const void* hw_lo, int J, const float* hbias, float* hm, void* stream) {
   if (int st = common_checks(dtype, x, w, hm, N, H, W, C, Cout, "posu_deconv4x4s2_head_fwd")) return st;
   POSU_REQUIRE(hw && Cout == 256 && J > 0 && J <= 16,
                "posu_deconv4x4s2_head_fwd: needs Cout == 256, 0 < J <= 16 and head weights");
@@ -1567,6 +1584,7 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   g.out_H = 2 * H;
   g.out_W = 2 * W;
   g.hw = hw;
+  g.hw_lo = (dtype == POSU_BF16 || dtype == POSU_F16) ? hw_lo : nullptr;  // f32 heads are exact already
   g.hbias = hbias;
   g.hm = hm;
   g.J = J;

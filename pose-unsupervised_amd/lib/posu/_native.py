@@ -50,7 +50,7 @@ _SIGNATURES = {
     'posu_bottleneck_down_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
-    'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _i, _p, _p, _p],
+    'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p],
     'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],
     'posu_maxpool3x3s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _p],
     'posu_softargmax2d_fwd': [_p, _i, _i, _i, _i, _f, _p, _p, _p, _p],

@@ -161,15 +161,17 @@ def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):
 
 
 def deconv4x4s2_head(x, wpk, cout, scale, shift, head_w, njoints, head_b, code, keep_f=True, hm_out=None,
-                     f_out=None):
-    """Last deconv + BN + ReLU fused with the 1x1 head: returns (heatmaps NCHW f32, f NHWC or None)."""
+                     f_out=None, head_w_lo=None):
+    """Last deconv + BN + ReLU fused with the 1x1 head: returns (heatmaps NCHW f32, f NHWC or None).
+    head_w_lo (2-byte dtypes): the head weight's rounding residual -> the split-precision head."""
     n, h, w, c = x.shape
     if hm_out is None:
         hm_out = torch.empty((n, njoints, 2 * h, 2 * w), dtype=torch.float32, device=x.device)
     if keep_f and f_out is None:
         f_out = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
     call('posu_deconv4x4s2_head_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(scale), ptr(shift),
-         ptr(f_out if keep_f else None), ptr(head_w), njoints, ptr(head_b), ptr(hm_out), stream_of(x.device))
+         ptr(f_out if keep_f else None), ptr(head_w), ptr(head_w_lo), njoints, ptr(head_b), ptr(hm_out),
+         stream_of(x.device))
     return hm_out, (f_out if keep_f else None)
 
 

@@ -27,6 +27,10 @@ STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
 
 # fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
 FUSED_STEM = True
+# bf16 / fp16 plans: the fused deconv+head sums the head in split precision (the deconv output and
+# the head weights as hi + lo pairs of the dtype): the rounding of the deconv output to the dtype
+# was the largest single term of the 2-byte chains' joint error (tools/precision_attribution.py)
+PRECISE_HEAD = True
 # the fused stem over all views of a forward in one launch (posu_stem_pool_views_fwd); False: one
 # launch per view
 STEM_VIEWS = True
@@ -367,6 +371,10 @@ class PoseResNetPlan:
         if fl.kernel_size != (1, 1):
             raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
         self.head_w = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, ops.torch_dtype(code))
+        self.head_w_lo = None   # the split-precision head's residual weights (2-byte dtypes)
+        if code in (ops.BF16, ops.F16):
+            w32 = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, torch.float32)
+            self.head_w_lo = (w32 - self.head_w.float()).to(ops.torch_dtype(code)).contiguous()
         self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None
                        else torch.zeros(fl.weight.shape[0], device=fl.weight.device))
         self.njoints = fl.weight.shape[0]
@@ -450,7 +458,8 @@ class PoseResNetPlan:
         dc = self.deconvs[-1]
         if self.fuse_head:
             return ops.deconv4x4s2_head(x, dc.w, dc.cout, dc.scale, dc.shift, self.head_w, self.njoints, self.head_b,
-                                        code, keep_f=keep_f, hm_out=hm_out, f_out=f_out)
+                                        code, keep_f=keep_f, hm_out=hm_out, f_out=f_out,
+                                        head_w_lo=self.head_w_lo if PRECISE_HEAD else None)
         f = dc(x, code, out=f_out)
         return ops.head1x1_nchw(f, self.head_w, self.njoints, self.head_b, code, out=hm_out), f
 

@@ -307,13 +307,50 @@ def _fused_deconv_head_case(cuda, code, tol, keep_f, shape):
     torch.testing.assert_close(hm, hm2, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+def test_split_precision_head(cuda, code):
+    """The fused deconv + head with the split-precision head (hw_lo, ABI 11): against the head
+    computed in fp64 from the deconv output of the SAME rounded operands (so only the head's own
+    arithmetic differs), at least 20x closer than the plain head, whose input is the deconv output
+    rounded to the dtype; f (stored) is unchanged by the split."""
+    g = torch.Generator().manual_seed(18)
+    n, h, w, J = 2, 24, 20, 16
+    cin, cout = 64, 256
+    dt = ops.torch_dtype(code)
+    x = torch.randn(n, cin, h, w, generator=g).to(dt).double()
+    wt = (torch.randn(cin, cout, 4, 4, generator=g) * (2.0 / (cin * 4)) ** 0.5).to(dt).double()
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.1
+    hw = torch.randn(J, cout, 1, 1, generator=g) * 0.06
+    hb = torch.randn(J, generator=g)
+    f64 = F.relu(F.conv_transpose2d(x, wt, stride=2, padding=1) * sc.double().view(1, -1, 1, 1) +
+                 sh.double().view(1, -1, 1, 1))
+    hm64 = F.conv2d(f64, hw.double(), hb.double())
+    bk = ops.conv_bk(code)
+    wp = packing.pack_deconv4x4_weight(wt.float().to(cuda), bk, dt)
+    hw32 = packing.pack_conv_weight(hw.to(cuda), cout, bk, torch.float32)
+    hwp = hw32.to(dt)
+    hwl = (hw32 - hwp.float()).to(dt)
+    xd = x.float().permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    args = (xd, wp, cout, sc.to(cuda), sh.to(cuda), hwp, J, hb.to(cuda), code)
+    hm1, f1 = ops.deconv4x4s2_head(*args)
+    hm2, f2 = ops.deconv4x4s2_head(*args, head_w_lo=hwl)
+    torch.cuda.synchronize()
+    e1 = float((hm1.double().cpu() - hm64).abs().max())
+    e2 = float((hm2.double().cpu() - hm64).abs().max())
+    print('head vs fp64: plain %.3g, split %.3g (%.0fx)' % (e1, e2, e1 / max(e2, 1e-30)))
+    assert torch.equal(f1, f2)
+    assert e2 * 20 < e1
+    assert e2 < (3e-4 if code == BF16 else 1e-4)
+
+
 @pytest.mark.parametrize('case', CONV_CASES[1:5])
 def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     got, ref = _conv_case(cuda, F32, *case, tile=16 + (1 if case[4] < 128 else 3))
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 16, 17, 18, 19, 20, 22, 23, 31, 32, 37])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 23, 31, 32, 37])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks, the single- /

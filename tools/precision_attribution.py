@@ -107,8 +107,13 @@ def main():
     torch.cuda.synchronize()
     out = {'fit_steps': steps, 'fit_s': round(time.time() - t0, 1), 'hip_chains': {}}
     ref = None
+    from posu import plan as pl
     for prec in ('fp32', 'bf16', 'fp16'):
         out['hip_chains'][prec], ref = peaked.parity(net, task, dev, prec, ref)
+        if prec != 'fp32':   # the plain head (round 3's chain) beside the split-precision one
+            pl.PRECISE_HEAD = False
+            out['hip_chains'][prec + '_plain_head'], _ = peaked.parity(net, task, dev, prec, ref)
+            pl.PRECISE_HEAD = True
     sd = {k: v.detach().float() for k, v in net.state_dict().items() if v.is_floating_point()}
     x = torch.cat(task['views'])
     torch.backends.cudnn.allow_tf32 = False
@@ -116,7 +121,9 @@ def main():
     with torch.no_grad():
         out['emulated'] = {'none': chain_metrics(forward(x, sd, (), torch.float32), ref, task)}
         for dname, dt in (('bf16', torch.bfloat16), ('fp16', torch.float16)):
-            res = {'all': chain_metrics(forward(x, sd, STAGES, dt), ref, task)}
+            res = {'all': chain_metrics(forward(x, sd, STAGES, dt), ref, task),
+                   # the plan's split-precision head (PRECISE_HEAD): every stage rounded but the head
+                   'all_but_head': chain_metrics(forward(x, sd, STAGES[:-1], dt), ref, task)}
             for s in STAGES:
                 res[s] = chain_metrics(forward(x, sd, (s,), dt), ref, task)
             out['emulated'][dname] = res
