@@ -13,3 +13,25 @@ for f in 1 0; do
   python3 tools/replay_breakdown.py $O/s2_$f/run_kernel_trace.csv --last 5 > $O/replay_s2_$f.txt || exit 1
   echo "S2_TAIL=$f"; head -14 $O/replay_s2_$f.txt; tail -1 $O/replay_s2_$f.txt
 done
+# L2 hit rate per kernel of one network replay (one PMC pass: TCC_HIT_sum, TCC_MISS_sum)
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace --output-format csv -d $O/pmc_l2 -o run -- \
+  python3 bench.py $C --steps 2 --warmup 1 > $O/pmc_l2.log 2>&1 || { tail -5 $O/pmc_l2.log; exit 1; }
+python3 - <<'PY' > $O/l2_hit_rate.txt
+import csv, collections
+rows = collections.defaultdict(dict)
+for r in csv.DictReader(open('gpurun_out/r4f/pmc_l2/run_counter_collection.csv')):
+    rows[int(r['Dispatch_Id'])][r['Counter_Name']] = float(r['Counter_Value'])
+    rows[int(r['Dispatch_Id'])]['name'] = r['Kernel_Name']
+ids = sorted(rows)
+# the last network replay: from the last stem launch to the next soft-argmax
+last = max(i for i in ids if 'stem_pool' in rows[i]['name'])
+for i in ids:
+    if i < last:
+        continue
+    n = rows[i]['name']
+    if 'softargmax' in n:
+        break
+    h, m = rows[i].get('TCC_HIT_sum', 0), rows[i].get('TCC_MISS_sum', 0)
+    print('%-70s hit %.3f  (%.1f M requests)' % (n.split('(')[0][:70], h / max(h + m, 1), (h + m) / 1e6))
+PY
+cat $O/l2_hit_rate.txt
