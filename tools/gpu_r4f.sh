@@ -35,3 +35,6 @@ for i in ids:
     print('%-70s hit %.3f  (%.1f M requests)' % (n.split('(')[0][:70], h / max(h + m, 1), (h + m) / 1e6))
 PY
 cat $O/l2_hit_rate.txt
+# the counter names of this rocprofv3 (for the next PMC passes)
+timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+grep -c "" $O/counters.txt
