@@ -102,6 +102,11 @@ def parse():
     ap.add_argument('--control-steps', type=int, default=10,
                     help='infer mode: timed steps of the same pipeline with this round\'s plan switches off '
                          '(CONTROL_FLAGS: the previous round\'s plan), reported as control (0: skip)')
+    ap.add_argument('--train-last', action='store_true',
+                    help='diagnostic: run the training leg after the fp32 / configs1 / control / configs4 legs (the '
+                         'round-3 order), optionally with --empty-cache-before-train')
+    ap.add_argument('--empty-cache-before-train', action='store_true',
+                    help='diagnostic: torch.cuda.empty_cache() before the training leg')
     ap.add_argument('--dry-run', action='store_true', help='launcher + rank plumbing on CPU (gloo), no GPU work')
     ap.add_argument('--train-stream', default='default', choices=['high', 'default'],
                     help='train mode: run the step on a high-priority stream (the weight-gradient side '
@@ -684,14 +689,21 @@ def infer_main(args):
             roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
     # the training leg right after the headline leg, before the other legs (see DESIGN.md section 6:
     # behind the fp32 / configs1 legs the same step read 23.98 instead of 21.6 ms)
-    train = None
-    if args.train_steps > 0:
+    def train_leg():
+        if args.empty_cache_before_train:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
         t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
-        train = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
-        train.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
-                     traffic=t['roofline']['traffic'] if t['roofline'] else None,
-                     parallelism=t['config']['parallelism'], workload=t['config']['workload'],
-                     optimizer=t['config']['optimizer'])
+        tr = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
+        tr.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
+                  traffic=t['roofline']['traffic'] if t['roofline'] else None,
+                  parallelism=t['config']['parallelism'], workload=t['config']['workload'],
+                  optimizer=t['config']['optimizer'])
+        return tr
+
+    train = None
+    if args.train_steps > 0 and not args.train_last:
+        train = train_leg()
     fp32 = None
     if args.fp32_steps > 0 and args.precision != 'fp32':
         r32 = time_pipeline(args, 'fp32', dev, rank, args.fp32_steps, 2, args.batches, False, dist, world)
@@ -703,6 +715,8 @@ def infer_main(args):
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
     control = time_control(args, dev, rank, world, dist) if args.control_steps > 0 else None
     c4 = time_configs4(args, dev, rank, world, dist) if args.c4_steps > 0 else None
+    if args.train_steps > 0 and args.train_last:
+        train = train_leg()
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()

@@ -38,3 +38,17 @@ cat $O/l2_hit_rate.txt
 # the counter names of this rocprofv3 (for the next PMC passes)
 timeout -k 10 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 grep -c "" $O/counters.txt
+# fp16 per-kernel times (the fp16 line ran ~1.6 % slower than bf16 in r4e)
+timeout -k 10 300 python3 bench.py $C --precision fp16 --tune-file $O/tiles16.json > $O/tune16.log 2>&1 || { tail -5 $O/tune16.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/f16 -o run -- \
+  python3 bench.py --no-cpu-baseline --no-mpjpe --fp32-steps 0 --train-steps 0 --c1-steps 0 --peaked-steps 0 --c4-steps 0 --control-steps 0 --tune-file $O/tiles16.json --precision fp16 --steps 10 --warmup 3 > $O/f16.log 2>&1 || { tail -5 $O/f16.log; exit 1; }
+python3 tools/replay_breakdown.py $O/f16/run_kernel_trace.csv --last 5 > $O/replay_f16.txt || exit 1
+tail -1 $O/replay_f16.txt
+# the training leg behind the other legs (the round-3 order), with and without emptying the allocator cache
+L="--no-cpu-baseline --no-mpjpe --peaked-steps 0"
+for e in "" "--empty-cache-before-train"; do
+  timeout -k 10 400 python3 bench.py $L --train-last $e > $O/trainlast.json 2> $O/trainlast.err || { tail -5 $O/trainlast.err; exit 1; }
+  python3 -c "import json;d=json.loads(open('$O/trainlast.json').read().strip().splitlines()[-1]);print('train-last $e', d['train_mode']['ms_per_step'], d['network_ms'])"
+done
+timeout -k 10 200 python3 bench.py --mode train --steps 10 --warmup 3 > $O/t.json 2> $O/t.err || exit 1
+python3 -c "import json;d=json.loads(open('$O/t.json').read().strip().splitlines()[-1]);print('standalone', d['ms_per_step'])"
