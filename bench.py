@@ -687,6 +687,14 @@ def infer_main(args):
         if traffic:
             roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward')
             roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
+        if (args.layers, args.size) == (50, 256) and args.precision in ('bf16', 'fp16'):
+            # compulsory bytes of the same launches (posu.roofline: inputs, weights read once, outputs
+            # written once); traffic / algorithmic = the forward's over-fetch
+            from posu import roofline as _rl
+            alg = _rl.r50_256_algorithmic_bytes(frames, 2)
+            roof['algorithmic_bytes'] = alg
+            if traffic:
+                roof['traffic_over_algorithmic'] = round(traffic / alg, 4)
     # the training leg right after the headline leg, before the other legs (see DESIGN.md section 6:
     # behind the fp32 / configs1 legs the same step read 23.98 instead of 21.6 ms)
     def train_leg():

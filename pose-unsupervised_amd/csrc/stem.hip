@@ -44,7 +44,6 @@ struct StemOp<uint16_t> {
   static __device__ __forceinline__ uint32_t pack2(float a, float b) {
     return f2bf2(a, b);
   }
-  static __device__ __forceinline__ float round(float a) { return bf2f(f2bf(a)); }
 };
 template <>
 struct StemOp<f16_t> {
@@ -57,7 +56,6 @@ struct StemOp<f16_t> {
     return static_cast<uint32_t>(__builtin_bit_cast(uint16_t, ha)) |
            (static_cast<uint32_t>(__builtin_bit_cast(uint16_t, hb)) << 16);
   }
-  static __device__ __forceinline__ float round(float a) { return static_cast<float>(static_cast<_Float16>(a)); }
 };
 
 // The views of one forward (the caller's NCHW f32 tensors, each [Nv, 3, H, W]) in one launch.
@@ -65,6 +63,17 @@ constexpr int kMaxViews = 8;
 struct StemViews {
   const float* x[kMaxViews];
 };
+
+// timing ablations (tools/stem_micro.py only; wrong results when non-zero): 1 no MFMAs, 2 no input
+// loads, 4 no output stores
+#ifndef POSU_STEM_ABLATE
+#define POSU_STEM_ABLATE 0
+#endif
+// input prefetch depth of the eight-wave kernel (items ahead; 1 = round-4 first version)
+#ifndef POSU_STEM_PFD
+#define POSU_STEM_PFD 2
+#endif
+constexpr int kStemAbl = POSU_STEM_ABLATE;
 
 // NW waves; wave w owns stem columns 16w .. 16w + 15 (one m-tile column group).  A block walks a
 // strip of consecutive pool-row pairs of one image (item k = pool rows 2k, 2k+1 = stem rows
@@ -85,10 +94,11 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   constexpr int RB = WP * 8;                 // bytes per ring row
   constexpr int RING = 16;
   constexpr int W_BYTES = 64 * kStemPitch * 2;
-  __shared__ __attribute__((aligned(16))) char smem[RING * RB + W_BYTES + NW * 2 * 64 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[RING * RB + W_BYTES + NW * 2 * 64 * 4 + 2 * 64 * 4];
   char* win = smem;
   char* wl = smem + RING * RB;
   float* edge = reinterpret_cast<float*>(smem + RING * RB + W_BYTES);  // [wave][pool row][64 ch]
+  float* bn = edge + NW * 2 * 64;                                       // scale [64], shift [64]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
@@ -99,7 +109,11 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   const float* __restrict__ xn = xs.x[n / Nv] + static_cast<size_t>(n % Nv) * 3 * H * W;
   const size_t plane = static_cast<size_t>(H) * W;
 
-  // ---- weights -> LDS (once per block)
+  // ---- weights and BN -> LDS (once per block)
+  if (tid < 64) {
+    bn[tid] = scale[tid];   // (used as |s|)
+    bn[64 + tid] = shift[tid];
+  }
   {
     constexpr int WCH = 64 * (kStemK / 8);
 #pragma unroll
@@ -107,7 +121,12 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       const int i = tid + it * NT;
       if (i < WCH) {
         const int co = i / (kStemK / 8), ck = i - co * (kStemK / 8);
-        *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = *reinterpret_cast<const u32x4*>(w + i * 8);
+        // the sign of the channel's BN scale folded into its weights (negation is exact, in the
+        // MFMA sums too): the accumulators are sgn(s) * conv, which the pool maximises directly
+        const unsigned sg = __float_as_uint(scale[co]) & 0x80000000u ? 0x80008000u : 0u;
+        u32x4 wv = *reinterpret_cast<const u32x4*>(w + i * 8);
+        wv ^= sg;
+        *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = wv;
       }
     }
   }
@@ -116,7 +135,7 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   // each plane (window columns 4 gk - 1 .. 4 gk + 2)
   constexpr int GPR = NW * 8 + 2;
   constexpr int XG8 = (8 * GPR + NT - 1) / NT;
-  auto load_rows = [&](int i0, auto nr, float4 (*xv)[3]) {
+  auto load_rows = [&](int i0, auto nr, float4 (*xv)[3]) __attribute__((always_inline)) {
     constexpr int NR = decltype(nr)::value, XG = (NR * GPR + NT - 1) / NT;
 #pragma unroll
     for (int it = 0; it < XG; ++it) {
@@ -125,6 +144,10 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       const int iy = i0 + r, c0 = 4 * (gk - 1);
 #pragma unroll
       for (int p = 0; p < 3; ++p) xv[it][p] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kStemAbl & 2) {
+        xv[it][0] = make_float4(iy, c0, 1.f, 0.5f);
+        continue;
+      }
       if (i < NR * GPR && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
           static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
         const size_t o = static_cast<size_t>(iy) * W + (hflip ? W - 4 - c0 : c0);
@@ -137,7 +160,7 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       }
     }
   };
-  auto store_rows = [&](int i0, auto nr, float4 (*xv)[3]) {
+  auto store_rows = [&](int i0, auto nr, float4 (*xv)[3]) __attribute__((always_inline)) {
     constexpr int NR = decltype(nr)::value, XG = (NR * GPR + NT - 1) / NT;
 #pragma unroll
     for (int it = 0; it < XG; ++it) {
@@ -158,11 +181,17 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   };
 
   const int sc = 16 * wid + r16;
-  // stem rows r0 .. r0 + M - 1 (m-tile rl = stem row r0 + rl; pixel column sc), BN + ReLU, rounded
-  // (zeros for rows outside the image), folded straight into the two pool rows' vertical maxima:
+  // Pool first, BN after: with t = sgn(s) * conv (the sign-folded weights' accumulator),
+  // relu(s conv + b) = relu(fma(|s|, t, b)) is non-decreasing in t, and so is its rounding to the
+  // compute dtype, so the max-pool of the rounded stem values equals that function of the max-pool
+  // of t -- bit for bit the two-launch result, with the BN / ReLU / rounding done once per pooled
+  // value instead of once per stem value.  Pool padding: -inf in t (the max of the rest is >= 0
+  // after the ReLU either way).
+  // stem rows r0 .. r0 + M - 1 (m-tile rl = stem row r0 + rl; pixel column sc), folded straight
+  // into the two pool rows' vertical maxima of t (rows outside the image: -inf):
   // M = 5: rows 4k-1 .. 4k+3; M = 4: rows 4k .. 4k+3 with row 4k-1 = carry.  carry <- row 4k+3.
   // (channel 16 j + 4 q + e)
-  auto stem_rows = [&](int r0, auto mrows, float (*carry)[4], float (*vm)[4][4]) {
+  auto stem_rows = [&](int r0, auto mrows, float (*carry)[4], float (*vm)[4][4]) __attribute__((always_inline)) {
     constexpr int M = decltype(mrows)::value;
     f32x4 acc[M][4];
 #pragma unroll
@@ -187,7 +216,10 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
 #pragma unroll
         for (int rl = 0; rl < M; ++rl)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) O::mma(acc[rl][j], bfr[j], af[rl]);
+          for (int j = 0; j < 4; ++j) {
+            if (kStemAbl & 1) acc[rl][j][0] += __uint_as_float(bfr[j].x ^ af[rl].y);
+            else O::mma(acc[rl][j], bfr[j], af[rl]);
+          }
       } else {  // twelve waves: fewer registers in flight
 #pragma unroll
         for (int rl = 0; rl < M; ++rl) {
@@ -201,12 +233,9 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = 16 * j + 4 * q + e;
-        const float s_ = scale[co], b_ = shift[co];
         float v[M];
 #pragma unroll
-        for (int rl = 0; rl < M; ++rl)
-          v[rl] = (r0 + rl >= 0) ? O::round(fmaxf(acc[rl][j][e] * s_ + b_, 0.f)) : 0.f;
+        for (int rl = 0; rl < M; ++rl) v[rl] = (r0 + rl >= 0) ? acc[rl][j][e] : -INFINITY;
         const float first = M == 5 ? v[0] : carry[j][e];
         const float* u = v + (M == 5 ? 1 : 0);   // stem rows 4k .. 4k+3
         vm[0][j][e] = fmaxf(fmaxf(first, u[0]), u[1]);
@@ -216,9 +245,9 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   };
 
   T* __restrict__ yn = y + static_cast<size_t>(n) * Hp * Wp * 64;
-  // pool rows 2k, 2k+1 from their vertical maxima: horizontal max with lane shuffles (a wave's
-  // left neighbour column through LDS), 8-byte NHWC stores
-  auto pool = [&](int k, const float (*vm)[4][4]) {
+  // pool rows 2k, 2k+1 from their vertical maxima: horizontal max with DPP row shifts (a wave's
+  // left neighbour column through LDS), then BN + ReLU + rounding, 8-byte NHWC stores
+  auto pool = [&](int k, const float (*vm)[4][4]) __attribute__((always_inline)) {
     if (r16 == 15) {
 #pragma unroll
       for (int p = 0; p < 2; ++p)
@@ -232,19 +261,26 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     for (int p = 0; p < 2; ++p)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
+        const float4 s4 = *reinterpret_cast<const float4*>(bn + 16 * j + 4 * q);
+        const float4 b4 = *reinterpret_cast<const float4*>(bn + 64 + 16 * j + 4 * q);
+        const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float self = vm[p][j][e];
-          const float right = __shfl_down(self, 1, 16);  // column sc + 1 (r16 even < 15)
-          float left = __shfl_up(self, 1, 16);           // column sc - 1
-          if (r16 == 0) left = wid > 0 ? edge[((wid - 1) * 2 + p) * 64 + 16 * j + 4 * q + e] : 0.f;
-          o[e] = fmaxf(fmaxf(left, self), right);
+          // DPP row shifts inside the 16-lane rows (= the wave's 16 columns): column sc + 1
+          // (used by even r16 < 15 only) and column sc - 1 (r16 = 0 takes the neighbour's edge)
+          const float right = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(self), 0x101, 0xf, 0xf, true));
+          float left = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(self), 0x111, 0xf, 0xf, true));
+          if (r16 == 0) left = wid > 0 ? edge[((wid - 1) * 2 + p) * 64 + 16 * j + 4 * q + e] : -INFINITY;
+          o[e] = fmaxf(fmaf(fabsf(sv[e]), fmaxf(fmaxf(left, self), right), bv[e]), 0.f);
         }
         if ((r16 & 1) == 0) {
           const int pc = 8 * wid + (r16 >> 1);
           T* dst = yn + (static_cast<size_t>(2 * k + p) * Wp + pc) * 64 + 16 * j + 4 * q;
-          *reinterpret_cast<uint2*>(dst) = make_uint2(O::pack2(o[0], o[1]), O::pack2(o[2], o[3]));
+          const uint2 u = make_uint2(O::pack2(o[0], o[1]), O::pack2(o[2], o[3]));
+          if (kStemAbl & 4) asm volatile("" ::"v"(u.x), "v"(u.y));
+          else *reinterpret_cast<uint2*>(dst) = u;
         }
       }
   };
@@ -254,32 +290,52 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   using I5 = std::integral_constant<int, 5>;
   using I8 = std::integral_constant<int, 8>;
   float carry[4][4], vm[2][4][4];
-  float4 xv[XG8][3];
+  // PF: the following items' new input rows are loaded into registers while this item computes
+  // (PFD items ahead, one register set each), and stem row 4k-1 is carried (eight waves); twelve
+  // waves per block (W = 384) have no registers left for either: rows loaded in turn, every item
+  // computes its 5 stem rows
+  constexpr bool PF = NW <= 8;
+  constexpr int PFD = PF ? POSU_STEM_PFD : 1;
+  static_assert(PFD == 1 || PFD == 2, "prefetch depth 1 or 2");
+  float4 xv[PFD][XG8][3];
   // (16 rows 8 k0 - 5 .. 8 k0 + 10: two 8-row loads through the prefetch registers; the last row
   // is not read by this item and is rewritten before item k0 + 1 reads it)
-  load_rows(8 * k0 - 5, I8{}, xv);
-  store_rows(8 * k0 - 5, I8{}, xv);
-  load_rows(8 * k0 + 3, I8{}, xv);
-  store_rows(8 * k0 + 3, I8{}, xv);
+  load_rows(8 * k0 - 5, I8{}, xv[0]);
+  store_rows(8 * k0 - 5, I8{}, xv[0]);
+  load_rows(8 * k0 + 3, I8{}, xv[0]);
+  store_rows(8 * k0 + 3, I8{}, xv[0]);
   __syncthreads();
-  // PF: the next item's new input rows are loaded into registers while this item computes, and
-  // stem row 4k-1 is carried (eight waves); twelve waves per block (W = 384) have no registers
-  // left for either: rows loaded in turn, every item computes its 5 stem rows
-  constexpr bool PF = NW <= 8;
   stem_rows(4 * k0 - 1, I5{}, carry, vm);
-  if (PF && k0 + 1 < k1) load_rows(8 * k0 + 10, I8{}, xv);   // item k0 + 1's new rows, during item k0's pool
+  // item k0 + d's new rows into set d % PFD, during item k0's pool
+  if constexpr (PF) {
+    if (k0 + 1 < k1) load_rows(8 * k0 + 10, I8{}, xv[PFD - 1]);
+    if (PFD == 2 && k0 + 2 < k1) load_rows(8 * k0 + 18, I8{}, xv[0]);
+  }
   pool(k0, vm);
-  for (int k = k0 + 1; k < k1; ++k) {
-    if (!PF) load_rows(8 * k + 2, I8{}, xv);
+  // item k: its rows are in set S = (k - k0) % PFD (a compile-time index: a register set picked
+  // at run time would live in scratch); once stored, the set takes item k + PFD's
+  auto item = [&](int k, auto sidx) __attribute__((always_inline)) {
+    constexpr int S = decltype(sidx)::value;
+    if (!PF) load_rows(8 * k + 2, I8{}, xv[S]);
     // every wave is past item k-1's window reads (the pool barrier): its dead rows take item k's
     __syncthreads();
-    store_rows(8 * k + 2, I8{}, xv);
+    store_rows(8 * k + 2, I8{}, xv[S]);
     __syncthreads();
-    if (PF && k + 1 < k1) load_rows(8 * k + 10, I8{}, xv);   // item k + 1's, during item k
+    if (PF && k + PFD < k1) load_rows(8 * (k + PFD) + 2, I8{}, xv[S]);
     if constexpr (PF) stem_rows(4 * k, I4{}, carry, vm);
     else stem_rows(4 * k - 1, I5{}, carry, vm);
     pool(k, vm);
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, PFD - 1>;
+  int k = k0 + 1;
+  if constexpr (PFD == 2) {
+    for (; k + 1 < k1; k += 2) {   // two items per trip
+      item(k, S1{});
+      item(k + 1, S0{});
+    }
   }
+  for (; k < k1; ++k) item(k, S1{});   // PFD 2: at most one item left, its rows in set 1
 }
 
 }  // namespace

@@ -1,0 +1,71 @@
+"""Algorithmic HBM bytes of one PoseResNet-50 forward at 256x256 in the benched launch order
+(measurement bookkeeping for bench.py and tools/pmc_traffic.py; no GPU work).
+
+Per launch: the bytes a kernel must move at least -- every input activation it needs read once
+(for a stride-2 1x1 source only its stride-2 pixels), its weights read once, its outputs written
+once.  The launch list is the default plan's (plan.py: fused stem over all views, fused layer1
+blocks, layer2 conv1 + strided tail, chained streamed tails, conv launches for layer3 block 0 and
+layer4, deconv1, deconv2, deconv3 with the fused head writing f32 heatmaps only):
+31 launches.  Comparing it with the PMC traffic of the same launches (FETCH_SIZE x 2 + WRITE_SIZE,
+tools/pmc_traffic.py) gives each kernel's over-fetch.
+"""
+
+# R50 PoseResNet stages: (blocks, planes, in channels, out channels, input spatial at 256x256)
+_R50 = ((3, 64, 64, 256, 64), (4, 128, 256, 512, 64), (6, 256, 512, 1024, 32), (3, 512, 1024, 2048, 16))
+
+
+def r50_256_launches(n=128, es=2, joints=17):
+    """[(name, read_bytes, write_bytes)] for one forward of n frames (es: activation bytes)."""
+    out = []
+    act = lambda hw, c: n * hw * hw * c * es  # noqa: E731
+    wb = lambda *dims: es * _prod(dims)  # noqa: E731
+    # stem: f32 NCHW input, 7x7x3x64 weight, pooled 64x64x64 output
+    out.append(('stem_pool (4 views)', n * 3 * 256 * 256 * 4 + wb(64, 147), act(64, 64)))
+    # layer1: fused blocks (block 0 with the downsample)
+    out.append(('layer1.0 bottleneck64 (down)', act(64, 64) + wb(64, 64) + wb(64, 576) + wb(256, 64) + wb(256, 64),
+                act(64, 256)))
+    for b in (1, 2):
+        out.append(('layer1.%d bottleneck64' % b, act(64, 256) + wb(64, 256) + wb(64, 576) + wb(256, 64),
+                    act(64, 256)))
+    # layer2: conv1 at 64x64, the strided tail, conv1 of block 1, chained tails, the last tail
+    out.append(('layer2.0 conv1', act(64, 256) + wb(128, 256), act(64, 128)))
+    out.append(('layer2.0 strided tail (conv2 s2 + conv3|down)',
+                act(64, 128) + act(32, 256) + wb(128, 1152) + wb(512, 384), act(32, 512)))
+    out.append(('layer2.1 conv1', act(32, 512) + wb(128, 512), act(32, 128)))
+    for b in (1, 2):
+        out.append(('layer2.%d chained tail' % b, act(32, 128) + act(32, 512) + wb(128, 1152) + wb(512, 128) +
+                    wb(128, 512), act(32, 512) + act(32, 128)))
+    out.append(('layer2.3 tail', act(32, 128) + act(32, 512) + wb(128, 1152) + wb(512, 128), act(32, 512)))
+    # layer3 block 0 as three convs, block 1 conv1, chained tails, the last tail
+    out.append(('layer3.0 conv1', act(32, 512) + wb(256, 512), act(32, 256)))
+    out.append(('layer3.0 conv2 s2', act(32, 256) + wb(256, 2304), act(16, 256)))
+    out.append(('layer3.0 conv3|down', act(16, 256) + act(16, 512) + wb(1024, 768), act(16, 1024)))
+    out.append(('layer3.1 conv1', act(16, 1024) + wb(256, 1024), act(16, 256)))
+    for b in (1, 2, 3, 4):
+        out.append(('layer3.%d chained tail' % b, act(16, 256) + act(16, 1024) + wb(256, 2304) + wb(1024, 256) +
+                    wb(256, 1024), act(16, 1024) + act(16, 256)))
+    out.append(('layer3.5 tail', act(16, 256) + act(16, 1024) + wb(256, 2304) + wb(1024, 256), act(16, 1024)))
+    # layer4: every conv a launch
+    out.append(('layer4.0 conv1', act(16, 1024) + wb(512, 1024), act(16, 512)))
+    out.append(('layer4.0 conv2 s2', act(16, 512) + wb(512, 4608), act(8, 512)))
+    out.append(('layer4.0 conv3|down', act(8, 512) + act(8, 1024) + wb(2048, 1536), act(8, 2048)))
+    for b in (1, 2):
+        out.append(('layer4.%d conv1' % b, act(8, 2048) + wb(512, 2048), act(8, 512)))
+        out.append(('layer4.%d conv2' % b, act(8, 512) + wb(512, 4608), act(8, 512)))
+        out.append(('layer4.%d conv3 + residual' % b, act(8, 512) + act(8, 2048) + wb(2048, 512), act(8, 2048)))
+    # deconvs (4 parity classes x 4 taps per class of the 4x4 kernel), the fused head
+    out.append(('deconv1', act(8, 2048) + wb(256, 2048, 16), act(16, 256)))
+    out.append(('deconv2', act(16, 256) + wb(256, 256, 16), act(32, 256)))
+    out.append(('deconv3 + head', act(32, 256) + wb(256, 256, 16) + wb(joints, 256), n * joints * 64 * 64 * 4))
+    return out
+
+
+def _prod(dims):
+    p = 1
+    for d in dims:
+        p *= d
+    return p
+
+
+def r50_256_algorithmic_bytes(n=128, es=2):
+    return sum(r + w for _, r, w in r50_256_launches(n, es))

@@ -10,8 +10,11 @@ compared with the CPU oracle chain (fp32 reference forward -> soft-argmax -> tra
 triangulate_poses, run/test/test_triangulate.py:98-101 arithmetic) on the same weights.
 
 Gates: fp32 -- BASELINE.json's bars: heatmaps 1e-3, triangulated joints 1e-2 mm (mean AND
-max).  bf16 -- bands from the measured deviation (round 3: heatmaps 0.038 max / 7.6e-4 mean,
-joints 0.26 px mean, 1.34 mm mean / 6.5 mm max MPJPE against the fp32 reference chain)."""
+max).  bf16 and fp16 (the plan's default split-precision head, plan.PRECISE_HEAD) -- 2 x the
+deviation measured at round 4 (profiles/r04/precision_attribution_r4e.json, deterministic: the
+same fitted net and the same chains give the same figures run to run):
+    bf16  heatmaps 0.0163 max / 3.2e-4 mean, joints 0.131 px mean, 0.656 mm mean / 3.03 mm max
+    fp16  heatmaps 0.00205 max / 3.9e-5 mean, joints 0.0147 px mean, 0.068 mm mean / 0.209 mm max"""
 import os
 import sys
 
@@ -30,25 +33,36 @@ def fitted(cuda):
     net, task = peaked.fit_peaked(cuda, steps=1200)
     res32, ref = peaked.parity(net, task, cuda, 'fp32')
     res16, _ = peaked.parity(net, task, cuda, 'bf16', ref)
+    resh, _ = peaked.parity(net, task, cuda, 'fp16', ref)
     print('fp32:', res32)
     print('bf16:', res16)
-    return res32, res16
+    print('fp16:', resh)
+    return res32, res16, resh
 
 
 def test_fitted_network_is_trained_like(fitted):
-    res32, _ = fitted
+    res32 = fitted[0]
     assert res32['heatmap_peak_mean'] > 0.8 and res32['heatmap_peak_min'] > 0.4
     assert res32['oracle_mpjpe_vs_gt_mm'] < 25.0
 
 
 def test_fp32_chain_meets_the_baseline_bars_on_peaked_heatmaps(fitted):
-    r, _ = fitted
+    r = fitted[0]
     assert r['heatmap_abs_err']['max'] < 1e-3
     assert r['mpjpe_vs_ref_mm']['mean'] < 1e-2 and r['mpjpe_vs_ref_mm']['max'] < 1e-2
 
 
 def test_bf16_chain_on_peaked_heatmaps(fitted):
-    _, r = fitted
-    assert r['heatmap_abs_err']['max'] < 0.1 and r['heatmap_abs_err']['mean'] < 5e-3
-    assert r['joints_px_err']['mean'] < 1.0
-    assert r['mpjpe_vs_ref_mm']['mean'] < 5.0 and r['mpjpe_vs_ref_mm']['max'] < 25.0
+    from posu import plan
+    assert plan.PRECISE_HEAD, 'the bands below are the split-precision head\'s'
+    r = fitted[1]
+    assert r['heatmap_abs_err']['max'] < 0.033 and r['heatmap_abs_err']['mean'] < 6.4e-4
+    assert r['joints_px_err']['mean'] < 0.27
+    assert r['mpjpe_vs_ref_mm']['mean'] < 1.32 and r['mpjpe_vs_ref_mm']['max'] < 6.1
+
+
+def test_fp16_chain_on_peaked_heatmaps(fitted):
+    r = fitted[2]
+    assert r['heatmap_abs_err']['max'] < 4.2e-3 and r['heatmap_abs_err']['mean'] < 7.8e-5
+    assert r['joints_px_err']['mean'] < 0.03
+    assert r['mpjpe_vs_ref_mm']['mean'] < 0.14 and r['mpjpe_vs_ref_mm']['max'] < 0.42

@@ -6,7 +6,7 @@ A replay = the dispatches from the first of a run of stem_pool_kernel launches (
 the round-3 plan, one for all views since round 4) up to (not including) the next soft-argmax
 kernel.  (The round-3 version restarted a replay at EVERY stem launch, so its breakdowns counted
 one of the four per-view stem launches of that plan.)  Prints, for the chosen replays, each launch's median duration (us)
-with its kernel name, and the replay's launch-time sum and wall span (first start to last
+its gap to the previous launch's end (negative: overlap), with its kernel name, and the replay's launch-time sum and wall span (first start to last
 end: the sum plus the gaps between launches)."""
 import argparse
 import csv
@@ -53,8 +53,9 @@ def main():
     tot = 0.0
     for i in range(k):
         d = statistics.median((r[i][1] - r[i][0]) / 1e3 for r in replays)
+        g = statistics.median((r[i][0] - r[i - 1][1]) / 1e3 for r in replays) if i else 0.0
         tot += d
-        print('%3d %9.1f us  %s' % (i, d, short(replays[0][i][2])))
+        print('%3d %9.1f us  gap %6.1f  %s' % (i, d, g, short(replays[0][i][2])))
     span = statistics.median((r[-1][1] - r[0][0]) / 1e3 for r in replays)
     print('sum of launches %.1f us, replay span %.1f us (gaps %.1f us)' % (tot, span, span - tot))
 
