@@ -69,9 +69,10 @@ struct StemViews {
 #ifndef POSU_STEM_ABLATE
 #define POSU_STEM_ABLATE 0
 #endif
-// input prefetch depth of the eight-wave kernel (items ahead; 1 = round-4 first version)
+// input prefetch depth of the eight-wave kernel (items ahead): 2 measured equal to 1
+// (profiles/r04/stem_micro_r4g.txt), so 1
 #ifndef POSU_STEM_PFD
-#define POSU_STEM_PFD 2
+#define POSU_STEM_PFD 1
 #endif
 constexpr int kStemAbl = POSU_STEM_ABLATE;
 
@@ -198,32 +199,51 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     for (int i = 0; i < M; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int kh = 0; kh < 7; ++kh) {
-      uint4 bfr[4];
+    // window row of (m-tile rl, kernel row kh): 2 (r0 + rl) - 3 + kh = 2 r0 - 3 + rho, rho = 2 rl + kh;
+    // column 2 sc + 2 q (= input col 2 sc - 3 + 2 q)
+    auto rd = [&](int rho) {
+      return *reinterpret_cast<const uint4*>(win + ((2 * r0 - 3 + rho) & (RING - 1)) * RB + (2 * sc + 2 * q) * 8);
+    };
+    auto bload = [&](int kh, uint4 (&bfr)[4]) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bfr[j] = *reinterpret_cast<const uint4*>(wl + ((16 * j + r16) * kStemPitch + kh * 32 + 8 * q) * 2);
-      // input row 2 (r0 + rl) - 3 + kh, window column 2 sc + 2 q (= input col 2 sc - 3 + 2 q)
-      auto rd = [&](int rl) {
-        return *reinterpret_cast<const uint4*>(win + ((2 * (r0 + rl) - 3 + kh) & (RING - 1)) * RB +
-                                               (2 * sc + 2 * q) * 8);
-      };
-      if constexpr (NW <= 8) {
-        uint4 af[M];
+    };
+    auto mmas = [&](const uint4 (&bfr)[4], const uint4 (&af)[M]) {
 #pragma unroll
-        for (int rl = 0; rl < M; ++rl) af[rl] = rd(rl);
+      for (int rl = 0; rl < M; ++rl)
 #pragma unroll
-        for (int rl = 0; rl < M; ++rl)
+        for (int j = 0; j < 4; ++j) {
+          if (kStemAbl & 1) acc[rl][j][0] += __uint_as_float(bfr[j].x ^ af[rl].y);
+          else O::mma(acc[rl][j], bfr[j], af[rl]);
+        }
+    };
+    if constexpr (NW <= 8) {
+      // kernel rows of one parity read the same window rows shifted by one m-tile: two rolling
+      // sets (even / odd kh) load 2 M + 5 distinct rows instead of 7 M
+      uint4 ev[M], od[M], bfr[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (kStemAbl & 1) acc[rl][j][0] += __uint_as_float(bfr[j].x ^ af[rl].y);
-            else O::mma(acc[rl][j], bfr[j], af[rl]);
-          }
-      } else {  // twelve waves: fewer registers in flight
+      for (int kh = 0; kh < 7; ++kh) {
+        uint4 (&set)[M] = (kh & 1) ? od : ev;
+        bload(kh, bfr);
+        if (kh < 2) {
+#pragma unroll
+          for (int rl = 0; rl < M; ++rl) set[rl] = rd(kh + 2 * rl);
+        } else {
+#pragma unroll
+          for (int rl = 0; rl + 1 < M; ++rl) set[rl] = set[rl + 1];
+          set[M - 1] = rd(kh + 2 * (M - 1));
+        }
+        mmas(bfr, set);
+      }
+    } else {  // twelve waves: fewer registers in flight
+#pragma unroll 1
+      for (int kh = 0; kh < 7; ++kh) {
+        uint4 bfr[4];
+        bload(kh, bfr);
 #pragma unroll
         for (int rl = 0; rl < M; ++rl) {
-          const uint4 af = rd(rl);
+          const uint4 af = rd(kh + 2 * rl);
 #pragma unroll
           for (int j = 0; j < 4; ++j) O::mma(acc[rl][j], bfr[j], af);
         }

@@ -39,6 +39,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--only', type=int, choices=(256, 384), help='one input size (PMC calibration runs)')
     a = ap.parse_args()
     dev = torch.device('cuda', 0)
     g = torch.Generator().manual_seed(0)
@@ -47,6 +48,8 @@ def main():
     scale = (torch.rand(64, generator=g) + 0.5).to(dev)
     shift = (torch.randn(64, generator=g) * 0.1).to(dev)
     for nv, hw in ((32, 256), (16, 384)):
+        if a.only and hw != a.only:
+            continue
         views = [torch.randn(nv, 3, hw, hw, generator=g).to(dev) for _ in range(4)]
         out = ops.stem_pool_views(views, wpk, scale, shift, BF16)
         us = timeit(lambda: ops.stem_pool_views(views, wpk, scale, shift, BF16, out=out), a.reps, a.rounds)
