@@ -120,7 +120,7 @@ def parse():
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` leg times it in the same process, so a gain shows on the driver's own box
-CONTROL_FLAGS = ('S2_TAIL', 'STEM_VIEWS', 'TILES_128X8', 'PRECISE_HEAD')
+CONTROL_FLAGS = ('S2_TAIL', 'S2_CHAIN', 'STEM_VIEWS', 'TILES_128X8', 'PRECISE_HEAD')
 
 
 def apply_plan_flags(flags):

@@ -50,7 +50,8 @@ const char* posu_last_error(void);
  * tails take their weight stream's byte size, the round-2 LDS-ring layer2 block / layer3 tail
  * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) the
  * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
- * optional split-precision head (hw_lo).  The ctypes binding refuses a library of another revision. */
+ * optional split-precision head (hw_lo); 12 the chained strided tail
+ * (posu_bottleneck_s2_tail_next_fwd).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -231,6 +232,19 @@ int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* 
 int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
                                 const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
                                 const float* shift, int Cout, void* y, void* stream);
+
+/* The same, chained with the next (identity) Bottleneck's conv1 + BN1 + ReLU (ABI 12), as
+ * posu_bottleneck_tail_stream_next_fwd chains the identity tails: while each 128-channel chunk of
+ * y is produced, the tail also runs the next block's conv1 over it, and writes
+ * t1n = relu(conv1n(y) * s1n + b1n) [N, H/2, 32, 128] -- bit-identical to posu_conv2d_fwd over y
+ * (lib/models/pose_resnet.py:79-81 of layer2's block 1), which then has no conv1 launch and y is
+ * not re-read for it.  wstream: packing.pack_s2_tail_stream(conv2 pack, dual pack, next conv1
+ * pack [128][512]), [4][100][2][64][8]; s1n / b1n the next conv1's folded BN [128] f32 (16-B
+ * aligned); t1n must alias no other operand. */
+int posu_bottleneck_s2_tail_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                                     const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
+                                     const float* shift, int Cout, void* y, const float* s1n, const float* b1n,
+                                     void* t1n, void* stream);
 
 /* The same fused block for the first Bottleneck of layer1 (lib/models/pose_resnet.py:61-99
  * with the downsample branch, pose_resnet.py:136-141): conv3/bn3 and the 1x1 downsample/bn

@@ -268,8 +268,9 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     }
     ld8(bn + c0, sc);
     ld8(bn + 64 + c0, sh);
+    pk_affine8(v, sc, sh);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ok ? fmaxf(v[e] * sc[e] + sh[e], 0.f) : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = ok ? fmaxf(v[e], 0.f) : 0.f;
     *reinterpret_cast<uint4*>(slot + swz(px + 1, c0 >> 3)) = O::store_vals(v);
   };
   // conv2 of output row y, n-tiles 2h, 2h+1, over ring rows y-1..y+1; BN2 + ReLU, rounded:
@@ -305,12 +306,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     const float4 hb = *reinterpret_cast<const float4*>(bn + 192 + cb2);
     const float s8[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
     const float h8[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
-    float v[8];
+    float v[8] = {acc2[0][0], acc2[0][1], acc2[0][2], acc2[0][3], acc2[1][0], acc2[1][1], acc2[1][2], acc2[1][3]};
+    pk_affine8(v, s8, h8);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      v[e] = fmaxf(acc2[0][e] * s8[e] + h8[e], 0.f);
-      v[4 + e] = fmaxf(acc2[1][e] * s8[4 + e] + h8[4 + e], 0.f);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     return O::store_vals(v);
   };
   // conv3 of output row y, channels 128 h .. 128 h + 127, + BN3 + residual (this wave's half
@@ -374,8 +373,10 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
         } else {
           ld8(bn + 256 + c0, sc);
           O::load_vals(res[2 * qh + jp], r);
+          pk_affine8(v, sc, sh);
+          pk_add8(v, r);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         // channels c0 .. c0 + 7 = 128 h + 32 (2 qh + jp) + cq, packed HERE (the empty asm
         // keeps the compiler from sinking the packing, and 8 live f32 per value, into the

@@ -91,7 +91,11 @@ constexpr int kEarlyNK = 8;
 
 // BM x BN tile, NW waves (NT = 64*NW threads) in a WGM x (NW/WGM) grid, S-slot ring.
 // SG: eight-wave tiles with waves 4-7 staggered by half a K-tile (two-slot ring).
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false>
+// HD: the instance that carries the fused 1x1 head in its epilogue (256x256 eight-wave tiles
+// only).  Its registers (head accumulators and weight fragments) made the 256x256 instance
+// spill 36 VGPRs to scratch in every launch until round 4, head or not; the plain instances
+// no longer hold that code (228 VGPRs, no scratch).
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false, bool HD = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int NT = NW * 64;
@@ -459,7 +463,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // wave's rounded outputs are already MFMA B fragments (8 consecutive channels of one
   // pixel per lane), so its partial heatmaps over its 64 channels are 2 MFMAs per m-tile;
   // the four column waves' partials are summed in LDS in a fixed order.
-  constexpr bool HEAD256 = BM == 256 && BN == 256 && NW == 8 && WGM == 2 && E == 8;
+  constexpr bool HEAD256 = HD && BM == 256 && BN == 256 && NW == 8 && WGM == 2 && E == 8;
+  static_assert(!HD || HEAD256, "the fused head runs on the 2-byte 256x256 eight-wave tile");
   if constexpr (SG && (POSU_IG_ABLATE & 16)) {  // timing ablation: no epilogue (results wrong)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -467,95 +472,68 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
     return;
   }
-  if (E == 8 && TN % 2 == 0 && g.mode == 0 && (!g.hm || HEAD256)) {
-    // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
-    // holds 8 consecutive channels (16-B stores, half the store instructions):
-    // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
+  if constexpr (HEAD256) {  // the HD instance: launched only with g.hm set, no other epilogue
     T* __restrict__ yp = reinterpret_cast<T*>(g.y);
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     constexpr int TP = TN / 2;
-    const bool head = HEAD256 && g.hm != nullptr;
-    uint4 hwf[HEAD256 ? TP : 1], hwl[HEAD256 ? TP : 1];
-    f32x4 hacc[HEAD256 ? TM : 1];
-    const bool split = HEAD256 && head && g.hw_lo != nullptr;
-    if constexpr (HEAD256) {
-      if (head) {
+    {
+        // fused head: pair jp outer, m-tile inner -- one pair's BN parameters and head fragments
+        // are live at a time and each accumulator pair dies once consumed (the 256x256 head
+        // instance spilled 38 VGPRs with m-tile outer); every hacc[i] still receives its MFMAs in
+        // the same order (pair 0's, then pair 1's), so the heatmaps are unchanged
+        const bool split = g.hw_lo != nullptr;
         const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
         const T* __restrict__ hwq = reinterpret_cast<const T*>(split ? g.hw_lo : g.hw);
-#pragma unroll
-        for (int jp = 0; jp < TP; ++jp) {  // joint r16, this lane's 8 channels of pair jp
-          const size_t o = static_cast<size_t>(r16) * g.hkp + n0 + colB(2 * jp) + 16 * (q & 1) + 8 * (q >> 1);
-          hwf[jp] = *reinterpret_cast<const uint4*>(hwp + o);
-          hwl[jp] = *reinterpret_cast<const uint4*>(hwq + o);
-        }
+        f32x4 hacc[TM];
 #pragma unroll
         for (int i = 0; i < TM; ++i) hacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    int cop[TP];
-    float sc[TP][8], sh[TP][8];
+        const bool need_pix = yp != nullptr || rp != nullptr;
 #pragma unroll
-    for (int jp = 0; jp < TP; ++jp) {
-      // 8 consecutive channels, all inside Cout or all past it (Cout is a multiple of 8): two
-      // 16-B loads per parameter instead of eight 4-B ones
-      cop[jp] = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
-      const bool in = cop[jp] < g.Cout;
-      const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 s0 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp]) : one;
-      const float4 s1 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp] + 4) : one;
-      const float4 h0 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp]) : zero;
-      const float4 h1 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp] + 4) : zero;
-      sc[jp][0] = s0.x; sc[jp][1] = s0.y; sc[jp][2] = s0.z; sc[jp][3] = s0.w;
-      sc[jp][4] = s1.x; sc[jp][5] = s1.y; sc[jp][6] = s1.z; sc[jp][7] = s1.w;
-      sh[jp][0] = h0.x; sh[jp][1] = h0.y; sh[jp][2] = h0.z; sh[jp][3] = h0.w;
-      sh[jp][4] = h1.x; sh[jp][5] = h1.y; sh[jp][6] = h1.z; sh[jp][7] = h1.w;
-    }
-    // the fused head without the deconv output stored reads no pixel address: skip the decode
-    const bool no_pix = head && yp == nullptr && rp == nullptr;
+        for (int jp = 0; jp < TP; ++jp) {
+          // 8 consecutive channels cp .. cp + 7 of this lane (all inside Cout or all past it)
+          const int cp = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
+          const bool in = cp < g.Cout;
+          const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 s0 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cp) : one;
+          const float4 s1 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cp + 4) : one;
+          const float4 h0 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cp) : zero;
+          const float4 h1 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cp + 4) : zero;
+          const float sc8[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+          const float sh8[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          // joint r16's weights over this lane's 8 channels
+          const size_t o = static_cast<size_t>(r16) * g.hkp + cp;
+          const uint4 hw = *reinterpret_cast<const uint4*>(hwp + o);
+          const uint4 hl = *reinterpret_cast<const uint4*>(hwq + o);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + rowA(i) + r16;
-      const bool mok = m < g.M;
-      size_t pix = 0;
-      if (!no_pix) {
-        const int mm = mok ? m : 0;
-        const int n = mm / HoWo, rem = mm - n * HoWo;
-        const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-        pix = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
-      }
-      uint4 rv[TP];
+          for (int i = 0; i < TM; ++i) {
+            const int m = m0 + rowA(i) + r16;
+            const bool mok = m < g.M;
+            size_t pix = 0;
+            if (need_pix) {
+              const int mm = mok ? m : 0;
+              const int n = mm / HoWo, rem = mm - n * HoWo;
+              const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+              pix = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+            }
+            float v[8], r[8];
 #pragma unroll
-      for (int jp = 0; jp < TP; ++jp) {
-        rv[jp] = make_uint4(0, 0, 0, 0);
-        if constexpr (EARLY) {
-          if (early) {
-            rv[jp] = rve[i][jp];
-            continue;
-          }
-        }
-        if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
-      }
+            for (int e = 0; e < 4; ++e) {
+              const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                               __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+              v[e] = __uint_as_float(sw[0]);
+              v[4 + e] = __uint_as_float(sw[1]);
+            }
+            uint4 rv = make_uint4(0, 0, 0, 0);
+            if (rp && mok && in) rv = *reinterpret_cast<const uint4*>(rp + pix + cp);
+            O::load_vals(rv, r);
+            pk_affine8(v, sc8, sh8);  // BN as packed FMAs
+            if (rp) pk_add8(v, r);
+            if (g.relu) {
 #pragma unroll
-      for (int jp = 0; jp < TP; ++jp) {
-        float v[8], r[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
-                                                           __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
-          v[e] = __uint_as_float(sw[0]);
-          v[4 + e] = __uint_as_float(sw[1]);
-        }
-        O::load_vals(rv[jp], r);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = v[e] * sc[jp][e] + sh[jp][e];
-          if (rp) v[e] += r[e];
-          if (g.relu) v[e] = fmaxf(v[e], 0.f);
-        }
-        if constexpr (HEAD256) {
-          if (head) {
+              for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+            }
             const uint4 pk = O::store_vals(v);
-            O::mma(hacc[i], hwf[jp], pk);  // rows = joints, cols = pixels
+            O::mma(hacc[i], hw, pk);  // rows = joints, cols = pixels
             if (split) {
               // the deconv output's rounding residual v - round(v) (exact in f32) rounded again: the
               // head sees v to 2 x the dtype's mantissa, its weights likewise (hi.hi + lo.hi + hi.lo)
@@ -564,18 +542,12 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) vl[e] = v[e] - vr[e];
               const uint4 pl = O::store_vals(vl);
-              O::mma(hacc[i], hwl[jp], pk);
-              O::mma(hacc[i], hwf[jp], pl);
+              O::mma(hacc[i], hl, pk);
+              O::mma(hacc[i], hw, pl);
             }
-            if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = pk;
-            continue;
+            if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cp) = pk;
           }
         }
-        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
-      }
-    }
-    if constexpr (HEAD256) {
-      if (head) {
         if constexpr (SG && (POSU_IG_ABLATE & 32)) {  // timing ablation: no head reduction / stores
 #pragma unroll
           for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(hacc[i]));
@@ -600,6 +572,72 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
           g.hm[(static_cast<size_t>(n) * g.J + j) * HWo + (oy * osc + oy_off) * g.out_W + ox * osc + ox_off] = sum;
         }
+        return;
+      }
+  } else if (E == 8 && TN % 2 == 0 && g.mode == 0 && !g.hm) {
+    // 2-byte outputs: v_permlane16_swap pairs the n-tiles (j, j+1) so that every lane
+    // holds 8 consecutive channels (16-B stores, half the store instructions):
+    // lane (r16, q) gets n-tile j + (q & 1), channels 8 * (q >> 1) .. + 7 of pixel r16
+    T* __restrict__ yp = reinterpret_cast<T*>(g.y);
+    const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
+    constexpr int TP = TN / 2;
+    int cop[TP];
+    float sc[TP][8], sh[TP][8];
+#pragma unroll
+    for (int jp = 0; jp < TP; ++jp) {
+      // 8 consecutive channels, all inside Cout or all past it (Cout is a multiple of 8): two
+      // 16-B loads per parameter instead of eight 4-B ones
+      cop[jp] = n0 + colB(2 * jp + (q & 1)) + 8 * (q >> 1);
+      const bool in = cop[jp] < g.Cout;
+      const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 s0 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp]) : one;
+      const float4 s1 = in && g.scale ? *reinterpret_cast<const float4*>(g.scale + cop[jp] + 4) : one;
+      const float4 h0 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp]) : zero;
+      const float4 h1 = in && g.shift ? *reinterpret_cast<const float4*>(g.shift + cop[jp] + 4) : zero;
+      sc[jp][0] = s0.x; sc[jp][1] = s0.y; sc[jp][2] = s0.z; sc[jp][3] = s0.w;
+      sc[jp][4] = s1.x; sc[jp][5] = s1.y; sc[jp][6] = s1.z; sc[jp][7] = s1.w;
+      sh[jp][0] = h0.x; sh[jp][1] = h0.y; sh[jp][2] = h0.z; sh[jp][3] = h0.w;
+      sh[jp][4] = h1.x; sh[jp][5] = h1.y; sh[jp][6] = h1.z; sh[jp][7] = h1.w;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + rowA(i) + r16;
+      const bool mok = m < g.M;
+      const int mm = mok ? m : 0;
+      const int n = mm / HoWo, rem = mm - n * HoWo;
+      const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
+      const size_t pix =
+          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+      uint4 rv[TP];
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        rv[jp] = make_uint4(0, 0, 0, 0);
+        if constexpr (EARLY) {
+          if (early) {
+            rv[jp] = rve[i][jp];
+            continue;
+          }
+        }
+        if (rp && mok && cop[jp] < g.Cout) rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + cop[jp]);
+      }
+#pragma unroll
+      for (int jp = 0; jp < TP; ++jp) {
+        float v[8], r[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * jp][e]),
+                                                           __float_as_uint(acc[i][2 * jp + 1][e]), false, false);
+          v[e] = __uint_as_float(sw[0]);
+          v[4 + e] = __uint_as_float(sw[1]);
+        }
+        O::load_vals(rv[jp], r);
+        pk_affine8(v, sc[jp], sh[jp]);  // BN as packed FMAs
+        if (rp) pk_add8(v, r);
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
       }
     }
   } else if (g.mode == 0 && !g.hm) {
@@ -1185,11 +1223,11 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
           v[4 + e] = __uint_as_float(sw[1]);
         }
         O::load_vals(rv[jp], r);
+        pk_affine8(v, sc[jp], sh[jp]);  // BN as packed FMAs
+        if (rp) pk_add8(v, r);
+        if (g.relu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = v[e] * sc[jp][e] + sh[jp][e];
-          if (rp) v[e] += r[e];
-          if (g.relu) v[e] = fmaxf(v[e], 0.f);
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
         const uint4 pk = O::store_vals(v);
         const u32x4 pv = {pk.x, pk.y, pk.z, pk.w};
@@ -1311,13 +1349,13 @@ bool tile_ok(int tile) {
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
-  if constexpr (sizeof(T) == 2) {  // fused head on the eight-wave 256x256 tile, direct epilogue
+  if constexpr (sizeof(T) == 2 && !DUAL) {  // fused head on the eight-wave 256x256 tile, direct epilogue
     if (g.hm && g.CoutPad == 256) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
       // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(g.mtiles * nclass), dim3(512), 0,
-                         s, g);
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true, true>), dim3(g.mtiles * nclass),
+                         dim3(512), 0, s, g);
       return check_launch(what);
     }
   }

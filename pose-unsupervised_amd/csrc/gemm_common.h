@@ -73,6 +73,44 @@ struct Op<float> {
   }
 };
 
+// v = v * s + b (+ r) over 8 values as four packed f32 FMAs (v_pk_fma_f32: two fused
+// multiply-adds per instruction, the same rounding as the scalar v_fma_f32) and packed adds;
+// the scalar loops spent one VALU issue per value on each.  POSU_PK_EPILOGUE=0: the scalar
+// loops (A/B builds only)
+#ifndef POSU_PK_EPILOGUE
+#define POSU_PK_EPILOGUE 1
+#endif
+__device__ __forceinline__ void pk_affine8(float* v, const float* s, const float* b) {
+  if (!POSU_PK_EPILOGUE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * s[e] + b[e];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x2v x = {v[2 * i], v[2 * i + 1]};
+    const f32x2v ss = {s[2 * i], s[2 * i + 1]}, bb = {b[2 * i], b[2 * i + 1]};
+    x = __builtin_elementwise_fma(x, ss, bb);
+    v[2 * i] = x.x;
+    v[2 * i + 1] = x.y;
+  }
+}
+__device__ __forceinline__ void pk_add8(float* v, const float* r) {
+  if (!POSU_PK_EPILOGUE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f32x2v x = {v[2 * i], v[2 * i + 1]};
+    const f32x2v rr = {r[2 * i], r[2 * i + 1]};
+    x = x + rr;
+    v[2 * i] = x.x;
+    v[2 * i + 1] = x.y;
+  }
+}
+
 __device__ __forceinline__ int swz(int row, int chunk) {
   return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4);
 }

@@ -41,13 +41,19 @@ struct TailS2Geom {
   const float* b2;
   const float* shift;  // b3 + bd [512]
   int N, Hin;
+  // NEXT (chained): the next identity block's conv1 + BN1 + ReLU over y while it is produced
+  // (t1n = relu(y conv1n * s1n + b1n), [N][Hin/2][32][128])
+  const float* s1n;
+  const float* b1n;
+  void* t1n;
 };
 
 #ifndef POSU_S2_KD
 #define POSU_S2_KD 4
 #endif
 
-struct S2 {
+template <bool NEXT>
+struct S2Cfg {
   static constexpr int kWin = 64, kC = 256, kP = 128, kCout = 512, kWout = 32;
   static constexpr int kRows = 4, kTW = 16, kNW = 4, kPx = kRows * kTW;   // 64 output px
   static constexpr int kWR = 2 * kRows + 1, kWC = 2 * kTW + 1;            // 9 x 33 window
@@ -62,19 +68,21 @@ struct S2 {
   static constexpr int kKT = kP / 32;                                     // k-steps per tap / over t2
   static constexpr int kKX = kC / 32;                                     // k-steps over x
   static constexpr int kNC = kCout / (32 * kNW);                          // dual chunks of 128 channels
-  static constexpr int kSteps2 = 9 * kKT, kStepsC = kKT + kKX;
-  static constexpr int kSteps = kSteps2 + kNC * kStepsC;                  // 36 + 4 x 12 = 84
+  // NEXT: after each dual chunk, the next conv1's kKT k-steps over that chunk's 128 y channels
+  static constexpr int kSteps2 = 9 * kKT, kStepsC = kKT + kKX + (NEXT ? kKT : 0);
+  static constexpr int kSteps = kSteps2 + kNC * kStepsC;                  // 36 + 4 x 12 = 84 (NEXT: 100)
+  static constexpr int kYC = kShift + kCout * 4;                          // NEXT: the y chunk [64 px][128 ch]
   static constexpr int kD = POSU_S2_KD;
-  static_assert(kShift + kCout * 4 <= kBN2, "t2, the x pixels and the shift fit over the window");
+  static_assert(kYC + (NEXT ? kPx * kRowB : 0) <= kBN2, "t2, the x pixels, the shift (and the y chunk) fit over the window");
   static_assert(2 * kLds <= 160 * 1024, "two workgroups per CU");
   static_assert(kKT % kD == 0 && kKX % kD == 0 && kSteps2 % kD == 0 && kStepsC % kD == 0,
                 "every block starts on ring slot 0");
 };
 
-template <typename T>
-__global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) {
+template <typename T, bool NEXT>
+__global__ __launch_bounds__(S2Cfg<NEXT>::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) {
   using O = Op<T>;
-  using K = S2;
+  using K = S2Cfg<NEXT>;
   constexpr int ES = 2, kD = K::kD, MT = K::kRows;
   __shared__ __attribute__((aligned(16))) char smem[K::kLds];
   const int tid = threadIdx.x;
@@ -129,16 +137,17 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
   lds_barrier();
 
   f32x4 acc[MT][2];
-  auto zero = [&]() {
+  f32x4 acc1[MT][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
+  auto zero = [&](f32x4 (&a)[MT][2]) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 2; ++j) a[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  auto pair = [&](int i, float* v) {
+  auto pair = [&](const f32x4 (&a)[MT][2], int i, float* v) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][0][e]), __float_as_uint(acc[i][1][e]),
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[i][0][e]), __float_as_uint(a[i][1][e]),
                                                        false, false);
       v[e] = __uint_as_float(sw[0]);
       v[4 + e] = __uint_as_float(sw[1]);
@@ -149,7 +158,7 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
   // compile-time d % kD) over an LDS image of RB-byte pixel rows: k-step d reads, for
   // m-tile i, the pixel lpix + coff(i) at 16-B chunk 4 d + q, XOR the lane's key (its LDS
   // column & 15).  The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run.
-  auto block = [&](auto nsteps, auto rowb, int p0, int base, int lpix, int key, auto coff) {
+  auto block = [&](f32x4 (&acc)[MT][2], auto nsteps, auto rowb, int p0, int base, int lpix, int key, auto coff) {
     constexpr int NS = decltype(nsteps)::value, RB = decltype(rowb)::value;
     uint4 b[2][MT];
     const char* lb = smem + base + lpix * RB + ((q ^ (key & 3)) << 4);
@@ -185,11 +194,11 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
 
   // ---- conv2: 9 taps x 4 channel steps; m-tile i = output row i: window row 2 i + dy, column
   // 2 r16 + dx
-  zero();
+  zero(acc);
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
     const int dy = t / 3, dx = t - 3 * (t / 3);
-    block(NKT{}, RBT{}, K::kKT * t, 0, dy * K::kWC + 2 * r16 + dx, (2 * r16 + dx) & 15,
+    block(acc, NKT{}, RBT{}, K::kKT * t, 0, dy * K::kWC + 2 * r16 + dx, (2 * r16 + dx) & 15,
           [&](int i) { return 2 * i * K::kWC; });
   }
   // every wave is done reading the window: the tile's stride-2 x pixels are DMA'd over it while
@@ -220,9 +229,10 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       float v[8];
-      pair(i, v);
+      pair(acc, i, v);
+      pk_affine8(v, sc, sh);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       *reinterpret_cast<uint4*>(smem + K::kT2 + (16 * i + r16) * K::kRowB + (((c0 >> 3) ^ r16) << 4)) =
           O::store_vals(v);
     }
@@ -234,24 +244,60 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
   // the 256 channels of x (2 oy, 2 ox)
   const float* shl = reinterpret_cast<const float*>(smem + K::kShift);
   T* yg = reinterpret_cast<T*>(g.y);
+  if constexpr (NEXT) zero(acc1);
 #pragma unroll
   for (int nc = 0; nc < K::kNC; ++nc) {
     const int p0 = K::kSteps2 + K::kStepsC * nc;
-    zero();
-    block(NKT{}, RBT{}, p0, K::kT2, r16, r16, [&](int i) { return 16 * i; });
-    block(NKX{}, RBX{}, p0 + K::kKT, K::kX, r16, r16, [&](int i) { return 16 * i; });
+    zero(acc);
+    block(acc, NKT{}, RBT{}, p0, K::kT2, r16, r16, [&](int i) { return 16 * i; });
+    block(acc, NKX{}, RBX{}, p0 + K::kKT, K::kX, r16, r16, [&](int i) { return 16 * i; });
     const int c0 = 128 * nc + 32 * cq + cpair;
     float sh[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) sh[e] = shl[c0 + e];
+    if constexpr (NEXT) {
+      if (nc > 0) lds_barrier();  // every wave is done reading the previous y chunk
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       float v[8];
-      pair(i, v);
+      pair(acc, i, v);
+      pk_add8(v, sh);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * 1.f + sh[e], 0.f);
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       const size_t pix = (static_cast<size_t>(n) * Hout + R0 + i) * K::kWout + C0 + r16;
-      *reinterpret_cast<uint4*>(yg + pix * K::kCout + c0) = O::store_vals(v);
+      const uint4 o = O::store_vals(v);
+      *reinterpret_cast<uint4*>(yg + pix * K::kCout + c0) = o;
+      // NEXT: the chunk's y (the rounded values just stored), laid out like t2
+      if constexpr (NEXT)
+        *reinterpret_cast<uint4*>(smem + K::kYC + (16 * i + r16) * K::kRowB + ((((c0 & 127) >> 3) ^ r16) << 4)) = o;
+    }
+    if constexpr (NEXT) {
+      // the next block's conv1 over this K slice (y channels 128 nc ..): the k order of a conv
+      // launch over y, so t1n is bit-identical to it
+      lds_barrier();
+      block(acc1, NKT{}, RBT{}, p0 + K::kKT + K::kKX, K::kYC, r16, r16, [&](int i) { return 16 * i; });
+    }
+  }
+  if constexpr (NEXT) {
+    // t1n = relu(conv1n * s1n + b1n): this lane's 8 channels of each m-tile's pixel
+    T* tg = reinterpret_cast<T*>(g.t1n);
+    const int c0 = 32 * cq + cpair;
+    float sc[8], sh[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sc[e] = g.s1n[c0 + e];
+      sh[e] = g.b1n[c0 + e];
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      float v[8];
+      pair(acc1, i, v);
+      pk_affine8(v, sc, sh);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      const size_t pix = (static_cast<size_t>(n) * Hout + R0 + i) * K::kWout + C0 + r16;
+      *reinterpret_cast<uint4*>(tg + pix * K::kP + c0) = O::store_vals(v);
     }
   }
 }
@@ -261,16 +307,18 @@ __global__ __launch_bounds__(S2::kNW * 64, 2) void tail_s2_kernel(TailS2Geom g) 
 
 using namespace posu;
 
-// The tail of the first Bottleneck of layer2 (see the top of this file).  wstream =
-// packing.pack_s2_tail_stream(conv2 pack [128][1152], dual pack [512][384]); wstream_bytes its size.
-extern "C" int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
-                                           int P, const void* wstream, long long wstream_bytes, const float* s2,
-                                           const float* b2, const float* shift, int Cout, void* y, void* stream) {
-  const std::string what = "posu_bottleneck_s2_tail_fwd";
-  using K = S2;
+namespace {
+int s2_tail_impl(const char* name, int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
+                 const void* wstream, long long wstream_bytes, const float* s2, const float* b2, const float* shift,
+                 int Cout, void* y, const float* s1n, const float* b1n, void* t1n, void* stream) {
+  const std::string what = name;
+  const bool next = t1n != nullptr;
+  using K = S2Cfg<false>;
   POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, what + ": dtype must be BF16 or F16");
   POSU_REQUIRE(t1 && x && wstream && s2 && b2 && shift && y, what + ": null pointer");
   POSU_REQUIRE(y != x && y != t1, what + ": the output must not alias an input");
+  POSU_REQUIRE(!next || (s1n && b1n && t1n != y && t1n != x && t1n != t1),
+               what + ": the next conv1 needs its BN and an output that aliases no other operand");
   POSU_REQUIRE(W == K::kWin && C == K::kC && P == K::kP && Cout == K::kCout,
                what + ": built for the first Bottleneck of layer2 of PoseResNet at 256x256 (input W = 64, C = 256, "
                       "planes = 128, output channels 512)");
@@ -278,10 +326,12 @@ extern "C" int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void
                what + ": H must be a positive multiple of " + std::to_string(2 * K::kRows));
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
-  const long long need = static_cast<long long>(K::kNW) * K::kSteps * 2 * 1024;
-  POSU_REQUIRE(wstream_bytes >= need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the kernel reads " +
-                                          std::to_string(need));
-  for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(shift)})
+  const long long need = static_cast<long long>(K::kNW) * (next ? S2Cfg<true>::kSteps : K::kSteps) * 2 * 1024;
+  POSU_REQUIRE(wstream_bytes >= need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
+                                          (next ? "chained" : "plain") + " kernel reads " + std::to_string(need));
+  for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(shift),
+                        next ? t1n : t1, static_cast<const void*>(next ? s1n : shift),
+                        static_cast<const void*>(next ? b1n : shift)})
     POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, what + ": pointers must be 16-byte aligned");
   TailS2Geom g{};
   g.t1 = t1;
@@ -293,11 +343,43 @@ extern "C" int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void
   g.shift = shift;
   g.N = N;
   g.Hin = H;
+  g.s1n = s1n;
+  g.b1n = b1n;
+  g.t1n = t1n;
   const dim3 grid(static_cast<unsigned>(N * (H / 2 / K::kRows) * (K::kWout / K::kTW)));
   hipStream_t s = as_stream(stream);
-  if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_s2_kernel<uint16_t>), grid, dim3(K::kNW * 64), 0, s, g);
-  else
-    hipLaunchKernelGGL((tail_s2_kernel<f16_t>), grid, dim3(K::kNW * 64), 0, s, g);
-  return check_launch(what.c_str());
+  if (dtype == POSU_BF16) {
+    if (next) hipLaunchKernelGGL((tail_s2_kernel<uint16_t, true>), grid, dim3(K::kNW * 64), 0, s, g);
+    else hipLaunchKernelGGL((tail_s2_kernel<uint16_t, false>), grid, dim3(K::kNW * 64), 0, s, g);
+  } else {
+    if (next) hipLaunchKernelGGL((tail_s2_kernel<f16_t, true>), grid, dim3(K::kNW * 64), 0, s, g);
+    else hipLaunchKernelGGL((tail_s2_kernel<f16_t, false>), grid, dim3(K::kNW * 64), 0, s, g);
+  }
+  return check_launch(name);
+}
+}  // namespace
+
+// The tail of the first Bottleneck of layer2 (see the top of this file).  wstream =
+// packing.pack_s2_tail_stream(conv2 pack [128][1152], dual pack [512][384]); wstream_bytes its size.
+extern "C" int posu_bottleneck_s2_tail_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                           int P, const void* wstream, long long wstream_bytes, const float* s2,
+                                           const float* b2, const float* shift, int Cout, void* y, void* stream) {
+  return s2_tail_impl("posu_bottleneck_s2_tail_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes, s2, b2,
+                      shift, Cout, y, nullptr, nullptr, nullptr, stream);
+}
+
+// The same, chained with the next (identity) block's conv1 + BN1 + ReLU over y, like
+// posu_bottleneck_tail_stream_next_fwd: t1n [N][H/2][32][128] is bit-identical to a conv launch
+// over y, and that block skips its conv1 launch.  wstream = packing.pack_s2_tail_stream(conv2
+// pack, dual pack, next conv1 pack [128][512]).
+extern "C" int posu_bottleneck_s2_tail_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                                int P, const void* wstream, long long wstream_bytes, const float* s2,
+                                                const float* b2, const float* shift, int Cout, void* y,
+                                                const float* s1n, const float* b1n, void* t1n, void* stream) {
+  if (!t1n) {
+    set_error("posu_bottleneck_s2_tail_next_fwd: null pointer (t1n)");
+    return POSU_ERR_ARG;
+  }
+  return s2_tail_impl("posu_bottleneck_s2_tail_next_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes, s2,
+                      b2, shift, Cout, y, s1n, b1n, t1n, stream);
 }

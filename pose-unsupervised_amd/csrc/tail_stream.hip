@@ -195,6 +195,20 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_
     }
   };
   const int cpair = 16 * (q & 1) + 8 * (q >> 1);
+  // relu(v * sc + sh (+ r)) over 8 values: packed FMAs / adds, except in the chained variant,
+  // whose second accumulator set leaves no room for the even-aligned register pairs they need
+  // (it spilled with them): there the round-3 scalar loop
+  auto bn_relu = [&](float* v, const float* sc, const float* sh, const float* r) {
+    if constexpr (NEXT) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + (r ? r[e] : 0.f), 0.f);
+    } else {
+      pk_affine8(v, sc, sh);
+      if (r) pk_add8(v, r);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+  };
   // m-tile i's tile pixel (row-major in the tile) for this lane
   auto tpix = [&](int i) { return 16 * MT * pg + 16 * i + r16; };
   // one block of kKT k-steps (one conv2 tap, or one conv3 output chunk over t2's P channels):
@@ -276,8 +290,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_
     for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc, i, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+      bn_relu(v, sc, sh, nullptr);
       *reinterpret_cast<uint4*>(smem + swzp<K::kRowB>(tpix(i), r16, c0 >> 3)) = O::store_vals(v);
     }
   }
@@ -302,8 +315,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_
       float v[8], r[8];
       pair(acc, i, v);
       O::load_vals(rv[i], r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + r[e], 0.f);
+      bn_relu(v, sc, sh, r);
       const uint4 o = O::store_vals(v);
       if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
       else *reinterpret_cast<uint4*>(yg + tpix(i) * C + c0) = o;
@@ -340,8 +352,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_
     for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc1, i, v);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e], 0.f);
+      bn_relu(v, sc, sh, nullptr);
       *reinterpret_cast<uint4*>(tg + tpix(i) * P + c0) = O::store_vals(v);
     }
   }

@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -47,6 +47,7 @@ _SIGNATURES = {
     'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _p],
     'posu_bottleneck_s2_tail_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p],
+    'posu_bottleneck_s2_tail_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p, _p, _p, _p],
     'posu_bottleneck_down_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],

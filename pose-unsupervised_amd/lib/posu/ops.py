@@ -123,6 +123,22 @@ def bottleneck_s2_tail_nhwc(t1, x, wstream, s2, b2, shift, code, out=None):
     return out
 
 
+def bottleneck_s2_tail_next_nhwc(t1, x, wstream, s2, b2, shift, s1n, b1n, code, out=None, t1n=None):
+    """The strided tail chained with the next identity block's conv1 + BN1 + ReLU over y
+    (posu_bottleneck_s2_tail_next_fwd); wstream = packing.pack_s2_tail_stream(conv2 pack, dual pack,
+    next conv1 pack).  Returns (y, t1n) with t1n [N, H/2, 32, 128] bit-identical to a conv launch of
+    the next conv1 over y."""
+    n, h, w, c = x.shape
+    if out is None:
+        out = torch.empty((n, h // 2, w // 2, shift.numel()), dtype=x.dtype, device=x.device)
+    if t1n is None:
+        t1n = torch.empty((n, h // 2, w // 2, s1n.numel()), dtype=x.dtype, device=x.device)
+    call('posu_bottleneck_s2_tail_next_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(shift), shift.numel(), ptr(out), ptr(s1n),
+         ptr(b1n), ptr(t1n), stream_of(x.device))
+    return out, t1n
+
+
 def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, code, out=None, t1n=None):
     """The tail above chained with the NEXT identity block's conv1 + BN1 + ReLU over its output
     (posu_bottleneck_tail_stream_next_fwd); wstream = packing.pack_tail_stream(conv2 pack, conv3

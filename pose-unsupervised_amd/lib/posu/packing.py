@@ -36,12 +36,16 @@ def mfma_fragments(wpk):
     return wpk.reshape(co // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).reshape(co // 16, k // 32, 64, 8)
 
 
-def pack_s2_tail_stream(w2pk, wdual):
+def pack_s2_tail_stream(w2pk, wdual, w1n=None):
     """The per-wave weight streams of posu_bottleneck_s2_tail_fwd (csrc/tail_s2.hip) from the conv2
     [128][1152] (posu_conv2d_fwd) and dual [512][384] (pack_dual_1x1_weight) packs:
     [4 channel groups][84 k-steps][2 n-tiles][64 lanes][8].  Group cq, k-step p < 36: conv2 n-tile
     2 cq + j, k-step p (tap-major K); p = 36 + 12 nc + c: dual n-tile 8 nc + 2 cq + j, k-step c
-    (t2's 4 k-steps, then x's 8)."""
+    (t2's 4 k-steps, then x's 8).
+
+    w1n (the next identity block's conv1 pack [128][512], posu_bottleneck_s2_tail_next_fwd): after
+    dual chunk nc's 12 k-steps come the next conv1's 4 k-steps over that chunk's 128 y channels --
+    [4][100][2][64][8], p = 36 + 16 nc + 12 + c: conv1n n-tile 2 cq + j, k-step 4 nc + c."""
     if tuple(w2pk.shape) != (128, 1152) or tuple(wdual.shape) != (512, 384):
         raise ValueError('pack_s2_tail_stream: conv2 pack [128][1152] and dual pack [512][384] expected, got %s / %s'
                          % (tuple(w2pk.shape), tuple(wdual.shape)))
@@ -49,7 +53,14 @@ def pack_s2_tail_stream(w2pk, wdual):
     s2 = f2.reshape(4, 2, 36, 64, 8).permute(0, 2, 1, 3, 4)       # [cq][36][j][64][8]
     fd = mfma_fragments(wdual)                                    # [32][12][64][8]
     sd = fd.reshape(4, 4, 2, 12, 64, 8).permute(1, 0, 3, 2, 4, 5)  # [cq][nc][12][j][64][8]
-    return torch.cat([s2, sd.reshape(4, 48, 2, 64, 8)], dim=1).contiguous()
+    if w1n is None:
+        return torch.cat([s2, sd.reshape(4, 48, 2, 64, 8)], dim=1).contiguous()
+    if tuple(w1n.shape) != (128, 512):
+        raise ValueError('pack_s2_tail_stream: the next conv1 pack must be [128][512], got %s' % (tuple(w1n.shape),))
+    f1 = mfma_fragments(w1n)                                      # [8][16][64][8]
+    s1 = f1.reshape(4, 2, 4, 4, 64, 8).permute(0, 2, 3, 1, 4, 5)  # [cq][nc][4][j][64][8]
+    sdn = torch.cat([sd, s1], dim=2)                              # [cq][nc][16][j][64][8]
+    return torch.cat([s2, sdn.reshape(4, 64, 2, 64, 8)], dim=1).contiguous()
 
 
 def pack_tail_stream(w2pk, w3pk, w1n=None):

@@ -185,6 +185,9 @@ S2_TAIL = True
 # is not re-read for it (tools/chain_micro.py: layer2 105.0 vs 130.0 us, layer3 76.3 vs 85.0 us
 # for a tail + the next conv1 launch; bit-identical)
 CHAINED_TAILS = True
+# layer2's strided tail chained with block 1's conv1 (posu_bottleneck_s2_tail_next_fwd, round 4;
+# under CHAINED_TAILS too)
+S2_CHAIN = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -197,7 +200,7 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -212,6 +215,7 @@ class _Block:
         self.chain = None            # the next identity block's conv1 (_Conv) when the tails chain
         self.wsn = None              # the streams with that conv1 appended (pack_tail_stream(.., w1n))
         self.ws2 = None              # layer2 block 0: the strided tail's weight streams (pack_s2_tail_stream)
+        self.ws2n = None             # ... with the next block's conv1 appended (the chained strided tail)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -249,6 +253,9 @@ class _Block:
         if (self.l2 and nxt.l2) or (self.l3 and nxt.l3):
             self.chain = nxt.convs[0]
             self.wsn = pack_tail_stream(self.convs[1].w, self.convs[2].w, self.chain.w)
+        elif self.ws2 is not None and nxt.l2:   # layer2's strided tail and block 1's conv1
+            self.chain = nxt.convs[0]
+            self.ws2n = pack_s2_tail_stream(self.convs[1].w, self.dual.w, self.chain.w)
 
     def _tail_kind(self, x):
         """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
@@ -268,6 +275,11 @@ class _Block:
         if kind is None:
             if t1 is not None:
                 raise RuntimeError('a chained conv1 output handed to a block without a streamed tail')
+            if self.ws2n is not None and CHAINED_TAILS and S2_CHAIN and self._s2_tail_ok(x):
+                c1, c2 = self.convs
+                n1 = self.chain
+                return ops.bottleneck_s2_tail_next_nhwc(c1(x, code), x, self.ws2n, c2.scale, c2.shift, self.dual.shift,
+                                                        n1.scale, n1.shift, code, out=out)
             return self(x, code, out=out), None
         c1, c2, c3 = self.convs
         if t1 is None:
@@ -278,6 +290,11 @@ class _Block:
                                                         n1.scale, n1.shift, code, out=out)
         return ops.bottleneck_tail_stream_nhwc(t1, x, self.wst, c2.scale, c2.shift, c3.scale, c3.shift, code,
                                                out=out), None
+
+    def _s2_tail_ok(self, x):
+        """layer2's first block runs conv1 + the strided tail (S2_TAIL)."""
+        return (self.ws2 is not None and S2_TAIL and FUSED_BOTTLENECK and _fused_fits(x, self.cout) and
+                x.shape[2] == 64 and x.shape[1] % 8 == 0)
 
     def _layer2_shape(self):
         c1, c2, c3 = self.convs
@@ -308,8 +325,7 @@ class _Block:
             c1, c2 = self.convs
             return ops.bottleneck_down_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3d,
                                             self.dual.shift, code, out=out)
-        if (self.ws2 is not None and S2_TAIL and FUSED_BOTTLENECK and fits and x.shape[2] == 64 and
-                x.shape[1] % 8 == 0):
+        if self._s2_tail_ok(x):
             c1, c2 = self.convs
             return ops.bottleneck_s2_tail_nhwc(c1(x, code), x, self.ws2, c2.scale, c2.shift, self.dual.shift, code,
                                                out=out)

@@ -4,10 +4,10 @@
 Per launch: the bytes a kernel must move at least -- every input activation it needs read once
 (for a stride-2 1x1 source only its stride-2 pixels), its weights read once, its outputs written
 once.  The launch list is the default plan's (plan.py: fused stem over all views, fused layer1
-blocks, layer2 conv1 + strided tail, chained streamed tails, conv launches for layer3 block 0 and
-layer4, deconv1, deconv2, deconv3 with the fused head writing f32 heatmaps only):
-31 launches.  Comparing it with the PMC traffic of the same launches (FETCH_SIZE x 2 + WRITE_SIZE,
-tools/pmc_traffic.py) gives each kernel's over-fetch.
+blocks, layer2 conv1 + the strided tail chained with block 1's conv1, chained streamed tails, conv
+launches for layer3 block 0 and layer4, deconv1, deconv2, deconv3 with the fused head writing f32
+heatmaps only): 30 launches.  Comparing it with the PMC traffic of the same launches
+(FETCH_SIZE x 2 + WRITE_SIZE, tools/pmc_traffic.py) gives each kernel's over-fetch.
 """
 
 # R50 PoseResNet stages: (blocks, planes, in channels, out channels, input spatial at 256x256)
@@ -27,11 +27,12 @@ def r50_256_launches(n=128, es=2, joints=17):
     for b in (1, 2):
         out.append(('layer1.%d bottleneck64' % b, act(64, 256) + wb(64, 256) + wb(64, 576) + wb(256, 64),
                     act(64, 256)))
-    # layer2: conv1 at 64x64, the strided tail, conv1 of block 1, chained tails, the last tail
+    # layer2: conv1 at 64x64, the strided tail (chained), chained tails, the last tail
     out.append(('layer2.0 conv1', act(64, 256) + wb(128, 256), act(64, 128)))
-    out.append(('layer2.0 strided tail (conv2 s2 + conv3|down)',
-                act(64, 128) + act(32, 256) + wb(128, 1152) + wb(512, 384), act(32, 512)))
-    out.append(('layer2.1 conv1', act(32, 512) + wb(128, 512), act(32, 128)))
+    # the strided tail chained with block 1's conv1 (S2_CHAIN): y and block 1's t1 written
+    out.append(('layer2.0 strided tail + layer2.1 conv1',
+                act(64, 128) + act(32, 256) + wb(128, 1152) + wb(512, 384) + wb(128, 512),
+                act(32, 512) + act(32, 128)))
     for b in (1, 2):
         out.append(('layer2.%d chained tail' % b, act(32, 128) + act(32, 512) + wb(128, 1152) + wb(512, 128) +
                     wb(128, 512), act(32, 512) + act(32, 128)))

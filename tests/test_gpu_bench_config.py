@@ -75,7 +75,13 @@ def _bench_plan_outputs(cuda, precision, autotune, layers=LAYERS, size=SIZE, gro
         rep.stage_geo(rep.stage_net())
         if autotune:
             plan.autotune(plan.pack_input(rep.views), keep_features=False, reps=2)
-            assert len(P.tuned_tiles()) >= 15   # every unfused conv geometry of the plan
+            # every unfused conv geometry of the plan: layer2 block 0's conv1 (64x64 input), layer3
+            # block 0's three convs + block 1's conv1, layer4's six distinct geometries, deconv1,
+            # deconv2; layer2 block 0's conv2 and dual GEMM run in the strided tail (else +2), which
+            # also computes block 1's conv1 when chained (else +1: a 32x32 conv1 launch)
+            s2 = P.S2_TAIL and P.FUSED_BOTTLENECK
+            expect = 12 + (0 if s2 else 2) + (0 if s2 and P.S2_CHAIN and P.CHAINED_TAILS else 1)
+            assert len(P.tuned_tiles()) >= expect
         rep.capture()
         rep.run_geo(rep.run_net())
         coords, loss, X = rep.run_geo(rep.run_net())

@@ -238,6 +238,41 @@ def test_layer2_first_block_strided_tail_matches_two_launches_and_torch(cuda, co
     assert float(err.max()) <= tol * float(ref.abs().max()) + tol, float(err.max())
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(1, 8), (2, 16), (3, 24), (128, 64)])
+def test_chained_strided_tail_matches_tail_and_next_conv1(cuda, code, n, h):
+    """posu_bottleneck_s2_tail_next_fwd: the strided tail computing layer2 block 1's conv1 + BN1 +
+    ReLU over its output while it is produced.  y and t1n are bit-identical to the plain strided
+    tail followed by a conv launch of that conv1 over y; both outputs start as NaN sentinels."""
+    g = torch.Generator().manual_seed(191 + h + n)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=512, p=128)
+    w1 = w1[:, :256].contiguous() * 2 ** 0.5
+    wd = torch.randn(512, 256, 1, 1, generator=g) * (2.0 / 256) ** 0.5 * 0.3
+    bnd = (torch.rand(512, generator=g) + 0.5, torch.randn(512, generator=g) * 0.1)
+    w1n = torch.randn(128, 512, 1, 1, generator=g) * (2.0 / 512) ** 0.5
+    bn1n = (torch.rand(128, generator=g) + 0.5, torch.randn(128, generator=g) * 0.1)
+    dt = ops.torch_dtype(code)
+    bk = ops.conv_bk(code)
+    xd = torch.randn(n, h, 64, 256, generator=g).abs().to(cuda, dt)
+    p1 = packing.pack_conv_weight(w1.to(cuda), 256, bk, dt)
+    p2 = packing.pack_conv_weight(w2.to(cuda), 128, bk, dt)
+    p1n = packing.pack_conv_weight(w1n.to(cuda), 512, bk, dt)
+    pdual = packing.pack_dual_1x1_weight(w3.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), dt)
+    shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn1n[0], bn1n[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, 128, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    y_ref = ops.bottleneck_s2_tail_nhwc(t1, xd, packing.pack_s2_tail_stream(p2, pdual), s[2], s[3], shift, code)
+    t1n_ref = ops.conv2d_nhwc(y_ref, p1n, 128, 1, 1, 1, 0, s[4], s[5], None, True, code)
+    y, t1n = ops.bottleneck_s2_tail_next_nhwc(t1, xd, packing.pack_s2_tail_stream(p2, pdual, p1n), s[2], s[3], shift,
+                                              s[4], s[5], code, out=_sentinel(xd, (n, h // 2, 32, 512)),
+                                              t1n=_sentinel(xd, (n, h // 2, 32, 128)))
+    torch.cuda.synchronize()
+    dy = int((y.view(torch.int16) != y_ref.view(torch.int16)).sum())
+    dt1 = int((t1n.view(torch.int16) != t1n_ref.view(torch.int16)).sum())
+    print('chained strided tail n=%d h=%d: y differing %d, t1n differing %d' % (n, h, dy, dt1))
+    assert dy == 0 and dt1 == 0
+
+
 def test_strided_tail_refuses_unsupported_shapes(cuda):
     x = torch.zeros(1, 8, 64, 256, device=cuda, dtype=torch.bfloat16)
     t1 = torch.zeros(1, 8, 64, 128, device=cuda, dtype=torch.bfloat16)
@@ -253,6 +288,16 @@ def test_strided_tail_refuses_unsupported_shapes(cuda):
         ops.bottleneck_s2_tail_nhwc(t1, x, ws[:3], s, s, s, BF16)
     with pytest.raises(ValueError, match='pack_s2_tail_stream'):
         packing.pack_s2_tail_stream(w2[:64], wdual)
+    # the chained variant: its longer stream, an aliasing t1n, a wrong next conv1 pack
+    w1n = torch.zeros(128, 512, device=cuda, dtype=torch.bfloat16)
+    wsn = packing.pack_s2_tail_stream(w2, wdual, w1n)
+    t1n = torch.zeros(1, 4, 32, 128, device=cuda, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match='wstream holds'):
+        ops.bottleneck_s2_tail_next_nhwc(t1, x, ws, s, s, s, s, s, BF16, t1n=t1n)
+    with pytest.raises(RuntimeError, match='alias'):
+        ops.bottleneck_s2_tail_next_nhwc(t1, x, wsn, s, s, s, s, s, BF16, t1n=t1)
+    with pytest.raises(ValueError, match='next conv1 pack'):
+        packing.pack_s2_tail_stream(w2, wdual, w1n[:, :256])
 
 
 def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
@@ -402,7 +447,8 @@ def test_plan_with_chained_tails_matches_unchained_plan(cuda, precision):
     net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
     net = net.to(cuda).eval()
     plan = net.plan(cuda)
-    assert [b.chain is not None for b in plan.layers[1]] == [False, True, True, False]
+    # layer2: the strided tail chains block 1's conv1 too (round 4)
+    assert [b.chain is not None for b in plan.layers[1]] == [True, True, True, False]
     assert [b.chain is not None for b in plan.layers[2]] == [False, True, True, True, True, False]
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=13)]
     saved = P.CHAINED_TAILS

@@ -12,7 +12,7 @@ is doubled; WRITE_SIZE is exact for 16-B stores.  Infinity-Cache hits are counte
 The stem's f32 input reads are calibrated on their own (tools/stem_micro.py under a FETCH_SIZE
 pass against the known input bytes, profiles/r04/stem_fetch_calibration.txt): --stem-fetch-scale
 is the factor that calibration found (default 2, the guide's).
-With the default plan's 31 launches, each launch is printed beside its algorithmic bytes
+With the default plan's launch count (posu.roofline), each launch is printed beside its algorithmic bytes
 (posu.roofline.r50_256_launches: inputs read once, weights once, outputs written once) and the
 JSON line carries the total and traffic / algorithmic.
 The JSON line carries the commit the passes ran at (env POSU_COMMIT, set by
@@ -72,8 +72,8 @@ def main():
             'traffic_bytes': sum(fb) + sum(wb), 'stem_fetch_scale': a.stem_fetch_scale,
             'commit': os.environ.get('POSU_COMMIT')}
     alg = None
-    if len(f) == 31:
-        from posu import roofline
+    from posu import roofline
+    if len(f) == len(roofline.r50_256_launches()):
         alg = roofline.r50_256_launches()
         line['algorithmic_bytes'] = sum(r + wr for _, r, wr in alg)
         line['traffic_over_algorithmic'] = round(line['traffic_bytes'] / line['algorithmic_bytes'], 4)
