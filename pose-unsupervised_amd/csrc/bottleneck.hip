@@ -268,7 +268,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     }
     ld8(bn + c0, sc);
     ld8(bn + 64 + c0, sh);
-    pk_affine8(v, sc, sh);
+    affine8<!DOWN>(v, sc, sh);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ok ? fmaxf(v[e], 0.f) : 0.f;
     *reinterpret_cast<uint4*>(slot + swz(px + 1, c0 >> 3)) = O::store_vals(v);
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
     const float s8[8] = {sa.x, sa.y, sa.z, sa.w, sb.x, sb.y, sb.z, sb.w};
     const float h8[8] = {ha.x, ha.y, ha.z, ha.w, hb.x, hb.y, hb.z, hb.w};
     float v[8] = {acc2[0][0], acc2[0][1], acc2[0][2], acc2[0][3], acc2[1][0], acc2[1][1], acc2[1][2], acc2[1][3]};
-    pk_affine8(v, s8, h8);
+    affine8<!DOWN>(v, s8, h8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
     return O::store_vals(v);
@@ -373,8 +373,8 @@ __global__ __launch_bounds__(512, 1) void bottleneck64_kernel(BottleGeom g) {
         } else {
           ld8(bn + 256 + c0, sc);
           O::load_vals(res[2 * qh + jp], r);
-          pk_affine8(v, sc, sh);
-          pk_add8(v, r);
+          affine8<!DOWN>(v, sc, sh);
+          add8<!DOWN>(v, r);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }

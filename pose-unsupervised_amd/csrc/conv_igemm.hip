@@ -526,8 +526,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
             uint4 rv = make_uint4(0, 0, 0, 0);
             if (rp && mok && in) rv = *reinterpret_cast<const uint4*>(rp + pix + cp);
             O::load_vals(rv, r);
-            pk_affine8(v, sc8, sh8);  // BN as packed FMAs
-            if (rp) pk_add8(v, r);
+            affine8<false>(v, sc8, sh8);
+            if (rp) add8<false>(v, r);
             if (g.relu) {
 #pragma unroll
               for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -631,8 +631,8 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           v[4 + e] = __uint_as_float(sw[1]);
         }
         O::load_vals(rv[jp], r);
-        pk_affine8(v, sc[jp], sh[jp]);  // BN as packed FMAs
-        if (rp) pk_add8(v, r);
+        affine8<false>(v, sc[jp], sh[jp]);
+        if (rp) add8<false>(v, r);
         if (g.relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -1223,8 +1223,8 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
           v[4 + e] = __uint_as_float(sw[1]);
         }
         O::load_vals(rv[jp], r);
-        pk_affine8(v, sc[jp], sh[jp]);  // BN as packed FMAs
-        if (rp) pk_add8(v, r);
+        affine8<false>(v, sc[jp], sh[jp]);
+        if (rp) add8<false>(v, r);
         if (g.relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);

@@ -73,41 +73,42 @@ struct Op<float> {
   }
 };
 
-// v = v * s + b (+ r) over 8 values as four packed f32 FMAs (v_pk_fma_f32: two fused
-// multiply-adds per instruction, the same rounding as the scalar v_fma_f32) and packed adds;
-// the scalar loops spent one VALU issue per value on each.  POSU_PK_EPILOGUE=0: the scalar
-// loops (A/B builds only)
-#ifndef POSU_PK_EPILOGUE
-#define POSU_PK_EPILOGUE 1
-#endif
-__device__ __forceinline__ void pk_affine8(float* v, const float* s, const float* b) {
-  if (!POSU_PK_EPILOGUE) {
+// v = v * s + b and v += r over 8 values.  PK: as four packed f32 FMAs / adds (v_pk_fma_f32, two
+// fused multiply-adds per instruction, the same rounding as v_fma_f32); else one scalar
+// instruction per value.  Measured in round 4 (profiles/r04/pk_epilogue_ab_r4l.txt): packed
+// helps the layer1 identity Bottleneck (150.7 vs 154.3 us) and costs elsewhere (the network
+// 2.518 vs 2.499 ms with every epilogue packed: the even-aligned register pairs they need add
+// moves and pressure), so only that kernel uses it.
+template <bool PK>
+__device__ __forceinline__ void affine8(float* v, const float* s, const float* b) {
+  if constexpr (!PK) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = v[e] * s[e] + b[e];
-    return;
-  }
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f32x2v x = {v[2 * i], v[2 * i + 1]};
-    const f32x2v ss = {s[2 * i], s[2 * i + 1]}, bb = {b[2 * i], b[2 * i + 1]};
-    x = __builtin_elementwise_fma(x, ss, bb);
-    v[2 * i] = x.x;
-    v[2 * i + 1] = x.y;
+    for (int i = 0; i < 4; ++i) {
+      f32x2v x = {v[2 * i], v[2 * i + 1]};
+      const f32x2v ss = {s[2 * i], s[2 * i + 1]}, bb = {b[2 * i], b[2 * i + 1]};
+      x = __builtin_elementwise_fma(x, ss, bb);
+      v[2 * i] = x.x;
+      v[2 * i + 1] = x.y;
+    }
   }
 }
-__device__ __forceinline__ void pk_add8(float* v, const float* r) {
-  if (!POSU_PK_EPILOGUE) {
+template <bool PK>
+__device__ __forceinline__ void add8(float* v, const float* r) {
+  if constexpr (!PK) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += r[e];
-    return;
-  }
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f32x2v x = {v[2 * i], v[2 * i + 1]};
-    const f32x2v rr = {r[2 * i], r[2 * i + 1]};
-    x = x + rr;
-    v[2 * i] = x.x;
-    v[2 * i + 1] = x.y;
+    for (int i = 0; i < 4; ++i) {
+      f32x2v x = {v[2 * i], v[2 * i + 1]};
+      const f32x2v rr = {r[2 * i], r[2 * i + 1]};
+      x = x + rr;
+      v[2 * i] = x.x;
+      v[2 * i + 1] = x.y;
+    }
   }
 }
 

@@ -230,7 +230,7 @@ __global__ __launch_bounds__(S2Cfg<NEXT>::kNW * 64, 2) void tail_s2_kernel(TailS
     for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc, i, v);
-      pk_affine8(v, sc, sh);
+      affine8<false>(v, sc, sh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       *reinterpret_cast<uint4*>(smem + K::kT2 + (16 * i + r16) * K::kRowB + (((c0 >> 3) ^ r16) << 4)) =
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(S2Cfg<NEXT>::kNW * 64, 2) void tail_s2_kernel(TailS
     for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc, i, v);
-      pk_add8(v, sh);
+      add8<false>(v, sh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       const size_t pix = (static_cast<size_t>(n) * Hout + R0 + i) * K::kWout + C0 + r16;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(S2Cfg<NEXT>::kNW * 64, 2) void tail_s2_kernel(TailS
     for (int i = 0; i < MT; ++i) {
       float v[8];
       pair(acc1, i, v);
-      pk_affine8(v, sc, sh);
+      affine8<false>(v, sc, sh);
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
       const size_t pix = (static_cast<size_t>(n) * Hout + R0 + i) * K::kWout + C0 + r16;

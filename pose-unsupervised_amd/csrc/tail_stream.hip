@@ -195,19 +195,10 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_
     }
   };
   const int cpair = 16 * (q & 1) + 8 * (q >> 1);
-  // relu(v * sc + sh (+ r)) over 8 values: packed FMAs / adds, except in the chained variant,
-  // whose second accumulator set leaves no room for the even-aligned register pairs they need
-  // (it spilled with them): there the round-3 scalar loop
+  // relu(v * sc + sh (+ r)) over this lane's 8 values
   auto bn_relu = [&](float* v, const float* sc, const float* sh, const float* r) {
-    if constexpr (NEXT) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + (r ? r[e] : 0.f), 0.f);
-    } else {
-      pk_affine8(v, sc, sh);
-      if (r) pk_add8(v, r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + (r ? r[e] : 0.f), 0.f);
   };
   // m-tile i's tile pixel (row-major in the tile) for this lane
   auto tpix = [&](int i) { return 16 * MT * pg + 16 * i + r16; };
