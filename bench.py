@@ -558,6 +558,21 @@ def triangulation_parity_all_ranks(res, dev):
     return {'mean': float('%.6g' % (tot / cnt)), 'max': float('%.6g' % mx), 'joints': int(cnt)}
 
 
+def _json_default(o):
+    """numpy values that reach the JSON line (arrays as lists, scalars as Python numbers); logged
+    to stderr so the producing leg can be fixed."""
+    import numpy as np
+    if isinstance(o, np.ndarray):
+        print('bench: numpy array of shape %s in the JSON line' % (o.shape,), file=sys.stderr)
+        return o.tolist()
+    if isinstance(o, np.generic):
+        return o.item()
+    if isinstance(o, torch.Tensor):
+        print('bench: tensor of shape %s in the JSON line' % (tuple(o.shape),), file=sys.stderr)
+        return o.tolist()
+    raise TypeError('%s is not JSON serializable' % type(o).__name__)
+
+
 def peaked_parity(args, dev):
     """tools/peaked.py: fit R50@256 to peaked targets through the training path, then the bf16 and
     fp32 chains against the CPU oracle chain on those weights (the checker leg; N = 1)."""
@@ -775,7 +790,7 @@ def infer_main(args):
         'configs1': c1, 'configs4': c4, 'control': control, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }
-    print(json.dumps(line))
+    print(json.dumps(line, default=_json_default))
     if dist is not None:
         dist.destroy_process_group()
 
@@ -906,7 +921,7 @@ def train_main(args):
     rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
     line = run_training(args, dev, rank, world, dist, args.steps, args.warmup)
     if rank == 0:
-        print(json.dumps(line))
+        print(json.dumps(line, default=_json_default))
     if dist is not None:
         dist.destroy_process_group()
 
@@ -917,8 +932,10 @@ def dump_tiles():
     path = os.environ.get('POSU_DUMP_TILES')
     if path:
         from posu import plan as pl
+        times = pl.tuning_times()
         with open(path, 'w') as f:
-            json.dump(sorted([[repr(k), t] for k, t in pl.tuned_tiles().items()]), f, indent=0)
+            json.dump(sorted([[repr(k), t, {str(c): round(ms, 4) for c, ms in times.get(k, {}).items()}]
+                              for k, t in pl.tuned_tiles().items()]), f, indent=0)
 
 
 def main():

@@ -69,6 +69,7 @@ TILES_128X8 = True
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
 _TUNE_CACHE = {}
+_TUNE_TIMES = {}   # geometry key -> {tile: best ms of the reps}, the last tuning's measurements
 
 
 class _Tuner:
@@ -102,19 +103,23 @@ def _tuned(key, cout, launch):
     # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan
     # switch such as TILES_128X8 turned off for a control run)
     if _Tuner.active and (key not in _TUNE_CACHE or _TUNE_CACHE[key] not in cands):
-        best = None
-        for t in cands:
-            launch(t)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(_Tuner.reps):
+        # two passes over the candidates, the second in reverse order, each tile's best of the two:
+        # one pass let the clock ramp and the neighbours' cache state pick tiles that run 20-25 %
+        # slower in the graph (layer4 3x3: 75 vs 60 us, profiles/r04/replay_breakdown_r4l.txt)
+        times = {}
+        for order in (cands, cands[::-1]):
+            for t in order:
                 launch(t)
-            b.record()
-            b.synchronize()
-            ms = a.elapsed_time(b)
-            if best is None or ms < best[0]:
-                best = (ms, t)
-        _TUNE_CACHE[key] = best[1]
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(_Tuner.reps):
+                    launch(t)
+                b.record()
+                b.synchronize()
+                ms = a.elapsed_time(b)
+                times[t] = min(ms, times.get(t, ms))
+        _TUNE_CACHE[key] = min(cands, key=lambda t: (times[t], cands.index(t)))
+        _TUNE_TIMES[key] = times
     t = _TUNE_CACHE.get(key, -1)
     return launch(t if t in cands else -1)
 
@@ -122,6 +127,11 @@ def _tuned(key, cout, launch):
 def tuned_tiles():
     """The autotuned table (geometry key -> tile), e.g. for logging."""
     return dict(_TUNE_CACHE)
+
+
+def tuning_times():
+    """The last tuning's per-tile times (geometry key -> {tile: ms for the reps}), for diagnostics."""
+    return {k: dict(v) for k, v in _TUNE_TIMES.items()}
 
 
 class _Conv:
