@@ -305,7 +305,7 @@ def cpu_baseline(layers, size, groups, seconds):
     from oracle import pose_resnet_ref as PR
     from posu import synthetic as syn
     from posu.pipeline import synthetic_meta
-    threads, host = host_cores()
+    threads, host_cpus = host_cores()
     torch.set_num_threads(threads)
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
@@ -328,7 +328,7 @@ def cpu_baseline(layers, size, groups, seconds):
         n1 += 1
     c1_ms = (time.perf_counter() - t1) / n1 * 1e3
     ref['host'] = host
-    return ({'value': round(frames / el, 3), 'unit': 'frames/s', 'cores': threads, 'host_cpus': host,
+    return ({'value': round(frames / el, 3), 'unit': 'frames/s', 'cores': threads, 'host_cpus': host_cpus,
              'kind': 'port',
              'sample': '%d frames = %d pass(es) of the full %dx4 batch (R%d@%d) through the CPU oracle chain: '
                        'torch-CPU fp32 forward + soft-argmax + transform_back + FundamentalLoss + numpy DLT/SVD '
