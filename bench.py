@@ -120,7 +120,9 @@ def parse():
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` leg times it in the same process, so a gain shows on the driver's own box
-CONTROL_FLAGS = ('S2_TAIL', 'S2_CHAIN', 'STEM_VIEWS', 'TILES_128X8', 'PRECISE_HEAD')
+# (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
+# control leg compares the plans at the same numerics)
+CONTROL_FLAGS = ('S2_TAIL', 'S2_CHAIN', 'STEM_VIEWS', 'TILES_128X8')
 
 
 def apply_plan_flags(flags):

@@ -93,7 +93,9 @@ def _tile_candidates(cout):
     # 23 / 31: the eight-wave tiles with waves 4-7 staggered by half a K-tile; 7 / 15: 128x128 with
     # eight staggered waves (2x4 / 4x2 wave grids)
     sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 and TILES_128X8 else [])
-    return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c] + sg
+    # (tile 32, the persistent 256x64 four-wave instance, is left out: it spills 928 B per lane to
+    # scratch and took ~1.2 ms per launch in the tuning trials, 10x the other tiles)
+    return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
 
 
 def _tuned(key, cout, launch):
