@@ -76,8 +76,10 @@ def forward(x, sd, rounded, dt):
         s, b = _fold(sd, 'deconv_layers.%d' % (i + 1))
         y = F.conv_transpose2d(_q(x, dt, on), _q(sd['deconv_layers.%d.weight' % i], dt, on), stride=2, padding=1)
         x = F.relu(y * s[None, :, None, None] + b[None, :, None, None])
-    on = 'head' in rounded
-    return F.conv2d(_q(x, dt, on), _q(sd['final_layer.weight'], dt, on), sd.get('final_layer.bias'))
+    # 'head' rounds both head operands; 'head_act' / 'head_w' only the deconv output / the weights
+    on_a = 'head' in rounded or 'head_act' in rounded
+    on_w = 'head' in rounded or 'head_w' in rounded
+    return F.conv2d(_q(x, dt, on_a), _q(sd['final_layer.weight'], dt, on_w), sd.get('final_layer.bias'))
 
 
 def chain_metrics(hm, ref, task):
@@ -124,7 +126,7 @@ def main():
             res = {'all': chain_metrics(forward(x, sd, STAGES, dt), ref, task),
                    # the plan's split-precision head (PRECISE_HEAD): every stage rounded but the head
                    'all_but_head': chain_metrics(forward(x, sd, STAGES[:-1], dt), ref, task)}
-            for s in STAGES:
+            for s in STAGES + ('head_act', 'head_w'):
                 res[s] = chain_metrics(forward(x, sd, (s,), dt), ref, task)
             out['emulated'][dname] = res
     print(json.dumps(out, indent=1))
