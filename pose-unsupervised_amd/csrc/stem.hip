@@ -112,7 +112,7 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
 
   // ---- weights and BN -> LDS (once per block)
   if (tid < 64) {
-    bn[tid] = scale[tid];   // (used as |s|)
+    bn[tid] = fabsf(scale[tid]);   // |s|: the sign is in the staged weights
     bn[64 + tid] = shift[tid];
   }
   {
@@ -255,7 +255,8 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       for (int e = 0; e < 4; ++e) {
         float v[M];
 #pragma unroll
-        for (int rl = 0; rl < M; ++rl) v[rl] = (r0 + rl >= 0) ? acc[rl][j][e] : -INFINITY;
+        for (int rl = 0; rl < M; ++rl)   // (only the strip's first item, M = 5, reaches above the image)
+          v[rl] = (M == 4 || r0 + rl >= 0) ? acc[rl][j][e] : -INFINITY;
         const float first = M == 5 ? v[0] : carry[j][e];
         const float* u = v + (M == 5 ? 1 : 0);   // stem rows 4k .. 4k+3
         vm[0][j][e] = fmaxf(fmaxf(first, u[0]), u[1]);
@@ -273,10 +274,14 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) edge[(wid * 2 + p) * 64 + 16 * j + 4 * q + e] = vm[p][j][e];
+          *reinterpret_cast<float4*>(edge + (wid * 2 + p) * 64 + 16 * j + 4 * q) =
+              make_float4(vm[p][j][0], vm[p][j][1], vm[p][j][2], vm[p][j][3]);
     }
     __syncthreads();
+    // the left neighbour wave's last column, read by every lane (16-B reads, no divergent branch)
+    // and taken by the r16 = 0 lanes; wave 0's left is the pool padding
+    const int wl = wid > 0 ? wid - 1 : 0;
+    const bool first_col = r16 == 0, pad_left = wid == 0;
 #pragma unroll
     for (int p = 0; p < 2; ++p)
 #pragma unroll
@@ -284,6 +289,8 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
         const float4 s4 = *reinterpret_cast<const float4*>(bn + 16 * j + 4 * q);
         const float4 b4 = *reinterpret_cast<const float4*>(bn + 64 + 16 * j + 4 * q);
         const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, bv[4] = {b4.x, b4.y, b4.z, b4.w};
+        const float4 l4 = *reinterpret_cast<const float4*>(edge + (wl * 2 + p) * 64 + 16 * j + 4 * q);
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -292,8 +299,8 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
           // (used by even r16 < 15 only) and column sc - 1 (r16 = 0 takes the neighbour's edge)
           const float right = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(self), 0x101, 0xf, 0xf, true));
           float left = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(self), 0x111, 0xf, 0xf, true));
-          if (r16 == 0) left = wid > 0 ? edge[((wid - 1) * 2 + p) * 64 + 16 * j + 4 * q + e] : -INFINITY;
-          o[e] = fmaxf(fmaf(fabsf(sv[e]), fmaxf(fmaxf(left, self), right), bv[e]), 0.f);
+          if (first_col) left = pad_left ? -INFINITY : lv[e];
+          o[e] = fmaxf(fmaf(sv[e], fmaxf(fmaxf(left, self), right), bv[e]), 0.f);
         }
         if ((r16 & 1) == 0) {
           const int pc = 8 * wid + (r16 >> 1);
