@@ -116,8 +116,12 @@ struct TailCfg {
 template <int RowB>
 __device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
 
+// waves per CU the four-m-tile variant is compiled for (A/B builds: 8 gives it 256 registers)
+#ifndef POSU_TS_MT4_WAVES
+#define POSU_TS_MT4_WAVES 12
+#endif
 template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
-__global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : 12) / NW) void tail_stream_kernel(TailSGeom g) {
+__global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT>;
   constexpr int kRows = ROWS, kThreads = NW * 64;

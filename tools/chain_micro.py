@@ -84,9 +84,13 @@ def main():
         torch.cuda.synchronize()
         eq_y, eq_t = bool(torch.equal(y_ref, y_ch)), bool(torch.equal(t1n_ref, t1n_ch))
         ndiff = int((t1n_ref != t1n_ch).sum())
+        def plain():
+            ops.bottleneck_tail_stream_nhwc(t1, x, wst, s[2], s[3], s[4], s[5], BF16, out=y_ref)
+
         us_2, us_c = timeit(two, a.reps, a.rounds), timeit(chained, a.reps, a.rounds)
-        print('%s batch %d: tail + next conv1 launch %.1f us | chained tail %.1f us | y bit-identical %s, t1n '
-              'bit-identical %s (%d differ)' % (layer, a.n, us_2, us_c, eq_y, eq_t, ndiff), flush=True)
+        us_p = timeit(plain, a.reps, a.rounds)
+        print('%s batch %d: tail %.1f us | tail + next conv1 launch %.1f us | chained tail %.1f us | y bit-identical '
+              '%s, t1n bit-identical %s (%d differ)' % (layer, a.n, us_p, us_2, us_c, eq_y, eq_t, ndiff), flush=True)
 
 
 if __name__ == '__main__':

@@ -65,14 +65,32 @@ def main():
     def fused():
         ops.bottleneck_s2_tail_nhwc(t1, x, ws, s2, b2, shift, BF16, out=y1)
 
+    # the chained variant (+ layer2 block 1's conv1 over y) against the tail + a conv1 launch
+    p1n = packing.pack_conv_weight((torch.randn(128, 512, 1, 1, generator=g) * 0.06).to(dev), 512, bk, dt)
+    s1n, b1n = (torch.rand(128, generator=g) + 0.5).to(dev), (torch.randn(128, generator=g) * 0.1).to(dev)
+    wsn = packing.pack_s2_tail_stream(p2, pd, p1n)
+    y3 = torch.empty_like(y2)
+    t1n = torch.empty(a.n, 32, 32, 128, device=dev, dtype=dt)
+    t1r = torch.empty_like(t1n)
+
+    def tail_conv1():
+        ops.bottleneck_s2_tail_nhwc(t1, x, ws, s2, b2, shift, BF16, out=y1)
+        ops.conv2d_nhwc(y1, p1n, 128, 1, 1, 1, 0, s1n, b1n, None, True, BF16, out=t1r)
+
+    def chained():
+        ops.bottleneck_s2_tail_next_nhwc(t1, x, wsn, s2, b2, shift, s1n, b1n, BF16, out=y3, t1n=t1n)
+
     flop = 2.0 * a.n * 1024 * (1152 * 128 + 384 * 512)
+    flop_c = flop + 2.0 * a.n * 1024 * 512 * 128
     nbytes = (t1.numel() + x.numel() // 4 + y1.numel()) * 2
-    for name, fn in (('two launches', two), ('strided tail', fused)):
+    for name, fn, fl in (('two launches', two, flop), ('strided tail', fused, flop),
+                         ('tail + conv1', tail_conv1, flop_c), ('chained tail', chained, flop_c)):
         us = timeit(fn, a.reps, a.rounds)
         print('%-14s %8.1f us  %6.1f TFLOP/s  %5.2f TB/s (algorithmic t1 + x/4 + y)'
-              % (name, us, flop / us / 1e6, nbytes / us / 1e6))
+              % (name, us, fl / us / 1e6, nbytes / us / 1e6))
     torch.cuda.synchronize()
-    print('bit-identical:', bool(torch.equal(y1, y2)))
+    print('bit-identical:', bool(torch.equal(y1, y2)), 'chained:', bool(torch.equal(y3, y1)),
+          bool(torch.equal(t1n, t1r)))
 
 
 if __name__ == '__main__':
