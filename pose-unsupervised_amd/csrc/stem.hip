@@ -344,8 +344,9 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   auto item = [&](int k, auto sidx) __attribute__((always_inline)) {
     constexpr int S = decltype(sidx)::value;
     if (!PF) load_rows(8 * k + 2, I8{}, xv[S]);
-    // every wave is past item k-1's window reads (the pool barrier): its dead rows take item k's
-    __syncthreads();
+    // every wave is past item k-1's window reads -- they precede the barrier in item k-1's pool --
+    // so its dead rows take item k's without another barrier (item k-1's edge reads after that
+    // barrier touch only the edge slots, which the next write reaches past the barrier below)
     store_rows(8 * k + 2, I8{}, xv[S]);
     __syncthreads();
     if (PF && k + PFD < k1) load_rows(8 * (k + PFD) + 2, I8{}, xv[S]);
