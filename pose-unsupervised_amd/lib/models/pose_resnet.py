@@ -169,7 +169,11 @@ class PoseResNet(nn.Module):
             return train_forward(self, self.train_plan(), list(views), len(views))
         plan = self.plan(views[0].device)
         hm, x1, f = plan.run(plan.pack_input(views))
-        # NHWC -> NCHW-shaped channels-last views (no copy)
+        # the reference returns f32 features (pose_resnet.py:197-205): a 2-byte plan's layer1 /
+        # deconv outputs are widened once here (the heatmaps are f32 already); NHWC ->
+        # NCHW-shaped channels-last views
+        if x1.dtype != torch.float32:
+            x1, f = x1.float(), f.float()
         return hm, x1.permute(0, 3, 1, 2), f.permute(0, 3, 1, 2)
 
     def forward(self, x):

@@ -52,7 +52,9 @@ def test_pose_resnet_low_precision_deviation_is_bounded(cuda, golden, precision,
     net = _model(num_layers, size, int(g['seed']), precision, cuda)
     x = torch.cat(syn.synthetic_views(1, int(g['batch']), size, seed=int(g['input_seed'])), 0)
     with torch.no_grad():
-        hm, _, _ = net(x.to(cuda))
+        hm, x1, f = net(x.to(cuda))
+    # the reference's f32 features whatever the plan's operand type (pose_resnet.py:197-205)
+    assert x1.dtype == torch.float32 and f.dtype == torch.float32 and torch.isfinite(x1).all()
     hm = hm.cpu().numpy()
     assert np.isfinite(hm).all()
     err = np.abs(hm - g['heatmaps'])
