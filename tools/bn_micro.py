@@ -40,7 +40,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--rounds', type=int, default=3)
+    ap.add_argument('--lib', default=None, help='another build of libposeu.so (experiments)')
     args = ap.parse_args()
+    if args.lib:
+        from posu import _native
+        _native._LIB_PATH = os.path.abspath(args.lib)
     dev = torch.device('cuda', 0)
     g = torch.Generator(device=dev).manual_seed(0)
     total = 0.0
