@@ -51,8 +51,7 @@ const char* posu_last_error(void);
  * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) the
  * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
  * optional split-precision head (hw_lo); 12 the chained strided tail
- * (posu_bottleneck_s2_tail_next_fwd); 13 split-K convolution (posu_conv2d_fwd_splitk).  The ctypes binding refuses a library of another
- * revision. */
+ * (posu_bottleneck_s2_tail_next_fwd).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -150,21 +149,6 @@ int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, int C,
                     const void* w, int Cout, int KH, int KW, int stride, int pad,
                     const float* scale, const float* shift, const void* residual,
                     int relu, void* y, int Ho, int Wo, int tile, void* stream);
-/* Split-K form of posu_conv2d_fwd (ABI 13) for GEMMs with too few output tiles to fill the
- * chip (layer4: 8192 pixels): the K-tiles of every output tile are cut into ksplit runs, one
- * block each (the grid's y); every block stores its f32 partial tile to the workspace and the
- * last block of a tile to arrive sums the ksplit partials in split order (deterministic) and
- * applies the BN / residual / ReLU epilogue.  2-byte dtypes, tile 7, 15, 23 or 31 (the
- * staggered eight-wave tiles), 2 <= ksplit <= min(16, K-tiles).  workspace: 256-byte aligned,
- * >= posu_conv_splitk_workspace(N*Ho*Wo, Cout, tile, ksplit) bytes, its head (the per-tile
- * arrival counters) zeroed once when allocated; every launch leaves it zero.  Same values as
- * posu_conv2d_fwd up to the f32 summation order of the K runs. */
-long long posu_conv_splitk_workspace(long long M, int Cout, int tile, int ksplit);
-int posu_conv2d_fwd_splitk(int dtype, const void* x, int N, int H, int W, int C,
-                           const void* w, int Cout, int KH, int KW, int stride, int pad,
-                           const float* scale, const float* shift, const void* residual,
-                           int relu, void* y, int Ho, int Wo, int tile, int ksplit,
-                           void* workspace, long long workspace_bytes, void* stream);
 
 /* Two 1x1 convolutions summed into one output (Bottleneck conv3/bn3 + the
  * downsample conv/bn residual branch, lib/models/pose_resnet.py:90-99, 136-141):

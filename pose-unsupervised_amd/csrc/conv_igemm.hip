@@ -71,12 +71,6 @@ struct ConvGeom {
   float* hm;
   int J, hkp;
   int mtiles, ntiles;
-  // split-K (staggered eight-wave tiles only): blockIdx.y = split of the K-tiles; every split
-  // stores its f32 partial tile to kpart, the last split of a tile to arrive (kcnt[tile], zero
-  // between launches) sums them in split order and runs the epilogue
-  int ksplit;
-  float* kpart;
-  int* kcnt;
 };
 
 template <int BM, int BN, int S>
@@ -340,7 +334,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // overlaps the operand fetch instead of following the main loop.
   constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16;
   constexpr int ETM = EARLY ? TM : 1, ETP = EARLY ? TN / 2 : 1;
-  const bool early = EARLY && g.res && g.mode == 0 && !g.hm && nk <= kEarlyNK && g.ksplit <= 1;
+  const bool early = EARLY && g.res && g.mode == 0 && !g.hm && nk <= kEarlyNK;
   uint4 rve[ETM][ETP];
   auto out_pix = [&](int i, bool& mok) -> size_t {  // element offset of the pixel of row i
     const int m = m0 + rowA(i) + r16;
@@ -416,20 +410,17 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         read(As_, Bs_, cb, a, b);
       }
     };
-    // split-K: this block's run of K-tiles [kt0, kt1)
-    const int kt0 = g.ksplit > 1 ? static_cast<int>(blockIdx.y) * nk / g.ksplit : 0;
-    const int kt1 = g.ksplit > 1 ? (static_cast<int>(blockIdx.y) + 1) * nk / g.ksplit : nk;
-    if constexpr (!(ABL & 4)) POSU_DMA_TILE(kt0, kt0 & 1);
+    if constexpr (!(ABL & 4)) POSU_DMA_TILE(0, 0);
     if (lag) __builtin_amdgcn_s_setprio(1);  // the lagging half wins issue arbitration (-2..-7 %)
-    for (int kt = kt0; kt < kt1; ++kt) {
+    for (int kt = 0; kt < nk; ++kt) {
       if constexpr (!(ABL & 2)) vm_wait<0>();
       __syncthreads();
       if constexpr (!(ABL & 4))
-        if (kt + 1 < kt1) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
+        if (kt + 1 < nk) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
       const char* As_ = smem + (kt & 1) * STAGE;
       const char* Bs_ = As_ + A_BYTES;
       uint4 af[TM], bfr[TN];
-      if (lag && kt > kt0) mmx(hA, hB);
+      if (lag && kt > 0) mmx(hA, hB);
       rdx(As_, Bs_, 0, af, bfr);
       mmx(af, bfr);
       rdx(As_, Bs_, 1, hA, hB);
@@ -464,38 +455,6 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   }
 #undef POSU_DMA_TILE
 #undef POSU_COMPUTE
-
-  // ---- split-K fixup: store this split's partial tile (lane layout, 16-B per lane per MFMA
-  // tile, coalesced), count the tile's arrivals; the last split sums every partial in split
-  // order (the result does not depend on which split finishes last) and goes on to the epilogue
-  if constexpr (SG) {
-    if (g.ksplit > 1) {
-      __shared__ int klast;
-      float* kp = g.kpart + static_cast<size_t>(wg) * g.ksplit * (BM * BN);
-      f32x4* mine = reinterpret_cast<f32x4*>(kp + static_cast<size_t>(blockIdx.y) * (BM * BN));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) mine[(i * TN + j) * NT + tid] = acc[i][j];
-      __threadfence();
-      __syncthreads();
-      if (tid == 0) klast = atomicAdd(g.kcnt + wg, 1) == g.ksplit - 1;
-      __syncthreads();
-      if (!klast) return;
-      __threadfence();
-      for (int p = 0; p < g.ksplit; ++p) {
-        const f32x4* part = reinterpret_cast<const f32x4*>(kp + static_cast<size_t>(p) * (BM * BN));
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const f32x4 v = part[(i * TN + j) * NT + tid];
-            acc[i][j] = p == 0 ? v : acc[i][j] + v;
-          }
-      }
-      if (tid == 0) atomicExch(g.kcnt + wg, 0);
-    }
-  }
 
   // ---- direct epilogue (NHWC outputs): each lane stores its 4
   // consecutive channels of one pixel straight from the accumulators (BN, residual,
@@ -1469,18 +1428,16 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       return check_launch(what);
     }
     if (sg) {
-      const dim3 grid(nb, g.ksplit > 1 ? g.ksplit : 1);  // split-K: the splits of a tile share its XCD
       if (cfg == 5)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), grid, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       else if (cfg == 7 && wg4)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL, true>), grid, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       else if (cfg == 7)
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, true>), grid, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       else
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, true>), grid, dim3(512), 0, s, g);
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
     }
-    POSU_REQUIRE(g.ksplit <= 1, std::string(what) + ": split-K runs on the staggered tiles 7, 15, 23, 31 only");
   }
   switch (cfg) {
     case 0: launch_cfg<T, 256, 64, 4, 4, DUAL>(g, nb, st, s); break;
@@ -1579,72 +1536,6 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   g.out_H = Ho;
   g.out_W = Wo;
   return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd", tile);
-}
-
-// ---- split-K (the staggered eight-wave tiles): tiles of a small-M GEMM x ksplit runs of K-tiles
-namespace posu {
-namespace {
-bool splitk_tile(int tile, int& bm, int& bn) {
-  bm = tile == 7 || tile == 15 ? 128 : 256;
-  bn = tile == 23 ? 256 : 128;
-  return tile == 7 || tile == 15 || tile == 23 || tile == 31;
-}
-long long splitk_tiles(long long M, int Cout, int bm, int bn) { return (M + bm - 1) / bm * (round_up(Cout, 64) / bn); }
-long long splitk_count_bytes(long long tiles) { return (tiles * 4 + 255) / 256 * 256; }
-}  // namespace
-}  // namespace posu
-
-extern "C" long long posu_conv_splitk_workspace(long long M, int Cout, int tile, int ksplit) {
-  int bm, bn;
-  if (!splitk_tile(tile, bm, bn) || M <= 0 || Cout <= 0 || ksplit < 1) return -1;
-  const long long tiles = splitk_tiles(M, Cout, bm, bn);
-  return splitk_count_bytes(tiles) + tiles * ksplit * bm * bn * 4LL;
-}
-
-extern "C" int posu_conv2d_fwd_splitk(int dtype, const void* x, int N, int H, int W, int C, const void* w, int Cout,
-                                      int KH, int KW, int stride, int pad, const float* scale, const float* shift,
-                                      const void* residual, int relu, void* y, int Ho, int Wo, int tile, int ksplit,
-                                      void* workspace, long long workspace_bytes, void* stream) {
-  int bm, bn;
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, "posu_conv2d_fwd_splitk: 2-byte dtypes only");
-  POSU_REQUIRE(splitk_tile(tile, bm, bn), "posu_conv2d_fwd_splitk: tile must be 7, 15, 23 or 31");
-  POSU_REQUIRE(Cout % (tile == 23 ? 256 : 128) == 0, "posu_conv2d_fwd_splitk: Cout must fill the tile's columns");
-  const int nk = round_up(KH * KW * C, bk_of(dtype)) / bk_of(dtype);
-  POSU_REQUIRE(ksplit >= 2 && ksplit <= 16 && ksplit <= nk, "posu_conv2d_fwd_splitk: 2 <= ksplit <= min(16, K-tiles)");
-  POSU_REQUIRE(workspace && (reinterpret_cast<size_t>(workspace) & 255) == 0,
-               "posu_conv2d_fwd_splitk: workspace must be 256-byte aligned");
-  const long long M = static_cast<long long>(N) * Ho * Wo;
-  POSU_REQUIRE(workspace_bytes >= posu_conv_splitk_workspace(M, Cout, tile, ksplit),
-               "posu_conv2d_fwd_splitk: workspace too small (posu_conv_splitk_workspace)");
-  if (int st = common_checks(dtype, x, w, y, N, H, W, C, Cout, "posu_conv2d_fwd_splitk")) return st;
-  POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd_splitk: bad window");
-  POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
-               "posu_conv2d_fwd_splitk: Ho/Wo larger than the window allows");
-  POSU_REQUIRE(M * Cout < (1LL << 31), "posu_conv2d_fwd_splitk: output too large");
-  POSU_REQUIRE(params_aligned(scale, shift), "posu_conv2d_fwd_splitk: scale / shift must be 16-byte aligned");
-  ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
-  g.scale = scale;
-  g.shift = shift;
-  g.res = residual;
-  g.y = y;
-  g.Ho = Ho;
-  g.Wo = Wo;
-  g.M = N * Ho * Wo;
-  g.K = KH * KW * C;
-  g.Kpad = round_up(g.K, bk_of(dtype));
-  g.KH = KH;
-  g.KW = KW;
-  g.stride = stride;
-  g.pad_h = pad;
-  g.pad_w = pad;
-  g.relu = relu;
-  g.out_H = Ho;
-  g.out_W = Wo;
-  g.ksplit = ksplit;
-  g.kcnt = static_cast<int*>(workspace);
-  g.kpart = reinterpret_cast<float*>(static_cast<char*>(workspace) +
-                                     splitk_count_bytes(splitk_tiles(M, Cout, bm, bn)));
-  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_fwd_splitk", tile);
 }
 
 extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int W, int C, const void* x2, int H2,

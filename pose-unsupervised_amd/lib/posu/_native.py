@@ -17,7 +17,7 @@ F64 = 2
 F16 = 3
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 13
+ABI_VERSION = 12
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -50,9 +50,6 @@ _SIGNATURES = {
     'posu_bottleneck_s2_tail_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p, _p, _p, _p],
     'posu_bottleneck_down_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_conv2d_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _p],
-    'posu_conv_splitk_workspace': [_ll, _i, _i, _i],
-    'posu_conv2d_fwd_splitk': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _i, _p, _i, _i, _i, _i,
-                               _p, _ll, _p],
     'posu_deconv4x4s2_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _i, _p, _i, _p],
     'posu_deconv4x4s2_head_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p, _p, _p, _i, _p, _p, _p],
     'posu_head1x1_nchw_fwd': [_i, _p, _i, _i, _i, _i, _p, _i, _p, _p, _p],
@@ -88,7 +85,7 @@ _SIGNATURES = {
 }
 _RESTYPES = {'posu_last_error': ctypes.c_char_p, 'posu_conv2d_wgrad_workspace': ctypes.c_longlong,
              'posu_pack_job_blocks': ctypes.c_longlong,
-             'posu_bn_workspace': ctypes.c_longlong, 'posu_conv_splitk_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong}
+             'posu_bn_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong}
 
 
 def library_path():

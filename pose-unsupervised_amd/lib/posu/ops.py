@@ -77,45 +77,6 @@ def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu,
     return out
 
 
-_SPLITK_WS = {}
-_SPLITK_RETIRED = []  # outgrown buffers stay allocated: a captured hipGraph may still hold them
-
-
-def splitk_workspace(device, nbytes):
-    """Grow-only split-K workspace per (device, current stream), zeroed when allocated (its head
-    holds the per-tile arrival counters, which every launch leaves at zero), at least 256 MiB
-    (layer4's partials at batch 128 take 64 MiB per split-4 launch).  Plans size it before graph
-    capture; a capture never grows it."""
-    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
-    buf = _SPLITK_WS.get(key)
-    if buf is None or buf.numel() < nbytes:
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError('split-K workspace must be sized before graph capture')
-        if buf is not None:
-            _SPLITK_RETIRED.append(buf)
-        buf = torch.zeros(max(int(nbytes), 256 << 20), dtype=torch.uint8, device=device)
-        _SPLITK_WS[key] = buf
-    return buf
-
-
-def conv2d_nhwc_splitk(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, tile, ksplit,
-                       out=None):
-    """conv2d_nhwc with the K-tiles of every output tile cut into ksplit runs (posu_conv2d_fwd_splitk)."""
-    n, h, w, c = x.shape
-    ho = (h + 2 * pad - kh) // stride + 1
-    wo = (w + 2 * pad - kw) // stride + 1
-    if out is None:
-        out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
-    nbytes = nat.load().posu_conv_splitk_workspace(n * ho * wo, cout, int(tile), int(ksplit))
-    if nbytes < 0:
-        raise ValueError('split-K: tile %d is not a staggered eight-wave tile' % tile)
-    ws = splitk_workspace(x.device, nbytes)
-    call('posu_conv2d_fwd_splitk', code, ptr(x), n, h, w, c, ptr(wpk), cout, kh, kw, stride, pad,
-         ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, int(tile), int(ksplit), ptr(ws),
-         ws.numel(), stream_of(x.device))
-    return out
-
-
 def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, tile=-1):  # noqa: D401
     """act(W[:, :C] x + W[:, C:] x2[::stride2, ::stride2] + shift) (two 1x1 sources, one output)."""
     n, h, w, c = x.shape

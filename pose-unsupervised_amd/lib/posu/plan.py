@@ -17,7 +17,6 @@ torch.cuda.CUDAGraph (hipGraph) by the caller.
 import torch
 
 from . import ops
-from ._native import F32
 from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
                       pack_conv_weight, pack_deconv4x4_weight,
                       pack_dual_1x1_weight, pack_s2_tail_stream, pack_stem_fused_weight, pack_stem_s2d_weight,
@@ -66,8 +65,6 @@ class RawViews:
 
 # the 128x128 eight-wave staggered conv tiles (7 / 15, round 4) among the autotuner's candidates
 TILES_128X8 = True
-# split-K launches (posu_conv2d_fwd_splitk) among the candidates of under-filled GEMMs (layer4)
-SPLIT_K = True
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -101,30 +98,10 @@ def _tile_candidates(cout):
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
 
 
-def _split_candidates(m, cout, kpad, code):
-    """Split-K candidates 100 * ksplit + tile for a 2-byte conv whose staggered eight-wave tiles
-    leave CUs idle: ksplit 2 / 4 runs of K-tiles per output tile (>= 4 K-tiles each), at most
-    1024 blocks in all."""
-    if not SPLIT_K or code == F32:
-        return []
-    cpad = (cout + 63) // 64 * 64
-    nk = kpad // 64
-    out = []
-    for tile, bm, bn in ((23, 256, 256), (7, 128, 128), (15, 128, 128)):
-        if cpad % bn or (tile != 23 and not TILES_128X8):
-            continue
-        tiles = -(-m // bm) * (cpad // bn)
-        if tiles >= 512:
-            continue
-        out += [100 * ks + tile for ks in (2, 4) if nk >= 4 * ks and tiles * ks <= 1024]
-    return out
-
-
-def _tuned(key, cout, launch, extra=()):
+def _tuned(key, cout, launch):
     """launch(tile) -> output.  While tuning, time every admissible tile once on the real
-    operands (HIP events) and keep the fastest for this geometry.  extra: more candidate ids
-    (split-K: 100 * ksplit + tile)."""
-    cands = _tile_candidates(cout) + list(extra)
+    operands (HIP events) and keep the fastest for this geometry."""
+    cands = _tile_candidates(cout)
     # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan
     # switch such as TILES_128X8 turned off for a control run)
     if _Tuner.active and (key not in _TUNE_CACHE or _TUNE_CACHE[key] not in cands):
@@ -180,15 +157,9 @@ class _Conv:
             wo = (x.shape[2] + 2 * self.pad - self.k) // self.stride + 1
             out = torch.empty((x.shape[0], ho, wo, self.cout), dtype=x.dtype, device=x.device)
         key = ('conv', code, tuple(x.shape), self.cout, self.k, self.stride, self.pad, residual is not None)
-
-        def launch(t):
-            if t >= 100:  # split-K
-                return ops.conv2d_nhwc_splitk(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale,
-                                              self.shift, residual, self.relu, code, t % 100, t // 100, out=out)
-            return ops.conv2d_nhwc(x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale,
-                                   self.shift, residual, self.relu, code, out=out, tile=t)
-        m = out.shape[0] * out.shape[1] * out.shape[2]
-        return _tuned(key, self.cout, launch, _split_candidates(m, self.cout, self.w.shape[1], code))
+        return _tuned(key, self.cout, lambda t: ops.conv2d_nhwc(
+            x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale, self.shift, residual, self.relu,
+            code, out=out, tile=t))
 
 
 class _DualTail:

@@ -582,63 +582,3 @@ def test_stem_pool_views_one_launch(cuda, size, nv, code, hflip):
     ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * ref.float().abs()
     assert bool((d <= 2 * ulp + 1e-3).all()), float(d.max())
     assert float((d > 0).float().mean()) < 0.05
-
-
-SPLITK_CASES = [
-    # n, cin, h, w, cout, k, stride, pad, residual, relu, tile, ksplit
-    (128, 512, 8, 8, 512, 3, 1, 1, False, True, 23, 4),     # layer4 conv2 (K = 4608)
-    (128, 2048, 8, 8, 512, 1, 1, 0, False, True, 7, 2),     # layer4 conv1 (K = 2048)
-    (128, 512, 8, 8, 2048, 1, 1, 0, True, True, 15, 4),     # layer4 conv3 + residual
-    (128, 512, 16, 16, 512, 3, 2, 1, False, True, 23, 2),   # layer4 block 0 conv2, stride 2
-    (3, 256, 7, 9, 256, 3, 1, 1, True, False, 15, 3),       # ragged M (189 px), odd split of 36 K-tiles
-]
-
-
-@pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('case', SPLITK_CASES)
-def test_conv2d_splitk_matches_the_unsplit_conv(cuda, code, case):
-    """Split-K (posu_conv2d_fwd_splitk): every split stores an f32 partial tile, the last split of
-    a tile to arrive sums them in split order and applies the epilogue.  Against the unsplit
-    launch of the same tile: equal up to the f32 summation order of the K runs (2-byte outputs:
-    at most 1 ulp apart, >= 99 % bit-identical); a repeated launch is bit-identical (the order
-    does not depend on which split arrives last); the arrival counters end at zero; close to
-    the torch fp32 conv."""
-    n, cin, h, w, cout, k, stride, pad, residual, relu, tile, ks = case
-    g = torch.Generator().manual_seed(5)
-    dt = ops.torch_dtype(code)
-    x = torch.randn(n, h, w, cin, generator=g).to(cuda, dt)
-    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
-    sc = (torch.rand(cout, generator=g) + 0.5).to(cuda)
-    sh = (torch.randn(cout, generator=g) * 0.1).to(cuda)
-    ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
-    res = torch.randn(n, ho, wo, cout, generator=g).to(cuda, dt) if residual else None
-    wp = packing.pack_conv_weight(wt.to(cuda), cin, ops.conv_bk(code), dt)
-    plain = ops.conv2d_nhwc(x, wp, cout, k, k, stride, pad, sc, sh, res, relu, code, tile=tile)
-    a = ops.conv2d_nhwc_splitk(x, wp, cout, k, k, stride, pad, sc, sh, res, relu, code, tile, ks)
-    b = ops.conv2d_nhwc_splitk(x, wp, cout, k, k, stride, pad, sc, sh, res, relu, code, tile, ks)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
-    ws = ops.splitk_workspace(cuda, 0)
-    tiles = -(-(n * ho * wo) // (128 if tile in (7, 15) else 256)) * (cout // (256 if tile == 23 else 128))
-    assert int(ws[:tiles * 4].count_nonzero()) == 0, 'arrival counters not reset'
-    d = (a.float() - plain.float()).abs()
-    ulp = plain.float().abs().clamp_min(2.0 ** -14) * (2.0 ** -7 if code == BF16 else 2.0 ** -10)
-    assert bool((d <= ulp * 1.01).all()), float((d / ulp).max())
-    assert float((d == 0).float().mean()) >= 0.99
-    ref = F.conv2d(x.float().permute(0, 3, 1, 2).cpu(), wt, stride=stride, padding=pad).permute(0, 2, 3, 1)
-    ref = ref * sc.cpu() + sh.cpu()
-    if residual:
-        ref = ref + res.float().cpu()
-    if relu:
-        ref = F.relu(ref)
-    tol = 3e-2 if code == BF16 else 4e-3
-    torch.testing.assert_close(a.float().cpu(), ref, atol=tol, rtol=tol)
-
-
-def test_conv2d_splitk_refuses_bad_arguments(cuda):
-    x = torch.zeros(2, 8, 8, 256, dtype=torch.bfloat16, device=cuda)
-    wp = torch.zeros(256, 9 * 256, dtype=torch.bfloat16, device=cuda)
-    sc, sh = torch.ones(256, device=cuda), torch.zeros(256, device=cuda)
-    for tile, ks in ((5, 2), (23, 1), (23, 64)):
-        with pytest.raises((RuntimeError, ValueError)):
-            ops.conv2d_nhwc_splitk(x, wp, 256, 3, 3, 1, 1, sc, sh, None, True, BF16, tile, ks)
