@@ -81,6 +81,9 @@ def parse():
     ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
                     help="train mode: torch.optim.Adam's fused kernel (default) or its foreach launches")
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
+    ap.add_argument('--train-graph', default='auto', choices=['auto', 'on', 'off'],
+                    help='training leg: capture the whole step (forward, backward, Adam) in one hipGraph and '
+                         'replay it (auto: single-GPU runs; DDP steps run eagerly)')
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
                          'after autotuning -- profile runs load it so traces hold no trial launches')
@@ -832,7 +835,9 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
     # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
     # launches (same math): 26.3 -> 22.8 ms per step measured A/B
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
+    graphed = args.train_graph == 'on' or (args.train_graph == 'auto' and dist is None)
+    # capturable: the step counts live on the GPU, so a captured step() replays the update
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused', capturable=graphed)
     subj = meta.subj
 
     def step():
@@ -855,10 +860,35 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     stream = torch.cuda.Stream(dev, priority=-1) if args.train_stream == 'high' else torch.cuda.current_stream(dev)
     stream.wait_stream(torch.cuda.current_stream(dev))   # inputs / parameters made on the default stream
     with torch.cuda.stream(stream):
-        return _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream)
+        return _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, graphed)
 
 
-def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
+def _capture_step(step, stream):
+    """The whole training step (forward, losses, backward with its weight-gradient side stream,
+    Adam) captured in one hipGraph on `stream`: the replay has no host launch gaps (the eager
+    step leaves ~0.9 ms of 21.8 ms idle, profiles/r04/train_breakdown.txt).  Returns
+    (replay, the captured loss tensor) or None when the capture is refused."""
+    try:
+        torch.cuda.synchronize()
+        # captured on a stream of its own (never the null stream), warmed there first so the
+        # per-stream workspaces exist before the capture
+        cap = stream if stream != torch.cuda.default_stream(stream.device) else torch.cuda.Stream(stream.device)
+        cap.wait_stream(stream)
+        with torch.cuda.stream(cap):
+            step()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cap):
+            loss = step()
+        stream.wait_stream(cap)
+        torch.cuda.synchronize()
+        return g, loss
+    except Exception as e:  # noqa: BLE001 -- report and keep the eager step
+        print('training step graph capture refused (%s: %s); eager steps' % (type(e).__name__, e), file=sys.stderr)
+        torch.cuda.synchronize()
+        return None
+
+
+def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, graphed=False):
     from posu import dist as pdist
     from posu import plan as pplan
     if not args.no_autotune:  # the first warm-up step times every admissible tile per conv geometry
@@ -869,13 +899,21 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
             pplan._Tuner.active = False
     for _ in range(max(1, warmup)):
         step()
+    cap = _capture_step(step, stream) if graphed else None
+    if cap is not None:
+        graph, loss = cap
+        run = graph.replay
+        graph.replay()  # one untimed replay
+    else:
+        run = step
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        loss = step()
+        out = run()
+        loss = loss if cap is not None else out
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -908,7 +946,8 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce overlapped with the '
                                   'staged backward)' % world,
-                   'optimizer': 'Adam lr 1e-3 (%s)' % args.adam},
+                   'optimizer': 'Adam lr 1e-3 (%s)' % args.adam,
+                   'step_launch': 'hipGraph replay of the whole step' if cap is not None else 'eager'},
         'per_rank_frames': [int(p[0]) for p in per_rank],
         'loss': round(float(loss.detach()), 5), 'roofline': roof, 'cpu_baseline': None,
     }
@@ -934,9 +973,10 @@ def dump_tiles():
     path = os.environ.get('POSU_DUMP_TILES')
     if path:
         from posu import plan as pl
-        times = pl.tuning_times()
+        times, ctx = pl.tuning_times(), pl.refine_times()
         with open(path, 'w') as f:
-            json.dump(sorted([[repr(k), t, {str(c): round(ms, 4) for c, ms in times.get(k, {}).items()}]
+            json.dump(sorted([[repr(k), t, {str(c): round(ms, 4) for c, ms in times.get(k, {}).items()},
+                               {str(c): round(ms, 4) for c, ms in ctx.get(k, {}).items()}]
                               for k, t in pl.tuned_tiles().items()]), f, indent=0)
 
 

@@ -70,11 +70,15 @@ TILES_128X8 = True
 # shared by every plan, so a re-packed plan does not re-tune)
 _TUNE_CACHE = {}
 _TUNE_TIMES = {}   # geometry key -> {tile: best ms of the reps}, the last tuning's measurements
+_REFINE_TIMES = {}  # geometry key -> {tile: ms per whole forward}, the in-context stage's measurements
+# the in-context second tuning stage (PoseResNetPlan._refine_in_context)
+REFINE_IN_CONTEXT = True
 
 
 class _Tuner:
     active = False
     reps = 3
+    seen = []   # geometry keys met by the current tuning run, in launch order
 
 
 def _tile_candidates(cout):
@@ -102,6 +106,8 @@ def _tuned(key, cout, launch):
     """launch(tile) -> output.  While tuning, time every admissible tile once on the real
     operands (HIP events) and keep the fastest for this geometry."""
     cands = _tile_candidates(cout)
+    if _Tuner.active and key not in _Tuner.seen:
+        _Tuner.seen.append(key)
     # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan
     # switch such as TILES_128X8 turned off for a control run)
     if _Tuner.active and (key not in _TUNE_CACHE or _TUNE_CACHE[key] not in cands):
@@ -134,6 +140,11 @@ def tuned_tiles():
 def tuning_times():
     """The last tuning's per-tile times (geometry key -> {tile: ms for the reps}), for diagnostics."""
     return {k: dict(v) for k, v in _TUNE_TIMES.items()}
+
+
+def refine_times():
+    """The in-context stage's whole-forward times (geometry key -> {tile: ms per forward})."""
+    return {k: dict(v) for k, v in _REFINE_TIMES.items()}
 
 
 class _Conv:
@@ -506,13 +517,50 @@ class PoseResNetPlan:
         """Time every admissible tile configuration of every conv launch of this forward
         (on the packed input x) and keep the fastest per layer geometry; later runs (and
         hipGraph captures) use the tuned tiles."""
-        _Tuner.active, _Tuner.reps = True, reps
+        _Tuner.active, _Tuner.reps, _Tuner.seen = True, reps, []
         try:
             with torch.no_grad():
                 out = self.run(x, chunks=chunks, keep_features=keep_features)
         finally:
             _Tuner.active = False
+        if REFINE_IN_CONTEXT:
+            with torch.no_grad():
+                self._refine_in_context(x, chunks, keep_features)
         return out
+
+    def _refine_in_context(self, x, chunks, keep_features, within=0.25, top=3, forwards=6):
+        """Second tuning stage: for every geometry of this forward whose best per-launch
+        candidates lie within 25 % of each other, run the whole forward with each of its top
+        three and keep the one whose forward is shortest (best of two rounds of `forwards`
+        forwards, HIP events).  The per-launch trials run one launch back to back; inside the
+        network a launch follows other kernels at sustained clocks, and the ranking can differ:
+        layer4's 3x3 took 53 us on two tiles in isolation and 62 vs 75 us on them in the graph
+        (profiles/r04/replay_breakdown*.txt)."""
+        def forward_ms():
+            self.run(x, chunks=chunks, keep_features=keep_features)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(forwards):
+                self.run(x, chunks=chunks, keep_features=keep_features)
+            b.record()
+            b.synchronize()
+            return a.elapsed_time(b) / forwards
+        for key in list(_Tuner.seen):
+            times = _TUNE_TIMES.get(key)
+            if not times or key not in _TUNE_CACHE:
+                continue
+            best = min(times.values())
+            cands = sorted((t for t in times if times[t] <= best * (1 + within)), key=lambda t: times[t])[:top]
+            if len(cands) < 2:
+                continue
+            res = {}
+            for order in (cands, cands[::-1]):
+                for t in order:
+                    _TUNE_CACHE[key] = t
+                    ms = forward_ms()
+                    res[t] = min(ms, res.get(t, ms))
+            _TUNE_CACHE[key] = min(cands, key=lambda t: (res[t], cands.index(t)))
+            _REFINE_TIMES[key] = res
 
     def run(self, x, chunks=1, keep_features=True):
         """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC).
