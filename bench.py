@@ -81,9 +81,6 @@ def parse():
     ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
                     help="train mode: torch.optim.Adam's fused kernel (default) or its foreach launches")
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
-    ap.add_argument('--train-graph', default='auto', choices=['auto', 'on', 'off'],
-                    help='training leg: capture the whole step (forward, backward, Adam) in one hipGraph and '
-                         'replay it (auto: single-GPU runs; DDP steps run eagerly)')
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
                          'after autotuning -- profile runs load it so traces hold no trial launches')
@@ -835,9 +832,7 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
     # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
     # launches (same math): 26.3 -> 22.8 ms per step measured A/B
-    graphed = args.train_graph == 'on' or (args.train_graph == 'auto' and dist is None)
-    # capturable: the step counts live on the GPU, so a captured step() replays the update
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused', capturable=graphed)
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
     subj = meta.subj
 
     def step():
@@ -860,35 +855,10 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     stream = torch.cuda.Stream(dev, priority=-1) if args.train_stream == 'high' else torch.cuda.current_stream(dev)
     stream.wait_stream(torch.cuda.current_stream(dev))   # inputs / parameters made on the default stream
     with torch.cuda.stream(stream):
-        return _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, graphed)
+        return _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream)
 
 
-def _capture_step(step, stream):
-    """The whole training step (forward, losses, backward with its weight-gradient side stream,
-    Adam) captured in one hipGraph on `stream`: the replay has no host launch gaps (the eager
-    step leaves ~0.9 ms of 21.8 ms idle, profiles/r04/train_breakdown.txt).  Returns
-    (replay, the captured loss tensor) or None when the capture is refused."""
-    try:
-        torch.cuda.synchronize()
-        # captured on a stream of its own (never the null stream), warmed there first so the
-        # per-stream workspaces exist before the capture
-        cap = stream if stream != torch.cuda.default_stream(stream.device) else torch.cuda.Stream(stream.device)
-        cap.wait_stream(stream)
-        with torch.cuda.stream(cap):
-            step()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=cap):
-            loss = step()
-        stream.wait_stream(cap)
-        torch.cuda.synchronize()
-        return g, loss
-    except Exception as e:  # noqa: BLE001 -- report and keep the eager step
-        print('training step graph capture refused (%s: %s); eager steps' % (type(e).__name__, e), file=sys.stderr)
-        torch.cuda.synchronize()
-        return None
-
-
-def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, graphed=False):
+def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
     from posu import dist as pdist
     from posu import plan as pplan
     if not args.no_autotune:  # the first warm-up step times every admissible tile per conv geometry
@@ -899,21 +869,13 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, gra
             pplan._Tuner.active = False
     for _ in range(max(1, warmup)):
         step()
-    cap = _capture_step(step, stream) if graphed else None
-    if cap is not None:
-        graph, loss = cap
-        run = graph.replay
-        graph.replay()  # one untimed replay
-    else:
-        run = step
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        out = run()
-        loss = loss if cap is not None else out
+        loss = step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -946,8 +908,7 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream, gra
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (DistributedDataParallel, RCCL gradient all-reduce overlapped with the '
                                   'staged backward)' % world,
-                   'optimizer': 'Adam lr 1e-3 (%s)' % args.adam,
-                   'step_launch': 'hipGraph replay of the whole step' if cap is not None else 'eager'},
+                   'optimizer': 'Adam lr 1e-3 (%s)' % args.adam},
         'per_rank_frames': [int(p[0]) for p in per_rank],
         'loss': round(float(loss.detach()), 5), 'roofline': roof, 'cpu_baseline': None,
     }
