@@ -1,3 +1,3 @@
 set -o pipefail
-bash tools/gpu_round.sh gpurun_out/r4final || exit $?
-timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4final/smoke.log 2>&1
+bash tools/gpu_round.sh gpurun_out/r4final2 || exit $?
+timeout -k 10 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r4final2/smoke.log 2>&1
