@@ -17,6 +17,13 @@
 namespace posu {
 namespace {
 
+#ifndef POSU_BN_U1
+#define POSU_BN_U1 4    // pixels in flight per thread in the backward partial pass
+#endif
+#ifndef POSU_BN_SEGU
+#define POSU_BN_SEGU 4  // chunks in flight per thread in the segment-major apply passes
+#endif
+
 constexpr int kMaxNB = 256;  // partial-sum blocks per segment
 
 struct RedShape {
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       }
     };
     // U pixels per step with all their loads issued first (memory-level parallelism)
-    constexpr int U = MODE == 0 ? 8 : 4;
+    constexpr int U = MODE == 0 ? 8 : POSU_BN_U1;
     const uint4 zero = make_uint4(0, 0, 0, 0);
     int p = pbeg + pl;
     for (; p + (U - 1) * rs.PL < pend; p += U * rs.PL) {
@@ -294,7 +301,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ z, 
 // chunk never changes (the grid stride is a multiple of 256), so the per-channel
 // parameters live in registers; U chunks per step with their loads issued first.
 // Same arithmetic per element as the kernels above.
-constexpr int kSegU = 4;
+constexpr int kSegU = POSU_BN_SEGU;
 
 // E consecutive per-channel f32 parameters as 16-B loads (E = 4 or 8; every parameter
 // row starts at a multiple of 8 channels of a 16-B aligned allocation)
