@@ -23,7 +23,18 @@
  *   - dtype codes: POSU_F32 (fp32 operands, exact-f32 MFMA, the parity mode)
  *                  POSU_BF16 (bf16 operands, f32 accumulate, the fast mode),
  *                  POSU_F16  (IEEE fp16 operands, f32 accumulate: BASELINE configs[4]'s
- *                             fp16 backbone; same kernels and speed as bf16).
+ *                             fp16 backbone; same kernels and speed as bf16),
+ *                  POSU_F16X3 (ABI 13, split fp16: the parity-bearing fast mode).  Every value
+ *                             is stored as a pair hi = fp16(v), lo = fp16(v - hi) -- v to ~22
+ *                             mantissa bits -- and every product is summed as hi.hi + lo.hi +
+ *                             hi.lo (three fp16 MFMAs, f32 accumulate; the lo.lo term dropped).
+ *                             Split layout of a tensor of C logical channels (C % 32 == 0): 2C
+ *                             fp16 per pixel, logical channel c's hi at (c / 32) * 64 + c % 32
+ *                             and its lo 32 elements later ([hi 32 | lo 32] per 32-channel
+ *                             block).  Entry points that accept it take LOGICAL channel counts;
+ *                             packed weights use the same interleave along K (k = tap * C + ci
+ *                             logical, then split per 32-block), so posu_conv_bk = 64 halves =
+ *                             32 logical k per K-tile.
  */
 #ifndef POSU_H_
 #define POSU_H_
@@ -40,6 +51,7 @@ extern "C" {
 #define POSU_BF16 1
 #define POSU_F64 2
 #define POSU_F16 3
+#define POSU_F16X3 4
 
 /* ---------------------------------------------------------------- runtime */
 const char* posu_last_error(void);
@@ -51,7 +63,8 @@ const char* posu_last_error(void);
  * kernels removed, the strided tail of layer2's first block (posu_bottleneck_s2_tail_fwd) the
  * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
  * optional split-precision head (hw_lo); 12 the chained strided tail
- * (posu_bottleneck_s2_tail_next_fwd).  The ctypes binding refuses a library of another revision. */
+ * (posu_bottleneck_s2_tail_next_fwd); 13 the split-fp16 dtype POSU_F16X3 (conv / dual / deconv /
+ * deconv+head / head / pack / s2d pack / max-pool / unpack entry points).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */

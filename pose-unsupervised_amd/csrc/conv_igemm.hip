@@ -101,6 +101,10 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int NT = NW * 64;
   constexpr int E = O::E;
   constexpr int ES = static_cast<int>(sizeof(T));
+  // split fp16: K-tiles of [hi 32 | lo 32] halves, three MFMAs per K-tile and fragment pair;
+  // outputs / residuals are (hi, lo) pairs, ocs halves per output pixel
+  constexpr bool SPL = O::SPLIT;
+  static_assert(!(SPL && SG), "split fp16 runs the unstaggered loops");
   constexpr int BK = 8 * E;                   // 128-byte LDS rows
   constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
@@ -163,6 +167,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   const int cL = (tid & 7) ^ ((tid >> 4) & 7);
   auto drow = [&](int i) { return (tid >> 3) + ROWS * i; };
   const int HoWo = g.Ho * g.Wo;
+  const int ocs = SPL ? 2 * g.Cout : g.Cout;  // elements per output pixel
   int hb[RA], wb[RA], nb[RA];   // generic window gather
   int o1[RA], o2[RA];           // DUAL: byte offsets of the two 1x1 sources
   u32x4 x2rs = xrs;
@@ -293,7 +298,31 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   {                                                                                                 \
     const char* As_ = smem + (BUF) * STAGE;                                                         \
     const char* Bs_ = As_ + A_BYTES;                                                                \
-    if constexpr (PRELOAD) {                                                                        \
+    if constexpr (SPL) {                                                                            \
+      /* k-step 0 = the hi halves, k-step 1 = the lo halves of the same 32 k: w.x as */             \
+      /* hi.hi + lo(w).hi(x) + hi(w).lo(x); at most TM + 2 TN fragments live */                     \
+      uint4 x0[TM], w0[TN];                                                                         \
+      _Pragma("unroll") for (int j = 0; j < TN; ++j)                                                \
+        w0[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, q));             \
+      _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                \
+        x0[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, q));             \
+      _Pragma("unroll") for (int i = 0; i < TM; ++i)                                                \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], w0[j], x0[i]);             \
+      {                                                                                             \
+        uint4 w1[TN];                                                                               \
+        _Pragma("unroll") for (int j = 0; j < TN; ++j)                                              \
+          w1[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, 4 + q));       \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], w1[j], x0[i]);           \
+      }                                                                                             \
+      {                                                                                             \
+        uint4 x1[TM];                                                                               \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          x1[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, 4 + q));       \
+        _Pragma("unroll") for (int i = 0; i < TM; ++i)                                              \
+          _Pragma("unroll") for (int j = 0; j < TN; ++j) O::mma(acc[i][j], w0[j], x1[i]);           \
+      }                                                                                             \
+    } else if constexpr (PRELOAD) {                                                                 \
       /* both k-steps' fragments first: the MFMAs then run back to back while the */                \
       /* second half's reads land, instead of stalling on them mid-tile */                          \
       uint4 af[2][TM], bfr[2][TN];                                                                  \
@@ -332,7 +361,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // Early residual prefetch (short-K Bottleneck tails): the residual chunks, in the direct
   // epilogue's lane layout, are loaded before the first operand DMA, so their HBM latency
   // overlaps the operand fetch instead of following the main loop.
-  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16;
+  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16 && !SPL;
   constexpr int ETM = EARLY ? TM : 1, ETP = EARLY ? TN / 2 : 1;
   const bool early = EARLY && g.res && g.mode == 0 && !g.hm && nk <= kEarlyNK;
   uint4 rve[ETM][ETP];
@@ -342,7 +371,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     const int mm = mok ? m : 0;
     const int n = mm / HoWo, rem = mm - n * HoWo;
     const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-    return (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+    return (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * ocs;
   };
   if constexpr (EARLY) {
     if (early) {
@@ -481,7 +510,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         // are live at a time and each accumulator pair dies once consumed (the 256x256 head
         // instance spilled 38 VGPRs with m-tile outer); every hacc[i] still receives its MFMAs in
         // the same order (pair 0's, then pair 1's), so the heatmaps are unchanged
-        const bool split = g.hw_lo != nullptr;
+        const bool split = SPL || g.hw_lo != nullptr;  // the split dtype's head is always split
         const T* __restrict__ hwp = reinterpret_cast<const T*>(g.hw);
         const T* __restrict__ hwq = reinterpret_cast<const T*>(split ? g.hw_lo : g.hw);
         f32x4 hacc[TM];
@@ -513,7 +542,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
               const int mm = mok ? m : 0;
               const int n = mm / HoWo, rem = mm - n * HoWo;
               const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
-              pix = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
+              pix = (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * ocs;
             }
             float v[8], r[8];
 #pragma unroll
@@ -523,9 +552,18 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
               v[e] = __uint_as_float(sw[0]);
               v[4 + e] = __uint_as_float(sw[1]);
             }
-            uint4 rv = make_uint4(0, 0, 0, 0);
-            if (rp && mok && in) rv = *reinterpret_cast<const uint4*>(rp + pix + cp);
-            O::load_vals(rv, r);
+            if constexpr (SPL) {
+              uint4 rh = make_uint4(0, 0, 0, 0), rl = rh;
+              if (rp && mok && in) {
+                rh = *reinterpret_cast<const uint4*>(rp + pix + split_ch(cp));
+                rl = *reinterpret_cast<const uint4*>(rp + pix + split_ch(cp) + 32);
+              }
+              join8(rh, rl, r);
+            } else {
+              uint4 rv = make_uint4(0, 0, 0, 0);
+              if (rp && mok && in) rv = *reinterpret_cast<const uint4*>(rp + pix + cp);
+              O::load_vals(rv, r);
+            }
             affine8<false>(v, sc8, sh8);
             if (rp) add8<false>(v, r);
             if (g.relu) {
@@ -534,6 +572,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
             }
             const uint4 pk = O::store_vals(v);
             O::mma(hacc[i], hw, pk);  // rows = joints, cols = pixels
+            uint4 pl = make_uint4(0, 0, 0, 0);
             if (split) {
               // the deconv output's rounding residual v - round(v) (exact in f32) rounded again: the
               // head sees v to 2 x the dtype's mantissa, its weights likewise (hi.hi + lo.hi + hi.lo)
@@ -541,11 +580,18 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
               O::load_vals(pk, vr);
 #pragma unroll
               for (int e = 0; e < 8; ++e) vl[e] = v[e] - vr[e];
-              const uint4 pl = O::store_vals(vl);
+              pl = O::store_vals(vl);
               O::mma(hacc[i], hl, pk);
               O::mma(hacc[i], hw, pl);
             }
-            if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cp) = pk;
+            if constexpr (SPL) {
+              if (yp && mok) {
+                *reinterpret_cast<uint4*>(yp + pix + split_ch(cp)) = pk;
+                *reinterpret_cast<uint4*>(yp + pix + split_ch(cp) + 32) = pl;
+              }
+            } else {
+              if (yp && mok) *reinterpret_cast<uint4*>(yp + pix + cp) = pk;
+            }
           }
         }
         if constexpr (SG && (POSU_IG_ABLATE & 32)) {  // timing ablation: no head reduction / stores
@@ -607,11 +653,19 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       const int n = mm / HoWo, rem = mm - n * HoWo;
       const int oy = rem / g.Wo, ox = rem - oy * g.Wo;
       const size_t pix =
-          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * g.Cout;
-      uint4 rv[TP];
+          (static_cast<size_t>(n * g.out_H + oy * osc + oy_off) * g.out_W + (ox * osc + ox_off)) * ocs;
+      uint4 rv[TP], rl[TP];
 #pragma unroll
       for (int jp = 0; jp < TP; ++jp) {
         rv[jp] = make_uint4(0, 0, 0, 0);
+        rl[jp] = rv[jp];
+        if constexpr (SPL) {
+          if (rp && mok && cop[jp] < g.Cout) {
+            rv[jp] = *reinterpret_cast<const uint4*>(rp + pix + split_ch(cop[jp]));
+            rl[jp] = *reinterpret_cast<const uint4*>(rp + pix + split_ch(cop[jp]) + 32);
+          }
+          continue;
+        }
         if constexpr (EARLY) {
           if (early) {
             rv[jp] = rve[i][jp];
@@ -630,17 +684,30 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
           v[e] = __uint_as_float(sw[0]);
           v[4 + e] = __uint_as_float(sw[1]);
         }
-        O::load_vals(rv[jp], r);
+        if constexpr (SPL) {
+          join8(rv[jp], rl[jp], r);
+        } else {
+          O::load_vals(rv[jp], r);
+        }
         affine8<false>(v, sc[jp], sh[jp]);
         if (rp) add8<false>(v, r);
         if (g.relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         }
-        if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
+        if constexpr (SPL) {
+          if (mok && cop[jp] < g.Cout) {
+            uint4 h, l;
+            split8(v, h, l);
+            *reinterpret_cast<uint4*>(yp + pix + split_ch(cop[jp])) = h;
+            *reinterpret_cast<uint4*>(yp + pix + split_ch(cop[jp]) + 32) = l;
+          }
+        } else {
+          if (mok && cop[jp] < g.Cout) *reinterpret_cast<uint4*>(yp + pix + cop[jp]) = O::store_vals(v);
+        }
       }
     }
-  } else if (g.mode == 0 && !g.hm) {
+  } else if (!SPL && g.mode == 0 && !g.hm) {
     T* __restrict__ yp = reinterpret_cast<T*>(g.y);
     const T* __restrict__ rp = reinterpret_cast<const T*>(g.res);
     float sc[TN][4], sh[TN][4];
@@ -707,7 +774,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr int CPR = BN / E;            // output chunks per tile row
   constexpr int ITER = PR * CPR / NT;    // chunks per thread per pass
   static_assert(ITER * NT == PR * CPR, "epilogue chunk split");
-  const bool mode0 = g.mode == 0 && !g.hm;
+  const bool mode0 = !SPL && g.mode == 0 && !g.hm;  // (split NHWC outputs take the direct epilogue)
   const bool relu_at_stage = g.relu && !mode0;  // mode 0: ReLU after the residual add
   float sc[TN][4], sh[TN][4];
 #pragma unroll
@@ -811,7 +878,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
         const int n = m / HoWo, pixo = m - n * HoWo;
         yp[(static_cast<size_t>(n) * g.Cout + n0 + col) * HoWo + pixo] = Cs[row * LD + col];
       }
-    } else if constexpr (BN == 256 && BM == 64 && PR == BM && NW == 4) {
+    } else if constexpr (!SPL && BN == 256 && BM == 64 && PR == BM && NW == 4) {
       // optional store of the deconv output f (NHWC), values rounded to T in place so
       // the head sees exactly what a separate head launch would read
       T* __restrict__ yp = reinterpret_cast<T*>(g.y);
@@ -1349,13 +1416,22 @@ bool tile_ok(int tile) {
 
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
+  // the split dtype runs the plain (unstaggered, non-persistent) loops: its K-tiles pair two
+  // k-steps, which the half-K-tile stagger would cut apart
+  constexpr bool SPL = Op<T>::SPLIT;
+  constexpr bool FAST2 = sizeof(T) == 2 && !SPL;
   if constexpr (sizeof(T) == 2 && !DUAL) {  // fused head on the eight-wave 256x256 tile, direct epilogue
     if (g.hm && g.CoutPad == 256) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
-      // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
-      hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true, true>), dim3(g.mtiles * nclass),
-                         dim3(512), 0, s, g);
+      if constexpr (SPL) {
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, true>), dim3(g.mtiles * nclass),
+                           dim3(512), 0, s, g);
+      } else {
+        // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true, true>), dim3(g.mtiles * nclass),
+                           dim3(512), 0, s, g);
+      }
       return check_launch(what);
     }
   }
@@ -1385,12 +1461,12 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   bool wg4 = false;  // tile 15: the 4 x 2 wave grid of the 128x128 eight-wave tile
   if (tile == 23 || tile == 31) {
     const int c = tile == 23 ? 5 : 6;
-    if (sizeof(T) == 2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
+    if (FAST2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
       cfg = c;
       sg = true;
     }
   } else if (tile == 7 || tile == 15) {
-    if (sizeof(T) == 2 && g.CoutPad % 128 == 0) {
+    if (FAST2 && g.CoutPad % 128 == 0) {
       cfg = 7;
       sg = true;
       wg4 = tile == 15;
@@ -1403,10 +1479,10 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       st = v == 1 ? (c <= 4 ? 1 : 2) : v == 2 ? 3 : 2;
       // persistent K-tile stream: 2-byte dtypes, direct NHWC epilogue, outputs addressable
       // by a 32-bit buffer offset
-      persist = (tile & 32) != 0 && sizeof(T) == 2 && g.mode == 0 &&
+      persist = (tile & 32) != 0 && FAST2 && g.mode == 0 &&
                 static_cast<long long>(g.N) * g.out_H * g.out_W * g.Cout * sizeof(T) < (1LL << 31) - 256;
     }
-  } else if (sizeof(T) == 2 && (cfg == 5 || cfg == 6)) {
+  } else if (FAST2 && (cfg == 5 || cfg == 6)) {
     sg = true;  // untuned eight-wave launches take the staggered loop (bit-exact with the plain one)
   }
   static const int kBM[] = {256, 128, 64, 128, 64, 256, 256, 128};
@@ -1414,7 +1490,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
-  if constexpr (sizeof(T) == 2) {
+  if constexpr (FAST2) {
     if (persist) {
       switch (cfg) {
         case 0: launch_persist<T, 256, 64, 4, 4, DUAL>(g, nb, s); break;
@@ -1457,6 +1533,7 @@ int dispatch(int dtype, ConvGeom& g, int nclass, void* stream, const char* what,
   if (dtype == POSU_BF16) return launch<uint16_t, DUAL>(g, nclass, s, what, tile);
   if (dtype == POSU_F32) return launch<float, DUAL>(g, nclass, s, what, tile);
   if (dtype == POSU_F16) return launch<f16_t, DUAL>(g, nclass, s, what, tile);
+  if (dtype == POSU_F16X3) return launch<f16s_t, DUAL>(g, nclass, s, what, tile);
   set_error(std::string(what) + ": unsupported dtype");
   return POSU_ERR_ARG;
 }
@@ -1468,15 +1545,19 @@ bool params_aligned(const float* scale, const float* shift) {
 
 int bk_of(int dtype) { return dtype == POSU_F32 ? 32 : 64; }
 int esz_of(int dtype) { return dtype == POSU_F32 ? 4 : 2; }
+// stored elements per logical channel (the split dtype keeps a (hi, lo) pair)
+int cm_of(int dtype) { return dtype == POSU_F16X3 ? 2 : 1; }
 
 int common_checks(int dtype, const void* x, const void* w, const void* y, int N, int H, int W, int C,
                   int Cout, const char* what) {
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F32 || dtype == POSU_F16,
-               std::string(what) + ": dtype must be F32, BF16 or F16");
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F32 || dtype == POSU_F16 || dtype == POSU_F16X3,
+               std::string(what) + ": dtype must be F32, BF16, F16 or F16X3");
   POSU_REQUIRE(x && w && y, std::string(what) + ": null pointer");
   POSU_REQUIRE(N > 0 && H > 0 && W > 0 && Cout > 0, std::string(what) + ": empty shape");
   POSU_REQUIRE(C >= 8 && ilog2(C) >= 0, std::string(what) + ": C must be a power of two >= 8");
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * esz_of(dtype) < (1LL << 31) - 256,
+  POSU_REQUIRE(dtype != POSU_F16X3 || (C % 32 == 0 && Cout % 32 == 0),
+               std::string(what) + ": split fp16 needs C and Cout multiples of 32");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * cm_of(dtype) * esz_of(dtype) < (1LL << 31) - 256,
                std::string(what) + ": input exceeds the 2 GiB buffer-descriptor range");
   return POSU_OK;
 }
@@ -1488,13 +1569,12 @@ ConvGeom base_geom(const void* x, int N, int H, int W, int C, const void* w, int
   g.N = N;
   g.H = H;
   g.W = W;
-  g.C = C;
-  g.logC = ilog2(C);
+  g.C = C * cm_of(dtype);  // stored channels (the GEMM's K per tap)
+  g.logC = ilog2(g.C);
   g.Cout = Cout;
   g.CoutPad = round_up(Cout, 64);
   g.stride = 1;
   g.KH = g.KW = 1;
-  (void)dtype;
   return g;
 }
 
@@ -1515,7 +1595,8 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   POSU_REQUIRE(KH > 0 && KW > 0 && stride > 0 && pad >= 0, "posu_conv2d_fwd: bad window");
   POSU_REQUIRE(Ho > 0 && Wo > 0 && Ho <= (H + 2 * pad - KH) / stride + 1 && Wo <= (W + 2 * pad - KW) / stride + 1,
                "posu_conv2d_fwd: Ho/Wo larger than the window allows");
-  POSU_REQUIRE(static_cast<long long>(N) * Ho * Wo * Cout < (1LL << 31), "posu_conv2d_fwd: output too large");
+  POSU_REQUIRE(static_cast<long long>(N) * Ho * Wo * Cout * cm_of(dtype) < (1LL << 31),
+               "posu_conv2d_fwd: output too large");
   POSU_REQUIRE(params_aligned(scale, shift), "posu_conv2d_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
@@ -1525,7 +1606,7 @@ extern "C" int posu_conv2d_fwd(int dtype, const void* x, int N, int H, int W, in
   g.Ho = Ho;
   g.Wo = Wo;
   g.M = N * Ho * Wo;
-  g.K = KH * KW * C;
+  g.K = KH * KW * g.C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.KH = KH;
   g.KW = KW;
@@ -1548,23 +1629,24 @@ extern "C" int posu_conv1x1_dual_fwd(int dtype, const void* x, int N, int H, int
   POSU_REQUIRE(C % BK == 0 && C2 % BK == 0, "posu_conv1x1_dual_fwd: C and C2 must be multiples of the K-tile");
   POSU_REQUIRE(stride2 > 0 && (H - 1) * stride2 < H2 && (W - 1) * stride2 < W2,
                "posu_conv1x1_dual_fwd: source-2 grid too small for the output grid");
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * Cout < (1LL << 31), "posu_conv1x1_dual_fwd: output too large");
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * Cout * cm_of(dtype) < (1LL << 31),
+               "posu_conv1x1_dual_fwd: output too large");
   POSU_REQUIRE(params_aligned(scale, shift), "posu_conv1x1_dual_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.x2 = x2;
   g.H2 = H2;
   g.W2 = W2;
-  g.C2 = C2;
+  g.C2 = C2 * cm_of(dtype);
   g.stride2 = stride2;
-  g.K1 = C;
+  g.K1 = g.C;
   g.scale = scale;
   g.shift = shift;
   g.y = y;
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.K = C + C2;
-  g.Kpad = C + C2;
+  g.K = g.C + g.C2;
+  g.Kpad = g.C + g.C2;
   g.relu = relu;
   g.out_H = H;
   g.out_W = W;
@@ -1578,7 +1660,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   POSU_REQUIRE(tile_ok(tile), "posu_deconv4x4s2_fwd: tile must be -1 (auto), cfg + 8 * variant (+ 32), 7, 15, 23 or 31");
   const int E = 16 / esz_of(dtype);
   POSU_REQUIRE(Cout % E == 0, "posu_deconv4x4s2_fwd: Cout must be a multiple of 16 bytes");
-  POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout < (1LL << 31),
+  POSU_REQUIRE(static_cast<long long>(N) * 4 * H * W * Cout * cm_of(dtype) < (1LL << 31),
                "posu_deconv4x4s2_fwd: output too large");
   POSU_REQUIRE(params_aligned(scale, shift), "posu_deconv4x4s2_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
@@ -1588,7 +1670,7 @@ extern "C" int posu_deconv4x4s2_fwd(int dtype, const void* x, int N, int H, int 
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.K = 4 * C;
+  g.K = 4 * g.C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.KH = 2;
   g.KW = 2;
@@ -1605,6 +1687,9 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   if (int st = common_checks(dtype, x, w, hm, N, H, W, C, Cout, "posu_deconv4x4s2_head_fwd")) return st;
   POSU_REQUIRE(hw && Cout == 256 && J > 0 && J <= 16,
                "posu_deconv4x4s2_head_fwd: needs Cout == 256, 0 < J <= 16 and head weights");
+  POSU_REQUIRE(dtype != POSU_F16X3 || hw_lo, "posu_deconv4x4s2_head_fwd: split fp16 needs hw_lo");
+  POSU_REQUIRE(((reinterpret_cast<size_t>(hw) | reinterpret_cast<size_t>(hw_lo)) & 15) == 0,
+               "posu_deconv4x4s2_head_fwd: hw / hw_lo must be 16-byte aligned");
   POSU_REQUIRE(params_aligned(scale, shift), "posu_deconv4x4s2_head_fwd: scale / shift must be 16-byte aligned");
   ConvGeom g = base_geom(x, N, H, W, C, w, Cout, dtype);
   g.scale = scale;
@@ -1613,7 +1698,7 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.K = 4 * C;
+  g.K = 4 * g.C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.KH = 2;
   g.KW = 2;
@@ -1622,7 +1707,7 @@ extern "C" int posu_deconv4x4s2_head_fwd(int dtype, const void* x, int N, int H,
   g.out_H = 2 * H;
   g.out_W = 2 * W;
   g.hw = hw;
-  g.hw_lo = (dtype == POSU_BF16 || dtype == POSU_F16) ? hw_lo : nullptr;  // f32 heads are exact already
+  g.hw_lo = (dtype == POSU_BF16 || dtype == POSU_F16 || dtype == POSU_F16X3) ? hw_lo : nullptr;  // f32: exact
   g.hbias = hbias;
   g.hm = hm;
   g.J = J;
@@ -1639,7 +1724,7 @@ extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int
   g.Ho = H;
   g.Wo = W;
   g.M = N * H * W;
-  g.K = C;
+  g.K = g.C;
   g.Kpad = round_up(g.K, bk_of(dtype));
   g.out_H = H;
   g.out_W = W;
@@ -1655,6 +1740,7 @@ extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int
 extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
                                  int Cin, int KH, int KW, int stride, int pad, const void* residual, void* dx, int H,
                                  int W, void* stream) {
+  POSU_REQUIRE(dtype != POSU_F16X3, "posu_conv2d_dgrad: the split dtype is inference-only");
   if (int st = common_checks(dtype, dy, wt, dx, N, Ho, Wo, Cout, Cin, "posu_conv2d_dgrad")) return st;
   POSU_REQUIRE(Cin % (16 / esz_of(dtype)) == 0, "posu_conv2d_dgrad: Cin must be a multiple of 16 bytes");
   POSU_REQUIRE(stride == 1 || stride == 2, "posu_conv2d_dgrad: stride 1 or 2");
@@ -1708,6 +1794,7 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
 // views come out of one launch, view-major.
 extern "C" int posu_gemm_rows_f32(int dtype, const void* x, int M, int K, const void* wt, int Ncol, int vblk,
                                   float* out, void* stream) {
+  POSU_REQUIRE(dtype != POSU_F16X3, "posu_gemm_rows_f32: the split dtype is not supported");
   if (int st = common_checks(dtype, x, wt, out, M, 1, 1, K, Ncol, "posu_gemm_rows_f32")) return st;
   POSU_REQUIRE(K % bk_of(dtype) == 0, "posu_gemm_rows_f32: K must be a multiple of the K-tile");
   POSU_REQUIRE(vblk > 0 && vblk % 8 == 0 && Ncol % vblk == 0, "posu_gemm_rows_f32: vblk must divide Ncol (x8)");

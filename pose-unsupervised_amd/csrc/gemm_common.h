@@ -12,6 +12,7 @@ struct Op;
 template <>
 struct Op<uint16_t> {  // bf16
   static constexpr int E = 8;
+  static constexpr bool SPLIT = false;
   static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
                                                   __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
@@ -35,6 +36,7 @@ struct Op<uint16_t> {  // bf16
 template <>
 struct Op<f16_t> {  // IEEE fp16
   static constexpr int E = 8;
+  static constexpr bool SPLIT = false;
   static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), acc,
                                                  0, 0, 0);
@@ -52,9 +54,24 @@ struct Op<f16_t> {  // IEEE fp16
   }
 };
 
+// split fp16 (POSU_F16X3): the operands are fp16 halves of (hi, lo) pairs; a K-tile of 64 halves
+// holds 32 logical k as [hi 32 | lo 32], i.e. its two MFMA k-steps are the hi and the lo halves of
+// the same k, and the kernels issue hi.hi + lo(w).hi(x) + hi(w).lo(x) per K-tile (SPLIT).
+template <>
+struct Op<f16s_t> {
+  static constexpr int E = 8;
+  static constexpr bool SPLIT = true;
+  static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
+    Op<f16_t>::mma(acc, a, b);
+  }
+  static __device__ __forceinline__ void load_vals(const uint4& u, float* v) { Op<f16_t>::load_vals(u, v); }
+  static __device__ __forceinline__ uint4 store_vals(const float* v) { return Op<f16_t>::store_vals(v); }
+};
+
 template <>
 struct Op<float> {
   static constexpr int E = 4;
+  static constexpr bool SPLIT = false;
   static __device__ __forceinline__ void mma(f32x4& acc, const uint4& a, const uint4& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);

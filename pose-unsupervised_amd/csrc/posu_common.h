@@ -35,6 +35,34 @@ struct f16_t {
   uint16_t bits;
 };
 
+// Split-fp16 storage type (POSU_F16X3): each value a (hi, lo) pair of fp16, [hi 32 | lo 32] per
+// 32-channel block (include/posu.h).  Its own type so the conv kernel's traits select the
+// three-MFMA products and the pair epilogue.
+struct f16s_t {
+  uint16_t bits;
+};
+
+// physical element offset of logical channel c's hi half in a split pixel (lo: + 32)
+__host__ __device__ __forceinline__ int split_ch(int c) { return ((c >> 5) << 6) + (c & 31); }
+
+// v -> (hi, lo): hi = fp16(v), lo = fp16(v - hi) (v - hi is exact in f32)
+__device__ __forceinline__ void split8(const float* v, uint4& hi, uint4& lo) {
+  f16x8 h, l;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    h[i] = static_cast<_Float16>(v[i]);
+    l[i] = static_cast<_Float16>(v[i] - static_cast<float>(h[i]));
+  }
+  hi = __builtin_bit_cast(uint4, h);
+  lo = __builtin_bit_cast(uint4, l);
+}
+// (hi, lo) -> hi + lo in f32 (exact: the pair spans at most 22 significant bits)
+__device__ __forceinline__ void join8(const uint4& hi, const uint4& lo, float* v) {
+  const f16x8 h = __builtin_bit_cast(f16x8, hi), l = __builtin_bit_cast(f16x8, lo);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(h[i]) + static_cast<float>(l[i]);
+}
+
 __device__ __forceinline__ float bf2f(uint16_t b) {
   return __uint_as_float(static_cast<uint32_t>(b) << 16);
 }

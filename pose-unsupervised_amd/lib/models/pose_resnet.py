@@ -148,8 +148,8 @@ class PoseResNet(nn.Module):
     def train_plan(self):
         """The training-mode launch sequence (posu.train_plan.TrainPlan); packs per step."""
         code = ops.dtype_code(self.precision)
-        if code == ops.F16:
-            raise NotImplementedError('training in fp16 needs loss scaling; use precision bf16 or fp32')
+        if code in (ops.F16, ops.F16X3):
+            raise NotImplementedError('training in fp16 / fp16x3 needs loss scaling; use precision bf16 or fp32')
         if self._train_plan is None or self._train_plan.code != code:
             self._train_plan = TrainPlan(self, code)
         return self._train_plan
@@ -173,7 +173,7 @@ class PoseResNet(nn.Module):
         # deconv outputs are widened once here (the heatmaps are f32 already); NHWC ->
         # NCHW-shaped channels-last views
         if x1.dtype != torch.float32:
-            x1, f = x1.float(), f.float()
+            x1, f = ops.widen(x1, plan.code), ops.widen(f, plan.code)
         return hm, x1.permute(0, 3, 1, 2), f.permute(0, 3, 1, 2)
 
     def forward(self, x):
@@ -209,7 +209,8 @@ resnet_spec = {18: (BasicBlock, [2, 2, 2, 2]),
 
 def get_pose_net(cfg, is_train, **kwargs):
     """Reference factory (pose_resnet.py:257-267); extra kwarg ``precision`` = 'fp32' (default,
-    reference numerics) | 'bf16' | 'fp16' (opt-in fast modes)."""
+    reference numerics) | 'fp16x3' (split fp16: reference-parity numerics on the fp16 MFMAs) |
+    'bf16' | 'fp16' (opt-in fast modes)."""
     block_class, layers = resnet_spec[cfg.POSE_RESNET.NUM_LAYERS]
     model = PoseResNet(block_class, layers, cfg, **kwargs)
     if is_train:

@@ -15,9 +15,10 @@ F32 = 0
 BF16 = 1
 F64 = 2
 F16 = 3
+F16X3 = 4   # split fp16 (hi + lo pairs, three MFMAs per product): include/posu.h
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()

@@ -8,9 +8,9 @@ through (soft-argmax, crop affine, epipolar loss, heatmap MSE).
 import torch
 
 from . import _native as nat
-from ._native import F32, BF16, F64, F16, ptr, call, stream_of, require_cuda
+from ._native import F32, BF16, F64, F16, F16X3, ptr, call, stream_of, require_cuda
 
-_TORCH_OF = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16}
+_TORCH_OF = {F32: torch.float32, BF16: torch.bfloat16, F16: torch.float16, F16X3: torch.float16}
 
 
 def dtype_code(dtype):
@@ -20,11 +20,33 @@ def dtype_code(dtype):
         return F32
     if dtype in ('fp16', 'f16', torch.float16, F16):
         return F16
-    raise ValueError('unsupported compute dtype %r (bf16 | fp16 | fp32)' % (dtype,))
+    if dtype in ('fp16x3', F16X3):
+        return F16X3
+    raise ValueError('unsupported compute dtype %r (bf16 | fp16 | fp16x3 | fp32)' % (dtype,))
 
 
 def torch_dtype(code):
     return _TORCH_OF[code]
+
+
+def cmul(code):
+    """Stored elements per logical channel: 2 for the split dtype (a (hi, lo) fp16 pair,
+    [hi 32 | lo 32] per 32-channel block, include/posu.h), else 1."""
+    return 2 if code == F16X3 else 1
+
+
+def channels(x, code):
+    """Logical channel count of an NHWC activation tensor."""
+    return x.shape[3] // cmul(code)
+
+
+def widen(x, code):
+    """NHWC activations -> f32 values (the split dtype's pairs summed: hi + lo is exact in f32)."""
+    if code != F16X3:
+        return x.float()
+    n, h, w, c2 = x.shape
+    t = x.view(n, h, w, c2 // 64, 2, 32).float()
+    return (t[..., 0, :] + t[..., 1, :]).reshape(n, h, w, c2 // 2)
 
 
 def conv_bk(code):
@@ -38,7 +60,7 @@ def pack_nchw_to_nhwc(x, code, cpad, out=None, hflip=False):
     x = x.contiguous().float()
     n, c, h, w = x.shape
     if out is None:
-        out = torch.empty((n, h, w, cpad), dtype=torch_dtype(code), device=x.device)
+        out = torch.empty((n, h, w, cpad * cmul(code)), dtype=torch_dtype(code), device=x.device)
     call('posu_pack_nchw_to_nhwc', code, ptr(x), n, c, h, w, ptr(out), cpad, int(hflip), stream_of(x.device))
     return out
 
@@ -49,7 +71,7 @@ def pack_s2d_nchw(x, code, cpad, out=None, hflip=False):
     x = x.contiguous().float()
     n, c, h, w = x.shape
     if out is None:
-        out = torch.empty((n, h // 2, w // 2, cpad), dtype=torch_dtype(code), device=x.device)
+        out = torch.empty((n, h // 2, w // 2, cpad * cmul(code)), dtype=torch_dtype(code), device=x.device)
     call('posu_pack_s2d_nchw', code, ptr(x), n, c, h, w, ptr(out), cpad, int(hflip), stream_of(x.device))
     return out
 
@@ -57,6 +79,7 @@ def pack_s2d_nchw(x, code, cpad, out=None, hflip=False):
 def nhwc_to_nchw_f32(x, code):
     require_cuda(x)
     n, h, w, c = x.shape
+    c //= cmul(code)
     out = torch.empty((n, c, h, w), dtype=torch.float32, device=x.device)
     call('posu_nhwc_to_nchw_f32', code, ptr(x), n, h, w, c, ptr(out), stream_of(x.device))
     return out
@@ -66,25 +89,29 @@ def nhwc_to_nchw_f32(x, code):
 def conv2d_nhwc(x, wpk, cout, kh, kw, stride, pad, scale, shift, residual, relu, code, out=None, out_hw=None,
                 tile=-1):
     n, h, w, c = x.shape
+    c //= cmul(code)
     ho = (h + 2 * pad - kh) // stride + 1
     wo = (w + 2 * pad - kw) // stride + 1
     if out_hw is not None:
         ho, wo = out_hw
     if out is None:
-        out = torch.empty((n, ho, wo, cout), dtype=x.dtype, device=x.device)
+        out = torch.empty((n, ho, wo, cout * cmul(code)), dtype=x.dtype, device=x.device)
     call('posu_conv2d_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, kh, kw, stride, pad,
          ptr(scale), ptr(shift), ptr(residual), int(relu), ptr(out), ho, wo, int(tile), stream_of(x.device))
     return out
 
 
-def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, tile=-1):  # noqa: D401
-    """act(W[:, :C] x + W[:, C:] x2[::stride2, ::stride2] + shift) (two 1x1 sources, one output)."""
+def conv1x1_dual_nhwc(x, x2, stride2, wpk, cout, shift, relu, code, out=None, tile=-1, scale=None):  # noqa: D401
+    """act((W[:, :C] x + W[:, C:] x2[::stride2, ::stride2]) * scale + shift) (two 1x1 sources, one
+    output; scale None = 1)."""
     n, h, w, c = x.shape
     _, h2, w2, c2 = x2.shape
+    c //= cmul(code)
+    c2 //= cmul(code)
     if out is None:
-        out = torch.empty((n, h, w, cout), dtype=x.dtype, device=x.device)
+        out = torch.empty((n, h, w, cout * cmul(code)), dtype=x.dtype, device=x.device)
     call('posu_conv1x1_dual_fwd', code, ptr(x), n, h, w, c, ptr(x2), h2, w2, c2, int(stride2), ptr(wpk), cout,
-         None, ptr(shift), int(relu), ptr(out), int(tile), stream_of(x.device))
+         ptr(scale), ptr(shift), int(relu), ptr(out), int(tile), stream_of(x.device))
     return out
 
 
@@ -169,8 +196,9 @@ def bottleneck_down_nhwc(x, w1, s1, b1, w2, s2, b2, w3d, shift3, code, out=None)
 
 def deconv4x4s2_nhwc(x, wpk, cout, scale, shift, relu, code, out=None, tile=-1):
     n, h, w, c = x.shape
+    c //= cmul(code)
     if out is None:
-        out = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
+        out = torch.empty((n, 2 * h, 2 * w, cout * cmul(code)), dtype=x.dtype, device=x.device)
     call('posu_deconv4x4s2_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(scale), ptr(shift),
          int(relu), ptr(out), int(tile), stream_of(x.device))
     return out
@@ -181,10 +209,11 @@ def deconv4x4s2_head(x, wpk, cout, scale, shift, head_w, njoints, head_b, code, 
     """Last deconv + BN + ReLU fused with the 1x1 head: returns (heatmaps NCHW f32, f NHWC or None).
     head_w_lo (2-byte dtypes): the head weight's rounding residual -> the split-precision head."""
     n, h, w, c = x.shape
+    c //= cmul(code)
     if hm_out is None:
         hm_out = torch.empty((n, njoints, 2 * h, 2 * w), dtype=torch.float32, device=x.device)
     if keep_f and f_out is None:
-        f_out = torch.empty((n, 2 * h, 2 * w, cout), dtype=x.dtype, device=x.device)
+        f_out = torch.empty((n, 2 * h, 2 * w, cout * cmul(code)), dtype=x.dtype, device=x.device)
     call('posu_deconv4x4s2_head_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(scale), ptr(shift),
          ptr(f_out if keep_f else None), ptr(head_w), ptr(head_w_lo), njoints, ptr(head_b), ptr(hm_out),
          stream_of(x.device))
@@ -193,6 +222,7 @@ def deconv4x4s2_head(x, wpk, cout, scale, shift, head_w, njoints, head_b, code, 
 
 def head1x1_nchw(x, wpk, cout, bias, code, out=None):
     n, h, w, c = x.shape
+    c //= cmul(code)
     if out is None:
         out = torch.empty((n, cout, h, w), dtype=torch.float32, device=x.device)
     call('posu_head1x1_nchw_fwd', code, ptr(x), n, h, w, c, ptr(wpk), cout, ptr(bias), ptr(out),
@@ -239,7 +269,7 @@ def maxpool3x3s2_nhwc(x, code, out=None):
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     if out is None:
         out = torch.empty((n, ho, wo, c), dtype=x.dtype, device=x.device)
-    call('posu_maxpool3x3s2_fwd', code, ptr(x), n, h, w, c, ptr(out), stream_of(x.device))
+    call('posu_maxpool3x3s2_fwd', code, ptr(x), n, h, w, c // cmul(code), ptr(out), stream_of(x.device))
     return out
 
 

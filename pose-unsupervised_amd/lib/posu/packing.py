@@ -199,6 +199,34 @@ def pack_deconv4x4_weight(w, bk, dtype):
     return out.to(dtype).contiguous()
 
 
+# the split dtype (POSU_F16X3) scales each packed weight by a power of two so that its largest
+# entry sits at 2^SPLIT_WEIGHT_EXP before the (hi, lo) split: the lo halves of small weights stay
+# out of the fp16 subnormal range (tools/precision_attribution.py 'fp16x3_wscale14'); the kernels'
+# f32 epilogue scale takes the inverse power (exact)
+SPLIT_WEIGHT_EXP = 14
+
+
+def split_exponent(w):
+    """Power-of-two exponent e with max |w| * 2^e in (2^(SPLIT_WEIGHT_EXP - 1), 2^SPLIT_WEIGHT_EXP]."""
+    m = float(w.detach().abs().max())
+    if m == 0.0:
+        return 0
+    return SPLIT_WEIGHT_EXP - int(np.ceil(np.log2(m)))
+
+
+def to_split(wpk, e=0):
+    """An f32 / f64 pack [..., K] (K % 32 == 0, k in the kernel's logical order) -> the split fp16
+    pack [..., 2K]: per 32-k block [hi 32 | lo 32] of wpk * 2^e, hi = fp16(v), lo = fp16(v - hi)."""
+    v = wpk.double() * (2.0 ** e)
+    if v.shape[-1] % 32:
+        raise ValueError('split packs need K a multiple of 32 (got %d)' % v.shape[-1])
+    hi = v.to(torch.float16)
+    lo = (v - hi.double()).to(torch.float16)
+    blk = v.shape[:-1] + (v.shape[-1] // 32, 1, 32)
+    out = torch.cat([hi.reshape(blk), lo.reshape(blk)], dim=-2)
+    return out.reshape(v.shape[:-1] + (2 * v.shape[-1],)).contiguous()
+
+
 def fold_bn(bn, conv_bias=None):
     """(scale, shift) f32 of an eval-mode BatchNorm2d (optionally after a biased conv)."""
     gamma = bn.weight.detach().double() if bn.weight is not None else torch.ones_like(bn.running_mean.double())

@@ -20,10 +20,31 @@ from . import ops
 from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
                       pack_conv_weight, pack_deconv4x4_weight,
                       pack_dual_1x1_weight, pack_s2_tail_stream, pack_stem_fused_weight, pack_stem_s2d_weight,
-                      pack_tail_stream)
+                      pack_tail_stream, split_exponent, to_split)
 
 STEM_CIN_PAD = 8      # direct 7x7 stem (odd input sizes)
 STEM_S2D_PAD = 16     # space-to-depth stem: 4 sub-pixels x 3 channels, padded
+SPLIT_PAD = 32        # the split dtype's channel granule (the stem pads to it)
+
+
+def _stem_pads(code):
+    """(direct-stem Cin pad, space-to-depth pad) in logical channels (distinct: run_stem tells the
+    two packed inputs apart by their channel count; the split dtype's direct stem, for odd input
+    sizes only, pads to 2 granules)."""
+    return (2 * SPLIT_PAD, SPLIT_PAD) if code == ops.F16X3 else (STEM_CIN_PAD, STEM_S2D_PAD)
+
+
+def _pack(pk32, code):
+    """An f32 / f64 pack in the logical K order -> (pack in the compute dtype, power-of-two weight
+    exponent e the epilogue scale must undo: 2^-e; 0 except for the split dtype)."""
+    if code == ops.F16X3:
+        e = split_exponent(pk32)
+        return to_split(pk32, e), e
+    return pk32.to(ops.torch_dtype(code)).contiguous(), 0
+
+
+def _unscale(scale, e):
+    return scale if e == 0 else (scale.double() * 2.0 ** -e).float().contiguous()
 
 # fused pack + stem + max-pool kernel (posu_stem_pool_fwd) for bf16 / fp16 plans
 FUSED_STEM = True
@@ -81,7 +102,7 @@ class _Tuner:
     seen = []   # geometry keys met by the current tuning run, in launch order
 
 
-def _tile_candidates(cout):
+def _tile_candidates(cout, code=None):
     """Tile ids (include/posu.h): cfg 0..6, cfg + 8 = single-slot ring (four-wave tiles;
     short-K layers: more blocks per CU), cfg + 16 = three-slot ring (two K-tiles in flight),
     cfg + 32 = persistent K-tile stream (epilogue stores overlap the next tile's fetch),
@@ -99,13 +120,15 @@ def _tile_candidates(cout):
     sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 and TILES_128X8 else [])
     # (tile 32, the persistent 256x64 four-wave instance, is left out: it spills 928 B per lane to
     # scratch and took ~1.2 ms per launch in the tuning trials, 10x the other tiles)
+    if code == ops.F16X3:   # the split dtype: plain rings only (no stagger, no persistent stream)
+        return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
 
 
 def _tuned(key, cout, launch):
     """launch(tile) -> output.  While tuning, time every admissible tile once on the real
     operands (HIP events) and keep the fastest for this geometry."""
-    cands = _tile_candidates(cout)
+    cands = _tile_candidates(cout, key[1])
     if _Tuner.active and key not in _Tuner.seen:
         _Tuner.seen.append(key)
     # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan
@@ -152,8 +175,11 @@ class _Conv:
 
     def __init__(self, conv, bn, relu, code, bk, cin_pad=None):
         cin = conv.weight.shape[1]
-        self.w = pack_conv_weight(conv.weight, cin_pad or cin, bk, ops.torch_dtype(code))
+        # (the split dtype packs 32 logical k per K-tile)
+        self.w, e = _pack(pack_conv_weight(conv.weight, cin_pad or cin, 32 if code == ops.F16X3 else bk,
+                                           torch.float32), code)
         self.scale, self.shift = fold_bn(bn, conv.bias)
+        self.scale = _unscale(self.scale, e)
         self.cout = conv.weight.shape[0]
         self.k = conv.kernel_size[0]
         if conv.kernel_size[0] != conv.kernel_size[1]:
@@ -166,7 +192,7 @@ class _Conv:
         if out is None:
             ho = (x.shape[1] + 2 * self.pad - self.k) // self.stride + 1
             wo = (x.shape[2] + 2 * self.pad - self.k) // self.stride + 1
-            out = torch.empty((x.shape[0], ho, wo, self.cout), dtype=x.dtype, device=x.device)
+            out = torch.empty((x.shape[0], ho, wo, self.cout * ops.cmul(code)), dtype=x.dtype, device=x.device)
         key = ('conv', code, tuple(x.shape), self.cout, self.k, self.stride, self.pad, residual is not None)
         return _tuned(key, self.cout, lambda t: ops.conv2d_nhwc(
             x, self.w, self.cout, self.k, self.k, self.stride, self.pad, self.scale, self.shift, residual, self.relu,
@@ -175,22 +201,23 @@ class _Conv:
 
 class _DualTail:
     """Bottleneck conv3/bn3 + downsample conv/bn as one two-source 1x1 GEMM."""
-    __slots__ = ('w', 'shift', 'cout', 'stride2')
+    __slots__ = ('w', 'scale', 'shift', 'cout', 'stride2')
 
     def __init__(self, conv3, bn3, dconv, dbn, code):
         s3, b3 = fold_bn(bn3, conv3.bias)
         sd, bd = fold_bn(dbn, dconv.bias)
-        self.w = pack_dual_1x1_weight(conv3.weight, s3, dconv.weight, sd, ops.torch_dtype(code))
+        self.w, e = _pack(pack_dual_1x1_weight(conv3.weight, s3, dconv.weight, sd, torch.float64), code)
         self.shift = (b3.double() + bd.double()).float().contiguous()
         self.cout = conv3.weight.shape[0]
+        self.scale = None if e == 0 else torch.full((self.cout,), 2.0 ** -e, device=self.shift.device)
         self.stride2 = dconv.stride[0]
 
     def __call__(self, mid, x, code, out=None):
         if out is None:
-            out = torch.empty(tuple(mid.shape[:3]) + (self.cout,), dtype=mid.dtype, device=mid.device)
+            out = torch.empty(tuple(mid.shape[:3]) + (self.cout * ops.cmul(code),), dtype=mid.dtype, device=mid.device)
         key = ('dual', code, tuple(mid.shape), tuple(x.shape), self.cout)
         return _tuned(key, self.cout, lambda t: ops.conv1x1_dual_nhwc(
-            mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out, tile=t))
+            mid, x, self.stride2, self.w, self.cout, self.shift, True, code, out=out, tile=t, scale=self.scale))
 
 
 # Bottlenecks of layer1 (planes 64, 64x64 maps) as ONE fused launch each in bf16 / fp16 plans
@@ -376,13 +403,15 @@ class _Deconv:
     def __init__(self, dc, bn, code, bk):
         if dc.stride != (2, 2) or dc.padding != (1, 1) or dc.output_padding != (0, 0):
             raise NotImplementedError('deconv supported for kernel 4, stride 2, padding 1')
-        self.w = pack_deconv4x4_weight(dc.weight, bk, ops.torch_dtype(code))
+        self.w, e = _pack(pack_deconv4x4_weight(dc.weight, 32 if code == ops.F16X3 else bk, torch.float32), code)
         self.scale, self.shift = fold_bn(bn, dc.bias)
+        self.scale = _unscale(self.scale, e)
         self.cout = dc.weight.shape[1]
 
     def __call__(self, x, code, out=None):
         if out is None:
-            out = torch.empty((x.shape[0], 2 * x.shape[1], 2 * x.shape[2], self.cout), dtype=x.dtype, device=x.device)
+            out = torch.empty((x.shape[0], 2 * x.shape[1], 2 * x.shape[2], self.cout * ops.cmul(code)), dtype=x.dtype,
+                              device=x.device)
         key = ('deconv', code, tuple(x.shape), self.cout)
         return _tuned(key, self.cout, lambda t: ops.deconv4x4s2_nhwc(
             x, self.w, self.cout, self.scale, self.shift, True, code, out=out, tile=t))
@@ -394,9 +423,15 @@ class PoseResNetPlan:
     def __init__(self, net, code):
         self.code = code
         bk = ops.conv_bk(code)
-        self.stem = _Conv(net.conv1, net.bn1, True, code, bk, cin_pad=STEM_CIN_PAD)
-        # the same stem as a 4x4/s1 conv over the 2x2 space-to-depth input (even sizes)
-        self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, STEM_S2D_PAD, bk, ops.torch_dtype(code))
+        self.cin_pad, self.s2d_pad = _stem_pads(code)
+        self.stem = _Conv(net.conv1, net.bn1, True, code, bk, cin_pad=self.cin_pad)
+        # the same stem as a 4x4/s1 conv over the 2x2 space-to-depth input (even sizes); the same
+        # weights, so the same split exponent (the stem's scale is shared)
+        if code == ops.F16X3:
+            self.stem_s2d_w = to_split(pack_stem_s2d_weight(net.conv1.weight, self.s2d_pad, 32, torch.float32),
+                                       split_exponent(net.conv1.weight.float()))
+        else:
+            self.stem_s2d_w = pack_stem_s2d_weight(net.conv1.weight, self.s2d_pad, bk, ops.torch_dtype(code))
         self.layers = [[_Block(b, code, bk) for b in layer] for layer in
                        (net.layer1, net.layer2, net.layer3, net.layer4)]
         for layer in self.layers:
@@ -409,11 +444,16 @@ class PoseResNetPlan:
         fl = net.final_layer
         if fl.kernel_size != (1, 1):
             raise NotImplementedError('final layer supported for FINAL_CONV_KERNEL = 1')
+        # the fused head reads hi / lo weight halves in the logical channel order (the split dtype
+        # too); a separate head launch of the split dtype reads a split pack (head_w_split)
         self.head_w = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, ops.torch_dtype(code))
         self.head_w_lo = None   # the split-precision head's residual weights (2-byte dtypes)
-        if code in (ops.BF16, ops.F16):
+        self.head_w_split = None
+        if code in (ops.BF16, ops.F16, ops.F16X3):
             w32 = pack_conv_weight(fl.weight, fl.weight.shape[1], bk, torch.float32)
             self.head_w_lo = (w32 - self.head_w.float()).to(ops.torch_dtype(code)).contiguous()
+        if code == ops.F16X3:
+            self.head_w_split = to_split(pack_conv_weight(fl.weight, fl.weight.shape[1], 32, torch.float32))
         self.head_b = (fl.bias.detach().float().contiguous() if fl.bias is not None
                        else torch.zeros(fl.weight.shape[0], device=fl.weight.device))
         self.njoints = fl.weight.shape[0]
@@ -433,13 +473,15 @@ class PoseResNetPlan:
         if fused and self.stem_fused_w is not None and h % 8 == 0 and w in (256, 384) and views[0].shape[1] == 3:
             return RawViews(self, list(views), hflip)
         s2d = h % 2 == 0 and w % 2 == 0
-        shape = (n * len(views), h // 2, w // 2, STEM_S2D_PAD) if s2d else (n * len(views), h, w, STEM_CIN_PAD)
+        cm = ops.cmul(self.code)
+        shape = ((n * len(views), h // 2, w // 2, self.s2d_pad * cm) if s2d else
+                 (n * len(views), h, w, self.cin_pad * cm))
         x = torch.empty(shape, dtype=ops.torch_dtype(self.code), device=views[0].device)
         for i, v in enumerate(views):
             if s2d:
-                ops.pack_s2d_nchw(v, self.code, STEM_S2D_PAD, out=x[i * n:(i + 1) * n], hflip=hflip)
+                ops.pack_s2d_nchw(v, self.code, self.s2d_pad, out=x[i * n:(i + 1) * n], hflip=hflip)
             else:
-                ops.pack_nchw_to_nhwc(v, self.code, STEM_CIN_PAD, out=x[i * n:(i + 1) * n], hflip=hflip)
+                ops.pack_nchw_to_nhwc(v, self.code, self.cin_pad, out=x[i * n:(i + 1) * n], hflip=hflip)
         return x
 
     def stem_pool(self, x):
@@ -463,9 +505,9 @@ class PoseResNetPlan:
         code = self.code
         if isinstance(x, RawViews):
             x = x.packed()
-        if x.shape[3] == STEM_S2D_PAD:
+        if x.shape[3] == self.s2d_pad * ops.cmul(code):
             st = self.stem
-            out = torch.empty(tuple(x.shape[:3]) + (st.cout,), dtype=x.dtype, device=x.device)
+            out = torch.empty(tuple(x.shape[:3]) + (st.cout * ops.cmul(code),), dtype=x.dtype, device=x.device)
             key = ('stem_s2d', code, tuple(x.shape), st.cout)
             return _tuned(key, st.cout, lambda t: ops.conv2d_nhwc(
                 x, self.stem_s2d_w, st.cout, 4, 4, 1, 2, st.scale, st.shift, None, True, code,
@@ -500,7 +542,8 @@ class PoseResNetPlan:
                                         code, keep_f=keep_f, hm_out=hm_out, f_out=f_out,
                                         head_w_lo=self.head_w_lo if PRECISE_HEAD else None)
         f = dc(x, code, out=f_out)
-        return ops.head1x1_nchw(f, self.head_w, self.njoints, self.head_b, code, out=hm_out), f
+        hw = self.head_w_split if code == ops.F16X3 else self.head_w
+        return ops.head1x1_nchw(f, hw, self.njoints, self.head_b, code, out=hm_out), f
 
     def _stage_late(self, x, hm_out=None, f_out=None, keep_f=True):
         """deconv2 .. last deconv -> head."""
@@ -586,14 +629,15 @@ class PoseResNetPlan:
         c = n // chunks
         dt = ops.torch_dtype(code)
         dev = x.device
-        if x.shape[3] == STEM_S2D_PAD:
+        if x.shape[3] == self.s2d_pad * ops.cmul(code):
             hs, ws = x.shape[1], x.shape[2]
         else:
             hs, ws = (x.shape[1] - 1) // 2 + 1, (x.shape[2] - 1) // 2 + 1
         hp, wp = (hs - 1) // 2 + 1, (ws - 1) // 2 + 1          # after maxpool = layer1 grid
         h2, w2 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1          # layer2 grid
-        x2 = torch.empty((n, h2, w2, self._block_cout(self.layers[1][-1])), dtype=dt, device=dev)
-        x1 = (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1])), dtype=dt, device=dev)
+        cm = ops.cmul(code)
+        x2 = torch.empty((n, h2, w2, self._block_cout(self.layers[1][-1]) * cm), dtype=dt, device=dev)
+        x1 = (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1]) * cm), dtype=dt, device=dev)
               if keep_features else None)
         for k in range(chunks):
             sl = slice(k * c, (k + 1) * c)
@@ -604,7 +648,7 @@ class PoseResNetPlan:
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)
-        f = (torch.empty((n, hf, wf, self.deconvs[-1].cout), dtype=dt, device=dev) if keep_features else None)
+        f = (torch.empty((n, hf, wf, self.deconvs[-1].cout * cm), dtype=dt, device=dev) if keep_features else None)
         for k in range(chunks):
             sl = slice(k * c, (k + 1) * c)
             self._stage_late(y[sl], hm_out=hm[sl], f_out=None if f is None else f[sl], keep_f=f is not None)

@@ -1,6 +1,7 @@
 """CPU-side checks: the C-ABI library loads and exports every declared symbol, and the
 host logic (weight packing / sub-pixel deconv decomposition, crop affines, camera
 tables, synthetic data determinism) is right.  No kernel is launched here."""
+import ctypes
 import os
 import re
 
@@ -27,8 +28,9 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _native.exported_symbols()
-    assert lib.posu_abi_version() == _native.ABI_VERSION == 12
+    assert lib.posu_abi_version() == _native.ABI_VERSION == 13
     assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
+    assert lib.posu_conv_bk(_native.F16X3) == 64   # halves: 32 logical k per K-tile
 
 
 def test_argument_errors_are_reported_without_a_gpu():
@@ -39,6 +41,26 @@ def test_argument_errors_are_reported_without_a_gpu():
     assert st == 1 and 'null pointer' in _native.last_error()
     st = lib.posu_triangulate_dlt(None, None, None, _native.F32, 128, 32, None, 1, 4, 16, 1, None, None)
     assert st == 1
+    # the split dtype needs logical channel counts in 32-channel granules, and is inference-only
+    p = ctypes.c_void_p(16)
+    st = lib.posu_conv2d_fwd(_native.F16X3, p, 1, 8, 8, 16, p, 64, 3, 3, 1, 1, None, None, None, 1, p, 8, 8, -1, None)
+    assert st == 1 and 'multiples of 32' in _native.last_error()
+    st = lib.posu_conv2d_dgrad(_native.F16X3, p, 1, 8, 8, 64, p, 64, 3, 3, 1, 1, None, p, 8, 8, None)
+    assert st == 1 and 'inference-only' in _native.last_error()
+
+
+def test_split_pack_layout():
+    """packing.to_split: per 32-k block [hi 32 | lo 32], hi = fp16(v 2^e), lo = fp16(v 2^e - hi)."""
+    torch.manual_seed(3)
+    w = torch.randn(64, 96, dtype=torch.float32) * 0.03
+    e = packing.split_exponent(w)
+    assert 2.0 ** (packing.SPLIT_WEIGHT_EXP - 1) < float(w.abs().max()) * 2.0 ** e <= 2.0 ** packing.SPLIT_WEIGHT_EXP
+    s = packing.to_split(w, e)
+    assert s.shape == (64, 192) and s.dtype == torch.float16
+    blk = s.view(64, 3, 2, 32).double()
+    v = (blk[:, :, 0] + blk[:, :, 1]).reshape(64, 96) * 2.0 ** -e
+    assert float((v - w.double()).abs().max()) <= float(w.abs().max()) * 2.0 ** -21
+    assert torch.equal(blk[:, :, 0].reshape(64, 96).half(), (w.double() * 2.0 ** e).half())
 
 
 def _im2col_nhwc(x, kh, kw, stride, pad):

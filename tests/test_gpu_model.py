@@ -22,10 +22,12 @@ def _model(num_layers, size, seed, precision, device):
     return net.to(device).eval()
 
 
+@pytest.mark.parametrize('precision', ['fp32', 'fp16x3'])
 @pytest.mark.parametrize('num_layers,size', [(18, 128), (50, 256), (152, 384)])
-def test_pose_resnet_fp32_matches_reference_heatmaps(cuda, golden, num_layers, size):
+def test_pose_resnet_fp32_matches_reference_heatmaps(cuda, golden, num_layers, size, precision):
+    """fp32 and the split-fp16 mode (fp16x3) both at the 1e-3 parity gate."""
     g = golden('pose_resnet_r%d_%d.npz' % (num_layers, size))
-    net = _model(num_layers, size, int(g['seed']), 'fp32', cuda)
+    net = _model(num_layers, size, int(g['seed']), precision, cuda)
     x = torch.cat(syn.synthetic_views(1, int(g['batch']), size, seed=int(g['input_seed'])), 0)
     with torch.no_grad():
         hm, x1, f = net(x.to(cuda))

@@ -9,8 +9,8 @@ Then bench's chain (eval plan -> soft-argmax + crop affine -> fp64 DLT) in bf16 
 compared with the CPU oracle chain (fp32 reference forward -> soft-argmax -> transform_back ->
 triangulate_poses, run/test/test_triangulate.py:98-101 arithmetic) on the same weights.
 
-Gates: fp32 -- BASELINE.json's bars: heatmaps 1e-3, triangulated joints 1e-2 mm (mean AND
-max).  bf16 and fp16 (the plan's default split-precision head, plan.PRECISE_HEAD) -- 2 x the
+Gates: fp32 and fp16x3 (the split-fp16 mode, round 5) -- BASELINE.json's bars: heatmaps 1e-3,
+triangulated joints 1e-2 mm (mean AND max).  bf16 and fp16 (the plan's default split-precision head, plan.PRECISE_HEAD) -- 2 x the
 deviation measured at round 4 (profiles/r04/precision_attribution_r4e.json, deterministic: the
 same fitted net and the same chains give the same figures run to run):
     bf16  heatmaps 0.0163 max / 3.2e-4 mean, joints 0.131 px mean, 0.656 mm mean / 3.03 mm max
@@ -34,10 +34,12 @@ def fitted(cuda):
     res32, ref = peaked.parity(net, task, cuda, 'fp32')
     res16, _ = peaked.parity(net, task, cuda, 'bf16', ref)
     resh, _ = peaked.parity(net, task, cuda, 'fp16', ref)
+    ress, _ = peaked.parity(net, task, cuda, 'fp16x3', ref)
     print('fp32:', res32)
     print('bf16:', res16)
     print('fp16:', resh)
-    return res32, res16, resh
+    print('fp16x3:', ress)
+    return res32, res16, resh, ress
 
 
 def test_fitted_network_is_trained_like(fitted):
@@ -46,8 +48,9 @@ def test_fitted_network_is_trained_like(fitted):
     assert res32['oracle_mpjpe_vs_gt_mm'] < 25.0
 
 
-def test_fp32_chain_meets_the_baseline_bars_on_peaked_heatmaps(fitted):
-    r = fitted[0]
+@pytest.mark.parametrize('which', [0, 3], ids=['fp32', 'fp16x3'])
+def test_chain_meets_the_baseline_bars_on_peaked_heatmaps(fitted, which):
+    r = fitted[which]
     assert r['heatmap_abs_err']['max'] < 1e-3
     assert r['mpjpe_vs_ref_mm']['mean'] < 1e-2 and r['mpjpe_vs_ref_mm']['max'] < 1e-2
 

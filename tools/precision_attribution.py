@@ -82,6 +82,77 @@ def forward(x, sd, rounded, dt):
     return F.conv2d(_q(x, dt, on_a), _q(sd['final_layer.weight'], dt, on_w), sd.get('final_layer.bias'))
 
 
+def _split(t, dt, scale=0):
+    """hi + lo pair of t in dtype dt (lo = the rounding residual rounded again), both as f32;
+    scale: a power-of-two exponent applied before the split (the weight scaling of the split pack)."""
+    t = t * (2.0 ** scale)
+    hi = t.to(dt).float()
+    lo = (t - hi).to(dt).float()
+    return hi, lo
+
+
+def forward_split(x, sd, dt, wscale=None):
+    """fp32 forward of R50 PoseResNet at the split-precision plan's rounding points: every activation
+    stored as a (hi, lo) pair of dt, every weight likewise (wscale: per-tensor power-of-two
+    exponent so that max |w| sits at 2^wscale before the split, undone in the f32 epilogue), every
+    conv summing hi.hi + lo.hi + hi.lo in f32 (the lo.lo term dropped)."""
+    def store(t):
+        h, l = _split(t, dt)
+        return h + l
+
+    def conv(x, w, stride=1, pad=0, transpose=False):
+        e = 0
+        if wscale is not None:
+            e = wscale - int(torch.ceil(torch.log2(w.abs().max())).item())
+        xh, xl = _split(x, dt)
+        wh, wl = _split(w, dt, e)
+        f = (lambda a, b: F.conv_transpose2d(a, b, stride=stride, padding=pad)) if transpose else \
+            (lambda a, b: F.conv2d(a, b, stride=stride, padding=pad))
+        return (f(xh, wh) + f(xl, wh) + f(xh, wl)) * (2.0 ** -e)
+
+    def conv_bn(x, wkey, bnkey, relu=True, stride=1, pad=0, res=None):
+        s, b = _fold(sd, bnkey)
+        y = conv(x, sd[wkey], stride=stride, pad=pad)
+        y = y * s[None, :, None, None] + b[None, :, None, None]
+        if res is not None:
+            y = y + res
+        return store(F.relu(y) if relu else y)
+
+    x = conv_bn(store(x), 'conv1.weight', 'bn1', stride=2, pad=3)
+    x = F.max_pool2d(x, 3, stride=2, padding=1)
+    for li, nb in enumerate(BLOCKS):
+        for bi in range(nb):
+            p = 'layer%d.%d' % (li + 1, bi)
+            stride = 2 if (li > 0 and bi == 0) else 1
+            t = conv_bn(x, p + '.conv1.weight', p + '.bn1')
+            t = conv_bn(t, p + '.conv2.weight', p + '.bn2', stride=stride, pad=1)
+            if bi == 0:
+                s3, b3 = _fold(sd, p + '.bn3')
+                sdn, bd = _fold(sd, p + '.downsample.1')
+                w3 = (sd[p + '.conv3.weight'].double() * s3.double()[:, None, None, None]).float()
+                wd = (sd[p + '.downsample.0.weight'].double() * sdn.double()[:, None, None, None]).float()
+                # one GEMM over [t | x(stride)]: one weight exponent for both halves
+                if wscale is not None:
+                    e = wscale - int(torch.ceil(torch.log2(torch.maximum(w3.abs().max(), wd.abs().max()))).item())
+                else:
+                    e = 0
+                th, tl = _split(t, dt)
+                xs = x[:, :, ::stride, ::stride]
+                xh, xl = _split(xs, dt)
+                w3h, w3l = _split(w3, dt, e)
+                wdh, wdl = _split(wd, dt, e)
+                y = (F.conv2d(th, w3h) + F.conv2d(tl, w3h) + F.conv2d(th, w3l) +
+                     F.conv2d(xh, wdh) + F.conv2d(xl, wdh) + F.conv2d(xh, wdl)) * (2.0 ** -e)
+                x = store(F.relu(y + (b3.double() + bd.double()).float()[None, :, None, None]))
+            else:
+                x = conv_bn(t, p + '.conv3.weight', p + '.bn3', res=x)
+    for i in (0, 3, 6):
+        s, b = _fold(sd, 'deconv_layers.%d' % (i + 1))
+        y = conv(x, sd['deconv_layers.%d.weight' % i], stride=2, pad=1, transpose=True)
+        x = store(F.relu(y * s[None, :, None, None] + b[None, :, None, None]))
+    return conv(x, sd['final_layer.weight']) + sd['final_layer.bias'][None, :, None, None]
+
+
 def chain_metrics(hm, ref, task):
     from oracle import geometry_ref as G
     from posu.metrics import mpjpe_stats
@@ -103,6 +174,7 @@ def main():
     import peaked
     dev = torch.device('cuda', 0)
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 1200
+    only_split = len(sys.argv) > 2 and sys.argv[2] == 'split'
     torch.set_num_threads(16)
     t0 = time.time()
     net, task = peaked.fit_peaked(dev, steps=steps)
@@ -110,7 +182,7 @@ def main():
     out = {'fit_steps': steps, 'fit_s': round(time.time() - t0, 1), 'hip_chains': {}}
     ref = None
     from posu import plan as pl
-    for prec in ('fp32', 'bf16', 'fp16'):
+    for prec in (('fp32',) if only_split else ('fp32', 'bf16', 'fp16')):
         out['hip_chains'][prec], ref = peaked.parity(net, task, dev, prec, ref)
         if prec != 'fp32':   # the plain head (round 3's chain) beside the split-precision one
             pl.PRECISE_HEAD = False
@@ -122,6 +194,15 @@ def main():
     torch.backends.cuda.matmul.allow_tf32 = False
     with torch.no_grad():
         out['emulated'] = {'none': chain_metrics(forward(x, sd, (), torch.float32), ref, task)}
+        # split-precision schemes (hi + lo operands, three MFMAs per product) for a parity-bearing
+        # 2-byte mode: fp16 / bf16 pairs, with and without the weights' power-of-two scaling
+        out['emulated']['split'] = {
+            'fp16x3': chain_metrics(forward_split(x, sd, torch.float16), ref, task),
+            'fp16x3_wscale14': chain_metrics(forward_split(x, sd, torch.float16, wscale=14), ref, task),
+            'bf16x3': chain_metrics(forward_split(x, sd, torch.bfloat16), ref, task)}
+        if only_split:
+            print(json.dumps(out, indent=1))
+            return
         for dname, dt in (('bf16', torch.bfloat16), ('fp16', torch.float16)):
             res = {'all': chain_metrics(forward(x, sd, STAGES, dt), ref, task),
                    # the plan's split-precision head (PRECISE_HEAD): every stage rounded but the head
