@@ -29,7 +29,11 @@ Also reported, on the same JSON line (rank 0):
                     computes MPJPE (mean / std / max per-joint error, mm);
   triangulation_same_2d_mm_all_ranks -- every rank's device triangulation against the oracle's
                     triangulation of the same device joints, reduced over ranks (posu.dist);
-  fp32_mode      -- frames/s of the same pipeline with the exact-f32 kernels (parity mode);
+  fp32_mode      -- frames/s of the same pipeline with the exact-f32 kernels;
+  parity_mode    -- frames/s of the same pipeline in split fp16 (precision fp16x3: every value a
+                    (hi, lo) fp16 pair, hi.hi + lo.hi + hi.lo on the fp16 MFMAs) -- the
+                    parity-bearing fast mode: within the BASELINE bars on peaked heatmaps
+                    (peaked_parity.fp16x3);
   configs1       -- BASELINE configs[1]: the R50 heatmap forward alone at batch 64, bf16;
   train_mode     -- BASELINE configs[3]: the training step (fwd + bwd + Adam, DDP over RCCL
                     when N > 1), time-bounded (--train-steps);
@@ -73,7 +77,7 @@ def parse():
     ap.add_argument('--batches', type=int, default=3, help='distinct input batches rotated over the timed steps')
     ap.add_argument('--layers', type=int, default=50)
     ap.add_argument('--size', type=int, default=256)
-    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32'])
+    ap.add_argument('--precision', default='bf16', choices=['bf16', 'fp16', 'fp32', 'fp16x3'])
     ap.add_argument('--no-graph', action='store_true')
     ap.add_argument('--serial-geo', action='store_true',
                     help='run each batch\'s decode + geometry after its network on one stream (default: on a '
@@ -89,7 +93,9 @@ def parse():
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-mpjpe', action='store_true', help='skip the oracle-chain MPJPE check')
-    ap.add_argument('--fp32-steps', type=int, default=5, help='timed steps of the fp32 parity mode (0: skip)')
+    ap.add_argument('--fp32-steps', type=int, default=5, help='timed steps of the exact-f32 mode (0: skip)')
+    ap.add_argument('--parity-steps', type=int, default=10,
+                    help='timed steps of the split-fp16 parity mode (fp16x3), reported as parity_mode (0: skip)')
     ap.add_argument('--train-steps', type=int, default=10,
                     help='infer mode: timed steps of the configs[3] training step reported as train_mode (0: skip)')
     ap.add_argument('--peaked-steps', type=int, default=1200,
@@ -587,7 +593,7 @@ def peaked_parity(args, dev):
     out = {}
     ref = None
     # fp32 (the parity mode) first, then both 2-byte modes (same MFMA rate), the benched one included
-    for prec in dict.fromkeys(('fp32', args.precision, 'bf16', 'fp16')):
+    for prec in dict.fromkeys(('fp32', args.precision, 'fp16x3', 'bf16', 'fp16')):
         out[prec], ref = peaked.parity(net, task, dev, prec, ref)
     out['fit'] = {'steps': args.peaked_steps, 'seconds': round(fit_s, 2), 'groups': task['groups'],
                   'heatmap_peak_mean': out['fp32']['heatmap_peak_mean'],
@@ -644,6 +650,9 @@ def time_control(args, dev, rank, world, dist):
     box: its network_ms beside the line's."""
     from posu import plan as pl
     saved = {f: getattr(pl, f) for f in CONTROL_FLAGS}
+    # the control plan re-tunes geometries it shares with the headline plan: keep the headline's
+    # tile table (and its tuning records) as they were, for later captures and the tile dump
+    tables = [(t, dict(t)) for t in (pl._TUNE_CACHE, pl._TUNE_TIMES, pl._REFINE_TIMES)]
     try:
         for f in CONTROL_FLAGS:
             setattr(pl, f, False)
@@ -652,6 +661,9 @@ def time_control(args, dev, rank, world, dist):
     finally:
         for f, v in saved.items():
             setattr(pl, f, v)
+        for t, snap in tables:
+            t.clear()
+            t.update(snap)
     return {'flags_off': list(CONTROL_FLAGS), 'network_ms': round(r['net_ms'], 4), 'steps': args.control_steps,
             'ms_per_step': round(r['elapsed'] / args.control_steps * 1e3, 4)}
 
@@ -691,7 +703,7 @@ def infer_main(args):
     value = pdist.throughput(frames, args.steps, world, elapsed)
     per_rank = gather_per_rank([frames * args.steps, res['elapsed']], dist, device=dev)
     gf = GFLOP_PER_FRAME.get((args.layers, args.size))
-    peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS  # fp16 dense peak == bf16
+    peak = PEAK_F32_TFLOPS if args.precision == 'fp32' else PEAK_BF16_TFLOPS  # fp16 (x3) dense peak == bf16
     roof = None
     if gf is not None:
         achieved = gf * frames / (res['net_ms'] * 1e-3) / 1e3  # TFLOP/s
@@ -737,6 +749,21 @@ def infer_main(args):
                 'network_ms': round(r32['net_ms'], 3), 'steps': args.fp32_steps,
                 'roofline_frac_f32': (round(gf * frames / (r32['net_ms'] * 1e-3) / 1e3 / PEAK_F32_TFLOPS, 4)
                                       if gf else None)}
+    par = None
+    if args.parity_steps > 0 and args.precision != 'fp16x3':
+        rp = time_pipeline(args, 'fp16x3', dev, rank, args.parity_steps, 3, args.batches, not args.no_autotune, dist,
+                           world)
+        elp = pdist.max_over_ranks(rp['elapsed'], device=dev)
+        par = {'precision': 'fp16x3', 'value': round(pdist.throughput(frames, args.parity_steps, world, elp), 2),
+               'unit': 'frames/s', 'network_ms': round(rp['net_ms'], 4), 'steps': args.parity_steps,
+               'ms_per_step': round(elp / args.parity_steps * 1e3, 4)}
+        if gf:
+            tfp = gf * frames / (rp['net_ms'] * 1e-3) / 1e3
+            # frac: the network's real flops against the dense fp16 peak; mfma_frac: the MFMA work
+            # issued (three fp16 products per multiply-add) against it
+            par['roofline'] = {'bound': 'mfma', 'achieved': round(tfp, 2), 'peak': PEAK_BF16_TFLOPS,
+                               'unit': 'TFLOP/s', 'frac': round(tfp / PEAK_BF16_TFLOPS, 4),
+                               'mfma_frac': round(3 * tfp / PEAK_BF16_TFLOPS, 4)}
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
     control = time_control(args, dev, rank, world, dist) if args.control_steps > 0 else None
     c4 = time_configs4(args, dev, rank, world, dist) if args.c4_steps > 0 else None
@@ -760,6 +787,8 @@ def infer_main(args):
                                 % args.precision)
             if fp32 is not None:
                 fp32['random_weight_chain_vs_ref'] = compare_with_reference(r32, ref, r32['meta'], dev)
+            if par is not None:
+                par['random_weight_chain_vs_ref'] = compare_with_reference(rp, ref, rp['meta'], dev)
     peaked = None
     if world == 1 and not args.no_mpjpe and args.peaked_steps > 0 and (args.layers, args.size) == (50, 256):
         peaked = peaked_parity(args, dev)
@@ -768,6 +797,10 @@ def infer_main(args):
                          'on a fitted R50@256 whose heatmaps peak (mean %.2f) where 8 synthetic 4-view poses project '
                          '(tools/peaked.py); per-joint 3-D error in mm, test_triangulate.py:98-101 arithmetic; '
                          'details in peaked_parity' % (args.precision, peaked['fit']['heatmap_peak_mean']))
+        if par is not None:
+            par['peaked_parity'] = {k: peaked['fp16x3'][k] for k in ('heatmap_abs_err', 'mpjpe_vs_ref_mm')}
+            par['within_baseline_bars'] = bool(peaked['fp16x3']['heatmap_abs_err']['max'] < 1e-3 and
+                                               peaked['fp16x3']['mpjpe_vs_ref_mm']['max'] < 1e-2)
     line = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
@@ -788,7 +821,7 @@ def infer_main(args):
         'per_rank_seconds': [round(p[1], 5) for p in per_rank],
         'mpjpe_vs_ref_mm': mpjpe, 'peaked_parity': peaked,
         'random_weight_chain_vs_ref': random_w if world == 1 and not args.no_mpjpe else None,
-        'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32,
+        'triangulation_same_2d_mm_all_ranks': tri_all, 'fp32_mode': fp32, 'parity_mode': par,
         'configs1': c1, 'configs4': c4, 'control': control, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }
@@ -798,13 +831,15 @@ def infer_main(args):
 
 
 # ------------------------------------------------------------------ training
-def run_training(args, dev, rank, world, dist, steps, warmup):
-    """configs[3]: one training step = 4-view batch (groups x 4 frames per GPU) through the
-    reference's step (core/function.py:154-366): train-mode forward with per-view BN,
-    JointsMSELoss per view + FundamentalLoss on soft-argmax coords, backward, Adam.
-    world > 1: DistributedDataParallel over RCCL (gradient all-reduce overlapped with the staged
-    backward), weak scaling.  Returns the training line (a dict)."""
-    from posu import dist as pdist
+TRAIN_FUND_WEIGHT = 1e-3   # the benched step's weight of the epipolar (FundamentalLoss) term
+
+
+def train_batch(args, dev, rank=0, world=1, dist=None):
+    """The configs[3] training batch of this rank and its loss (tests/test_gpu_train_full.py checks
+    exactly this step): the bench's calibrated R50 (train mode, per-view BN) wrapped in
+    MultiViewPose (DDP when dist is given), the rank's 4-view shard of synthetic crops, Gaussian
+    targets at seeded positions, loss() = sum over views of JointsMSELoss + TRAIN_FUND_WEIGHT x the
+    epipolar loss of the soft-argmax joints (core/function.py:154-366).  Returns a dict."""
     from posu import synthetic as syn
     from core.loss import JointsMSELoss, FundamentalLoss
     from models.multiview_pose_resnet import get_multiview_pose_net
@@ -818,7 +853,7 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], output_device=local,
                                                           bucket_cap_mb=64)
     nb, nv, hs = args.groups, 4, args.size // 4
-    shard, meta, _ = rank_meta(args, rank, world, dev)
+    shard, meta, host = rank_meta(args, rank, world, dev)
     views = input_views(shard, args.size, 0, dev)
     g = torch.Generator().manual_seed(7 + rank)
     ys, xs = torch.meshgrid(torch.arange(hs, dtype=torch.float32), torch.arange(hs, dtype=torch.float32),
@@ -829,19 +864,37 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     weight = torch.ones(nb, 16, 1, device=dev)
     mse = JointsMSELoss(use_target_weight=True)
     fund = FundamentalLoss(cfg, fundamental_matrix_dict=syn.fundamental_dict(), device=dev)
-    # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
-    # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
-    # launches (same math): 26.3 -> 22.8 ms per step measured A/B
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
-    subj = meta.subj
+    out = {'net': net, 'model': model, 'views': views, 'target': target, 'weight': weight, 'meta': meta,
+           'host': host, 'F': fund.F}
 
-    def step():
+    def loss_fn():
         raw, _, _, _ = model(views)
         loss = 0
         for v in range(nv):
             loss = loss + mse(raw[v], target[v], weight)
         coords = integral_preds_image_th(torch.cat(raw, 0), meta.affines).view(nv, nb, 16, 2)
-        loss = loss + 1e-3 * ops.epipolar_loss(coords, None, fund.F, subj)
+        epi = ops.epipolar_loss(coords, None, fund.F, meta.subj)
+        out['last'] = (raw, loss, epi)
+        return loss + TRAIN_FUND_WEIGHT * epi
+    out['loss'] = loss_fn
+    return out
+
+
+def run_training(args, dev, rank, world, dist, steps, warmup):
+    """configs[3]: one training step = 4-view batch (groups x 4 frames per GPU) through the
+    reference's step (core/function.py:154-366): train-mode forward with per-view BN,
+    JointsMSELoss per view + FundamentalLoss on soft-argmax coords, backward, Adam.
+    world > 1: DistributedDataParallel over RCCL (gradient all-reduce overlapped with the staged
+    backward), weak scaling.  Returns the training line (a dict)."""
+    tb = train_batch(args, dev, rank, world, dist)
+    net, nv, nb = tb['net'], 4, args.groups
+    # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
+    # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
+    # launches (same math): 26.3 -> 22.8 ms per step measured A/B
+    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
+
+    def step():
+        loss = tb['loss']()
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()

@@ -327,7 +327,7 @@ int s2_tail_impl(const char* name, int dtype, const void* t1, const void* x, int
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
   const long long need = static_cast<long long>(K::kNW) * (next ? S2Cfg<true>::kSteps : K::kSteps) * 2 * 1024;
-  POSU_REQUIRE(wstream_bytes >= need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
+  POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                           (next ? "chained" : "plain") + " kernel reads " + std::to_string(need));
   for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(shift),
                         next ? t1n : t1, static_cast<const void*>(next ? s1n : shift),

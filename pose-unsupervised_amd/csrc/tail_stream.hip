@@ -401,7 +401,7 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream)
     const long long kt = P / 32, nc = C / P;
     const long long need = (P / 32) * (9 * kt + (next ? 2 : 1) * nc * kt) * 2 * 64 * 8 * 2;
-    POSU_REQUIRE(wstream_bytes >= need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
+    POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
   const int rows = l3 ? 8 : kL2Rows;

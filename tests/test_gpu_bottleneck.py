@@ -333,6 +333,23 @@ def test_fused_bottleneck_refuses_unsupported_shapes(cuda):
                                   torch.zeros(1024, 256, device=cuda, dtype=torch.bfloat16))
     with pytest.raises(RuntimeError, match='multiple of 8'):
         ops.bottleneck_tail_stream_nhwc(t3[:, :4], x3[:, :4], p3, s3, s3, s3, s3, BF16)
+    # a stream that is too LONG is refused too (the kernel would read it with the wrong per-group
+    # stride): the chained pack handed to the plain entry point, a layer3 pack to a layer2 launch
+    p2n = packing.pack_tail_stream(torch.zeros(128, 1152, device=cuda, dtype=torch.bfloat16),
+                                   torch.zeros(512, 128, device=cuda, dtype=torch.bfloat16),
+                                   torch.zeros(128, 512, device=cuda, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError, match='wstream holds'):
+        ops.bottleneck_tail_stream_nhwc(t2[:, :4], x2[:, :4], p2n, s2, s2, s2, s2, BF16)
+    with pytest.raises(RuntimeError, match='wstream holds'):
+        ops.bottleneck_tail_stream_nhwc(t2[:, :4], x2[:, :4], p3, s2, s2, s2, s2, BF16)
+    xs = torch.zeros(1, 8, 64, 256, device=cuda, dtype=torch.bfloat16)
+    ts = torch.zeros(1, 8, 64, 128, device=cuda, dtype=torch.bfloat16)
+    sh = torch.ones(512, device=cuda)
+    ps2n = packing.pack_s2_tail_stream(torch.zeros(128, 1152, device=cuda, dtype=torch.bfloat16),
+                                       torch.zeros(512, 384, device=cuda, dtype=torch.bfloat16),
+                                       torch.zeros(128, 512, device=cuda, dtype=torch.bfloat16))
+    with pytest.raises(RuntimeError, match='wstream holds'):
+        ops.bottleneck_s2_tail_nhwc(ts, xs, ps2n, sh, sh, sh, BF16)
 
 
 @pytest.mark.parametrize('precision', ['bf16', 'fp16'])

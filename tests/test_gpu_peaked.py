@@ -18,6 +18,7 @@ same fitted net and the same chains give the same figures run to run):
 import os
 import sys
 
+import numpy as np
 import pytest
 import torch
 
@@ -39,7 +40,7 @@ def fitted(cuda):
     print('bf16:', res16)
     print('fp16:', resh)
     print('fp16x3:', ress)
-    return res32, res16, resh, ress
+    return res32, res16, resh, ress, net, task
 
 
 def test_fitted_network_is_trained_like(fitted):
@@ -69,3 +70,43 @@ def test_fp16_chain_on_peaked_heatmaps(fitted):
     assert r['heatmap_abs_err']['max'] < 4.2e-3 and r['heatmap_abs_err']['mean'] < 7.8e-5
     assert r['joints_px_err']['mean'] < 0.03
     assert r['mpjpe_vs_ref_mm']['mean'] < 0.14 and r['mpjpe_vs_ref_mm']['max'] < 0.42
+
+
+@pytest.mark.parametrize('fund_weight', [10.0, 0.0], ids=['mse+fund', 'mse-only'])
+def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
+    """The bf16 training step (JointsMSE + fund_weight x FundamentalLoss, per-view batch BN) on the
+    FITTED network, whose heatmaps peak, against the oracle's autograd of the same step: with
+    peaked heatmaps the soft-argmax joints no longer follow the heatmaps' rounding noise, so this
+    separates the bf16 backward's own deviation from the FundamentalLoss's amplification of flat
+    heatmaps (test_gpu_train.py's random-init network)."""
+    import copy
+    from test_gpu_train import _step
+    from test_oracle_golden import train_step_oracle
+    net0, task = fitted[4], fitted[5]
+    net = copy.deepcopy(net0)
+    groups = task['groups']
+    host = task['host']
+    g = {'num_layers': 50, 'image_size': 256, 'nviews': 4, 'batch': groups, 'seed': 0, 'fund_weight': fund_weight,
+         'targets': task['target'].cpu().numpy(), 'target_weight': np.ones((4, groups, 16, 1), np.float32),
+         'centers': host['centers'], 'scales': host['scales'], 'subjects': np.asarray(host['subjects'])}
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    net, hm, joints, mse, fund = _step(cuda, g, 'bf16', net=net, views=task['views'])
+    params, _, hm_r, _, mse_r, fund_r = train_step_oracle(g, sd=sd, views=[v.cpu() for v in task['views']])
+    named = dict(net.named_parameters())
+    names = list(named)
+    rel = np.abs(np.array([named[n].grad.norm().item() / params[n].grad.norm().item() - 1 for n in names]))
+    ga = torch.cat([named[n].grad.detach().double().cpu().ravel() for n in names])
+    gr = torch.cat([params[n].grad.detach().double().ravel() for n in names])
+    cos = float(ga @ gr / (ga.norm() * gr.norm()))
+    hm_err = float((torch.stack(hm).detach().cpu() - hm_r.detach()).abs().max())
+    print('peaked bf16 train step (fund_weight %g) vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs %.6g, '
+          'grad-norm rel median %.3g max %.3g (%s), cosine %.6f'
+          % (fund_weight, hm_err, mse.item(), mse_r.item(), float(fund), float(fund_r), np.median(rel), rel.max(),
+             names[int(rel.argmax())], cos))
+    b = PEAKED_TRAIN_BF16
+    assert hm_err < b['hm']
+    assert abs(mse.item() / mse_r.item() - 1) < b['loss']
+    assert np.median(rel) < b['norm_median'] and cos > b['cos']
+
+
+PEAKED_TRAIN_BF16 = {'hm': 0.1, 'loss': 2e-2, 'norm_median': 0.6, 'cos': 0.5}

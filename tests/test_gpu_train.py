@@ -12,18 +12,25 @@ from posu import synthetic as syn
 pytestmark = pytest.mark.gpu
 
 
-def _step(cuda, g, precision):
+def _step(cuda, g, precision, net=None, views=None):
+    """One reference-style training step (no optimizer) of the seeded golden network, or of `net`
+    (a PoseResNet on the device, set to train mode here) on `views` (device tensors)."""
     from core.loss import FundamentalLoss, JointsMSELoss
     from models.multiview_pose_resnet import get_multiview_pose_net
     from models.pose_resnet import get_pose_net
     from utils.transforms import generate_integral_preds_2d_th, transform_back_th
     nl, size, nv, b, seed = (int(g[k]) for k in ('num_layers', 'image_size', 'nviews', 'batch', 'seed'))
     cfg = syn.make_cfg(num_layers=nl, image_size=size)
-    net = get_pose_net(cfg, is_train=False, precision=precision)
-    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=seed))
-    net = net.to(cuda).train()
+    if net is None:
+        net = get_pose_net(cfg, is_train=False, precision=precision)
+        net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=seed))
+        net = net.to(cuda)
+    net.precision = precision
+    net = net.train()
+    net.zero_grad(set_to_none=True)
     model = get_multiview_pose_net(net, cfg)
-    views = [v.to(cuda) for v in syn.synthetic_views(nv, b, size, seed=seed + 1)]
+    if views is None:
+        views = [v.to(cuda) for v in syn.synthetic_views(nv, b, size, seed=seed + 1)]
     meta = [{'center': torch.from_numpy(g['centers'][v]), 'scale': torch.from_numpy(g['scales'][v]),
              'subject': torch.from_numpy(g['subjects'])} for v in range(nv)]
     target = [torch.from_numpy(g['targets'][v]).to(cuda) for v in range(nv)]
@@ -198,12 +205,14 @@ def _inputs_r50_256(groups=2, seed=3):
 # the FundamentalLoss (weight 10) reads joints from their soft-argmax at beta = 100, which weights
 # a 0.02 heatmap difference by e^2 (section 5 of DESIGN.md): the bf16 gradients of that term
 # follow the rounding noise, so the fp32 step is the parity-bearing gate of this shape.
-TRAIN_256_BANDS = {'fp32': {'hm': 1e-3, 'loss': 1e-4, 'norm_rel_max': 2e-3},
-                   'bf16': {'hm': 0.4, 'loss': 2e-2, 'norm_rel_median': 0.6}}
+TRAIN_256_BANDS = {'fp32': {'hm': 1e-3, 'loss': 1e-4, 'norm_rel_max': 2e-3, 'norm_rel_median': 2e-3, 'cos': 1 - 1e-4},
+                   'bf16': {'hm': 0.4, 'loss': 2e-2, 'norm_rel_max': 1.0, 'norm_rel_median': 0.6, 'cos': 0.0},
+                   'bf16-mse': {'hm': 0.4, 'loss': 2e-2, 'norm_rel_max': 1.0, 'norm_rel_median': 0.6, 'cos': 0.0}}
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
-def test_train_step_r50_256_matches_oracle_autograd(cuda, precision):
+@pytest.mark.parametrize('precision,fund_weight', [('fp32', 10.0), ('bf16', 10.0), ('bf16', 0.0)],
+                         ids=['fp32', 'bf16', 'bf16-mse-only'])
+def test_train_step_r50_256_matches_oracle_autograd(cuda, precision, fund_weight):
     """configs[3]'s training step at its image size: R50@256, 4 views x 2 groups, per-view batch
     statistics, JointsMSE + 10 x FundamentalLoss, through the staged training plan with the
     training conv tiles AUTOTUNED as bench.py tunes them (a throwaway first step), against the
@@ -217,6 +226,7 @@ def test_train_step_r50_256_matches_oracle_autograd(cuda, precision):
     from posu import plan as pplan
     torch.set_num_threads(16)
     g = _inputs_r50_256()
+    g['fund_weight'] = fund_weight
     pplan._Tuner.active, pplan._Tuner.reps = True, 2
     try:
         _step(cuda, g, precision)   # tunes the raw training convolutions at these geometries
@@ -233,18 +243,18 @@ def test_train_step_r50_256_matches_oracle_autograd(cuda, precision):
     ga = torch.cat([named[n].grad.detach().double().cpu().ravel() for n in names])
     gr = torch.cat([params[n].grad.detach().double().ravel() for n in names])
     cos = float(ga @ gr / (ga.norm() * gr.norm()))
-    b = TRAIN_256_BANDS[precision]
-    print('%s R50@256 4x2 train step vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs %.6g, grad-norm '
-          'rel median %.3g max %.3g (%s), whole-gradient cosine %.6f'
-          % (precision, hm_err, mse.item(), mse_r.item(), fund.item(), fund_r.item(), np.median(rel), rel.max(),
-             names[int(rel.argmax())], cos))
+    b = TRAIN_256_BANDS[precision if fund_weight else precision + '-mse']
+    print('%s fund_weight %g R50@256 4x2 train step vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs '
+          '%.6g, grad-norm rel median %.3g max %.3g (%s), whole-gradient cosine %.6f'
+          % (precision, fund_weight, hm_err, mse.item(), mse_r.item(), fund.item(), fund_r.item(), np.median(rel),
+             rel.max(), names[int(rel.argmax())], cos))
     assert hm_err < b['hm']
     np.testing.assert_allclose(mse.item(), mse_r.item(), rtol=b['loss'])
-    np.testing.assert_allclose(fund.item(), fund_r.item(), rtol=b['loss'] * 10)
-    if 'norm_rel_max' in b:
-        assert rel.max() < b['norm_rel_max'], names[int(rel.argmax())]
-    else:
-        assert np.median(rel) < b['norm_rel_median']
+    if fund_weight:
+        np.testing.assert_allclose(fund.item(), fund_r.item(), rtol=b['loss'] * 10)
+    assert rel.max() < b['norm_rel_max'], names[int(rel.argmax())]
+    assert np.median(rel) < b['norm_rel_median']
+    assert cos > b['cos']
     sd = net.state_dict()
     for k, v in bufs.items():
         np.testing.assert_allclose(sd[k].cpu().numpy(), v.numpy(), atol=1e-4 if precision == 'fp32' else 2e-2,

@@ -159,18 +159,21 @@ def test_ransac_oracle_known_answers():
     assert rv[2 * 4:2 * 4 + 4, 7].sum() == 0
 
 
-def train_step_oracle(g, num_layers=None, size=None):
+def train_step_oracle(g, num_layers=None, size=None, sd=None, views=None):
     """The reference's training step (core/function.py:154-366, train mode, per-view BatchNorm)
     restated on the oracle: -> (params, buffers, heatmaps [V, B, J, h, w], joints [V, B, J, 2],
-    mse, fund); the loss is back-propagated into params[k].grad."""
+    mse, fund); the loss is back-propagated into params[k].grad.  sd / views (CPU): another
+    network's state and crops than the golden's seeded ones."""
     nl = int(g['num_layers']) if num_layers is None else num_layers
     size = int(g['image_size']) if size is None else size
     nv, b, seed = int(g['nviews']), int(g['batch']), int(g['seed'])
-    sd = syn.synthetic_state_dict(_reference_shaped_state(nl, size), seed=seed)
-    params = {k: v.clone().requires_grad_(True) for k, v in sd.items()
+    if sd is None:
+        sd = syn.synthetic_state_dict(_reference_shaped_state(nl, size), seed=seed)
+    params = {k: v.detach().float().clone().requires_grad_(True) for k, v in sd.items()
               if not ('running_' in k or 'num_batches' in k)}
     bufs = {k: v.clone() for k, v in sd.items() if 'running_' in k}
-    views = syn.synthetic_views(nv, b, size, seed=seed + 1)
+    if views is None:
+        views = syn.synthetic_views(nv, b, size, seed=seed + 1)
     hms, joints, mse = [], [], 0
     for v in range(nv):
         hm, _, _ = PR.pose_resnet_train_forward(views[v], params, bufs, nl)

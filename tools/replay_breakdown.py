@@ -24,7 +24,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('csv')
     ap.add_argument('--last', type=int, default=5, help='replays (from the end of the trace) to aggregate')
+    ap.add_argument('--start', default='stem_pool_kernel',
+                    help='kernel-name substring of a replay\'s first launch(es) (pack_split_kernel: the fp16x3 plan)')
     a = ap.parse_args()
+    st = a.start
     rows = []
     with open(a.csv) as f:
         for r in csv.DictReader(f):
@@ -32,8 +35,8 @@ def main():
     rows.sort()
     replays, cur = [], None
     for s, e, n in rows:
-        if 'stem_pool_kernel' in n:
-            if cur is not None and len(cur) and all('stem_pool_kernel' in c[2] for c in cur) and s - cur[-1][1] <= 20000:
+        if st in n:
+            if cur is not None and len(cur) and all(st in c[2] for c in cur) and s - cur[-1][1] <= 20000:
                 cur.append((s, e, n))   # the next view's stem launch of the same replay
             else:
                 cur = [(s, e, n)]
