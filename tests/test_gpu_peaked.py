@@ -79,11 +79,14 @@ def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
     peaked heatmaps the soft-argmax joints no longer follow the heatmaps' rounding noise, so this
     separates the bf16 backward's own deviation from the FundamentalLoss's amplification of flat
     heatmaps (test_gpu_train.py's random-init network)."""
-    import copy
+    from models.pose_resnet import get_pose_net
+    from posu import synthetic as syn
     from test_gpu_train import _step
     from test_oracle_golden import train_step_oracle
     net0, task = fitted[4], fitted[5]
-    net = copy.deepcopy(net0)
+    net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision='bf16')
+    net.load_state_dict(net0.state_dict())
+    net = net.to(cuda)
     groups = task['groups']
     host = task['host']
     g = {'num_layers': 50, 'image_size': 256, 'nviews': 4, 'batch': groups, 'seed': 0, 'fund_weight': fund_weight,
@@ -103,10 +106,14 @@ def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
           'grad-norm rel median %.3g max %.3g (%s), cosine %.6f'
           % (fund_weight, hm_err, mse.item(), mse_r.item(), float(fund), float(fund_r), np.median(rel), rel.max(),
              names[int(rel.argmax())], cos))
-    b = PEAKED_TRAIN_BF16
+    b = PEAKED_TRAIN_BF16[fund_weight > 0]
     assert hm_err < b['hm']
     assert abs(mse.item() / mse_r.item() - 1) < b['loss']
     assert np.median(rel) < b['norm_median'] and cos > b['cos']
 
 
-PEAKED_TRAIN_BF16 = {'hm': 0.1, 'loss': 2e-2, 'norm_median': 0.6, 'cos': 0.5}
+# about 2 x the round-5 measurement (call r5e): heatmaps 0.0351 max, MSE 1.3e-2 relative (a small
+# residual near the fit's optimum, so the bf16 heatmap rounding is a visible fraction of it);
+# gradients: with the FundamentalLoss median 0.059 / cosine 0.792, MSE only 0.030 / 0.970
+PEAKED_TRAIN_BF16 = {True: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.12, 'cos': 0.6},
+                     False: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.06, 'cos': 0.94}}

@@ -199,15 +199,24 @@ def _inputs_r50_256(groups=2, seed=3):
             'subjects': host['subjects']}
 
 
-# fp32: the reference golden's gates.  bf16: 2 x the deviation measured at round 4 (call r4i:
-# heatmaps 0.186 max, MSE 2.7e-4 and fundamental loss 2.5e-3 relative, grad-norm relative
-# deviation median 0.278 / max 0.451).  The random-init network's heatmaps are flat noise and
-# the FundamentalLoss (weight 10) reads joints from their soft-argmax at beta = 100, which weights
-# a 0.02 heatmap difference by e^2 (section 5 of DESIGN.md): the bf16 gradients of that term
-# follow the rounding noise, so the fp32 step is the parity-bearing gate of this shape.
-TRAIN_256_BANDS = {'fp32': {'hm': 1e-3, 'loss': 1e-4, 'norm_rel_max': 2e-3, 'norm_rel_median': 2e-3, 'cos': 1 - 1e-4},
-                   'bf16': {'hm': 0.4, 'loss': 2e-2, 'norm_rel_max': 1.0, 'norm_rel_median': 0.6, 'cos': 0.0},
-                   'bf16-mse': {'hm': 0.4, 'loss': 2e-2, 'norm_rel_max': 1.0, 'norm_rel_median': 0.6, 'cos': 0.0}}
+# fp32: the reference golden's gates.  bf16, from the round-5 split by cause (call r5d, this test):
+#   fund_weight 10 (the reference's loss on a random-init network's FLAT heatmaps): heatmaps 0.186 max,
+#     MSE 2.7e-4 and FundamentalLoss 2.5e-3 relative, grad-norm relative deviation median 0.278 /
+#     max 0.451, whole-gradient cosine 0.33;
+#   fund_weight 0 (JointsMSE only, same network and batch): median 0.0066 / max 0.114, cosine 0.9986.
+# So the bf16 backward itself agrees with the oracle's autograd; what moves the fund_weight-10
+# gradients is the FundamentalLoss reading joints from the soft-argmax at beta = 100 of flat
+# heatmaps, which weights a 0.02 heatmap difference by e^2 -- on the fitted
+# network's peaked heatmaps the same loss is gated in tests/test_gpu_peaked.py.  The bf16 gradient
+# gates are therefore on the MSE-only step (about 3 x / 2 x its measured median / max, cosine
+# 0.995); the fund_weight-10 step gates its forward (heatmaps, both losses) only.  Heatmaps: 0.186
+# max abs on heatmaps up to ~13 (hm_scale printed below): bf16's 2^-8 relative rounding through
+# 50 layers; gated at 0.3.
+TRAIN_256_BANDS = {'fp32': {'hm': 1e-3, 'loss': 1e-4, 'fund': 1e-3, 'norm_rel_max': 2e-3, 'norm_rel_median': 2e-3,
+                            'cos': 1 - 1e-4},
+                   'bf16': {'hm': 0.3, 'loss': 1e-3, 'fund': 1e-2},
+                   'bf16-mse': {'hm': 0.3, 'loss': 1e-3, 'norm_rel_max': 0.25, 'norm_rel_median': 0.02,
+                                'cos': 0.995}}
 
 
 @pytest.mark.parametrize('precision,fund_weight', [('fp32', 10.0), ('bf16', 10.0), ('bf16', 0.0)],
@@ -244,17 +253,18 @@ def test_train_step_r50_256_matches_oracle_autograd(cuda, precision, fund_weight
     gr = torch.cat([params[n].grad.detach().double().ravel() for n in names])
     cos = float(ga @ gr / (ga.norm() * gr.norm()))
     b = TRAIN_256_BANDS[precision if fund_weight else precision + '-mse']
-    print('%s fund_weight %g R50@256 4x2 train step vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs '
-          '%.6g, grad-norm rel median %.3g max %.3g (%s), whole-gradient cosine %.6f'
-          % (precision, fund_weight, hm_err, mse.item(), mse_r.item(), fund.item(), fund_r.item(), np.median(rel),
-             rel.max(), names[int(rel.argmax())], cos))
+    print('%s fund_weight %g R50@256 4x2 train step vs oracle: heatmaps max %.3g (hm_scale %.3g), mse %.6g vs %.6g, '
+          'fund %.6g vs %.6g, grad-norm rel median %.3g max %.3g (%s), whole-gradient cosine %.6f'
+          % (precision, fund_weight, hm_err, float(hm_r.abs().max()), mse.item(), mse_r.item(), fund.item(),
+             fund_r.item(), np.median(rel), rel.max(), names[int(rel.argmax())], cos))
     assert hm_err < b['hm']
     np.testing.assert_allclose(mse.item(), mse_r.item(), rtol=b['loss'])
     if fund_weight:
-        np.testing.assert_allclose(fund.item(), fund_r.item(), rtol=b['loss'] * 10)
-    assert rel.max() < b['norm_rel_max'], names[int(rel.argmax())]
-    assert np.median(rel) < b['norm_rel_median']
-    assert cos > b['cos']
+        np.testing.assert_allclose(fund.item(), fund_r.item(), rtol=b['fund'])
+    if 'cos' in b:
+        assert rel.max() < b['norm_rel_max'], names[int(rel.argmax())]
+        assert np.median(rel) < b['norm_rel_median']
+        assert cos > b['cos']
     sd = net.state_dict()
     for k, v in bufs.items():
         np.testing.assert_allclose(sd[k].cpu().numpy(), v.numpy(), atol=1e-4 if precision == 'fp32' else 2e-2,

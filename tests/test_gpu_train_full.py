@@ -94,8 +94,10 @@ def test_full_step_fp32_forward_matches_oracle(full_step):
     assert hm < 1e-3 and mse < 1e-4 and epi < 1e-3
 
 
-# bf16 bands: measured in round 5 (r5?) on this batch; see DESIGN.md section 5
-FULL_BF16 = {'hm': 0.4, 'mse': 2e-2, 'epi': 0.2, 'cos': 0.5, 'norm_median': 0.6}
+# bf16 bands, about 2 x what round 5 measured on this batch (call r5d): heatmaps 0.22 max, MSE 2.9e-4
+# and epipolar 0.014 relative; gradients against the fp32 step: cosine 0.999923 (gated at 1 - 2e-4),
+# per-tensor norm deviation median 0.0045 / max 0.094 (layer1.1.bn2.weight)
+FULL_BF16 = {'hm': 0.45, 'mse': 6e-4, 'epi': 0.03, 'cos': 1 - 2e-4, 'norm_median': 0.01, 'norm_max': 0.2}
 
 
 def test_full_step_bf16_forward_and_gradients(full_step):
@@ -114,7 +116,7 @@ def test_full_step_bf16_forward_and_gradients(full_step):
         assert np.isfinite(r['loss']) and all(torch.isfinite(g).all() for g in r['grads'].values())
     assert hm < FULL_BF16['hm'] and mse < FULL_BF16['mse'] and epi < FULL_BF16['epi']
     assert cos > FULL_BF16['cos']
-    assert np.median(np.abs(rel)) < FULL_BF16['norm_median']
+    assert np.median(np.abs(rel)) < FULL_BF16['norm_median'] and np.abs(rel).max() < FULL_BF16['norm_max']
 
 
 def test_full_step_is_deterministic(full_step):
