@@ -149,7 +149,10 @@ int posu_conv_bk(int dtype);
  * maxpool, and the input pack): x NCHW f32 [N, 3, H, W] (the reference's input tensor,
  * mirrored along W when hflip), w packed [64][224] dtype (k = kh*32 + kw*4 + c, zero for
  * kw = 7 / c = 3; posu/packing.py:pack_stem_fused_weight), BN scale/shift [64] f32,
- * y NHWC [N, H/4, W/4, 64] dtype.  BF16 / F16, H % 8 == 0, W in {256, 384}. */
+ * y NHWC [N, H/4, W/4, 64] dtype.  BF16 / F16, H % 8 == 0, W in {256, 384}; F16X3 (ABI 13, W = 256):
+ * w = the hi plane [64][224] followed by the lo plane [64][224] of the weights (scaled by the
+ * caller's power of two, undone in `scale`), the input split into (hi, lo) fp16 as it is staged,
+ * three MFMAs per kernel row, y split [N, H/4, W/4, 128]. */
 int posu_stem_pool_fwd(int dtype, const float* x, int N, int H, int W, int hflip, const void* w,
                        const float* scale, const float* shift, void* y, void* stream);
 /* posu_stem_pool_fwd over the views of one forward in ONE launch (lib/models/multiview_pose_resnet.py

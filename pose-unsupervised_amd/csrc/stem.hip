@@ -84,7 +84,12 @@ constexpr int kStemAbl = POSU_STEM_ABLATE;
 //     registers while item k-1 computes and written to the ring behind it;
 //   * stem row 4k-1 (the first row of pool row 2k's window) is item k-1's last stem row, carried
 //     in registers: an item computes 4 stem rows (the strip's first item 5), not 5.
-template <typename T, int NW>
+// SPL (round 5, the split-fp16 dtype POSU_F16X3, T = f16_t): the input window is staged twice, as
+// its fp16 hi and lo halves (two rings), the weights likewise ([hi 64][224] then [lo 64][224] in
+// w), every kernel row issues w_hi.x_hi + w_lo.x_hi + w_hi.x_lo, and the pooled outputs are stored
+// as (hi, lo) pairs in the split layout (128 halves per pixel).  Eight waves (W = 256) only: the
+// twelve-wave rings do not fit twice.
+template <typename T, int NW, bool SPL = false>
 __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int Nv, int N, int H, int W, int hflip,
                                                                int strips, const T* __restrict__ w,
                                                                const float* __restrict__ scale,
@@ -95,11 +100,16 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   constexpr int RB = WP * 8;                 // bytes per ring row
   constexpr int RING = 16;
   constexpr int W_BYTES = 64 * kStemPitch * 2;
-  __shared__ __attribute__((aligned(16))) char smem[RING * RB + W_BYTES + NW * 2 * 64 * 4 + 2 * 64 * 4];
+  constexpr int NS = SPL ? 2 : 1;            // halves staged (hi [, lo])
+  constexpr int CPX = SPL ? 128 : 64;        // stored elements per output pixel
+  static_assert(!SPL || (NW == 8 && std::is_same<T, f16_t>::value), "split stem: fp16 halves, eight waves");
+  __shared__ __attribute__((aligned(16))) char smem[NS * (RING * RB + W_BYTES) + NW * 2 * 64 * 4 + 2 * 64 * 4];
   char* win = smem;
-  char* wl = smem + RING * RB;
-  float* edge = reinterpret_cast<float*>(smem + RING * RB + W_BYTES);  // [wave][pool row][64 ch]
-  float* bn = edge + NW * 2 * 64;                                       // scale [64], shift [64]
+  char* winl = smem + RING * RB;              // SPL: the lo ring
+  char* wl = smem + NS * RING * RB;
+  char* wll = wl + W_BYTES;                   // SPL: the lo weights
+  float* edge = reinterpret_cast<float*>(smem + NS * (RING * RB + W_BYTES));  // [wave][pool row][64 ch]
+  float* bn = edge + NW * 2 * 64;                                             // scale [64], shift [64]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int r16 = lane & 15, q = lane >> 4;
@@ -118,16 +128,17 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   {
     constexpr int WCH = 64 * (kStemK / 8);
 #pragma unroll
-    for (int it = 0; it < (WCH + NT - 1) / NT; ++it) {
+    for (int it = 0; it < (NS * WCH + NT - 1) / NT; ++it) {
       const int i = tid + it * NT;
-      if (i < WCH) {
-        const int co = i / (kStemK / 8), ck = i - co * (kStemK / 8);
+      if (i < NS * WCH) {
+        const int h = i / WCH, ii = i - h * WCH;   // h = 1: the lo plane (SPL)
+        const int co = ii / (kStemK / 8), ck = ii - co * (kStemK / 8);
         // the sign of the channel's BN scale folded into its weights (negation is exact, in the
         // MFMA sums too): the accumulators are sgn(s) * conv, which the pool maximises directly
         const unsigned sg = __float_as_uint(scale[co]) & 0x80000000u ? 0x80008000u : 0u;
         u32x4 wv = *reinterpret_cast<const u32x4*>(w + i * 8);
         wv ^= sg;
-        *reinterpret_cast<u32x4*>(wl + (co * kStemPitch + ck * 8) * 2) = wv;
+        *reinterpret_cast<u32x4*>((h ? wll : wl) + (co * kStemPitch + ck * 8) * 2) = wv;
       }
     }
   }
@@ -175,8 +186,15 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int wc = 4 * gk - 1 + e;
-        if (wc >= 0 && wc < WP)
+        if (wc >= 0 && wc < WP) {
           *reinterpret_cast<uint2*>(row + wc * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
+          if constexpr (SPL) {   // lo = fp16(v - hi) (exact difference in f32)
+            const float l0 = a0[e] - static_cast<float>(static_cast<_Float16>(a0[e]));
+            const float l1 = a1[e] - static_cast<float>(static_cast<_Float16>(a1[e]));
+            const float l2 = a2[e] - static_cast<float>(static_cast<_Float16>(a2[e]));
+            *reinterpret_cast<uint2*>(row - win + winl + wc * 8) = make_uint2(O::pack2(l0, l1), O::pack2(l2, 0.f));
+          }
+        }
       }
     }
   };
@@ -204,10 +222,18 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     auto rd = [&](int rho) {
       return *reinterpret_cast<const uint4*>(win + ((2 * r0 - 3 + rho) & (RING - 1)) * RB + (2 * sc + 2 * q) * 8);
     };
+    auto rdl = [&](int rho) {   // SPL: the lo ring
+      return *reinterpret_cast<const uint4*>(winl + ((2 * r0 - 3 + rho) & (RING - 1)) * RB + (2 * sc + 2 * q) * 8);
+    };
     auto bload = [&](int kh, uint4 (&bfr)[4]) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bfr[j] = *reinterpret_cast<const uint4*>(wl + ((16 * j + r16) * kStemPitch + kh * 32 + 8 * q) * 2);
+    };
+    auto bloadl = [&](int kh, uint4 (&bfr)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = *reinterpret_cast<const uint4*>(wll + ((16 * j + r16) * kStemPitch + kh * 32 + 8 * q) * 2);
     };
     auto mmas = [&](const uint4 (&bfr)[4], const uint4 (&af)[M]) {
 #pragma unroll
@@ -218,7 +244,36 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
           else O::mma(acc[rl][j], bfr[j], af[rl]);
         }
     };
-    if constexpr (NW <= 8) {
+    if constexpr (SPL) {
+      // w_hi.x_hi + w_lo.x_hi + w_hi.x_lo per kernel row; the rolling sets of the plain kernel for
+      // both halves of the window
+      uint4 ev[M], od[M], evl[M], odl[M], bfr[4], bfl[4];
+#pragma unroll
+      for (int kh = 0; kh < 7; ++kh) {
+        uint4 (&set)[M] = (kh & 1) ? od : ev;
+        uint4 (&setl)[M] = (kh & 1) ? odl : evl;
+        bload(kh, bfr);
+        bloadl(kh, bfl);
+        if (kh < 2) {
+#pragma unroll
+          for (int rl = 0; rl < M; ++rl) {
+            set[rl] = rd(kh + 2 * rl);
+            setl[rl] = rdl(kh + 2 * rl);
+          }
+        } else {
+#pragma unroll
+          for (int rl = 0; rl + 1 < M; ++rl) {
+            set[rl] = set[rl + 1];
+            setl[rl] = setl[rl + 1];
+          }
+          set[M - 1] = rd(kh + 2 * (M - 1));
+          setl[M - 1] = rdl(kh + 2 * (M - 1));
+        }
+        mmas(bfr, set);
+        mmas(bfl, set);
+        mmas(bfr, setl);
+      }
+    } else if constexpr (NW <= 8) {
       // kernel rows of one parity read the same window rows shifted by one m-tile: two rolling
       // sets (even / odd kh) load 2 M + 5 distinct rows instead of 7 M
       uint4 ev[M], od[M], bfr[4];
@@ -265,7 +320,7 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
       }
   };
 
-  T* __restrict__ yn = y + static_cast<size_t>(n) * Hp * Wp * 64;
+  T* __restrict__ yn = y + static_cast<size_t>(n) * Hp * Wp * CPX;
   // pool rows 2k, 2k+1 from their vertical maxima: horizontal max with DPP row shifts (a wave's
   // left neighbour column through LDS), then BN + ReLU + rounding, 8-byte NHWC stores
   auto pool = [&](int k, const float (*vm)[4][4]) __attribute__((always_inline)) {
@@ -304,10 +359,20 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
         }
         if ((r16 & 1) == 0) {
           const int pc = 8 * wid + (r16 >> 1);
-          T* dst = yn + (static_cast<size_t>(2 * k + p) * Wp + pc) * 64 + 16 * j + 4 * q;
+          const int c0 = 16 * j + 4 * q;
+          T* dst = yn + (static_cast<size_t>(2 * k + p) * Wp + pc) * CPX + (SPL ? split_ch(c0) : c0);
           const uint2 u = make_uint2(O::pack2(o[0], o[1]), O::pack2(o[2], o[3]));
-          if (kStemAbl & 4) asm volatile("" ::"v"(u.x), "v"(u.y));
-          else *reinterpret_cast<uint2*>(dst) = u;
+          if (kStemAbl & 4) {
+            asm volatile("" ::"v"(u.x), "v"(u.y));
+          } else {
+            *reinterpret_cast<uint2*>(dst) = u;
+            if constexpr (SPL) {
+              float l[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) l[e] = o[e] - static_cast<float>(static_cast<_Float16>(o[e]));
+              *reinterpret_cast<uint2*>(dst + 32) = make_uint2(O::pack2(l[0], l[1]), O::pack2(l[2], l[3]));
+            }
+          }
         }
       }
   };
@@ -375,7 +440,8 @@ namespace {
 int stem_launch(int dtype, const float* const* views, int nviews, int Nv, int H, int W, int hflip, const void* w,
                 const float* scale, const float* shift, void* y, void* stream, const char* what) {
   const std::string wh(what);
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, wh + ": dtype must be BF16 or F16");
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16 || dtype == POSU_F16X3, wh + ": dtype must be BF16, F16 or F16X3");
+  POSU_REQUIRE(dtype != POSU_F16X3 || W == 256, wh + ": the split-fp16 stem is built for W = 256");
   POSU_REQUIRE(views && nviews >= 1 && nviews <= kMaxViews, wh + ": 1 .. 8 views");
   for (int v = 0; v < nviews; ++v) POSU_REQUIRE(views[v], wh + ": null view pointer");
   POSU_REQUIRE(w && scale && shift && y, wh + ": null pointer");
@@ -390,7 +456,10 @@ int stem_launch(int dtype, const float* const* views, int nviews, int Nv, int H,
   while (N * strips * 2 <= 256 && pairs % (strips * 2) == 0) strips *= 2;
   hipStream_t s = as_stream(stream);
   const dim3 grid(static_cast<unsigned>(N * strips));
-  if (dtype == POSU_BF16) {
+  if (dtype == POSU_F16X3) {
+    hipLaunchKernelGGL((stem_pool_kernel<f16_t, 8, true>), grid, dim3(512), 0, s, xs, Nv, N, H, W, hflip, strips,
+                       static_cast<const f16_t*>(w), scale, shift, static_cast<f16_t*>(y));
+  } else if (dtype == POSU_BF16) {
     if (W == 256)
       hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 8>), grid, dim3(512), 0, s, xs, Nv, N, H, W, hflip, strips,
                          static_cast<const uint16_t*>(w), scale, shift, static_cast<uint16_t*>(y));

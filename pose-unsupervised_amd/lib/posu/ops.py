@@ -241,7 +241,8 @@ def stem_pool_views(views, wpk, scale, shift, code, out=None, hflip=False):
         raise ValueError('stem_pool_views: views of one shape [N, 3, H, W] expected')
     views = [v.contiguous().float() for v in views]
     if out is None:
-        out = torch.empty((n * len(views), h // 4, w // 4, 64), dtype=torch_dtype(code), device=views[0].device)
+        out = torch.empty((n * len(views), h // 4, w // 4, 64 * cmul(code)), dtype=torch_dtype(code),
+                          device=views[0].device)
     arr = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
     call('posu_stem_pool_views_fwd', code, ctypes.cast(arr, ctypes.c_void_p), len(views), n, h, w, int(bool(hflip)),
          ptr(wpk), ptr(scale), ptr(shift), ptr(out), stream_of(views[0].device))
@@ -258,7 +259,7 @@ def stem_pool(x, wpk, scale, shift, code, out=None, hflip=False):
         raise ValueError('stem_pool: 3 input channels expected')
     x = x.contiguous().float()
     if out is None:
-        out = torch.empty((n, h // 4, w // 4, 64), dtype=torch_dtype(code), device=x.device)
+        out = torch.empty((n, h // 4, w // 4, 64 * cmul(code)), dtype=torch_dtype(code), device=x.device)
     call('posu_stem_pool_fwd', code, ptr(x), n, h, w, int(bool(hflip)), ptr(wpk), ptr(scale), ptr(shift), ptr(out),
          stream_of(x.device))
     return out

@@ -460,9 +460,14 @@ class PoseResNetPlan:
         last = self.deconvs[-1] if self.deconvs else None
         self.fuse_head = last is not None and last.cout == 256 and self.njoints <= 16
         self.stem_fused_w = None
-        if (FUSED_STEM and code in (ops.BF16, ops.F16) and tuple(net.conv1.weight.shape) == (64, 3, 7, 7)
+        if (FUSED_STEM and code in (ops.BF16, ops.F16, ops.F16X3) and tuple(net.conv1.weight.shape) == (64, 3, 7, 7)
                 and net.conv1.stride == (2, 2) and net.conv1.padding == (3, 3)):
-            self.stem_fused_w = pack_stem_fused_weight(net.conv1.weight, ops.torch_dtype(code))
+            if code == ops.F16X3:   # hi plane, then lo plane (posu_stem_pool_fwd); the stem conv's exponent
+                v = pack_stem_fused_weight(net.conv1.weight, torch.float64) * 2.0 ** split_exponent(net.conv1.weight)
+                hi = v.to(torch.float16)
+                self.stem_fused_w = torch.cat([hi, (v - hi.double()).to(torch.float16)], dim=0).contiguous()
+            else:
+                self.stem_fused_w = pack_stem_fused_weight(net.conv1.weight, ops.torch_dtype(code))
 
     def pack_input(self, views, hflip=False, fused=True):
         """List of NCHW f32 tensors (same shape) -> one NHWC batch (views stacked on N):
@@ -470,7 +475,8 @@ class PoseResNetPlan:
         every image along W (flip test).  Where the fused stem applies (bf16 / fp16,
         H % 8 == 0, W in {256, 384}) the views are handed over as they are (RawViews)."""
         n, _, h, w = views[0].shape
-        if fused and self.stem_fused_w is not None and h % 8 == 0 and w in (256, 384) and views[0].shape[1] == 3:
+        if fused and self.stem_fused_w is not None and h % 8 == 0 and w in ((256,) if self.code == ops.F16X3 else
+                                                                             (256, 384)) and views[0].shape[1] == 3:
             return RawViews(self, list(views), hflip)
         s2d = h % 2 == 0 and w % 2 == 0
         cm = ops.cmul(self.code)
@@ -491,8 +497,8 @@ class PoseResNetPlan:
             if STEM_VIEWS and len({tuple(v.shape) for v in x.views}) == 1 and len(x.views) <= 8:
                 return ops.stem_pool_views(x.views, self.stem_fused_w, self.stem.scale, self.stem.shift, code,
                                            hflip=x.hflip)
-            out = torch.empty((x.shape[0], x.h // 4, x.w // 4, self.stem.cout), dtype=ops.torch_dtype(code),
-                              device=x.device)
+            out = torch.empty((x.shape[0], x.h // 4, x.w // 4, self.stem.cout * ops.cmul(code)),
+                              dtype=ops.torch_dtype(code), device=x.device)
             base = 0
             for v in x.views:
                 ops.stem_pool(v, self.stem_fused_w, self.stem.scale, self.stem.shift, code,

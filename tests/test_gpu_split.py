@@ -125,3 +125,33 @@ def test_split_layout_ops(cuda):
     ref = F.max_pool2d(from_split(a_s), 3, 2, 1)
     assert torch.equal(from_split(mp), ref)
     assert torch.equal(mp, to_split_act(ref))
+
+
+@pytest.mark.parametrize('hflip', [False, True])
+def test_split_fused_stem_matches_fp64(cuda, hflip):
+    """posu_stem_pool_views_fwd in split fp16 (input split while staged, hi / lo weight planes,
+    three MFMAs per kernel row, pool first / BN after) against the f64 stem + BN + ReLU + max-pool."""
+    from posu.packing import pack_stem_fused_weight
+    torch.manual_seed(11)
+    views = [torch.randn(3, 3, 256, 256, device=cuda) for _ in range(2)]
+    w = torch.randn(64, 3, 7, 7, dtype=torch.float64, device=cuda) * 0.05
+    scale = (torch.rand(64, device=cuda) + 0.5) * torch.where(torch.rand(64, device=cuda) < 0.2, -1.0, 1.0)
+    shift = torch.randn(64, device=cuda) * 0.1
+    e = split_exponent(w)
+    v = pack_stem_fused_weight(w.float(), torch.float64) * 2.0 ** e
+    hi = v.to(torch.float16)
+    wpk = torch.cat([hi, (v - hi.double()).to(torch.float16)], dim=0).contiguous()
+    y = ops.stem_pool_views(views, wpk, (scale.double() * 2.0 ** -e).float(), shift, S, hflip=hflip)
+    assert y.shape == (6, 64, 64, 128)
+    x = torch.cat(views).double()
+    if hflip:
+        x = x.flip(3)
+    xf = x.float()
+    xh = xf.half().float()
+    xq = (xh.double() + (xf - xh).half().double())     # the input as its (hi, lo) pair
+    wq = w.float().double()
+    ref = F.max_pool2d(F.relu(F.conv2d(xq, wq, stride=2, padding=3) * scale.double()[None, :, None, None] +
+                              shift.double()[None, :, None, None]), 3, 2, 1)
+    mag = F.max_pool2d(F.conv2d(xq.abs(), wq.abs(), stride=2, padding=3) * scale.double().abs()[None, :, None, None],
+                       3, 2, 1) + 1
+    assert rel_err(from_split(y), ref, mag) < 2e-6
