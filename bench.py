@@ -126,9 +126,10 @@ def parse():
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` leg times it in the same process, so a gain shows on the driver's own box
+# (round 5: the two-K-group tile 39 among the inference tile candidates)
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control leg compares the plans at the same numerics)
-CONTROL_FLAGS = ('S2_TAIL', 'S2_CHAIN', 'STEM_VIEWS', 'TILES_128X8')
+CONTROL_FLAGS = ('TILES_KSPLIT',)
 
 
 def apply_plan_flags(flags):

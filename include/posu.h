@@ -139,8 +139,11 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *     variant 1: single-slot LDS ring (cfg 0-4), 2: three-slot ring (cfg != 5);
  *     + 32 (bf16 / f16): the persistent K-tile stream;
  *     23 / 31 (bf16 / f16): 256x256 / 256x128 with waves 4-7 staggered by half a K-tile;
- *     7 / 15 (bf16 / f16, ABI 11): 128x128 with eight staggered waves (2x4 / 4x2 wave grids).
- *   The tile only changes speed (every configuration computes the same sums in the same
+ *     7 / 15 (bf16 / f16, ABI 11): 128x128 with eight staggered waves (2x4 / 4x2 wave grids);
+ *     39 (bf16 / f16, ABI 13, NHWC outputs): 128x128 with two K groups of four waves (each group
+ *        sums every other K-tile over the whole tile, the halves added in LDS at the end: a
+ *        different K order, so not bit-identical to the other tiles).
+ *   The tile only changes speed (every configuration but 39 computes the same sums in the same
  *   K order); the Python plan picks it per layer by timing every admissible
  *   configuration once (PoseResNetPlan.autotune).  The library keeps no mutable state:
  *   every knob is an argument. */

@@ -95,7 +95,15 @@ constexpr int kEarlyNK = 8;
 // only).  Its registers (head accumulators and weight fragments) made the 256x256 instance
 // spill 36 VGPRs to scratch in every launch until round 4, head or not; the plain instances
 // no longer hold that code (228 VGPRs, no scratch).
-template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false, bool HD = false>
+// KS (round 5): eight waves as two K groups of four -- the K-tiles come in pairs (two LDS sub-slots
+// per ring slot), group g multiplies K-tile 2t + g of every pair over the WHOLE BM x BN tile, and
+// the two partial sums meet in LDS at the end (each group adds the other's half of the m-tiles and
+// stores that half).  Per wave 64 x 64 (TM = TN = 4) instead of the 64 x 32 of the eight-wave
+// 128 x 128 tile: half the LDS fragment reads per MFMA, for grids of few tiles (layer4's M = 8192
+// convs: 256 tiles of 128 x 128, one per CU).  The K order differs from the other tiles (the even
+// and the odd K-tiles summed apart, then added), so KS results are not bit-identical to them.
+template <typename T, int BM, int BN, int NW, int WGM, int S, bool DUAL, bool SG = false, bool HD = false,
+          bool KS = false>
 __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   using O = Op<T>;
   constexpr int NT = NW * 64;
@@ -106,24 +114,28 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   constexpr bool SPL = O::SPLIT;
   static_assert(!(SPL && SG), "split fp16 runs the unstaggered loops");
   constexpr int BK = 8 * E;                   // 128-byte LDS rows
-  constexpr int WGN = NW / WGM;               // wave grid WGM x WGN
+  static_assert(!KS || (NW == 8 && S == 2 && !SG && !HD && E == 8), "K groups: eight waves, two slots of pairs");
+  constexpr int NWG = KS ? NW / 2 : NW;       // waves per K group
+  constexpr int SL = KS ? 2 * S : S;          // LDS K-tile slots (KS: a pair per ring slot)
+  constexpr int WGN = NWG / WGM;              // wave grid WGM x WGN (of a K group)
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int ROWS = NW * 8;                // LDS rows filled per DMA round (1 KiB per wave)
   constexpr int RA = BM / ROWS, RB = BN / ROWS;
   constexpr int ND = RA + RB;                 // DMA instructions per thread per K-tile
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
-  constexpr int PR = pass_rows<BM, BN, S>();
+  constexpr int PR = pass_rows<BM, BN, SL>();
   constexpr bool PRELOAD = TM + TN <= 8;  // both k-steps' fragments fit the VGPR budget
   static_assert(S >= 1 && S <= 4, "1..4 stages");
   static_assert(ND * (S - 2) < 64, "vmcnt range");
-  static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, S>(), "epilogue staging must fit in the ring");
+  static_assert(PR * (BN + 4) * 4 <= ring_bytes<BM, BN, SL>(), "epilogue staging must fit in the ring");
   static_assert(RA * ROWS == BM && RB * ROWS == BN, "tile rows must be a multiple of 8 * waves");
-  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, S>()];
+  __shared__ __attribute__((aligned(16))) char smem[ring_bytes<BM, BN, SL>()];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const int wm = wid / WGN, wn = wid % WGN;
+  const int grp = KS ? wid / NWG : 0, wl = KS ? wid % NWG : wid;   // K group, wave in the group
+  const int wm = wl / WGN, wn = wl % WGN;
   const int r16 = lane & 15, q = lane >> 4;
   // tile row of the wave's m-tile i / tile column of its n-tile j
   auto rowA = [&](int i) { return wm * WTM + i * 16; };
@@ -361,7 +373,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // Early residual prefetch (short-K Bottleneck tails): the residual chunks, in the direct
   // epilogue's lane layout, are loaded before the first operand DMA, so their HBM latency
   // overlaps the operand fetch instead of following the main loop.
-  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16 && !SPL;
+  constexpr bool EARLY = E == 8 && TN % 2 == 0 && TM * TN <= 16 && !SPL && !KS;
   constexpr int ETM = EARLY ? TM : 1, ETP = EARLY ? TN / 2 : 1;
   const bool early = EARLY && g.res && g.mode == 0 && !g.hm && nk <= kEarlyNK;
   uint4 rve[ETM][ETP];
@@ -394,7 +406,47 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
   // barrier (makes the DMA visible to every wave and retires the slot the next DMA
   // overwrites, which every wave finished reading in the previous iteration)
-  if constexpr (SG) {
+  if constexpr (KS) {
+    // K-tile pairs: pair t in slots 2 (t & 1) and 2 (t & 1) + 1, DMA'd by all eight waves one pair
+    // ahead; group g multiplies the pair's K-tile 2t + g (a missing last odd K-tile is skipped)
+    const int np = (nk + 1) / 2;
+    POSU_DMA_TILE(0, 0);
+    if (1 < nk) POSU_DMA_TILE(1, 1);
+    for (int t = 0; t < np; ++t) {
+      vm_wait<0>();
+      __syncthreads();
+      if (t + 1 < np) {
+        const int b = 2 * ((t + 1) & 1);
+        POSU_DMA_TILE(2 * t + 2, b);
+        if (2 * t + 3 < nk) POSU_DMA_TILE(2 * t + 3, b + 1);
+      }
+      if (2 * t + grp < nk) POSU_COMPUTE(2 * (t & 1) + grp);
+    }
+    // the two groups' partial sums: group 0 keeps m-tiles 0 .. TM/2 - 1, group 1 the rest; each hands
+    // the other its half through LDS (f32, lane-major) and adds the half it keeps (a + b == b + a)
+    __syncthreads();  // every wave is done reading the ring
+    constexpr int HT = TM / 2, PER = HT * TN * 64;   // f32x4 per wave's hand-off
+    f32x4* xch = reinterpret_cast<f32x4*>(smem);
+    auto give = [&](auto g0) {
+      constexpr bool G0 = decltype(g0)::value;
+#pragma unroll
+      for (int i = 0; i < HT; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) xch[(G0 ? 0 : NWG) * PER + wl * PER + (i * TN + j) * 64 + lane] = acc[G0 ? HT + i : i][j];
+    };
+    auto take = [&](auto g0) {
+      constexpr bool G0 = decltype(g0)::value;
+#pragma unroll
+      for (int i = 0; i < HT; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[G0 ? i : HT + i][j] += xch[(G0 ? NWG : 0) * PER + wl * PER + (i * TN + j) * 64 + lane];
+    };
+    if (grp == 0) give(std::true_type{});
+    else give(std::false_type{});
+    __syncthreads();
+    if (grp == 0) take(std::true_type{});
+    else take(std::false_type{});
+  } else if constexpr (SG) {
     // Stagger (two-slot ring, one barrier per K-tile): waves 4-7 run half a K-tile behind
     // waves 0-3 -- they keep the second k-step's fragments of K-tile t in registers and
     // issue its MFMAs after the next barrier, while waves 0-3 wait for their first
@@ -647,6 +699,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      if (KS && (i < TM / 2) != (grp == 0)) continue;   // (wave-uniform) the other group's half
       const int m = m0 + rowA(i) + r16;
       const bool mok = m < g.M;
       const int mm = mok ? m : 0;
@@ -1408,7 +1461,7 @@ void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
 //   block, and eight waves two per SIMD);
 //   -1: the built-in heuristic.
 bool tile_ok(int tile) {
-  if (tile == -1 || tile == 23 || tile == 31 || tile == 7 || tile == 15) return true;
+  if (tile == -1 || tile == 23 || tile == 31 || tile == 7 || tile == 15 || tile == 39) return true;
   if (tile < 0 || tile >= 64) return false;
   const int c = tile & 7, v = (tile >> 3) & 3;
   return c <= 6 && v <= 2 && !(v == 1 && c > 4) && !(v == 2 && c == 5);
@@ -1459,7 +1512,13 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   int st = 2;
   bool sg = false, persist = false;
   bool wg4 = false;  // tile 15: the 4 x 2 wave grid of the 128x128 eight-wave tile
-  if (tile == 23 || tile == 31) {
+  bool ks = false;   // tile 39: the 128x128 tile with two K groups of four waves
+  if (tile == 39) {
+    if (FAST2 && g.CoutPad % 128 == 0 && g.mode == 0 && !g.hm) {
+      cfg = 3;
+      ks = true;
+    }
+  } else if (tile == 23 || tile == 31) {
     const int c = tile == 23 ? 5 : 6;
     if (FAST2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
       cfg = c;
@@ -1493,7 +1552,9 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   if constexpr (FAST2) {
     if (persist) {
       switch (cfg) {
-        case 0: launch_persist<T, 256, 64, 4, 4, DUAL>(g, nb, s); break;
+        // (no persistent 256x64 instance: dynamic indexing of its store registers put 960 B per lane
+        // in scratch; tile 32 runs the plain 256x64 tile)
+        case 0: launch_cfg<T, 256, 64, 4, 4, DUAL>(g, nb, st, s); break;
         case 1: launch_persist<T, 128, 64, 4, 2, DUAL>(g, nb, s); break;
         case 2: launch_persist<T, 64, 64, 4, 2, DUAL>(g, nb, s); break;
         case 3: launch_persist<T, 128, 128, 4, 2, DUAL>(g, nb, s); break;
@@ -1501,6 +1562,11 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
         case 5: launch_persist<T, 256, 256, 8, 2, DUAL>(g, nb, s); break;
         default: launch_persist<T, 256, 128, 8, 4, DUAL>(g, nb, s); break;
       }
+      return check_launch(what);
+    }
+    if (ks) {
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, false, false, true>), dim3(nb), dim3(512), 0,
+                         s, g);
       return check_launch(what);
     }
     if (sg) {

@@ -86,6 +86,9 @@ class RawViews:
 
 # the 128x128 eight-wave staggered conv tiles (7 / 15, round 4) among the autotuner's candidates
 TILES_128X8 = True
+# the 128x128 tile with two K groups of four waves (39, round 5; inference plans only: its K order
+# differs from the other tiles', and the training plan relies on every candidate summing alike)
+TILES_KSPLIT = True
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -102,7 +105,7 @@ class _Tuner:
     seen = []   # geometry keys met by the current tuning run, in launch order
 
 
-def _tile_candidates(cout, code=None):
+def _tile_candidates(cout, code=None, ksplit=False):
     """Tile ids (include/posu.h): cfg 0..6, cfg + 8 = single-slot ring (four-wave tiles;
     short-K layers: more blocks per CU), cfg + 16 = three-slot ring (two K-tiles in flight),
     cfg + 32 = persistent K-tile stream (epilogue stores overlap the next tile's fetch),
@@ -122,13 +125,15 @@ def _tile_candidates(cout, code=None):
     # scratch and took ~1.2 ms per launch in the tuning trials, 10x the other tiles)
     if code == ops.F16X3:   # the split dtype: plain rings only (no stagger, no persistent stream)
         return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5]
+    if ksplit and code in (ops.BF16, ops.F16) and cpad % 128 == 0:
+        sg = sg + [39]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
 
 
 def _tuned(key, cout, launch):
     """launch(tile) -> output.  While tuning, time every admissible tile once on the real
     operands (HIP events) and keep the fastest for this geometry."""
-    cands = _tile_candidates(cout, key[1])
+    cands = _tile_candidates(cout, key[1], ksplit=TILES_KSPLIT and key[0] in ('conv', 'dual', 'deconv'))
     if _Tuner.active and key not in _Tuner.seen:
         _Tuner.seen.append(key)
     # (re)tune a geometry not in the table, or whose tuned tile is no longer a candidate (a plan

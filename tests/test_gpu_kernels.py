@@ -350,7 +350,8 @@ def test_conv2d_three_stage_ring_matches_torch(cuda, case):
     torch.testing.assert_close(got, ref, atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 23, 31, 32, 37])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 15, 16, 17, 18, 19, 20, 22, 23, 31, 33, 37,
+                                 39])
 @pytest.mark.parametrize('code', [F32, BF16, F16])
 def test_every_tile_configuration_matches_torch(cuda, cfg, code):
     """Each tile shape (incl. LDS rings above 64 KiB, eight-wave blocks, the single- /
@@ -368,7 +369,7 @@ def test_every_tile_configuration_matches_torch(cuda, cfg, code):
 def test_invalid_tile_is_refused(cuda):
     x = torch.zeros(1, 8, 8, 64, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 64, device=cuda, dtype=torch.bfloat16)
-    for bad in (39, 47, 29, 64, 70, 40 + 5):   # (7 / 15: the 128x128 eight-wave tiles since round 4)
+    for bad in (47, 29, 64, 70, 40 + 5):   # (7 / 15: the 128x128 eight-wave tiles since round 4; 39 round 5)
         with pytest.raises(RuntimeError, match='tile must be'):
             ops.conv2d_nhwc(x, w, 64, 1, 1, 1, 0, None, None, None, False, BF16, tile=bad)
 
@@ -582,3 +583,40 @@ def test_stem_pool_views_one_launch(cuda, size, nv, code, hflip):
     ulp = (2.0 ** -7 if code == BF16 else 2.0 ** -10) * ref.float().abs()
     assert bool((d <= 2 * ulp + 1e-3).all()), float(d.max())
     assert float((d > 0).float().mean()) < 0.05
+
+
+@pytest.mark.parametrize('code', [BF16, F16])
+def test_ksplit_tile_close_to_the_plain_tile(cuda, code):
+    """Tile 39 (two K groups of four waves, partial sums added in LDS): the same products as the
+    plain 128 x 128 tile, summed in another order -- outputs within a rounding step of it, every
+    epilogue path (residual, stride 2, deconv parity classes, the dual GEMM, ragged M, an odd
+    K-tile count)."""
+    dt = ops.torch_dtype(code)
+    g = torch.Generator(device=cuda).manual_seed(9)
+    sc = torch.rand(256, device=cuda, generator=g) + 0.5
+    sh = torch.randn(256, device=cuda, generator=g) * 0.1
+
+    def rnd(*shape, s=1.0):
+        return (torch.randn(*shape, device=cuda, generator=g) * s).to(dt)
+
+    x = rnd(5, 23, 19, 128)
+    res = rnd(5, 23, 19, 256)
+    w3 = rnd(256, 9 * 128, s=0.03)
+    x2 = rnd(5, 46, 38, 64)
+    wd = rnd(256, 128 + 64, s=0.05)   # K = 192: three K-tiles (the last pair half empty)
+    wdc = rnd(4, 256, 4 * 128, s=0.03)
+    outs = {}
+    for t in (3, 39):
+        outs[t] = [
+            ops.conv2d_nhwc(x, w3, 256, 3, 3, 1, 1, sc, sh, res, True, code, tile=t),
+            ops.conv2d_nhwc(x, w3[:, :128].contiguous(), 256, 1, 1, 2, 0, sc, sh, None, False, code, tile=t),
+            ops.deconv4x4s2_nhwc(x, wdc, 256, sc, sh, True, code, tile=t),
+            ops.conv1x1_dual_nhwc(x, x2, 2, wd, 256, sh, True, code, tile=t),
+        ]
+    torch.cuda.synchronize()
+    ulp = 2.0 ** (-7 if code == BF16 else -10)
+    for a, b in zip(outs[3], outs[39]):
+        a, b = a.float(), b.float()
+        d = (a - b).abs()
+        assert float(d.max()) <= 2 * ulp * float(a.abs().max()) + 1e-6
+        assert float((d > 0).float().mean()) < 0.1   # most outputs round identically

@@ -25,6 +25,8 @@ SHAPES = [
     ('l2 c2 3x3 32x32x128', 'conv', (128, 32, 32, 128), 128, 3),
     ('l3 c1 1x1 16x16x1024', 'conv', (128, 16, 16, 1024), 256, 1),
     ('l4 c3 1x1 8x8x512', 'conv', (128, 8, 8, 512), 2048, 1),
+    ('l4 c1 1x1 8x8x2048', 'conv', (128, 8, 8, 2048), 512, 1),
+    ('l3 c3 1x1 16x16x256', 'conv', (128, 16, 16, 256), 1024, 1),
 ]
 
 
