@@ -103,6 +103,8 @@ class _Tuner:
     active = False
     reps = 3
     seen = []   # geometry keys met by the current tuning run, in launch order
+    probe = None      # in-context stage: the geometry whose launches are bracketed by HIP events
+    probe_events = []
 
 
 def _tile_candidates(cout, code=None, ksplit=False):
@@ -157,6 +159,13 @@ def _tuned(key, cout, launch):
         _TUNE_CACHE[key] = min(cands, key=lambda t: (times[t], cands.index(t)))
         _TUNE_TIMES[key] = times
     t = _TUNE_CACHE.get(key, -1)
+    if _Tuner.probe is not None and key == _Tuner.probe:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = launch(t if t in cands else -1)
+        b.record()
+        _Tuner.probe_events.append((a, b))
+        return out
     return launch(t if t in cands else -1)
 
 
@@ -171,7 +180,7 @@ def tuning_times():
 
 
 def refine_times():
-    """The in-context stage's whole-forward times (geometry key -> {tile: ms per forward})."""
+    """The in-context stage's times (geometry key -> {tile: median ms of its launches inside a forward})."""
     return {k: dict(v) for k, v in _REFINE_TIMES.items()}
 
 
@@ -585,20 +594,26 @@ class PoseResNetPlan:
     def _refine_in_context(self, x, chunks, keep_features, within=0.25, top=3, forwards=6):
         """Second tuning stage: for every geometry of this forward whose best per-launch
         candidates lie within 25 % of each other, run the whole forward with each of its top
-        three and keep the one whose forward is shortest (best of two rounds of `forwards`
-        forwards, HIP events).  The per-launch trials run one launch back to back; inside the
-        network a launch follows other kernels at sustained clocks, and the ranking can differ:
-        layer4's 3x3 took 53 us on two tiles in isolation and 62 vs 75 us on them in the graph
-        (profiles/r04/replay_breakdown*.txt)."""
-        def forward_ms():
+        three and keep the one whose launches of that geometry took least INSIDE the forward
+        (HIP events around exactly those launches, median over two rounds of `forwards`
+        forwards).  The per-launch trials run one launch back to back; inside the network a
+        launch follows other kernels at sustained clocks, and the ranking can differ: layer4's
+        3x3 took 53 us on two tiles in isolation and 62 vs 75 us on them in the graph
+        (profiles/r04/replay_breakdown*.txt).  (Round 4 compared whole-forward times, whose
+        run-to-run spread -- ~0.5 % of 2.5 ms -- is as large as the differences it had to
+        resolve: deconv1 went to a tile 15 us slower in one tuning, profiles/r05.)"""
+        def forward_ms(key):
             self.run(x, chunks=chunks, keep_features=keep_features)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            for _ in range(forwards):
-                self.run(x, chunks=chunks, keep_features=keep_features)
-            b.record()
-            b.synchronize()
-            return a.elapsed_time(b) / forwards
+            torch.cuda.synchronize()
+            _Tuner.probe, _Tuner.probe_events = key, []
+            try:
+                for _ in range(forwards):
+                    self.run(x, chunks=chunks, keep_features=keep_features)
+                torch.cuda.synchronize()
+                ms = sorted(a.elapsed_time(b) for a, b in _Tuner.probe_events)
+            finally:
+                _Tuner.probe, _Tuner.probe_events = None, []
+            return ms[len(ms) // 2] if ms else float('inf')
         for key in list(_Tuner.seen):
             times = _TUNE_TIMES.get(key)
             if not times or key not in _TUNE_CACHE:
@@ -611,7 +626,7 @@ class PoseResNetPlan:
             for order in (cands, cands[::-1]):
                 for t in order:
                     _TUNE_CACHE[key] = t
-                    ms = forward_ms()
+                    ms = forward_ms(key)
                     res[t] = min(ms, res.get(t, ms))
             _TUNE_CACHE[key] = min(cands, key=lambda t: (res[t], cands.index(t)))
             _REFINE_TIMES[key] = res

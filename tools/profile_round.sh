@@ -14,7 +14,7 @@ OUT=${1:-gpurun_out/profile}
 COMMIT=${2:-unknown}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-COMMON="--no-cpu-baseline --no-mpjpe --fp32-steps 0 --train-steps 0 --c1-steps 0 --peaked-steps 0 --c4-steps 0 --control-steps 0 --tune-file $OUT/tiles.json"
+COMMON="--no-cpu-baseline --no-mpjpe --fp32-steps 0 --parity-steps 0 --train-steps 0 --c1-steps 0 --peaked-steps 0 --c4-steps 0 --control-steps 0 --tune-file $OUT/tiles.json"
 timeout -k 10 300 python3 bench.py $COMMON > "$OUT/tune_bench.log" 2>&1
 echo tuned
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/infer" -o run -- \
