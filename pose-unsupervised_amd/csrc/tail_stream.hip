@@ -23,6 +23,9 @@
 //        channel step c (p = 9 KT + KT nc + c).
 // MFMA operands swapped (A = weights, B = pixels): lane (r16, q) accumulates channels
 // 4q .. 4q+3 of pixel r16; v_permlane16_swap pairs the 2 n-tiles into 8 consecutive channels.
+#include <cstddef>
+#include <type_traits>
+
 #include "gemm_common.h"
 
 namespace posu {
@@ -98,11 +101,16 @@ struct TailCfg {
   static constexpr int kLdsAll = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
   // weight prefetch depth (k-steps); NEXT keeps a second accumulator set live, so its stream
   // runs POSU_TS_KD_NEXT deep
-  static constexpr int kDW = !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : (W == 32 && MT == 8) ? 1 : 2;
-  static constexpr int kNB = !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : (W == 32 && MT == 8) ? 1 : 2;
+  // (W = 24: nine m-tiles per wave, one fragment set and a two-deep stream -- 256 VGPRs, no
+  // spills; no chained W = 24 variant: its second accumulator set does not fit)
+  static constexpr int kDW = W == 24 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : (W == 32 && MT == 8) ? 1 : 2;
+  static constexpr int kNB = W == 24 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : (W == 32 && MT == 8) ? 1 : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
   static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % (16 * MT) == 0 && (16 * MT) % W == 0,
                 "every wave: 16 MT px (whole image rows) x 32 channels");
+  // W = 24 (R152@384's layer3, round 5): m-tiles straddle image rows -- m-tile i = 3 m + c holds
+  // tile pixels 48 m + 16 c .. (rows 2 m, 2 m + 1), three lane-address classes c
+  static_assert(W % 16 == 0 || (W == 24 && MT % 3 == 0 && kNPG == 1), "W a multiple of 16, or 24 in 3-m-tile periods");
   static_assert(kS3 + 2 * C * 4 <= kBN2, "t2 and BN3 fit over the window");
   static_assert(kLdsAll <= 160 * 1024, "LDS");
   static_assert(!NEXT || kChunk == P, "the next conv1 takes one y chunk per K slice of P channels");
@@ -115,6 +123,14 @@ struct TailCfg {
 // four per-block base registers plus compile-time offsets (no address arithmetic in the loop).
 template <int RowB>
 __device__ __forceinline__ int swzp(int pix, int key, int chunk) { return pix * RowB + ((chunk ^ key) << 4); }
+
+// swizzle key of the t1 window's pixel (window row wr, column wc): the column & 15 for W a multiple
+// of 16; for W = 24 the column plus 8 on odd rows, so the 16 lanes of an m-tile that straddles two
+// image rows (columns 16 .. 23 of one, 0 .. 7 of the next) still hit 16 distinct chunk slots
+template <int W>
+__device__ __forceinline__ int wkey(int wr, int wc) {
+  return W % 16 == 0 ? (wc & 15) : ((wc + 8 * (wr & 1)) & 15);
+}
 
 // waves per CU the four-m-tile variant is compiled for (A/B builds: 8 gives it 256 registers)
 #ifndef POSU_TS_MT4_WAVES
@@ -157,7 +173,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : POSU_TS_MT4_WAVES) / NW) vo
         const int pix = kPixPerInst * m + sub;
         const int wr = pix / K::kWinCols, wc = pix - wr * K::kWinCols;
         const int yy = y0 + wr - 1, xx = wc - 1;
-        const int lc = pc ^ (wc & 15);
+        const int lc = pc ^ wkey<W>(wr, wc);
         const bool ok = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < W;
         dma16(t1s, ok ? (((n * H + yy) * W + xx) * P + 8 * lc) * ES : kOOB, lds0 + static_cast<unsigned>(m) * 1024u);
       }
@@ -211,17 +227,36 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : POSU_TS_MT4_WAVES) / NW) vo
   // with `cols` pixels per row at 16-B chunk 4 d + q, swizzled by the lane's key (column & 15).
   // The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run (two register
   // sets); the scheduling barriers keep the compiler from hoisting more of them.
+  // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3)): four base
+  // pointers per (lane pixel, key), the k-step's 16 B at kb[d & 3] + (d & 4) * 64
+  auto bases = [&](const char* (&kb)[4], int base, int lpix, int key) {
+    const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) kb[k] = lb + ((k ^ (key >> 2)) << 6);
+  };
   auto block = [&](f32x4 (&acc)[MT][2], int blk, int base, int lpix, int key, auto coff) {
     constexpr int NB = K::kNB;  // pixel-fragment register sets
     uint4 b[NB][MT];
-    // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3))
-    const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
     const char* kb[4];
+    bases(kb, base, lpix, key);
+    // W = 24 window reads (conv2, coff = nullptr_t): m-tile i = 3 m + c reads from its class's
+    // bases at + 2 m window rows
+    const char* kc[3][4];
+    constexpr bool W24 = W % 16 != 0 && std::is_same<decltype(coff), std::nullptr_t>::value;
+    if constexpr (W24) {
+      const int dy = lpix, dx = key;   // (the W = 24 window call passes the tap here)
+      const int bb = r16 >= 8;
+      const int ro[3] = {0, bb, 1}, co[3] = {r16, 16 + r16 - 24 * bb, 8 + r16};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) kb[k] = lb + ((k ^ (key >> 2)) << 6);
+      for (int c = 0; c < 3; ++c)
+        bases(kc[c], base, (ro[c] + dy) * K::kWinCols + co[c] + dx, wkey<W>(ro[c] + dy, co[c] + dx));
+    }
     auto rd = [&](int i, int d) -> uint4 {
       if (kAbl & 4) return make_uint4(i, d, lane, blk);
-      return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d & 4) * 64);
+      if constexpr (W24)
+        return *reinterpret_cast<const uint4*>(kc[i % 3][d & 3] + (i / 3) * 2 * K::kWinCols * K::kRowB + (d & 4) * 64);
+      else
+        return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d & 4) * 64);
     };
 #pragma unroll
     for (int i = 0; i < MT; ++i) b[0][i] = rd(i, 0);
@@ -256,9 +291,13 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : POSU_TS_MT4_WAVES) / NW) vo
 #pragma unroll 1
   for (int t = 0; t < 9; ++t) {
     const int dy = t / 3, dx = t - 3 * (t / 3);
-    // window pixel of m-tile i: tile row (16 MT pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
-    block(acc, t, 0, ((16 * MT / W) * pg + dy) * K::kWinCols + r16 + dx, (r16 + dx) & 15,
-          [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
+    if constexpr (W % 16 != 0) {
+      block(acc, t, 0, dy, dx, nullptr);   // W = 24: per-class lane addresses (one pixel group)
+    } else {
+      // window pixel of m-tile i: tile row (16 MT pg + 16 i) / W + dy, column (16 i) % W + r16 + dx
+      block(acc, t, 0, ((16 * MT / W) * pg + dy) * K::kWinCols + r16 + dx, wkey<W>(0, r16 + dx),
+            [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
+    }
   }
   const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
   T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C;
@@ -394,8 +433,9 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   POSU_REQUIRE(!next || (s1n && b1n && t1n != y && t1n != x && t1n != t1),
                what + ": the next conv1 needs its BN and an output that aliases no other operand");
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
-  POSU_REQUIRE(l2 || l3, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16, C = 1024, "
-                                "planes = 256) of PoseResNet at 256x256");
+  const bool l3w = W == 24 && C == 1024 && P == 256;   // layer3 at 384x384 (R152 configs[4])
+  POSU_REQUIRE(l2 || l3 || l3w, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16 or 24, "
+                                       "C = 1024, planes = 256) of PoseResNet at 256x256 / 384x384");
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream)
@@ -404,7 +444,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
-  const int rows = l3 ? 8 : kL2Rows;
+  POSU_REQUIRE(!(l3w && next), what + ": no chained variant at W = 24 (run the tail and a conv1 launch)");
+  const int rows = l3 ? 8 : l3w ? 6 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
@@ -431,6 +472,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   if (l3) {
     if (next) launch_tail<16, 256, 1024, 8, 8, true>(dtype, g, s);
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
+  } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave
+    launch_tail<24, 256, 1024, 6, 8, false, 9>(dtype, g, s);
   } else {
     if (next) launch_tail<32, 128, 512, kL2Rows, kL2Waves, true, kL2MT>(dtype, g, s);
     else launch_tail<32, 128, 512, kL2Rows, kL2Waves, false, kL2MT>(dtype, g, s);

@@ -252,6 +252,9 @@ CHAINED_TAILS = True
 # layer2's strided tail chained with block 1's conv1 (posu_bottleneck_s2_tail_next_fwd, round 4;
 # under CHAINED_TAILS too)
 S2_CHAIN = True
+# layer3's identity Bottlenecks at W = 24 (R152@384, BASELINE configs[4]) as conv1 + the streamed
+# tail (round 5; not chained)
+TAIL_W24 = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -329,6 +332,8 @@ class _Block:
             return 'l2'
         if self.l3 and x.shape[2] == 16 and x.shape[1] % 8 == 0:
             return 'l3'
+        if self.l3 and x.shape[2] == 24 and x.shape[1] % 6 == 0 and TAIL_W24:   # R152@384 (configs[4])
+            return 'l3w'
         return None
 
     def run(self, x, code, out=None, t1=None):
@@ -348,7 +353,7 @@ class _Block:
         c1, c2, c3 = self.convs
         if t1 is None:
             t1 = c1(x, code)
-        if self.chain is not None and CHAINED_TAILS:
+        if self.chain is not None and CHAINED_TAILS and kind != 'l3w':   # (no chained tail at W = 24)
             n1 = self.chain
             return ops.bottleneck_tail_stream_next_nhwc(t1, x, self.wsn, c2.scale, c2.shift, c3.scale, c3.shift,
                                                         n1.scale, n1.shift, code, out=out)

@@ -119,10 +119,11 @@ def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precisio
         assert ours_sa.mean() < 4 * ref_sa.mean() + 1e-5
 
 
-def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda):
+def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda, monkeypatch):
     """configs[4]'s per-GPU pipeline at its per-GPU shape: R152 backbone at 384x384, fp16 compute,
     fp64 triangulation, 16 groups x 4 views, per-layer AUTOTUNED tiles, bench's replay path
-    (hipGraph, fused stem; layer1 unfused at 96x96 maps).
+    (hipGraph, fused stem; layer1 unfused at 96x96 maps; layer3's 35 identity blocks as conv1 + the
+    W = 24 streamed tail -- asserted taken).
       * oracle subset (CPU-feasible): groups 0-1 against the fp32 CPU oracle chain;
       * full size, property checks: every output finite; the device triangulation of all 16
         groups against the oracle's DLT on the same device joints (BASELINE's 1e-2 mm); the
@@ -136,8 +137,22 @@ def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda):
     net = get_pose_net(syn.make_cfg(num_layers=layers, image_size=size), is_train=False)
     sd = syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(layers, size),
                                   bn_stats=syn.load_bn_stats(layers, size))
+    from posu import ops, plan as P
+    calls = []
+    tail = ops.bottleneck_tail_stream_nhwc
+
+    def counted(t1, x, *a, **k):
+        calls.append(tuple(x.shape))
+        return tail(t1, x, *a, **k)
+    monkeypatch.setattr(ops, 'bottleneck_tail_stream_nhwc', counted)
+    # (the two-K-group tile 39 sums K in another order: kept out of this bit-for-bit batch
+    # invariance check)
+    monkeypatch.setattr(P, 'TILES_KSPLIT', False)
     full = _bench_plan_outputs(cuda, 'fp16', True, layers=layers, size=size, groups=groups)
+    n_full = sum(1 for c in calls if c == (64, 24, 24, 1024))
     small = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=sub)
+    # every eager forward of the plan runs layer3's 35 identity blocks on the W = 24 tail
+    assert n_full > 0 and n_full % 35 == 0, n_full
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
     # full size: triangulation and loss consistency of every group
     V, J = 4, full['coords0'].shape[2]

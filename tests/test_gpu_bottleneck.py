@@ -160,17 +160,20 @@ def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n,
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(2, 16), (1, 8), (3, 24), (128, 16)])
-def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h):
-    """Layer3's identity block tail (16-wide maps, 1024 channels, planes 256): conv2 + conv3
-    (+ residual) in one launch, bit-identical to the two unfused launches (conv_igemm's K order
-    per accumulator, same epilogue arithmetic) and within the dtype's tolerance of torch fp32."""
-    g = torch.Generator().manual_seed(71 + h)
+@pytest.mark.parametrize('n,h,w', [(2, 16, 16), (1, 8, 16), (3, 24, 16), (128, 16, 16),
+                                   (2, 24, 24), (1, 6, 24), (3, 18, 24), (64, 24, 24)])
+def test_fused_layer3_tail_matches_two_launches_and_torch(cuda, code, n, h, w):
+    """Layer3's identity block tail (16-wide maps at 256x256, 24-wide at 384x384 -- R152's 36
+    blocks, m-tiles straddling image rows --, 1024 channels, planes 256): conv2 + conv3 (+
+    residual) in one launch, bit-identical to the two unfused launches (conv_igemm's K order per
+    accumulator, same epilogue arithmetic) and within the dtype's tolerance of torch fp32.
+    (128, 16, 16) / (64, 24, 24): the production grids, against the launches only."""
+    g = torch.Generator().manual_seed(71 + h + w)
     w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=1024, p=256)
-    x = torch.randn(n, 1024, h, 16, generator=g)
+    x = torch.randn(n, 1024, h, w, generator=g)
     dt = ops.torch_dtype(code)
     xq = x.to(dt).float()
-    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 128 else None
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 64 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 1024, bk, dt)
