@@ -137,7 +137,7 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 #define POSU_TS_MT4_WAVES 12
 #endif
 template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
-__global__ __launch_bounds__(NW * 64, (MT == 8 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
+__global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
@@ -434,8 +434,9 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                what + ": the next conv1 needs its BN and an output that aliases no other operand");
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
   const bool l3w = W == 24 && C == 1024 && P == 256;   // layer3 at 384x384 (R152 configs[4])
-  POSU_REQUIRE(l2 || l3 || l3w, what + ": built for layer2 (W = 32, C = 512, planes = 128) and layer3 (W = 16 or 24, "
-                                       "C = 1024, planes = 256) of PoseResNet at 256x256 / 384x384");
+  const bool l2w = W == 48 && C == 512 && P == 128;    // layer2 at 384x384
+  POSU_REQUIRE(l2 || l3 || l3w || l2w, what + ": built for layer2 (W = 32 or 48, C = 512, planes = 128) and layer3 "
+                                              "(W = 16 or 24, C = 1024, planes = 256) of PoseResNet at 256x256 / 384x384");
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream)
@@ -445,7 +446,7 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
   POSU_REQUIRE(!(l3w && next), what + ": no chained variant at W = 24 (run the tail and a conv1 launch)");
-  const int rows = l3 ? 8 : l3w ? 6 : kL2Rows;
+  const int rows = l3 ? 8 : l3w ? 6 : l2w ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
@@ -474,6 +475,9 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
   } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave
     launch_tail<24, 256, 1024, 6, 8, false, 9>(dtype, g, s);
+  } else if (l2w) {   // 2 rows x 48 px = 96 px, 6 m-tiles per wave, 4 waves
+    if (next) launch_tail<48, 128, 512, 2, 4, true, 6>(dtype, g, s);
+    else launch_tail<48, 128, 512, 2, 4, false, 6>(dtype, g, s);
   } else {
     if (next) launch_tail<32, 128, 512, kL2Rows, kL2Waves, true, kL2MT>(dtype, g, s);
     else launch_tail<32, 128, 512, kL2Rows, kL2Waves, false, kL2MT>(dtype, g, s);

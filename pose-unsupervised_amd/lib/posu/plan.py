@@ -252,8 +252,8 @@ CHAINED_TAILS = True
 # layer2's strided tail chained with block 1's conv1 (posu_bottleneck_s2_tail_next_fwd, round 4;
 # under CHAINED_TAILS too)
 S2_CHAIN = True
-# layer3's identity Bottlenecks at W = 24 (R152@384, BASELINE configs[4]) as conv1 + the streamed
-# tail (round 5; not chained)
+# the identity Bottlenecks at 384x384 (R152, BASELINE configs[4]) as conv1 + the streamed tail
+# (round 5): layer3 at W = 24 (not chained), layer2 at W = 48 (chained)
 TAIL_W24 = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
@@ -334,6 +334,8 @@ class _Block:
             return 'l3'
         if self.l3 and x.shape[2] == 24 and x.shape[1] % 6 == 0 and TAIL_W24:   # R152@384 (configs[4])
             return 'l3w'
+        if self.l2 and x.shape[2] == 48 and x.shape[1] % 2 == 0 and TAIL_W24:   # layer2 at 384x384
+            return 'l2w'
         return None
 
     def run(self, x, code, out=None, t1=None):

@@ -123,18 +123,19 @@ def test_fused_first_bottleneck_matches_unfused_launches_and_torch(cuda, code, n
 
 
 @pytest.mark.parametrize('code', [BF16, F16])
-@pytest.mark.parametrize('n,h', [(2, 32), (1, 4), (3, 8), (1, 12), (128, 32), (1, 16)])
-def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n, h):
-    """Layer2's identity block (32-wide maps, 512 channels, planes 128) as conv1 + the
-    register-streamed tail (4-row tiles): bit-identical to the three unfused launches (same K
+@pytest.mark.parametrize('n,h,w', [(2, 32, 32), (1, 4, 32), (3, 8, 32), (1, 12, 32), (128, 32, 32), (1, 16, 32),
+                                   (2, 48, 48), (1, 2, 48), (3, 10, 48), (64, 48, 48)])
+def test_fused_layer2_bottleneck_matches_three_launches_and_torch(cuda, code, n, h, w):
+    """Layer2's identity block (32-wide maps at 256x256, 48-wide at 384x384; 512 channels, planes
+    128) as conv1 + the register-streamed tail (4-row / 2-row tiles): bit-identical to the three unfused launches (same K
     order per accumulator, same epilogue arithmetic) and within the dtype's tolerance of torch
     fp32."""
-    g = torch.Generator().manual_seed(41 + h)
+    g = torch.Generator().manual_seed(41 + h + w)
     w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=512, p=128)
-    x = torch.randn(n, 512, h, 32, generator=g)
+    x = torch.randn(n, 512, h, w, generator=g)
     dt = ops.torch_dtype(code)
     xq = x.to(dt).float()
-    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 128 else None
+    ref = _torch_block(xq, w1, bn1, w2, bn2, w3, bn3) if n < 64 else None
     bk = ops.conv_bk(code)
     xd = xq.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     p1 = packing.pack_conv_weight(w1.to(cuda), 512, bk, dt)
@@ -413,13 +414,14 @@ def test_plan_strided_tail_is_bit_identical_to_two_launches(cuda, precision):
 
 @pytest.mark.parametrize('code', [BF16, F16])
 @pytest.mark.parametrize('layer,n,h', [('layer3', 2, 16), ('layer3', 1, 8), ('layer3', 3, 24), ('layer3', 128, 16),
-                                       ('layer2', 2, 32), ('layer2', 1, 4), ('layer2', 3, 12), ('layer2', 128, 32)])
+                                       ('layer2', 2, 32), ('layer2', 1, 4), ('layer2', 3, 12), ('layer2', 128, 32),
+                                       ('layer2w', 2, 48), ('layer2w', 1, 2), ('layer2w', 3, 10), ('layer2w', 64, 48)])
 def test_chained_tail_matches_tail_and_next_conv1(cuda, code, layer, n, h):
     """Chained streamed tail (posu_bottleneck_tail_stream_next_fwd): block i's tail computing block
     i+1's conv1 + BN1 + ReLU over its output y.  y and t1n are bit-identical to the plain tail
     followed by a conv launch of the next conv1 over y (the same K order per accumulator); both
     outputs start as NaN sentinels, so a store that never lands fails."""
-    c, p, w = (1024, 256, 16) if layer == 'layer3' else (512, 128, 32)
+    c, p, w = {'layer3': (1024, 256, 16), 'layer2': (512, 128, 32), 'layer2w': (512, 128, 48)}[layer]
     g = torch.Generator().manual_seed(97 + h + n)
     w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
     w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5

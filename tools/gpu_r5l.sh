@@ -1,8 +1,8 @@
 #!/bin/bash
-OUT=gpurun_out/r5l
+OUT=gpurun_out/${1:-r5l}
 mkdir -p $OUT
 timeout -k 10 500 python -u -m pytest -x -v --timeout 300 --timeout-method thread -s tests/test_gpu_bottleneck.py \
-  -k "layer3_tail or refuses" tests/test_gpu_bench_config.py::test_r152_384_fp16_pipeline_matches_the_oracle_chain \
+  -k "layer3_tail or layer2_bottleneck or chained_tail or refuses" tests/test_gpu_bench_config.py::test_r152_384_fp16_pipeline_matches_the_oracle_chain \
   > $OUT/tests.log 2>&1
 rc=$?
 grep -E "passed|failed|FAIL|Error|R152|layer3 tail" $OUT/tests.log | tail -30
