@@ -104,7 +104,7 @@ def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
     hm_err = float((torch.stack(hm).detach().cpu() - hm_r.detach()).abs().max())
     print('peaked bf16 train step (fund_weight %g) vs oracle: heatmaps max %.3g, mse %.6g vs %.6g, fund %.6g vs %.6g, '
           'grad-norm rel median %.3g max %.3g (%s), cosine %.6f'
-          % (fund_weight, hm_err, mse.item(), mse_r.item(), float(fund), float(fund_r), np.median(rel), rel.max(),
+          % (fund_weight, hm_err, mse.item(), mse_r.item(), float(fund.detach()), float(fund_r.detach()), np.median(rel), rel.max(),
              names[int(rel.argmax())], cos))
     b = PEAKED_TRAIN_BF16[fund_weight > 0]
     assert hm_err < b['hm']
