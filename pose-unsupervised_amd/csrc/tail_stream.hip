@@ -401,6 +401,10 @@ void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
     hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT>), grid, dim3(NW * 64), 0, s, g);
 }
 
+// layer3's 4-row tiles below this many 8-row workgroups (A/B builds: 0 never, a large value always)
+#ifndef POSU_TS_L3_SMALL_GRID
+#define POSU_TS_L3_SMALL_GRID 256
+#endif
 // tiles: layer3 8 rows x 16 px with 8 waves (one workgroup per CU, 256 at batch 128); layer2
 // 4 rows x 32 px with 4 waves, two workgroups per CU, so one's conv3 epilogue (residual loads,
 // y stores) overlaps the other's MFMAs
@@ -446,7 +450,11 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
   POSU_REQUIRE(!(l3w && next), what + ": no chained variant at W = 24 (run the tail and a conv1 launch)");
-  const int rows = l3 ? 8 : l3w ? 6 : l2w ? 2 : kL2Rows;
+  // layer3 at W = 16: 8-row tiles (128 px, 8 m-tiles per wave) while they give every CU a
+  // workgroup, else 4-row tiles (64 px, 4 m-tiles per wave): at batch 64 (BASELINE configs[1]) the
+  // 8-row grid left half the CUs idle (128 workgroups)
+  const bool l3h = l3 && N > 0 && H % 4 == 0 && static_cast<long long>(N) * (H / 8) < POSU_TS_L3_SMALL_GRID;
+  const int rows = l3 ? (l3h ? 4 : 8) : l3w ? 6 : l2w ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
@@ -470,7 +478,10 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   g.b1n = b1n;
   g.t1n = t1n;
   hipStream_t s = as_stream(stream);
-  if (l3) {
+  if (l3h) {
+    if (next) launch_tail<16, 256, 1024, 4, 8, true, 4>(dtype, g, s);
+    else launch_tail<16, 256, 1024, 4, 8, false, 4>(dtype, g, s);
+  } else if (l3) {
     if (next) launch_tail<16, 256, 1024, 8, 8, true>(dtype, g, s);
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
   } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave
