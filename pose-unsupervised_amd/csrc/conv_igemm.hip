@@ -1513,8 +1513,9 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   bool sg = false, persist = false;
   bool wg4 = false;  // tile 15: the 4 x 2 wave grid of the 128x128 eight-wave tile
   bool ks = false;   // tile 39: the 128x128 tile with two K groups of four waves
+  bool w8 = false;   // SPL: tiles 7 / 15 as the unstaggered eight-wave 128x128 tile
   if (tile == 39) {
-    if (FAST2 && g.CoutPad % 128 == 0 && g.mode == 0 && !g.hm) {
+    if (sizeof(T) == 2 && g.CoutPad % 128 == 0 && g.mode == 0 && !g.hm) {
       cfg = 3;
       ks = true;
     }
@@ -1525,9 +1526,10 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       sg = true;
     }
   } else if (tile == 7 || tile == 15) {
-    if (FAST2 && g.CoutPad % 128 == 0) {
+    if (sizeof(T) == 2 && g.CoutPad % 128 == 0) {
       cfg = 7;
-      sg = true;
+      sg = FAST2;
+      w8 = SPL;
       wg4 = tile == 15;
     }
   } else if (tile >= 0) {
@@ -1549,6 +1551,20 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   g.ntiles = g.CoutPad / kBN[cfg];
   g.mtiles = (g.M + kBM[cfg] - 1) / kBM[cfg];
   const int nb = g.mtiles * g.ntiles * nclass;
+  if constexpr (SPL) {   // the split dtype's eight-wave 128x128 tiles: two K groups (39) or one (7 / 15)
+    if (ks) {
+      hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, false, false, true>), dim3(nb), dim3(512), 0,
+                         s, g);
+      return check_launch(what);
+    }
+    if (w8) {
+      if (wg4)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL>), dim3(nb), dim3(512), 0, s, g);
+      else
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL>), dim3(nb), dim3(512), 0, s, g);
+      return check_launch(what);
+    }
+  }
   if constexpr (FAST2) {
     if (persist) {
       switch (cfg) {

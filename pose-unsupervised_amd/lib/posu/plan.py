@@ -125,8 +125,10 @@ def _tile_candidates(cout, code=None, ksplit=False):
     sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 and TILES_128X8 else [])
     # (tile 32, the persistent 256x64 four-wave instance, is left out: it spills 928 B per lane to
     # scratch and took ~1.2 ms per launch in the tuning trials, 10x the other tiles)
-    if code == ops.F16X3:   # the split dtype: plain rings only (no stagger, no persistent stream)
-        return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5]
+    if code == ops.F16X3:   # the split dtype: plain rings only (no stagger, no persistent stream), the
+        # unstaggered eight-wave 128x128 tiles (7 / 15) and the two-K-group tile (39)
+        return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + (
+            [7, 15] + ([39] if ksplit else []) if cpad % 128 == 0 else [])
     if ksplit and code in (ops.BF16, ops.F16) and cpad % 128 == 0:
         sg = sg + [39]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg

@@ -31,7 +31,7 @@ def rel_err(got, ref, absref):
 
 @pytest.mark.parametrize('cin,cout,k,stride,n,hw', [(64, 128, 3, 1, 2, 16), (256, 64, 1, 1, 3, 8),
                                                     (128, 256, 3, 2, 2, 16), (32, 64, 1, 1, 1, 5)])
-@pytest.mark.parametrize('tile', [-1, 0, 3, 5, 9, 18])
+@pytest.mark.parametrize('tile', [-1, 0, 3, 5, 9, 18, 7, 15, 39])
 def test_split_conv_matches_fp64(cuda, cin, cout, k, stride, n, hw, tile):
     torch.manual_seed(cin + cout + k + tile)
     pad = k // 2
