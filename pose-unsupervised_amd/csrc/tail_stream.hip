@@ -301,12 +301,26 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
   }
   const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
   T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C;
+  // the tile's x / y (/ t1n) through buffer descriptors: a lane's 32-bit byte offset plus
+  // compile-time per-m-tile / per-chunk steps, instead of a 64-bit address per m-tile (the
+  // chained layer3 tail spilled such addresses: 34 VGPRs, round 4); stores keep soffset 0 (the
+  // store-data hazard)
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xg), 0, K::kPx * C * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yg, 0, K::kPx * C * ES, 0x00020000);
+  const int lane_xy = ((16 * MT * pg + r16) * C + 32 * cq + cpair) * ES;   // m-tile 0, chunk 0
   // conv3 chunk nc's residual in the epilogue's lane layout
   auto res_load = [&](int nc, uint4 (&rv)[MT]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
-      rv[i] = (kAbl & 72) ? make_uint4(i, c0, 0, 0) : *reinterpret_cast<const uint4*>(xg + tpix(i) * C + c0);
+    for (int i = 0; i < MT; ++i) {
+      if (kAbl & 72) {
+        rv[i] = make_uint4(i, c0, 0, 0);
+      } else {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, 0);
+        rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
   };
   // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
   lds_barrier();
@@ -352,7 +366,9 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       bn_relu(v, sc, sh, r);
       const uint4 o = O::store_vals(v);
       if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
-      else *reinterpret_cast<uint4*>(yg + tpix(i) * C + c0) = o;
+      else
+        __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, yrs,
+                                               lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, 0);
       // NEXT: the chunk's y, laid out like t2 ([pixel][P] rows, column-keyed swizzle)
       if constexpr (NEXT)
         *reinterpret_cast<uint4*>(smem + K::kYC + swzp<K::kRowB>(tpix(i), r16, (32 * cq + cpair) >> 3)) = o;
@@ -378,6 +394,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
   if constexpr (NEXT) {
     // t1n = relu(conv1n * s1n + b1n), this lane's 8 channels of each m-tile's pixel
     T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * P;
+    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(tg, 0, K::kPx * P * ES, 0x00020000);
     const int c0 = 32 * cq + cpair;
     float sc[8], sh[8];
     ld8(g.s1n + c0, sc);
@@ -387,7 +404,9 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       float v[8];
       pair(acc1, i, v);
       bn_relu(v, sc, sh, nullptr);
-      *reinterpret_cast<uint4*>(tg + tpix(i) * P + c0) = O::store_vals(v);
+      const uint4 o = O::store_vals(v);
+      __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, trs,
+                                             (tpix(i) * P + c0) * ES, 0, 0);
     }
   }
 }
