@@ -59,11 +59,10 @@ constexpr int kAbl = POSU_TS_ABLATE;
 #ifndef POSU_TS_KD
 #define POSU_TS_KD 4
 #endif
-// NEXT (chained) variant: weight prefetch depth and pixel-fragment register sets.  The second
-// accumulator set leaves no room for the plain tail's 4-deep stream and two fragment sets; per
-// layer the fastest spill-free-ish point measured (tools/chain_micro.py, profiles/r03/chain_r3s.txt:
-// layer2 kD 1 / one set 105.0 us (no spills) vs 110.9 (2 / two) vs 116.8 (2 / one) vs 128.6
-// (4 / one); layer3 kD 2 / two sets 76.3 us vs 77.0 (2 / one), 78.6 (1 / one), 95.9 (4 / one))
+// NEXT (chained) variant: weight prefetch depth and pixel-fragment register sets (0: the default
+// below).  Until round 4 the second accumulator set left no room for the plain tail's 4-deep stream
+// and two fragment sets (profiles/r03/chain_r3s.txt: layer2 kD 1 / one set, layer3 kD 2 / two sets,
+// the latter spilling 34 VGPRs); round 5's 32-bit buffer addressing freed the registers.
 #ifndef POSU_TS_KD_NEXT
 #define POSU_TS_KD_NEXT 0  // 0: per layer, as measured
 #endif
@@ -103,8 +102,11 @@ struct TailCfg {
   // runs POSU_TS_KD_NEXT deep
   // (W = 24: nine m-tiles per wave, one fragment set and a two-deep stream -- 256 VGPRs, no
   // spills; no chained W = 24 variant: its second accumulator set does not fit)
-  static constexpr int kDW = W == 24 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : (W == 32 && MT == 8) ? 1 : 2;
-  static constexpr int kNB = W == 24 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : (W == 32 && MT == 8) ? 1 : 2;
+  // (round 5: with x / y / t1n behind buffer descriptors the chained variants fit the plain tail's
+  // 4-deep stream and two fragment sets without spills -- network 2.3529 / 2.3514 vs 2.3991 / 2.3966
+  // ms with round 4's 1-deep / one set (layer2) and 2-deep / two sets (layer3), profiles/r05)
+  static constexpr int kDW = W == 24 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
+  static constexpr int kNB = W == 24 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
   static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % (16 * MT) == 0 && (16 * MT) % W == 0,
                 "every wave: 16 MT px (whole image rows) x 32 channels");
