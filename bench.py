@@ -951,6 +951,15 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
         if traffic:
             roof['traffic_source'] = dict(src, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per training step')
             roof['hbm_floor_ms'] = round(traffic / 6.3e12 * 1e3, 4)  # at the ~6.3 TB/s achievable
+        if (args.layers, args.size, args.precision) == (50, 256, 'bf16'):
+            # every tensor once per launch of the step's classes (posu/roofline.py); traffic /
+            # algorithmic = the step's over-fetch (batchnorm's four passes are in the floor: it
+            # prices the launch structure, the fusions are DESIGN.md's)
+            from posu import roofline as _rl
+            alg = _rl.r50_256_train_algorithmic_bytes(frames, 2)
+            roof['algorithmic_bytes'] = alg
+            if traffic and nb == 32:
+                roof['traffic_over_algorithmic'] = round(traffic / alg, 4)
     return {
         'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
         'steps': steps, 'warmup': warmup, 'ms_per_step': round(elapsed / steps * 1e3, 4),

@@ -70,3 +70,77 @@ def _prod(dims):
 
 def r50_256_algorithmic_bytes(n=128, es=2):
     return sum(r + w for _, r, w in r50_256_launches(n, es))
+
+
+# ---- the training step (bench.py --mode train / the train_mode leg): algorithmic bytes by class
+def r50_256_train_classes(n=128, es=2, joints=16):
+    """{class: (read_bytes, write_bytes)} of one training step of n frames (posu.train_plan's launch
+    classes): per conv + BatchNorm unit -- conv: x (a stride-2 1x1 only its stride-2 pixels) and the
+    packed weight read, z written; BN statistics: z read; BN apply: z (+ the residual) read, y
+    written; backward: BN partial sums and BN apply each read gy and z (+ y where the ReLU follows a
+    residual add), the apply writing dz (+ the residual branch's gradient); weight gradient: dz and x
+    read, the f32 weight gradient written; data gradient: dz and the packed weight read, dx written
+    (+ read where it accumulates into the identity branch's gradient).  Max-pool, the 1x1 head,
+    packing (f32 parameters read, forward + data-gradient packs written) and Adam (parameters,
+    gradients and both moments read, parameters and moments written) complete it.  Every tensor
+    once per launch: the floor the kernels' PMC traffic is compared with."""
+    cls = {k: [0, 0] for k in ('conv fwd / dgrad', 'conv wgrad', 'batchnorm', 'maxpool', 'weight packing',
+                                 'adam (torch)', 'heads / losses')}
+
+    def add(c, r, w):
+        cls[c][0] += r
+        cls[c][1] += w
+
+    act = lambda hw, c: n * hw * hw * c * es  # noqa: E731
+    nparam = [0]
+
+    def unit(hw_in, cin, hw_out, cout, k, stride, residual=False, want_gres=False, dx=True, dx_acc=False,
+             relu_after_res=False):
+        wts = cout * cin * k * k
+        nparam[0] += wts + 2 * cout
+        xin = act(hw_out, cin) if (k == 1 and stride == 2) else act(hw_in, cin)
+        z = act(hw_out, cout)
+        add('conv fwd / dgrad', xin + wts * es, z)                        # conv
+        add('batchnorm', z, 0)                                            # statistics
+        add('batchnorm', z + (z if residual else 0), z)                   # apply (+ residual)
+        extra = z if relu_after_res else 0                                # the mask read from y
+        add('batchnorm', 2 * z + extra, 0)                                # backward partial sums
+        add('batchnorm', 2 * z + extra, z + (z if want_gres else 0))      # backward apply
+        add('conv wgrad', z + xin, wts * 4)
+        if dx:
+            add('conv fwd / dgrad', z + wts * es + (act(hw_in, cin) if dx_acc else 0), act(hw_in, cin))
+        add('weight packing', wts * 4, wts * es * (2 if dx else 1))
+
+    # stem (direct 7x7 over the 8-channel packed input) + max-pool
+    unit(256, 8, 128, 64, 7, 2, dx=False)
+    add('maxpool', act(128, 64), act(64, 64))                            # forward
+    add('maxpool', act(128, 64) + act(64, 64), act(128, 64))             # backward (x, gy -> gx)
+    hw = 64
+    for blocks, planes, cin, cout, hw_in in _R50:
+        for b in range(blocks):
+            s = 2 if (hw_in != 64 or cin != 64) and b == 0 and planes != 64 else 1
+            ci = cin if b == 0 else cout
+            h_in = hw_in if b == 0 else hw
+            h_out = h_in // s
+            unit(h_in, ci, h_in, planes, 1, 1)                                   # conv1
+            unit(h_in, planes, h_out, planes, 3, s)                              # conv2
+            unit(h_out, planes, h_out, cout, 1, 1, residual=True, want_gres=True, relu_after_res=True)
+            if b == 0:
+                unit(h_in, ci, h_out, cout, 1, s, dx_acc=True)                   # downsample
+            hw = h_out
+    # deconvs (4 classes x 4 taps of the 4x4 kernel), BN + ReLU
+    for cin, h in ((2048, 8), (256, 16), (256, 32)):
+        unit(h, cin, 2 * h, 256, 4, 1)
+    # the 1x1 head: forward writes f32 heatmaps; backward its data / weight gradients
+    hm = n * joints * 64 * 64 * 4
+    add('heads / losses', act(64, 256) + 256 * joints * es, hm)
+    add('heads / losses', 3 * hm, hm)                                    # losses + their gradient
+    add('conv fwd / dgrad', hm + 256 * 64 * es, act(64, 256))
+    add('conv wgrad', hm + act(64, 256), 256 * joints * 4)
+    nparam[0] += 256 * joints + joints
+    add('adam (torch)', 4 * nparam[0] * 4, 3 * nparam[0] * 4)
+    return {k: tuple(v) for k, v in cls.items()}
+
+
+def r50_256_train_algorithmic_bytes(n=128, es=2):
+    return sum(r + w for r, w in r50_256_train_classes(n, es).values())
