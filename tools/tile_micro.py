@@ -1,7 +1,10 @@
 """Times conv tile configurations on the compute-heavy R50@256 batch-128 layer shapes (bf16,
 HIP events, min over rounds) and checks that loops with the same K order agree bit for bit.
 
-    python tools/tile_micro.py [--tiles 5,23,37] [--reps 10] [--rounds 3] [--lib PATH]
+    python tools/tile_micro.py [--tiles 5,23,37] [--reps 10] [--rounds 3] [--lib PATH] [--flush]
+
+--flush: every launch timed alone (its own HIP events) after a 512 MB write that evicts the L2s
+and the Infinity Cache, median over reps x rounds -- the cold-cache figure beside the warm one.
 """
 import argparse
 import os
@@ -30,6 +33,20 @@ SHAPES = [
 ]
 
 
+def timeit_cold(fn, reps, rounds, junk):
+    ts = []
+    for _ in range(reps * rounds):
+        junk.fill_(1.0)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def timeit(fn, reps, rounds):
     best = 1e9
     for _ in range(rounds):
@@ -52,6 +69,7 @@ def main():
     ap.add_argument('--reps', type=int, default=10)
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--only', default='', help='comma-separated substrings of the shape names to run')
+    ap.add_argument('--flush', action='store_true', help='cold caches: evict before every timed launch')
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(',')]
     if a.lib:
@@ -60,6 +78,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     dt = torch.bfloat16
     bk = ops.conv_bk(BF16)
+    junk = torch.empty(128 << 20, device=dev, dtype=torch.float32) if a.flush else None
     for name, kind, (n, h, w, cin), cout, k in SHAPES:
         if a.only and not any(o in name for o in a.only.split(',')):
             continue
@@ -85,7 +104,7 @@ def main():
             except RuntimeError as e:
                 line.append('%d: n/a' % t)
                 continue
-            us = timeit(lambda: fn(t), a.reps, a.rounds)
+            us = timeit_cold(lambda: fn(t), a.reps, a.rounds, junk) if a.flush else timeit(lambda: fn(t), a.reps, a.rounds)
             line.append('%d: %7.1f us %6.0f TF' % (t, us, flop / us / 1e6))
         torch.cuda.synchronize()
         ref = outs.get(tiles[0])
