@@ -33,10 +33,12 @@ SHAPES = [
 ]
 
 
-def timeit_cold(fn, reps, rounds, junk):
+def timeit_cold(fn, reps, rounds, junk, touch=()):
     ts = []
     for _ in range(reps * rounds):
         junk.fill_(1.0)
+        for t in touch:   # re-read after the eviction (torch reductions): which operand's fetch costs
+            t.sum(dtype=torch.float32)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         fn()
@@ -70,6 +72,8 @@ def main():
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--only', default='', help='comma-separated substrings of the shape names to run')
     ap.add_argument('--flush', action='store_true', help='cold caches: evict before every timed launch')
+    ap.add_argument('--touch', default='', choices=('', 'w', 'x', 'wx'),
+                    help='with --flush: re-read the weights (w), the input (x) or both after the eviction')
     a = ap.parse_args()
     tiles = [int(t) for t in a.tiles.split(',')]
     if a.lib:
@@ -104,7 +108,8 @@ def main():
             except RuntimeError as e:
                 line.append('%d: n/a' % t)
                 continue
-            us = timeit_cold(lambda: fn(t), a.reps, a.rounds, junk) if a.flush else timeit(lambda: fn(t), a.reps, a.rounds)
+            touch = [v for k, v in (('w', wk), ('x', x)) if k in a.touch]
+            us = timeit_cold(lambda: fn(t), a.reps, a.rounds, junk, touch) if a.flush else timeit(lambda: fn(t), a.reps, a.rounds)
             line.append('%d: %7.1f us %6.0f TF' % (t, us, flop / us / 1e6))
         torch.cuda.synchronize()
         ref = outs.get(tiles[0])
