@@ -129,7 +129,7 @@ def parse():
 # (round 5: the two-K-group tile 39 among the inference tile candidates)
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control leg compares the plans at the same numerics)
-CONTROL_FLAGS = ('TILES_KSPLIT',)
+CONTROL_FLAGS = ('TILES_KSPLIT', 'PREFETCH')
 
 
 def apply_plan_flags(flags):

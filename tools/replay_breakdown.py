@@ -7,7 +7,8 @@ the round-3 plan, one for all views since round 4) up to (not including) the nex
 kernel.  (The round-3 version restarted a replay at EVERY stem launch, so its breakdowns counted
 one of the four per-view stem launches of that plan.)  Prints, for the chosen replays, each launch's median duration (us)
 its gap to the previous launch's end (negative: overlap), with its kernel name, and the replay's launch-time sum and wall span (first start to last
-end: the sum plus the gaps between launches)."""
+end: the sum plus the gaps between launches).  The side-stream weight prefetches (prefetch_kernel,
+plan.PREFETCH) run beside the network's launches: they are listed apart, not in the sequence."""
 import argparse
 import csv
 import re
@@ -33,6 +34,8 @@ def main():
         for r in csv.DictReader(f):
             rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
     rows.sort()
+    pre = [r for r in rows if 'prefetch_kernel' in r[2]]
+    rows = [r for r in rows if 'prefetch_kernel' not in r[2]]
     replays, cur = [], None
     for s, e, n in rows:
         if st in n:
@@ -61,6 +64,12 @@ def main():
         print('%3d %9.1f us  gap %6.1f  %s' % (i, d, g, short(replays[0][i][2])))
     span = statistics.median((r[-1][1] - r[0][0]) / 1e3 for r in replays)
     print('sum of launches %.1f us, replay span %.1f us (gaps %.1f us)' % (tot, span, span - tot))
+    if pre:
+        a0, a1 = replays[0][0][0], replays[-1][-1][1]
+        inside = [r for r in pre if a0 <= r[0] <= a1]
+        if inside:
+            print('side-stream prefetches: %d launches per replay, %.1f us each on median (overlapped)'
+                  % (round(len(inside) / len(replays)), statistics.median((e - s) / 1e3 for s, e, _ in inside)))
 
 
 if __name__ == '__main__':
