@@ -118,15 +118,16 @@ def parse():
                     help='train mode: run the step on a high-priority stream (the weight-gradient side '
                          'stream keeps normal priority, so the data-gradient chain wins dispatch) or on '
                          'the default stream (default; measured equal: 21.82 vs 21.80 ms per step)')
-    ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=0|1',
-                    help='A/B runs: set a boolean switch of posu.plan / posu.train_plan (e.g. '
-                         'STREAMED_LAYER2_TAIL=0, FUSED_BN_STATS=0) before the plans are built')
+    ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=VALUE',
+                    help='A/B runs: set a boolean (0 / 1) or integer switch of posu.plan / posu.train_plan '
+                         '(e.g. S2_CHAIN=0, PREFETCH_WORKGROUPS=8) before the plans are built')
     return ap.parse_args()
 
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` leg times it in the same process, so a gain shows on the driver's own box
-# (round 5: the two-K-group tile 39 among the inference tile candidates)
+# (round 5: the two-K-group tile 39 among the inference tile candidates, the side-stream weight
+# prefetch)
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control leg compares the plans at the same numerics)
 CONTROL_FLAGS = ('TILES_KSPLIT', 'PREFETCH')
@@ -136,10 +137,18 @@ def apply_plan_flags(flags):
     from posu import plan as pl, train_plan as tpl
     for f in flags:
         name, _, val = f.partition('=')
-        mod = next((m for m in (pl, tpl) if isinstance(getattr(m, name, None), bool)), None)
-        if mod is None or val not in ('0', '1'):
-            raise SystemExit('--plan-flag %s: not a boolean switch of posu.plan / posu.train_plan' % f)
-        setattr(mod, name, val == '1')
+        mod = next((m for m in (pl, tpl) if isinstance(getattr(m, name, None), (bool, int))), None)
+        if mod is None:
+            raise SystemExit('--plan-flag %s: not a switch of posu.plan / posu.train_plan' % f)
+        if isinstance(getattr(mod, name), bool):
+            if val not in ('0', '1'):
+                raise SystemExit('--plan-flag %s: a boolean switch takes 0 or 1' % f)
+            setattr(mod, name, val == '1')
+        else:
+            try:
+                setattr(mod, name, int(val))
+            except ValueError:
+                raise SystemExit('--plan-flag %s: an integer switch takes an integer' % f) from None
 
 
 # ------------------------------------------------------------------ launcher

@@ -377,15 +377,17 @@ __global__ __launch_bounds__(256) void prefetch_kernel(const unsigned* __restric
 }  // namespace
 }  // namespace posu
 
-extern "C" int posu_prefetch(const void* p, long long bytes, void* stream) {
+extern "C" int posu_prefetch(const void* p, long long bytes, int max_workgroups, void* stream) {
   POSU_REQUIRE(p && bytes >= 0, "posu_prefetch: null pointer or negative size");
   POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, "posu_prefetch: the buffer must be 16-byte aligned");
   if (bytes == 0) return POSU_OK;
   POSU_REQUIRE(bytes >= 4, "posu_prefetch: buffers under 4 bytes are not prefetched");
   const long long n64 = (bytes - 4) / 64 + 1;   // the 64-B segments whose first dword lies inside
-  // 4 segments per thread and pass, at most 1024 workgroups
+  POSU_REQUIRE(max_workgroups >= 0, "posu_prefetch: negative workgroup cap");
+  // 4 segments per thread and pass, at most max_workgroups (0: 1024) workgroups
+  const long long cap = max_workgroups > 0 ? max_workgroups : 1024;
   const long long want = (n64 + 1023) / 1024;
-  const int grid = static_cast<int>(want < 1 ? 1 : (want > 1024 ? 1024 : want));
+  const int grid = static_cast<int>(want < 1 ? 1 : (want > cap ? cap : want));
   hipLaunchKernelGGL(prefetch_kernel, dim3(grid), dim3(256), 0, as_stream(stream), static_cast<const unsigned*>(p), n64);
   return check_launch("posu_prefetch");
 }

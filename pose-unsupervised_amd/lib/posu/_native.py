@@ -34,7 +34,7 @@ _d = ctypes.c_double
 _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
-    'posu_prefetch': [_p, _ll, _p],
+    'posu_prefetch': [_p, _ll, _i, _p],
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_pack_job_blocks': [_i, _i, _i, _i, _i, _i, _i, _i],
     'posu_pack_weights': [_i, _p, _i, _ll, _p],

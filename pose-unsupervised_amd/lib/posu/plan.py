@@ -97,6 +97,7 @@ TILES_KSPLIT = True
 # The side stream joins the caller's at the end of run(), so a captured forward stays one graph.
 PREFETCH = True
 PREFETCH_FROM_LAYER = 2   # layers[2:] (layer3, layer4) and the deconvs
+PREFETCH_WORKGROUPS = 32  # per prefetch launch: few, so the launch beside it keeps its CUs
 
 
 class _Prefetch:
@@ -116,7 +117,7 @@ class _Prefetch:
         side.wait_stream(main)   # after everything enqueued so far: runs beside the next launch
         with torch.cuda.stream(side):
             for t in tensors:
-                ops.prefetch(t)
+                ops.prefetch(t, PREFETCH_WORKGROUPS)
         cls.pending.add(side)
 
     @classmethod

@@ -353,3 +353,16 @@ def test_u2a_indices_and_mpjpe_follow_test_triangulate():
     pred_sel = pred_union[:, u, :]                     # read from the validate() h5 (already u-selected)
     st2 = mpjpe_stats(pred_sel, gt, u, a, pred_in_union_order=True)
     assert st2['mean'] == st['mean'] and np.array_equal(st2['per_joint'], norm)
+
+
+def test_bench_plan_flags_boolean_and_integer(monkeypatch):
+    """bench.py --plan-flag: booleans take 0 / 1, integer switches an integer; anything else exits."""
+    import bench
+    from posu import plan as P
+    monkeypatch.setattr(P, 'PREFETCH', True)
+    monkeypatch.setattr(P, 'PREFETCH_WORKGROUPS', 32)
+    bench.apply_plan_flags(['PREFETCH=0', 'PREFETCH_WORKGROUPS=8'])
+    assert P.PREFETCH is False and P.PREFETCH_WORKGROUPS == 8
+    for bad in ('PREFETCH=2', 'PREFETCH_WORKGROUPS=x', 'NO_SUCH_SWITCH=1'):
+        with pytest.raises(SystemExit):
+            bench.apply_plan_flags([bad])

@@ -15,7 +15,8 @@ def test_prefetch_sizes_and_refusals(cuda):
     buf = torch.arange(1 << 20, device=cuda, dtype=torch.int32)
     ref = buf.clone()
     for nbytes in (4, 60, 64, 68, 1000, 4096, (1 << 22) - 4, 1 << 22):
-        ops.prefetch(buf.view(torch.uint8)[:nbytes])
+        for wg in (0, 1, 7, 32):
+            ops.prefetch(buf.view(torch.uint8)[:nbytes], wg)
     ops.prefetch(buf[:0])   # empty: no launch
     torch.cuda.synchronize()
     assert torch.equal(buf, ref)   # nothing written
@@ -23,6 +24,8 @@ def test_prefetch_sizes_and_refusals(cuda):
         ops.prefetch(buf[1:])
     with pytest.raises(RuntimeError, match='under 4 bytes'):
         ops.prefetch(buf.view(torch.uint8)[:2])
+    with pytest.raises(RuntimeError, match='negative'):
+        ops.prefetch(buf, -1)
 
 
 def _net(cuda):

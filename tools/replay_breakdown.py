@@ -2,7 +2,7 @@
 
     python tools/replay_breakdown.py gpurun_out/prof/run_kernel_trace.csv [--last 5]
 
-A replay = the dispatches from the first of a run of stem_pool_kernel launches (one per view in
+A replay = the network kernels from the first of a run of stem_pool_kernel launches (one per view in
 the round-3 plan, one for all views since round 4) up to (not including) the next soft-argmax
 kernel.  (The round-3 version restarted a replay at EVERY stem launch, so its breakdowns counted
 one of the four per-view stem launches of that plan.)  Prints, for the chosen replays, each launch's median duration (us)
@@ -36,22 +36,28 @@ def main():
     rows.sort()
     pre = [r for r in rows if 'prefetch_kernel' in r[2]]
     rows = [r for r in rows if 'prefetch_kernel' not in r[2]]
+    # the network's own kernels only (the decode / loss / triangulation graph runs on another
+    # stream and may overlap the next replay); a replay starts at the first of a run of stem launches
+    net = ('conv_igemm_kernel', 'conv_persist_kernel', 'bottleneck', 'tail_stream_kernel', 'tail_s2_kernel',
+           'maxpool', 'pack_s2d_kernel', 'pack_kernel', 'pack_split_kernel', 'unpack', st)
+    rows = [r for r in rows if any(k in r[2] for k in net)]
     replays, cur = [], None
     for s, e, n in rows:
-        if st in n:
-            if cur is not None and len(cur) and all(st in c[2] for c in cur) and s - cur[-1][1] <= 20000:
-                cur.append((s, e, n))   # the next view's stem launch of the same replay
-            else:
-                cur = [(s, e, n)]
+        if st in n and (cur is None or st not in cur[-1][2]):
+            if cur is not None:
+                replays.append(cur)
+            cur = [(s, e, n)]
         elif cur is not None:
             if s - cur[-1][1] > 20000:   # a graph replay runs back to back: a gap ends it (incomplete)
                 cur = None
-            elif 'softargmax' in n:   # only complete replays (the configs1 leg has no soft-argmax)
-                replays.append(cur)
-                cur = None
             else:
                 cur.append((s, e, n))
-    replays = [r for r in replays if len(r) == len(replays[-1])][-a.last:]
+    if cur is not None:
+        replays.append(cur)
+    if replays:   # complete replays: the most common length
+        k = statistics.mode(len(r) for r in replays)
+        replays = [r for r in replays if len(r) == k]
+    replays = replays[-a.last:]
     if not replays:
         raise SystemExit('no replay found')
     k = len(replays[0])
