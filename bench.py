@@ -120,17 +120,16 @@ def parse():
                          'the default stream (default; measured equal: 21.82 vs 21.80 ms per step)')
     ap.add_argument('--plan-flag', action='append', default=[], metavar='NAME=VALUE',
                     help='A/B runs: set a boolean (0 / 1) or integer switch of posu.plan / posu.train_plan '
-                         '(e.g. S2_CHAIN=0, PREFETCH_WORKGROUPS=8) before the plans are built')
+                         '(e.g. S2_CHAIN=0, STEM_CIN_PAD=16) before the plans are built')
     return ap.parse_args()
 
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` leg times it in the same process, so a gain shows on the driver's own box
-# (round 5: the two-K-group tile 39 among the inference tile candidates, the side-stream weight
-# prefetch)
+# (round 5: the two-K-group tile 39 among the inference tile candidates)
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control leg compares the plans at the same numerics)
-CONTROL_FLAGS = ('TILES_KSPLIT', 'PREFETCH')
+CONTROL_FLAGS = ('TILES_KSPLIT',)
 
 
 def apply_plan_flags(flags):

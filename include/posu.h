@@ -64,15 +64,8 @@ const char* posu_last_error(void);
  * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
  * optional split-precision head (hw_lo); 12 the chained strided tail
  * (posu_bottleneck_s2_tail_next_fwd); 13 the split-fp16 dtype POSU_F16X3 (conv / dual / deconv /
- * deconv+head / head / pack / s2d pack / max-pool / unpack entry points); 14 the weight prefetch
- * (posu_prefetch).  The ctypes binding refuses a library of another revision. */
+ * deconv+head / head / pack / s2d pack / max-pool / unpack entry points).  The ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
-/* Touch every 64-B segment of `bytes` (16-B aligned, >= 4 B; 0 is a no-op) once through L2 and the
- * Infinity Cache, storing nothing, with at most max_workgroups 256-thread workgroups (0: 1024; few
- * workgroups leave the CUs to the launch it runs beside): the plan's side-stream prefetch of the
- * next block's weights (ABI 14; no reference counterpart -- a scheduling hint, results do not
- * depend on it). */
-int posu_prefetch(const void* p, long long bytes, int max_workgroups, void* stream);
 
 /* ------------------------------------------------------------ input prep */
 /* NCHW fp32 image batch -> NHWC activations with Cpad (>= C) channels,

@@ -356,38 +356,3 @@ extern "C" int posu_pack_view_rows(int dtype, const float* src, int V, int M, in
   POSU_REQUIRE(ok, "posu_pack_view_rows: unsupported dtype");
   return check_launch("posu_pack_view_rows");
 }
-
-// ---- weight prefetch: read a buffer once through the caches, keep nothing.  The plan issues it on
-// a side stream for the NEXT block's weights while the current block's first launch runs
-// (plan.PREFETCH): a launch whose weights come from HBM instead of the Infinity Cache runs up to
-// 10-15 us longer on layer4 (tools/tile_micro.py --flush --touch, profiles/r05).  One dword per 64-B
-// segment is loaded (the caches fill whole lines); each thread XORs its loads into a register that
-// an empty asm consumes, so the loads stay; nothing is stored.
-namespace posu {
-namespace {
-__global__ __launch_bounds__(256) void prefetch_kernel(const unsigned* __restrict__ p, long long n64) {
-  unsigned acc = 0;
-  const long long stride = static_cast<long long>(gridDim.x) * 256;
-  long long i = blockIdx.x * 256LL + threadIdx.x;
-  for (; i + 3 * stride < n64; i += 4 * stride)  // four loads in flight per thread
-    acc ^= p[16 * i] ^ p[16 * (i + stride)] ^ p[16 * (i + 2 * stride)] ^ p[16 * (i + 3 * stride)];
-  for (; i < n64; i += stride) acc ^= p[16 * i];
-  asm volatile("" ::"v"(acc));
-}
-}  // namespace
-}  // namespace posu
-
-extern "C" int posu_prefetch(const void* p, long long bytes, int max_workgroups, void* stream) {
-  POSU_REQUIRE(p && bytes >= 0, "posu_prefetch: null pointer or negative size");
-  POSU_REQUIRE((reinterpret_cast<size_t>(p) & 15) == 0, "posu_prefetch: the buffer must be 16-byte aligned");
-  if (bytes == 0) return POSU_OK;
-  POSU_REQUIRE(bytes >= 4, "posu_prefetch: buffers under 4 bytes are not prefetched");
-  const long long n64 = (bytes - 4) / 64 + 1;   // the 64-B segments whose first dword lies inside
-  POSU_REQUIRE(max_workgroups >= 0, "posu_prefetch: negative workgroup cap");
-  // 4 segments per thread and pass, at most max_workgroups (0: 1024) workgroups
-  const long long cap = max_workgroups > 0 ? max_workgroups : 1024;
-  const long long want = (n64 + 1023) / 1024;
-  const int grid = static_cast<int>(want < 1 ? 1 : (want > cap ? cap : want));
-  hipLaunchKernelGGL(prefetch_kernel, dim3(grid), dim3(256), 0, as_stream(stream), static_cast<const unsigned*>(p), n64);
-  return check_launch("posu_prefetch");
-}

@@ -18,7 +18,7 @@ F16 = 3
 F16X3 = 4   # split fp16 (hi + lo pairs, three MFMAs per product): include/posu.h
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 14
+ABI_VERSION = 13
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -34,7 +34,6 @@ _d = ctypes.c_double
 _SIGNATURES = {
     'posu_last_error': [],
     'posu_abi_version': [],
-    'posu_prefetch': [_p, _ll, _i, _p],
     'posu_pack_nchw_to_nhwc': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _p],
     'posu_pack_job_blocks': [_i, _i, _i, _i, _i, _i, _i, _i],
     'posu_pack_weights': [_i, _p, _i, _ll, _p],

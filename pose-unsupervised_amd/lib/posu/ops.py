@@ -265,14 +265,6 @@ def stem_pool(x, wpk, scale, shift, code, out=None, hflip=False):
     return out
 
 
-def prefetch(t, max_workgroups=0):
-    """Read a (16-B aligned, contiguous) tensor once through the caches on the current stream
-    (posu_prefetch, at most max_workgroups workgroups; 0: 1024): warms the Infinity Cache for a
-    launch that follows."""
-    if t.numel():
-        call('posu_prefetch', ptr(t), t.numel() * t.element_size(), int(max_workgroups), stream_of(t.device))
-
-
 def maxpool3x3s2_nhwc(x, code, out=None):
     n, h, w, c = x.shape
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1

@@ -90,44 +90,6 @@ TILES_128X8 = True
 # differs from the other tiles', and the training plan relies on every candidate summing alike)
 TILES_KSPLIT = True
 
-# the next block's (deconv's) weights read through the caches on a side stream while the current
-# block's first launch runs (posu_prefetch), from layer3 on: launches whose weights come from HBM
-# rather than the Infinity Cache ran 5-15 us longer (layer4 3x3: 59.4 vs 49.7 us with cold vs
-# warm weights, tools/tile_micro.py --flush --touch, profiles/r05/tile_cold_touch_r5v.txt).
-# The side stream joins the caller's at the end of run(), so a captured forward stays one graph.
-PREFETCH = True
-PREFETCH_FROM_LAYER = 2   # layers[2:] (layer3, layer4) and the deconvs
-PREFETCH_WORKGROUPS = 32  # per prefetch launch: few, so the launch beside it keeps its CUs
-
-
-class _Prefetch:
-    """The side stream per device and whether it has unjoined work."""
-    streams = {}
-    pending = set()
-
-    @classmethod
-    def issue(cls, tensors):
-        tensors = [t for t in tensors if t is not None]
-        if not PREFETCH or not tensors or not tensors[0].is_cuda:
-            return
-        main = torch.cuda.current_stream(tensors[0].device)
-        side = cls.streams.get(main.device)
-        if side is None:
-            side = cls.streams[main.device] = torch.cuda.Stream(main.device)
-        side.wait_stream(main)   # after everything enqueued so far: runs beside the next launch
-        with torch.cuda.stream(side):
-            for t in tensors:
-                ops.prefetch(t, PREFETCH_WORKGROUPS)
-        cls.pending.add(side)
-
-    @classmethod
-    def join(cls):
-        """The caller's stream (on each side stream's device) waits for the prefetches."""
-        for side in cls.pending:
-            torch.cuda.current_stream(side.device).wait_stream(side)
-        cls.pending.clear()
-
-
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
 _TUNE_CACHE = {}
@@ -364,16 +326,6 @@ class _Block:
             self.chain = nxt.convs[0]
             self.ws2n = pack_s2_tail_stream(self.convs[1].w, self.dual.w, self.chain.w)
 
-    def weights(self):
-        """Every packed weight tensor a launch of this block may read (the prefetch set)."""
-        ts = [c.w for c in self.convs] + [self.dual.w if self.dual is not None else None,
-                                         self.down.w if self.down is not None else None,
-                                         self.w1f, self.w3f, self.w3d]
-        # the streamed tails read the chained stream when they chain, else the plain one
-        ts += [self.wsn if self.wsn is not None and CHAINED_TAILS else self.wst,
-               self.ws2n if self.ws2n is not None and CHAINED_TAILS and S2_CHAIN else self.ws2]
-        return [t for t in ts if t is not None]
-
     def _tail_kind(self, x):
         """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
         if not FUSED_BOTTLENECK or not _fused_fits(x, self.cout):
@@ -600,15 +552,11 @@ class PoseResNetPlan:
         return x, x1
 
     @staticmethod
-    def _run_layer(layer, x, code, out=None, prefetch=False, after=()):
+    def _run_layer(layer, x, code, out=None):
         """The blocks of one layer in order (out: the last block's output buffer); chained
-        streamed tails hand the next block its conv1 output.  prefetch: before each block, the
-        next block's weights (after the last: `after`, the next layer's first unit's) go through
-        the caches on the side stream (PREFETCH)."""
+        streamed tails hand the next block its conv1 output."""
         t1 = None
         for bi, blk in enumerate(layer):
-            if prefetch:
-                _Prefetch.issue(layer[bi + 1].weights() if bi + 1 < len(layer) else list(after))
             x, t1 = blk.run(x, code, out=out if bi == len(layer) - 1 else None, t1=t1)
         if t1 is not None:
             raise RuntimeError('the last block of a layer produced a chained conv1 output')
@@ -629,8 +577,7 @@ class PoseResNetPlan:
     def _stage_late(self, x, hm_out=None, f_out=None, keep_f=True):
         """deconv2 .. last deconv -> head."""
         code = self.code
-        for i, dc in enumerate(self.deconvs[1:-1], 1):
-            _Prefetch.issue([self.deconvs[i + 1].w])
+        for dc in self.deconvs[1:-1]:
             x = dc(x, code)
         return self._last_deconv_head(x, keep_f, hm_out=hm_out, f_out=f_out)
 
@@ -701,32 +648,16 @@ class PoseResNetPlan:
         activations stay resident in the 256 MiB Infinity Cache between producer and
         consumer; layer3..deconv1 run on the whole batch.  keep_features=False skips
         materialising the full layer1 / deconv outputs (returned as None)."""
-        try:
-            return self._run(x, chunks, keep_features)
-        finally:
-            _Prefetch.join()
-
-    def _next_weights(self, li):
-        """The weights of the unit after layer li (the next layer's first block, or deconv1)."""
-        if li + 1 < len(self.layers):
-            return self.layers[li + 1][0].weights()
-        return [self.deconvs[0].w] if self.deconvs else []
-
-    def _run(self, x, chunks, keep_features):
         code = self.code
         n = x.shape[0]
-        pf = PREFETCH_FROM_LAYER
         if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
             x = self.stem_pool(x)
             x1 = None
             for li, layer in enumerate(self.layers):
-                if li == pf:   # the first prefetched unit's own weights, beside the previous launch
-                    _Prefetch.issue(layer[0].weights())
-                x = self._run_layer(layer, x, code, prefetch=li >= pf, after=self._next_weights(li))
+                x = self._run_layer(layer, x, code)
                 if li == 0:
                     x1 = x
-            for i, dc in enumerate(self.deconvs[:-1]):
-                _Prefetch.issue([self.deconvs[i + 1].w])
+            for dc in self.deconvs[:-1]:
                 x = dc(x, code)
             hm, f = self._last_deconv_head(x, keep_features)
             return hm, (x1 if keep_features else None), f
@@ -747,11 +678,8 @@ class PoseResNetPlan:
             sl = slice(k * c, (k + 1) * c)
             self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
         y = x2
-        for li, layer in enumerate(self.layers[2:], 2):
-            if li == pf:
-                _Prefetch.issue(layer[0].weights())
-            y = self._run_layer(layer, y, code, prefetch=li >= pf, after=self._next_weights(li))
-        _Prefetch.issue([self.deconvs[1].w])
+        for layer in self.layers[2:]:
+            y = self._run_layer(layer, y, code)
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _native.exported_symbols()
-    assert lib.posu_abi_version() == _native.ABI_VERSION == 14
+    assert lib.posu_abi_version() == _native.ABI_VERSION == 13
     assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
     assert lib.posu_conv_bk(_native.F16X3) == 64   # halves: 32 logical k per K-tile
 
@@ -359,10 +359,10 @@ def test_bench_plan_flags_boolean_and_integer(monkeypatch):
     """bench.py --plan-flag: booleans take 0 / 1, integer switches an integer; anything else exits."""
     import bench
     from posu import plan as P
-    monkeypatch.setattr(P, 'PREFETCH', True)
-    monkeypatch.setattr(P, 'PREFETCH_WORKGROUPS', 32)
-    bench.apply_plan_flags(['PREFETCH=0', 'PREFETCH_WORKGROUPS=8'])
-    assert P.PREFETCH is False and P.PREFETCH_WORKGROUPS == 8
-    for bad in ('PREFETCH=2', 'PREFETCH_WORKGROUPS=x', 'NO_SUCH_SWITCH=1'):
+    monkeypatch.setattr(P, 'S2_CHAIN', True)
+    monkeypatch.setattr(P, 'STEM_CIN_PAD', 8)
+    bench.apply_plan_flags(['S2_CHAIN=0', 'STEM_CIN_PAD=16'])
+    assert P.S2_CHAIN is False and P.STEM_CIN_PAD == 16
+    for bad in ('S2_CHAIN=2', 'STEM_CIN_PAD=x', 'NO_SUCH_SWITCH=1'):
         with pytest.raises(SystemExit):
             bench.apply_plan_flags([bad])
