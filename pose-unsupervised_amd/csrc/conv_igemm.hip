@@ -75,21 +75,11 @@ struct ConvGeom {
   long long wseg;    // the weight tensor's 64-B segments (all parity classes)
 };
 
-// Weight warm-up (round 5).  In the network a launch's weights come from HBM (the Infinity Cache
-// held the other layers' activations since the last forward), and every workgroup walks K in the
-// same order: all of them miss on the same weight K-tile at once, K-tile after K-tile.  Layer4's
-// 3x3 ran 59.4 us so against 49.7 us with its weights re-read beforehand (tools/tile_micro.py
-// --flush --touch, profiles/r05/tile_cold_touch_r5v.txt).  Here the first workgroups each load one
-// dword of a few distinct 64-B segments of the weights right before their first K-tile DMAs, so the
-// whole tensor is requested at once, at the start; the loaded values are discarded.  Nothing is
-// stored and no result depends on it.  (A side-stream prefetch launch inside the captured graph
-// lost: its launches serialised with the network's, profiles/r05/prefetch_ab_r5x.txt.)
-#ifndef POSU_IG_WARM
-#define POSU_IG_WARM 1
-#endif
-constexpr long long kWarmMinBytes = 1 << 20;   // smaller weight tensors are not warmed
-constexpr int kWarmWG = 512;                   // workgroups that take part (about one round of the grid)
-constexpr int kWarmLoads = 4;                  // segments per lane at most
+// Weight warm-up (round 5, gemm_common.h warm_issue): layer4's 3x3 ran 59.4 us with its weights
+// coming from HBM against 49.7 us with them re-read beforehand (tools/tile_micro.py --flush --touch,
+// profiles/r05/tile_cold_touch_r5v.txt); with the warm-up the network ran 2.355-2.363 vs
+// 2.405-2.413 ms (profiles/r05/weight_warmup_ab_r5y.txt).  (A side-stream prefetch launch inside
+// the captured graph lost: its launches serialised with the network's, prefetch_ab_r5x.txt.)
 
 template <int BM, int BN, int S>
 constexpr int ring_bytes() {
@@ -420,25 +410,11 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     }
   }
 
-  // weight warm-up: this workgroup's segments requested now, consumed (an empty asm) right after
-  // the first K-tile DMAs are issued
+  // weight warm-up: this workgroup's segments requested now, consumed right after the first
+  // K-tile DMAs are issued
   unsigned wv[kWarmLoads];
-#pragma unroll
-  for (int k = 0; k < kWarmLoads; ++k) wv[k] = 0;
-  const int nwarm = min(g.warm, nwg);
-  if (bid < nwarm) {
-    const unsigned* __restrict__ w32 = reinterpret_cast<const unsigned*>(g.w);
-    const long long s0 = static_cast<long long>(bid) * NT + tid, st = static_cast<long long>(nwarm) * NT;
-#pragma unroll
-    for (int k = 0; k < kWarmLoads; ++k)
-      if (s0 + k * st < g.wseg) wv[k] = w32[16 * (s0 + k * st)];
-  }
-  auto warm_done = [&] {
-    unsigned a = 0;
-#pragma unroll
-    for (int k = 0; k < kWarmLoads; ++k) a ^= wv[k];
-    asm volatile("" ::"v"(a));
-  };
+  warm_issue(wv, g.w, g.wseg, g.warm, NT);
+  auto warm_done = [&] { warm_use(wv); };
 
   // S-slot ring, DMA running S-1 K-tiles ahead; per K-tile one counted vmcnt (the
   // K-tile being consumed has landed, up to S-2 younger tiles stay in flight) and one
@@ -1517,7 +1493,7 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   constexpr bool FAST2 = sizeof(T) == 2 && !SPL;
   {
     const long long wbytes = static_cast<long long>(g.CoutPad) * g.Kpad * static_cast<long long>(sizeof(T)) * nclass;
-    g.warm = POSU_IG_WARM && wbytes >= kWarmMinBytes ? kWarmWG : 0;
+    g.warm = warm_wgs(wbytes);
     g.wseg = wbytes / 64;
   }
   if constexpr (sizeof(T) == 2 && !DUAL) {  // fused head on the eight-wave 256x256 tile, direct epilogue

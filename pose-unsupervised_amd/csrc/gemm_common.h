@@ -258,5 +258,48 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
   }
 }
 
+// ---- weight warm-up (round 5; conv_igemm.hip explains the measurement).  In the network a launch's
+// weights come from HBM, and every workgroup walks its weights in the same order, so all of them
+// miss on the same lines at once, step after step.  Workgroups 0 .. nwarm-1 instead each load one
+// dword of distinct 64-B segments of the whole tensor at their start (kWarmLoads per lane), so
+// every line is requested once, together, up front; warm_use() consumes the values (an empty asm)
+// after the launch's first operand loads are issued.  Loads only: nothing is stored, no result
+// depends on it.
+#ifndef POSU_WARM
+#define POSU_WARM 1
+#endif
+#ifndef POSU_WARM_MIN_KB
+#define POSU_WARM_MIN_KB 1024
+#endif
+constexpr long long kWarmMinBytes = POSU_WARM_MIN_KB * 1024LL;   // smaller weight tensors are not warmed
+constexpr int kWarmWG = 512;                   // workgroups that take part (about one round of a grid)
+constexpr int kWarmLoads = 4;                  // segments per lane at most
+
+// the warm-up's workgroup count for a weight tensor of `bytes` (0: none)
+inline int warm_wgs(long long bytes) { return POSU_WARM && bytes >= kWarmMinBytes ? kWarmWG : 0; }
+
+__device__ __forceinline__ void warm_issue(unsigned (&v)[kWarmLoads], const void* w, long long nseg, int nwarm,
+                                           int threads) {
+#pragma unroll
+  for (int k = 0; k < kWarmLoads; ++k) v[k] = 0;
+  const int bid = blockIdx.x;
+  nwarm = min(nwarm, static_cast<int>(gridDim.x));
+  if (bid < nwarm) {
+    const unsigned* __restrict__ w32 = reinterpret_cast<const unsigned*>(w);
+    const long long s0 = static_cast<long long>(bid) * threads + threadIdx.x;
+    const long long st = static_cast<long long>(nwarm) * threads;
+#pragma unroll
+    for (int k = 0; k < kWarmLoads; ++k)
+      if (s0 + k * st < nseg) v[k] = w32[16 * (s0 + k * st)];
+  }
+}
+
+__device__ __forceinline__ void warm_use(const unsigned (&v)[kWarmLoads]) {
+  unsigned a = 0;
+#pragma unroll
+  for (int k = 0; k < kWarmLoads; ++k) a ^= v[k];
+  asm volatile("" ::"v"(a));
+}
+
 }  // namespace
 }  // namespace posu

@@ -46,6 +46,8 @@ struct TailS2Geom {
   const float* s1n;
   const float* b1n;
   void* t1n;
+  long long wseg;  // the weight stream's 64-B segments (warm-up, gemm_common.h)
+  int warm;        // warm-up workgroups (0: none)
 };
 
 #ifndef POSU_S2_KD
@@ -133,7 +135,10 @@ __global__ __launch_bounds__(S2Cfg<NEXT>::kNW * 64, 2) void tail_s2_kernel(TailS
     wa[d][0] = *frag(d, 0);
     wa[d][1] = *frag(d, 1);
   }
+  unsigned wv[kWarmLoads];   // the stream's warm-up (gemm_common.h)
+  warm_issue(wv, g.wst, g.wseg, g.warm, K::kNW * 64);
   vm_wait<0>();  // the window (LDS-DMA) and the first fragments
+  warm_use(wv);
   lds_barrier();
 
   f32x4 acc[MT][2];
@@ -346,6 +351,8 @@ int s2_tail_impl(const char* name, int dtype, const void* t1, const void* x, int
   g.s1n = s1n;
   g.b1n = b1n;
   g.t1n = t1n;
+  g.wseg = wstream_bytes / 64;
+  g.warm = warm_wgs(wstream_bytes);
   const dim3 grid(static_cast<unsigned>(N * (H / 2 / K::kRows) * (K::kWout / K::kTW)));
   hipStream_t s = as_stream(stream);
   if (dtype == POSU_BF16) {

@@ -46,6 +46,8 @@ struct TailSGeom {
   const float* s1n;
   const float* b1n;
   void* t1n;
+  long long wseg;  // the weight stream's 64-B segments (warm-up, gemm_common.h)
+  int warm;        // warm-up workgroups (0: none)
 };
 
 // timing ablations (tools/tail_ablations.sh; never set in the product build, wrong results):
@@ -195,7 +197,10 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
     wa[d][0] = *frag(d, 0);
     wa[d][1] = *frag(d, 1);
   }
+  unsigned wv[kWarmLoads];   // the stream's warm-up (gemm_common.h): every line requested up front
+  warm_issue(wv, g.wst, g.wseg, g.warm, kThreads);
   vm_wait<0>();  // the window (LDS-DMA) and the first fragments
+  warm_use(wv);
   lds_barrier();
 
   f32x4 acc[MT][2];   // [m-tile i: tile pixels 16 MT pg + 16 i ..][n-tile j]
@@ -498,6 +503,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   g.s1n = s1n;
   g.b1n = b1n;
   g.t1n = t1n;
+  g.wseg = wstream_bytes / 64;
+  g.warm = warm_wgs(wstream_bytes);
   hipStream_t s = as_stream(stream);
   if (l3h) {
     if (next) launch_tail<16, 256, 1024, 4, 8, true, 4>(dtype, g, s);
