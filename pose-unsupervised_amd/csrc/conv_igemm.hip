@@ -1381,9 +1381,12 @@ __global__ __launch_bounds__(NW * 64) void conv_persist_kernel(ConvGeom g) {
   };
 
   zero_acc();
+  unsigned wv[kWarmLoads];   // weight warm-up (gemm_common.h), consumed after the first DMAs
+  warm_issue(wv, g.w, g.wseg, g.warm, NW * 64);
 #pragma unroll
   for (int sq = 0; sq < S - 1; ++sq)
     if (sq < total) dma_ktile(sq);
+  warm_use(wv);
   for (int sq = 0; sq < total; ++sq) {
     const bool tile_end = (sq + 1) % nk == 0;
     if (ares && tile_end) res_issue(sq / nk);

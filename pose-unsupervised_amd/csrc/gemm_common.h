@@ -269,7 +269,7 @@ __device__ __forceinline__ void vm_wait_dyn(int n) {
 #define POSU_WARM 1
 #endif
 #ifndef POSU_WARM_MIN_KB
-#define POSU_WARM_MIN_KB 1024
+#define POSU_WARM_MIN_KB 64
 #endif
 constexpr long long kWarmMinBytes = POSU_WARM_MIN_KB * 1024LL;   // smaller weight tensors are not warmed
 constexpr int kWarmWG = 512;                   // workgroups that take part (about one round of a grid)
