@@ -741,8 +741,10 @@ def infer_main(args):
             torch.cuda.empty_cache()
         t = run_training(args, dev, rank, world, dist, args.train_steps, 3)
         tr = {k: t[k] for k in ('value', 'unit', 'ms_per_step', 'loss', 'steps', 'warmup')}
-        tr.update(metric=TRAIN_METRIC, n_gpus=world, frac=t['roofline']['frac'] if t['roofline'] else None,
-                  traffic=t['roofline']['traffic'] if t['roofline'] else None,
+        roof = t['roofline'] or {}
+        tr.update(metric=TRAIN_METRIC, n_gpus=world, frac=roof.get('frac'), traffic=roof.get('traffic'),
+                  algorithmic_bytes=roof.get('algorithmic_bytes'),
+                  traffic_over_algorithmic=roof.get('traffic_over_algorithmic'),
                   parallelism=t['config']['parallelism'], workload=t['config']['workload'],
                   optimizer=t['config']['optimizer'])
         return tr
