@@ -64,7 +64,10 @@ const char* posu_last_error(void);
  * one-launch multi-view stem (posu_stem_pool_views_fwd) added, the fused deconv+head takes an
  * optional split-precision head (hw_lo); 12 the chained strided tail
  * (posu_bottleneck_s2_tail_next_fwd); 13 the split-fp16 dtype POSU_F16X3 (conv / dual / deconv /
- * deconv+head / head / pack / s2d pack / max-pool / unpack entry points).  The ctypes binding refuses a library of another revision. */
+ * deconv+head / head / pack / s2d pack / max-pool / unpack entry points); 14 (training) the ReLU
+ * bit mask (posu_bn_apply_mask / posu_bn_train_bwd_mask) and the fused stem BN + ReLU + max-pool
+ * with stored argmax taps (posu_bn_relu_maxpool3x3s2_fwd / posu_maxpool3x3s2_bwd_idx).  The
+ * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
 /* ------------------------------------------------------------ input prep */
@@ -521,6 +524,18 @@ int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const float* rel
                       int C, const float* mean, const float* rstd, const float* gamma,
                       float* dgamma, float* dbeta, void* dz, void* gres, void* workspace,
                       long long workspace_bytes, void* stream);
+/* ABI 14: the residual Bottleneck output's ReLU mask as bits.  posu_bn_apply_mask = posu_bn_apply
+ * with relu = 1 that also writes mask [nseg*Pseg*C/E] bytes (E = 8 for BF16 / F16, 4 for F32:
+ * one byte per 16-B chunk, bit e = [y_e > 0] of the stored y); posu_bn_train_bwd_mask =
+ * posu_bn_train_bwd reading that mask instead of y (16x fewer bytes than y, read twice per
+ * backward).  Replaces the reference's autograd ReLU / BatchNorm2d backward
+ * (lib/models/pose_resnet.py:92-97), results identical to the y-masked path. */
+int posu_bn_apply_mask(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                       const float* shift, const void* residual, void* y, void* mask, void* stream);
+int posu_bn_train_bwd_mask(int dtype, const void* gy, const void* mask, const void* z, int nseg,
+                           int Pseg, int C, const float* mean, const float* rstd,
+                           const float* gamma, float* dgamma, float* dbeta, void* dz, void* gres,
+                           void* workspace, long long workspace_bytes, void* stream);
 /* out[c] = sum_p x[p][c] (f32), e.g. the final layer's bias gradient;
  * workspace >= posu_bn_workspace(1, C). */
 int posu_channel_sum(int dtype, const void* x, int P, int C, float* out, void* workspace,
@@ -530,6 +545,17 @@ int posu_channel_sum(int dtype, const void* x, int P, int C, float* out, void* w
 long long posu_maxpool3x3s2_bwd_workspace(int N, int H, int W, int C);
 int posu_maxpool3x3s2_bwd(int dtype, const void* x, int N, int H, int W, int C, const void* gy,
                           void* gx, void* workspace, long long workspace_bytes, void* stream);
+/* ABI 14, the training stem (lib/models/pose_resnet.py:192-195: bn1, relu, maxpool): from the
+ * raw conv output z [N,H,W,C] (N = nseg equal segments) and posu_bn_train_fwd's scale/shift,
+ * y [N,Ho,Wo,C] = maxpool3x3s2(relu(z*scale[seg] + shift[seg]) rounded to dtype) and idx
+ * [N,Ho,Wo,C] bytes = the argmax tap 0..8 (first maximum in window order) -- the activation
+ * itself is never written.  posu_maxpool3x3s2_bwd_idx: gx [N,H,W,C] from those taps and gy
+ * [N,Ho,Wo,C]; identical to posu_maxpool3x3s2_bwd over the activation. */
+int posu_bn_relu_maxpool3x3s2_fwd(int dtype, const void* z, int nseg, int N, int H, int W, int C,
+                                  const float* scale, const float* shift, void* y, void* idx,
+                                  void* stream);
+int posu_maxpool3x3s2_bwd_idx(int dtype, const void* idx, const void* gy, int N, int H, int W,
+                              int C, void* gx, void* stream);
 
 #ifdef __cplusplus
 }

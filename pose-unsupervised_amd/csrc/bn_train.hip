@@ -53,7 +53,9 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
 //         segment's first pixel when kout is non-null (shifted sums: a channel whose
 //         mean is large against its spread keeps its variance in the f32 partials),
 //         else 0.  Block 0 of each segment stores K to kout [nseg][C].
-// MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0] (y optional)
+// MODE 1: (sum g', sum g' * xhat)     -- backward, g' = gy * [y > 0]: the ReLU mask from the
+//         forward's bit mask (ym, one byte per 16-B chunk, bn_apply_mask), from y, or recomputed
+//         from z (msc / msh); none of them: no ReLU
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z, const T* __restrict__ gy,
                                                          const T* __restrict__ y, const float* __restrict__ msc,
@@ -61,7 +63,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
                                                          const float* __restrict__ mean,
                                                          const float* __restrict__ rstd, int Pseg, int C,
                                                          RedShape rs, double* __restrict__ part,
-                                                         float* __restrict__ kout) {
+                                                         float* __restrict__ kout, const uint8_t* __restrict__ ym) {
   constexpr int E = Vec<T>::E;
   __shared__ double red[2][256][E];
   const int tid = threadIdx.x;
@@ -104,7 +106,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
     const int pbeg = blk * rs.PPB, pend = min(Pseg, pbeg + rs.PPB);
     const size_t sbase = static_cast<size_t>(seg) * Pseg * C + ch * E;
     // one pixel's contribution, accumulated in pixel order (the sums do not depend on U)
-    auto acc = [&](const uint4& zq, const uint4& gq, const uint4& yq) {
+    auto acc = [&](const uint4& zq, const uint4& gq, const uint4& yq, unsigned mq) {
       float v[E];
       Vec<T>::unpack(zq, v);
       if constexpr (MODE == 0) {
@@ -117,7 +119,10 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
       } else {
         float gv[E];
         Vec<T>::unpack(gq, gv);
-        if (y) {
+        if (ym) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) gv[e] = (mq >> e) & 1u ? gv[e] : 0.f;
+        } else if (y) {
           float yv[E];
           Vec<T>::unpack(yq, yv);
 #pragma unroll
@@ -139,20 +144,22 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
     int p = pbeg + pl;
     for (; p + (U - 1) * rs.PL < pend; p += U * rs.PL) {
       uint4 zq[U], gq[U], yq[U];
+      unsigned mq[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const size_t off = sbase + static_cast<size_t>(p + u * rs.PL) * C;
         zq[u] = *reinterpret_cast<const uint4*>(z + off);
         gq[u] = MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero;
-        yq[u] = MODE == 1 && y ? *reinterpret_cast<const uint4*>(y + off) : zero;
+        yq[u] = MODE == 1 && y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero;
+        mq[u] = MODE == 1 && ym ? ym[off / E] : 0u;
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) acc(zq[u], gq[u], yq[u]);
+      for (int u = 0; u < U; ++u) acc(zq[u], gq[u], yq[u], mq[u]);
     }
     for (; p < pend; p += rs.PL) {
       const size_t off = sbase + static_cast<size_t>(p) * C;
       acc(*reinterpret_cast<const uint4*>(z + off), MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero,
-          MODE == 1 && y ? *reinterpret_cast<const uint4*>(y + off) : zero);
+          MODE == 1 && y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero, MODE == 1 && ym ? ym[off / E] : 0u);
     }
   }
 #pragma unroll
@@ -271,12 +278,22 @@ __global__ __launch_bounds__(256) void bn_stats_finalize_kernel(const double* __
   }
 }
 
-// y = act(z * scale[seg] + shift[seg] (+ res)), one thread per 16-B chunk
+// y = act(z * scale[seg] + shift[seg] (+ res)), one thread per 16-B chunk; mask (optional, ReLU
+// only): one byte per chunk, bit e = [y_e > 0] -- the backward's ReLU mask at 1/16 of y's bytes
+template <typename T>
+__device__ __forceinline__ uint8_t pos_bits(const float* v) {
+  unsigned m = 0;
+#pragma unroll
+  for (int e = 0; e < Vec<T>::E; ++e) m |= (v[e] > 0.f ? 1u : 0u) << e;
+  return static_cast<uint8_t>(m);
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ z, int Pseg, int C,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, const T* __restrict__ res,
-                                                       int relu, T* __restrict__ y, long long total) {
+                                                       int relu, T* __restrict__ y, long long total,
+                                                       uint8_t* __restrict__ mask) {
   constexpr int E = Vec<T>::E;
   const int CPR = C / E;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
@@ -293,7 +310,12 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ z, 
       if (res) t += r[e];
       v[e] = relu ? fmaxf(t, 0.f) : t;
     }
-    *reinterpret_cast<uint4*>(y + i * E) = Vec<T>::pack(v);
+    const uint4 o = Vec<T>::pack(v);
+    *reinterpret_cast<uint4*>(y + i * E) = o;
+    if (mask) {
+      Vec<T>::unpack(o, v);   // the stored (rounded) values: the mask the backward would read from y
+      mask[i] = pos_bits<T>(v);
+    }
   }
 }
 
@@ -321,7 +343,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void bn_apply_seg_kernel(const T* __restrict__ z, int Pseg, int C,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
-                                                           const T* __restrict__ res, int relu, T* __restrict__ y) {
+                                                           const T* __restrict__ res, int relu, T* __restrict__ y,
+                                                           uint8_t* __restrict__ mask) {
   constexpr int E = Vec<T>::E, U = kSegU;
   const int CPR = C / E, seg = blockIdx.y;
   const int c0 = (threadIdx.x % CPR) * E;
@@ -332,6 +355,7 @@ __global__ __launch_bounds__(256) void bn_apply_seg_kernel(const T* __restrict__
   const T* __restrict__ zs = z + static_cast<size_t>(seg) * Pseg * C;
   const T* __restrict__ rs = res ? res + static_cast<size_t>(seg) * Pseg * C : nullptr;
   T* __restrict__ ys = y + static_cast<size_t>(seg) * Pseg * C;
+  uint8_t* __restrict__ ms = mask ? mask + static_cast<size_t>(seg) * Pseg * CPR : nullptr;
   auto one = [&](int i, const uint4& zq, const uint4& rq) {
     float v[E], r[E];
     Vec<T>::unpack(zq, v);
@@ -342,7 +366,12 @@ __global__ __launch_bounds__(256) void bn_apply_seg_kernel(const T* __restrict__
       if (rs) t += r[e];
       v[e] = relu ? fmaxf(t, 0.f) : t;
     }
-    *reinterpret_cast<uint4*>(ys + static_cast<size_t>(i) * E) = Vec<T>::pack(v);
+    const uint4 o = Vec<T>::pack(v);
+    *reinterpret_cast<uint4*>(ys + static_cast<size_t>(i) * E) = o;
+    if (ms) {
+      Vec<T>::unpack(o, v);
+      ms[i] = pos_bits<T>(v);
+    }
   };
   const uint4 zero = make_uint4(0, 0, 0, 0);
   int i = blockIdx.x * 256 + threadIdx.x;
@@ -369,7 +398,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ rstd,
                                                                const float* __restrict__ coef, T* __restrict__ dz,
-                                                               T* __restrict__ gres) {
+                                                               T* __restrict__ gres, const uint8_t* __restrict__ ym) {
   constexpr int E = Vec<T>::E, U = kSegU;
   const int CPR = C / E, seg = blockIdx.y;
   const int c0 = (threadIdx.x % CPR) * E;
@@ -388,12 +417,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
   }
   const int n = Pseg * CPR, stride = gridDim.x * 256;
   const size_t sb = static_cast<size_t>(seg) * Pseg * C;
-  auto one = [&](int i, const uint4& gq, const uint4& zq, const uint4& yq) {
+  auto one = [&](int i, const uint4& gq, const uint4& zq, const uint4& yq, unsigned mq) {
     const size_t off = sb + static_cast<size_t>(i) * E;
     float g[E], v[E];
     Vec<T>::unpack(gq, g);
     Vec<T>::unpack(zq, v);
-    if (y) {
+    if (ym) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = (mq >> e) & 1u ? g[e] : 0.f;
+    } else if (y) {
       float yv[E];
       Vec<T>::unpack(yq, yv);
 #pragma unroll
@@ -414,20 +446,22 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
   int i = blockIdx.x * 256 + threadIdx.x;
   for (; i + (U - 1) * stride < n; i += U * stride) {
     uint4 gq[U], zq[U], yq[U];
+    unsigned mq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t off = sb + static_cast<size_t>(i + u * stride) * E;
       gq[u] = *reinterpret_cast<const uint4*>(gy + off);
       zq[u] = *reinterpret_cast<const uint4*>(z + off);
-      yq[u] = y ? *reinterpret_cast<const uint4*>(y + off) : zero;
+      yq[u] = y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero;
+      mq[u] = ym ? ym[off / E] : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < U; ++u) one(i + u * stride, gq[u], zq[u], yq[u]);
+    for (int u = 0; u < U; ++u) one(i + u * stride, gq[u], zq[u], yq[u], mq[u]);
   }
   for (; i < n; i += stride) {
     const size_t off = sb + static_cast<size_t>(i) * E;
     one(i, *reinterpret_cast<const uint4*>(gy + off), *reinterpret_cast<const uint4*>(z + off),
-        y ? *reinterpret_cast<const uint4*>(y + off) : zero);
+        y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero, ym ? ym[off / E] : 0u);
   }
 }
 
@@ -498,7 +532,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ mean,
                                                            const float* __restrict__ rstd,
                                                            const float* __restrict__ coef, T* __restrict__ dz,
-                                                           T* __restrict__ gres, long long total) {
+                                                           T* __restrict__ gres, long long total,
+                                                           const uint8_t* __restrict__ ym) {
   constexpr int E = Vec<T>::E;
   const int CPR = C / E;
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
@@ -508,7 +543,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     float g[E], v[E];
     Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + i * E), g);
     Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + i * E), v);
-    if (y) {
+    if (ym) {
+      const unsigned mq = ym[i];
+#pragma unroll
+      for (int e = 0; e < E; ++e) g[e] = (mq >> e) & 1u ? g[e] : 0.f;
+    } else if (y) {
       float yv[E];
       Vec<T>::unpack(*reinterpret_cast<const uint4*>(y + i * E), yv);
 #pragma unroll
@@ -621,6 +660,65 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint8_t* __restr
   }
 }
 
+// Training stem (round 5): a = relu(z * scale[seg] + shift[seg]) rounded to the dtype, its 3x3 /
+// s2 / p1 max-pool (maxpool_kernel's fmaxf over the window) and the argmax tap per output element
+// (maxpool_argmax_kernel's rule: the first maximum in window scan order, NaN taken) in one pass
+// over z, without writing a: the backward takes the taps (maxpool_bwd_kernel) and its ReLU mask
+// from z.  Replaces bn_apply + maxpool + the backward's argmax pass (1.17 GB -> 0.37 GB per step
+// at the training stem's 128 x 128 x 128 x 64).
+template <typename T>
+__global__ __launch_bounds__(256) void bn_relu_maxpool_kernel(const T* __restrict__ z, int N, int nimg, int H, int W,
+                                                              int C, int Ho, int Wo, const float* __restrict__ scale,
+                                                              const float* __restrict__ shift, T* __restrict__ y,
+                                                              uint8_t* __restrict__ idx) {
+  constexpr int E = Vec<T>::E;
+  const int chunks = C / E;
+  const long long total = static_cast<long long>(N) * Ho * Wo * chunks;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
+    const int ch = static_cast<int>(i % chunks);
+    const long long pix = i / chunks;
+    const int ox = static_cast<int>(pix % Wo);
+    const long long t = pix / Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const long long n = t / Ho;
+    const int seg = static_cast<int>(n / nimg);
+    float sc[E], sh[E], m[E], bm[E];
+    int am[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      sc[e] = scale[seg * C + ch * E + e];
+      sh[e] = shift[seg * C + ch * E + e];
+      m[e] = -INFINITY;
+      bm[e] = 0.f;
+      am[e] = -1;
+    }
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap - 3 * dy;
+      const int iy = oy * 2 - 1 + dy, ix = ox * 2 - 1 + dx;
+      if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+      float v[E];
+      Vec<T>::unpack(*reinterpret_cast<const uint4*>(z + ((n * H + iy) * W + ix) * C + ch * E), v);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float tv = v[e] * sc[e] + sh[e];   // bn_apply's expression
+        v[e] = fmaxf(tv, 0.f);
+      }
+      Vec<T>::unpack(Vec<T>::pack(v), v);        // rounded like the stored activation
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        m[e] = fmaxf(m[e], v[e]);
+        const bool take = am[e] < 0 || v[e] > bm[e] || v[e] != v[e];
+        bm[e] = take ? v[e] : bm[e];
+        am[e] = take ? tap : am[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(y + pix * C + ch * E) = Vec<T>::pack(m);
+    uint8_t* dst = idx + pix * C + ch * E;
+#pragma unroll
+    for (int e = 0; e < E; ++e) dst[e] = static_cast<uint8_t>(am[e]);
+  }
+}
+
 inline int grid_for(long long total) {
   long long g = (total + 255) / 256;
   return static_cast<int>(g < 8192 ? (g > 0 ? g : 1) : 8192);
@@ -662,7 +760,7 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
                        static_cast<const T*>(z), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, Pseg, C, rs, part,
-                       kshift);
+                       kshift, nullptr);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
   hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
@@ -670,49 +768,53 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
   return check_launch("posu_bn_train_fwd");
 }
 
-extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
-                             const float* shift, const void* residual, int relu, void* y, void* stream) {
-  POSU_REQUIRE(z && scale && shift && y, "posu_bn_apply: null pointer");
-  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_bn_apply: bad shape");
+namespace {
+int bn_apply_impl(const char* name, int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                  const float* shift, const void* residual, int relu, void* y, void* mask, void* stream) {
+  const std::string what = name;
+  POSU_REQUIRE(z && scale && shift && y, what + ": null pointer");
+  POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0, what + ": bad shape");
   hipStream_t s = as_stream(stream);
   const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
   const int E = chunk_elems(dtype);
+  uint8_t* mk = static_cast<uint8_t*>(mask);
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     if (seg_major(C, E, nseg, Pseg, {scale, shift})) {
       hipLaunchKernelGGL(bn_apply_seg_kernel<T>, dim3(seg_blocks(Pseg, C, E, nseg), nseg), dim3(256), 0, s,
                          static_cast<const T*>(z), Pseg, C, scale, shift, static_cast<const T*>(residual), relu,
-                         static_cast<T*>(y));
+                         static_cast<T*>(y), mk);
       return;
     }
     hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(z), Pseg,
-                       C, scale, shift, static_cast<const T*>(residual), relu, static_cast<T*>(y), total);
+                       C, scale, shift, static_cast<const T*>(residual), relu, static_cast<T*>(y), total, mk);
   });
-  POSU_REQUIRE(ok, "posu_bn_apply: unsupported dtype");
-  return check_launch("posu_bn_apply");
+  POSU_REQUIRE(ok, what + ": unsupported dtype");
+  return check_launch(name);
 }
 
-extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const float* relu_scale,
-                                 const float* relu_shift, const void* z, int nseg, int Pseg, int C,
-                                 const float* mean, const float* rstd, const float* gamma, float* dgamma,
-                                 float* dbeta, void* dz, void* gres, void* workspace, long long workspace_bytes,
-                                 void* stream) {
-  POSU_REQUIRE(gy && z && mean && rstd && dz && workspace, "posu_bn_train_bwd: null pointer");
+int bn_bwd_impl(const char* name, int dtype, const void* gy, const void* y, const void* ymask,
+                const float* relu_scale, const float* relu_shift, const void* z, int nseg, int Pseg, int C,
+                const float* mean, const float* rstd, const float* gamma, float* dgamma, float* dbeta, void* dz,
+                void* gres, void* workspace, long long workspace_bytes, void* stream) {
+  const std::string what = name;
+  POSU_REQUIRE(gy && z && mean && rstd && dz && workspace, what + ": null pointer");
   POSU_REQUIRE(nseg > 0 && Pseg > 0 && C > 0 && C % chunk_elems(dtype) == 0 && reducible(C, dtype),
-               "posu_bn_train_bwd: bad shape (C / chunk must be a power of two or a multiple of 256)");
-  POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), "posu_bn_train_bwd: workspace too small");
+               what + ": bad shape (C / chunk must be a power of two or a multiple of 256)");
+  POSU_REQUIRE(workspace_bytes >= posu_bn_workspace(nseg, C), what + ": workspace too small");
   hipStream_t s = as_stream(stream);
   double* part = static_cast<double*>(workspace);
   float* coef = reinterpret_cast<float*>(static_cast<char*>(workspace) + partial_bytes(nseg, C));
   const RedShape rs = red_shape(Pseg, C, chunk_elems(dtype), nseg);
   const long long total = static_cast<long long>(nseg) * Pseg * C / chunk_elems(dtype);
+  const uint8_t* ym = static_cast<const uint8_t*>(ymask);
   bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 1>), dim3(rs.NB, rs.CG, nseg), dim3(256), 0, s,
                        static_cast<const T*>(z), static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale,
-                       relu_shift, mean, rstd, Pseg, C, rs, part, nullptr);
+                       relu_shift, mean, rstd, Pseg, C, rs, part, nullptr, ym);
   });
-  POSU_REQUIRE(ok, "posu_bn_train_bwd: unsupported dtype");
+  POSU_REQUIRE(ok, what + ": unsupported dtype");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
                      rstd, coef, dgamma, dbeta);
   with_storage(dtype, [&](auto tag) {
@@ -722,14 +824,45 @@ extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const
       hipLaunchKernelGGL(bn_bwd_apply_seg_kernel<T>, dim3(seg_blocks(Pseg, C, E, nseg), nseg), dim3(256), 0, s,
                          static_cast<const T*>(gy), static_cast<const T*>(y), relu_scale, relu_shift,
                          static_cast<const T*>(z), Pseg, C, mean, rstd, coef, static_cast<T*>(dz),
-                         static_cast<T*>(gres));
+                         static_cast<T*>(gres), ym);
       return;
     }
     hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(total)), dim3(256), 0, s, static_cast<const T*>(gy),
                        static_cast<const T*>(y), relu_scale, relu_shift, static_cast<const T*>(z), Pseg, C, mean, rstd, coef,
-                       static_cast<T*>(dz), static_cast<T*>(gres), total);
+                       static_cast<T*>(dz), static_cast<T*>(gres), total, ym);
   });
-  return check_launch("posu_bn_train_bwd");
+  return check_launch(name);
+}
+}  // namespace
+
+extern "C" int posu_bn_apply(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                             const float* shift, const void* residual, int relu, void* y, void* stream) {
+  return bn_apply_impl("posu_bn_apply", dtype, z, nseg, Pseg, C, scale, shift, residual, relu, y, nullptr, stream);
+}
+
+extern "C" int posu_bn_apply_mask(int dtype, const void* z, int nseg, int Pseg, int C, const float* scale,
+                                  const float* shift, const void* residual, void* y, void* mask, void* stream) {
+  POSU_REQUIRE(mask, "posu_bn_apply_mask: null pointer (mask)");
+  POSU_REQUIRE(mask != y && mask != z && mask != residual, "posu_bn_apply_mask: the mask must not alias a tensor");
+  return bn_apply_impl("posu_bn_apply_mask", dtype, z, nseg, Pseg, C, scale, shift, residual, 1, y, mask, stream);
+}
+
+extern "C" int posu_bn_train_bwd(int dtype, const void* gy, const void* y, const float* relu_scale,
+                                 const float* relu_shift, const void* z, int nseg, int Pseg, int C,
+                                 const float* mean, const float* rstd, const float* gamma, float* dgamma,
+                                 float* dbeta, void* dz, void* gres, void* workspace, long long workspace_bytes,
+                                 void* stream) {
+  return bn_bwd_impl("posu_bn_train_bwd", dtype, gy, y, nullptr, relu_scale, relu_shift, z, nseg, Pseg, C, mean,
+                     rstd, gamma, dgamma, dbeta, dz, gres, workspace, workspace_bytes, stream);
+}
+
+extern "C" int posu_bn_train_bwd_mask(int dtype, const void* gy, const void* mask, const void* z, int nseg, int Pseg,
+                                      int C, const float* mean, const float* rstd, const float* gamma, float* dgamma,
+                                      float* dbeta, void* dz, void* gres, void* workspace, long long workspace_bytes,
+                                      void* stream) {
+  POSU_REQUIRE(mask, "posu_bn_train_bwd_mask: null pointer (mask)");
+  return bn_bwd_impl("posu_bn_train_bwd_mask", dtype, gy, nullptr, mask, nullptr, nullptr, z, nseg, Pseg, C, mean,
+                     rstd, gamma, dgamma, dbeta, dz, gres, workspace, workspace_bytes, stream);
 }
 
 extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* out, void* workspace,
@@ -744,7 +877,7 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     hipLaunchKernelGGL((bn_partial_kernel<T, 0>), dim3(rs.NB, rs.CG, 1), dim3(256), 0, s, static_cast<const T*>(x),
-                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr);
+                       nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr, nullptr);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
   hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);
@@ -775,4 +908,40 @@ extern "C" int posu_maxpool3x3s2_bwd(int dtype, const void* x, int N, int H, int
   });
   POSU_REQUIRE(ok, "posu_maxpool3x3s2_bwd: unsupported dtype");
   return check_launch("posu_maxpool3x3s2_bwd");
+}
+
+extern "C" int posu_bn_relu_maxpool3x3s2_fwd(int dtype, const void* z, int nseg, int N, int H, int W, int C,
+                                             const float* scale, const float* shift, void* y, void* idx,
+                                             void* stream) {
+  POSU_REQUIRE(z && scale && shift && y && idx, "posu_bn_relu_maxpool3x3s2_fwd: null pointer");
+  POSU_REQUIRE(nseg > 0 && N > 0 && N % nseg == 0 && H > 0 && W > 0 && C > 0 && C % chunk_elems(dtype) == 0,
+               "posu_bn_relu_maxpool3x3s2_fwd: bad shape (N a multiple of nseg, C of the 16-B chunk)");
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipStream_t s = as_stream(stream);
+  const int E = chunk_elems(dtype);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(bn_relu_maxpool_kernel<T>, dim3(grid_for(static_cast<long long>(N) * Ho * Wo * C / E)),
+                       dim3(256), 0, s, static_cast<const T*>(z), N, N / nseg, H, W, C, Ho, Wo, scale, shift,
+                       static_cast<T*>(y), static_cast<uint8_t*>(idx));
+  });
+  POSU_REQUIRE(ok, "posu_bn_relu_maxpool3x3s2_fwd: unsupported dtype");
+  return check_launch("posu_bn_relu_maxpool3x3s2_fwd");
+}
+
+extern "C" int posu_maxpool3x3s2_bwd_idx(int dtype, const void* idx, const void* gy, int N, int H, int W, int C,
+                                         void* gx, void* stream) {
+  POSU_REQUIRE(idx && gy && gx, "posu_maxpool3x3s2_bwd_idx: null pointer");
+  POSU_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_maxpool3x3s2_bwd_idx: bad shape");
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  hipStream_t s = as_stream(stream);
+  const int E = chunk_elems(dtype);
+  const bool ok = with_storage(dtype, [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(maxpool_bwd_kernel<T>, dim3(grid_for(static_cast<long long>(N) * H * W * C / E)), dim3(256),
+                       0, s, static_cast<const uint8_t*>(idx), static_cast<const T*>(gy), N, H, W, C, Ho, Wo,
+                       static_cast<T*>(gx));
+  });
+  POSU_REQUIRE(ok, "posu_maxpool3x3s2_bwd_idx: unsupported dtype");
+  return check_launch("posu_maxpool3x3s2_bwd_idx");
 }

@@ -136,17 +136,6 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
   return W % 16 == 0 ? (wc & 15) : ((wc + 8 * (wr & 1)) & 15);
 }
 
-// phase stagger (A/B experiment, 0 = off): at W = 32 (two workgroups per CU) every workgroup
-// starts with conv2 (MFMA-bound) and reaches conv3 (x in, y out: HBM-bound) at the same time; a
-// workgroup selected by POSU_TS_STAGGER_SEL first sleeps POSU_TS_STAGGER x 8128 cycles so the two
-// workgroups of a CU run opposite phases
-#ifndef POSU_TS_STAGGER
-#define POSU_TS_STAGGER 0
-#endif
-#ifndef POSU_TS_STAGGER_SEL
-#define POSU_TS_STAGGER_SEL 8
-#endif
-
 // waves per CU the four-m-tile variant is compiled for (A/B builds: 8 gives it 256 registers)
 #ifndef POSU_TS_MT4_WAVES
 #define POSU_TS_MT4_WAVES 12
@@ -164,11 +153,6 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
   const int wu = __builtin_amdgcn_readfirstlane(wid);
   const int pg = wu / K::kNCQ, cq = wu - pg * K::kNCQ;
   const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
-  if constexpr (POSU_TS_STAGGER > 0 && W == 32) {
-    if ((blockIdx.x >> POSU_TS_STAGGER_SEL) & 1) {
-      for (int i = 0; i < POSU_TS_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-  }
   const int H = g.H;
   const int tiles_per_img = H / kRows;
   const int n = blockIdx.x / tiles_per_img;

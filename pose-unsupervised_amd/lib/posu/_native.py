@@ -18,7 +18,7 @@ F16 = 3
 F16X3 = 4   # split fp16 (hi + lo pairs, three MFMAs per product): include/posu.h
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -78,6 +78,10 @@ _SIGNATURES = {
     'posu_conv2d_wgrad': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _ll, _p],
     'posu_bn_workspace': [_i, _i],
     'posu_bn_train_fwd': [_i, _p, _i, _i, _i, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
+    'posu_bn_apply_mask': [_i, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p],
+    'posu_bn_train_bwd_mask': [_i, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
+    'posu_bn_relu_maxpool3x3s2_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
+    'posu_maxpool3x3s2_bwd_idx': [_i, _p, _p, _i, _i, _i, _i, _p, _p],
     'posu_bn_apply': [_i, _p, _i, _i, _i, _p, _p, _p, _i, _p, _p],
     'posu_bn_train_bwd': [_i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_channel_sum': [_i, _p, _i, _i, _p, _p, _ll, _p],

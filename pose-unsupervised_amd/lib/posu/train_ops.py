@@ -96,9 +96,24 @@ def bn_apply(z, nseg, scale, shift, residual=None, relu=True, out=None):
     return out
 
 
-def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None, dbeta=None, relu_from=None):
+def bn_apply_mask(z, nseg, scale, shift, residual=None):
+    """y = relu(bn(z) (+ residual)) and its ReLU bit mask (uint8, one byte per 16-B chunk of y,
+    bit e = [y_e > 0]) for bn_train_bwd(mask=...): the backward reads 1/16 of y's bytes."""
+    require_cuda(z)
+    c = z.shape[-1]
+    pix = z.numel() // c
+    y = torch.empty_like(z)
+    mask = torch.empty(z.numel() * z.element_size() // 16, dtype=torch.uint8, device=z.device)
+    call('posu_bn_apply_mask', nat.dtype_code_of(z), ptr(z), nseg, pix // nseg, c, ptr(scale), ptr(shift),
+         ptr(residual), ptr(y), ptr(mask), stream_of(z.device))
+    return y, mask
+
+
+def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None, dbeta=None, relu_from=None,
+                 mask=None):
     """Backward of y = relu?(bn(z) (+ r)); y=None and relu_from=None means no ReLU;
-    relu_from=(scale, shift) recomputes the ReLU mask from z (no residual) instead of reading y.
+    relu_from=(scale, shift) recomputes the ReLU mask from z (no residual) instead of reading y;
+    mask (bn_apply_mask's bits) replaces y.
     Returns (dz, gres or None, dgamma [C] f32, dbeta [C] f32)."""
     require_cuda(gy, z)
     c = z.shape[-1]
@@ -110,6 +125,13 @@ def bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=False, dgamma=None
     if dbeta is None:
         dbeta = torch.empty((c,), dtype=torch.float32, device=z.device)
     ws = _bn_ws(z.device, nseg, c)
+    if mask is not None:
+        if y is not None or relu_from is not None:
+            raise ValueError('bn_train_bwd: give one ReLU mask source (mask, y or relu_from)')
+        call('posu_bn_train_bwd_mask', nat.dtype_code_of(z), ptr(gy), ptr(mask), ptr(z), nseg, pix // nseg, c,
+             ptr(mean), ptr(rstd), ptr(gamma), ptr(dgamma), ptr(dbeta), ptr(dz), ptr(gres), ptr(ws), ws.numel(),
+             stream_of(z.device))
+        return dz, gres, dgamma, dbeta
     msc, msh = relu_from if relu_from is not None else (None, None)
     call('posu_bn_train_bwd', nat.dtype_code_of(z), ptr(gy), ptr(y), ptr(msc), ptr(msh), ptr(z), nseg, pix // nseg, c,
          ptr(mean),
@@ -137,4 +159,28 @@ def maxpool3x3s2_bwd(x, gy):
     gx = torch.empty_like(x)
     call('posu_maxpool3x3s2_bwd', nat.dtype_code_of(x), ptr(x), n, h, w, c, ptr(gy), ptr(gx), ptr(ws), ws.numel(),
          stream_of(x.device))
+    return gx
+
+
+def bn_relu_maxpool(z, nseg, scale, shift):
+    """Training stem: (maxpool3x3s2(relu(bn(z))), argmax taps uint8) without writing the
+    activation; the backward is maxpool3x3s2_bwd_idx(taps, gy, (H, W))."""
+    require_cuda(z)
+    n, h, w, c = z.shape
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    y = torch.empty((n, ho, wo, c), dtype=z.dtype, device=z.device)
+    idx = torch.empty((n, ho, wo, c), dtype=torch.uint8, device=z.device)
+    call('posu_bn_relu_maxpool3x3s2_fwd', nat.dtype_code_of(z), ptr(z), nseg, n, h, w, c, ptr(scale), ptr(shift),
+         ptr(y), ptr(idx), stream_of(z.device))
+    return y, idx
+
+
+def maxpool3x3s2_bwd_idx(idx, gy, hw):
+    """Max-pool backward from stored argmax taps: gx [N, H, W, C], (H, W) = hw."""
+    require_cuda(idx, gy)
+    n, _, _, c = gy.shape
+    h, w = hw
+    gx = torch.empty((n, h, w, c), dtype=gy.dtype, device=gy.device)
+    call('posu_maxpool3x3s2_bwd_idx', nat.dtype_code_of(gy), ptr(idx), ptr(gy), n, h, w, c, ptr(gx),
+         stream_of(gy.device))
     return gx

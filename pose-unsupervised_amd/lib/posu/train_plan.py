@@ -33,6 +33,11 @@ STEM_CIN_PAD = 8
 # weight gradients on a side stream, overlapping the data-gradient chain (_Grads)
 SIDE_STREAM_WGRAD = True
 HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
+# round 5: the residual units' ReLU mask kept as bits (bn_apply_mask: the backward reads 1/16 of
+# y's bytes, twice) and the stem's BN + ReLU + max-pool in one pass that stores the argmax taps
+# (the activation before the pool is never written, the backward needs no argmax pass)
+RELU_BITMASK = True
+FUSED_STEM_POOL = True
 
 
 def _conv_tuned(x, w, cout, k, stride, pad, code):
@@ -120,17 +125,31 @@ class _ConvBN:
         bn = self.bn
         mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
                                             bn.running_var)
+        if RELU_BITMASK and self.relu and residual is not None:
+            y, mask = T.bn_apply_mask(z, nseg, sc, sh, residual)
+            return y, (x, z, None, mean, rstd, sc, sh, True, mask)
         y = T.bn_apply(z, nseg, sc, sh, residual, self.relu)
-        return y, (x, z, y, mean, rstd, sc, sh, residual is not None)
+        return y, (x, z, y, mean, rstd, sc, sh, residual is not None, None)
+
+    def forward_pooled(self, x, nseg, code):
+        """The stem: conv -> BN (train) -> ReLU -> max-pool 3x3 / s2 in one pass after the
+        statistics (T.bn_relu_maxpool); returns (pooled, saved, argmax taps)."""
+        z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
+        bn = self.bn
+        mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
+                                            bn.running_var)
+        y, idx = T.bn_relu_maxpool(z, nseg, sc, sh)
+        return y, (x, z, None, mean, rstd, sc, sh, False, None), idx
 
     def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None,
                  inplace=False):
-        x, z, y, mean, rstd, sc, sh, has_res = saved
-        # ReLU mask: from y after a residual add, else recomputed from z (one tensor read less)
-        mask_y = y if (self.relu and has_res) else None
+        x, z, y, mean, rstd, sc, sh, has_res, mask = saved
+        # ReLU mask: the forward's bits, or y after a residual add, else recomputed from z (one
+        # tensor read less)
+        mask_y = y if (self.relu and has_res and mask is None) else None
         relu_from = (sc, sh) if (self.relu and not has_res) else None
         dz, gres, dgam, dbet = T.bn_train_bwd(gy, mask_y, z, nseg, mean, rstd, self.bn.weight, want_gres=want_gres,
-                                              relu_from=relu_from)
+                                              relu_from=relu_from, mask=mask)
         grads.wgrad(self.conv.weight, lambda: T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad,
                                                              code), dz, x)
         grads[self.bn.weight] = dgam
@@ -301,9 +320,13 @@ class TrainPlan:
             xin = torch.empty((n * len(x), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(code), device=x[0].device)
             for k, v in enumerate(x):
                 ops.pack_nchw_to_nhwc(v, code, STEM_CIN_PAD, out=xin[k * n:(k + 1) * n])
-            a0, s0 = self.stem.forward(xin, nseg, code)
-            y = ops.maxpool3x3s2_nhwc(a0, code)
-            saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
+            if FUSED_STEM_POOL:
+                y, s0, idx = self.stem.forward_pooled(xin, nseg, code)
+                saved = {'stem': s0, 'pool_idx': idx, 'blocks': []}
+            else:
+                a0, s0 = self.stem.forward(xin, nseg, code)
+                y = ops.maxpool3x3s2_nhwc(a0, code)
+                saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
             for b in self.layers[0]:
                 y, sb = b.forward(y, nseg, code)
                 saved['blocks'].append(sb)
@@ -365,7 +388,10 @@ class TrainPlan:
         for b, sb in zip(reversed(blocks), reversed(sblocks)):
             g = b.backward(g, sb, nseg, code, grads)
         if i == 0:
-            g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
+            if 'pool_idx' in saved:
+                g = T.maxpool3x3s2_bwd_idx(saved['pool_idx'], g, saved['stem'][1].shape[1:3])
+            else:
+                g = T.maxpool3x3s2_bwd(saved['pool_in'], g)
             self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
             g = None
         return g, grads.close()

@@ -185,6 +185,58 @@ def test_bn_train_forward_and_backward_match_autograd(cuda, c, nseg, residual, r
         _close_lowp(dbet.cpu(), grads[2], 0.03)
 
 
+@pytest.mark.parametrize('code', [F32, BF16, F16])
+@pytest.mark.parametrize('c,nseg,size', [(256, 2, (2, 9, 7)), (64, 4, (3, 24, 20)), (2048, 1, (2, 5, 3))])
+def test_bn_relu_bitmask_equals_the_y_masked_backward(cuda, code, c, nseg, size):
+    """ABI 14: bn_apply_mask writes the same y as bn_apply plus bit e = [y_e > 0] per 16-B chunk,
+    and the backward reading those bits equals the one reading y, bit for bit."""
+    g = torch.Generator().manual_seed(41)
+    b, h, w = size
+    dt = ops.torch_dtype(code)
+    z = _nhwc(torch.randn(nseg * b, c, h, w, generator=g) * 2 + 0.3, cuda, dt)
+    r = _nhwc(torch.randn(nseg * b, c, h, w, generator=g), cuda, dt)
+    gy = _nhwc(torch.randn(nseg * b, c, h, w, generator=g), cuda, dt)
+    gamma = (torch.rand(c, generator=g) + 0.5).to(cuda)
+    beta = (torch.randn(c, generator=g) * 0.1).to(cuda)
+    mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, gamma, beta, 1e-5, 0.1)
+    y = T.bn_apply(z, nseg, sc, sh, r, True)
+    y2, mask = T.bn_apply_mask(z, nseg, sc, sh, r)
+    ref = T.bn_train_bwd(gy, y, z, nseg, mean, rstd, gamma, want_gres=True)
+    got = T.bn_train_bwd(gy, None, z, nseg, mean, rstd, gamma, want_gres=True, mask=mask)
+    torch.cuda.synchronize()
+    assert torch.equal(y2, y)
+    e = 16 // y.element_size()
+    pos = (y.float() > 0).reshape(-1, e).to(torch.int32)
+    bits = (pos << torch.arange(e, device=cuda, dtype=torch.int32)).sum(dim=1)
+    assert torch.equal(mask.to(torch.int32), bits)
+    for a, b_ in zip(got, ref):
+        assert torch.equal(a, b_)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+@pytest.mark.parametrize('shape', [(4, 17, 16, 64), (2, 32, 30, 64), (2, 9, 9, 128)])
+def test_fused_stem_bn_relu_maxpool_equals_the_two_pass_path(cuda, code, shape):
+    """ABI 14, the training stem: bn_relu_maxpool = max-pool of bn_apply(relu) bit for bit, and the
+    backward from its stored taps = maxpool3x3s2_bwd over the activation (ReLU zeros: many ties)."""
+    g = torch.Generator().manual_seed(42)
+    n, h, w, c = shape
+    nseg = 2
+    dt = ops.torch_dtype(code)
+    z = (torch.randint(-3, 4, shape, generator=g).float() * 0.5).to(cuda, dt)   # ties in every window
+    gamma = (torch.rand(c, generator=g) + 0.5).to(cuda)
+    beta = (torch.randn(c, generator=g) * 0.1).to(cuda)
+    _, _, sc, sh = T.bn_train_fwd(z, nseg, gamma, beta, 1e-5, 0.1)
+    a = T.bn_apply(z, nseg, sc, sh, None, True)
+    ref = ops.maxpool3x3s2_nhwc(a, code)
+    y, idx = T.bn_relu_maxpool(z, nseg, sc, sh)
+    gy = torch.randint(-4, 5, ref.shape, generator=g).float().to(cuda, dt)
+    gx_ref = T.maxpool3x3s2_bwd(a, gy)
+    gx = T.maxpool3x3s2_bwd_idx(idx, gy, (h, w))
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref)
+    assert torch.equal(gx, gx_ref)
+
+
 def test_channel_sum(cuda):
     g = torch.Generator().manual_seed(15)
     x = torch.randn(3, 17, 11, 64, generator=g)
