@@ -66,7 +66,9 @@ const char* posu_last_error(void);
  * (posu_bottleneck_s2_tail_next_fwd); 13 the split-fp16 dtype POSU_F16X3 (conv / dual / deconv /
  * deconv+head / head / pack / s2d pack / max-pool / unpack entry points); 14 (training) the ReLU
  * bit mask (posu_bn_apply_mask / posu_bn_train_bwd_mask) and the fused stem BN + ReLU + max-pool
- * with stored argmax taps (posu_bn_relu_maxpool3x3s2_fwd / posu_maxpool3x3s2_bwd_idx).  The
+ * with stored argmax taps (posu_bn_relu_maxpool3x3s2_fwd / posu_maxpool3x3s2_bwd_idx), the training
+ * stem's convolution and weight gradient from the NCHW f32 views (posu_stem_conv_views_fwd /
+ * posu_stem_wgrad_views).  The
  * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
@@ -556,6 +558,19 @@ int posu_bn_relu_maxpool3x3s2_fwd(int dtype, const void* z, int nseg, int N, int
                                   void* stream);
 int posu_maxpool3x3s2_bwd_idx(int dtype, const void* idx, const void* gy, int N, int H, int W,
                               int C, void* gx, void* stream);
+/* ABI 14, the training stem's convolution (lib/models/pose_resnet.py:192, nn.Conv2d(3, 64, 7, 2, 3,
+ * bias=False)) straight from the caller's NCHW f32 views (views[v] = [Nv, 3, H, W], a host array of
+ * device pointers, stacked view-major like posu_stem_pool_views_fwd): z [nviews*Nv, H/2, W/2, 64]
+ * of dtype (BF16 / F16) from the parameter's own f32 weight w [64][3][7][7]; and its weight
+ * gradient dw [64][3][7][7] f32 from dz [nviews*Nv, H/2, W/2, 64] (workspace:
+ * posu_stem_wgrad_workspace bytes of per-block partials, summed in a fixed order).  W = 256,
+ * H % 8 == 0. */
+int posu_stem_conv_views_fwd(int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                             const float* w, void* z, void* stream);
+long long posu_stem_wgrad_workspace(int N, int H, int W);
+int posu_stem_wgrad_views(int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                          const void* dz, float* dw, void* workspace, long long workspace_bytes,
+                          void* stream);
 
 #ifdef __cplusplus
 }

@@ -89,9 +89,13 @@ constexpr int kStemAbl = POSU_STEM_ABLATE;
 // w), every kernel row issues w_hi.x_hi + w_lo.x_hi + w_hi.x_lo, and the pooled outputs are stored
 // as (hi, lo) pairs in the split layout (128 halves per pixel).  Eight waves (W = 256) only: the
 // twelve-wave rings do not fit twice.
-template <typename T, int NW, bool SPL = false>
+// RAW (round 5, the training step's stem, lib/models/pose_resnet.py:192): the raw convolution
+// [N, H/2, W/2, 64] (no BN / ReLU / pool: the batch statistics need it), from the parameter's own
+// f32 [64][3][7][7] weights (re-laid out into LDS by every block: no per-step pack); every item
+// computes its 4 stem rows and stores them (8-byte NHWC stores).
+template <typename T, int NW, bool SPL = false, bool RAW = false>
 __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int Nv, int N, int H, int W, int hflip,
-                                                               int strips, const T* __restrict__ w,
+                                                               int strips, const void* __restrict__ wv_,
                                                                const float* __restrict__ scale,
                                                                const float* __restrict__ shift, T* __restrict__ y) {
   using O = StemOp<T>;
@@ -103,6 +107,8 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   constexpr int NS = SPL ? 2 : 1;            // halves staged (hi [, lo])
   constexpr int CPX = SPL ? 128 : 64;        // stored elements per output pixel
   static_assert(!SPL || (NW == 8 && std::is_same<T, f16_t>::value), "split stem: fp16 halves, eight waves");
+  static_assert(!RAW || (!SPL && NW == 8), "raw stem: one dtype, eight waves");
+  const T* __restrict__ w = static_cast<const T*>(wv_);
   __shared__ __attribute__((aligned(16))) char smem[NS * (RING * RB + W_BYTES) + NW * 2 * 64 * 4 + 2 * 64 * 4];
   char* win = smem;
   char* winl = smem + RING * RB;              // SPL: the lo ring
@@ -121,6 +127,20 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   const size_t plane = static_cast<size_t>(H) * W;
 
   // ---- weights and BN -> LDS (once per block)
+  if constexpr (RAW) {
+    // w = f32 [64 co][3 ci][7 kh][7 kw] -> LDS [co][kh * 32 + kw * 4 + ci] (tap 7 and ci 3 zero)
+    const float* __restrict__ wf = static_cast<const float*>(wv_);
+    for (int i = tid; i < 64 * kStemK / 2; i += NT) {
+      const int co = i / (kStemK / 2), k0 = 2 * (i - co * (kStemK / 2));
+      float v[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int k = k0 + u, kh = k >> 5, kw = (k >> 2) & 7, ci = k & 3;
+        v[u] = (kw < 7 && ci < 3) ? wf[((co * 3 + ci) * 7 + kh) * 7 + kw] : 0.f;
+      }
+      *reinterpret_cast<uint32_t*>(wl + (co * kStemPitch + k0) * 2) = O::pack2(v[0], v[1]);
+    }
+  } else {
   if (tid < 64) {
     bn[tid] = fabsf(scale[tid]);   // |s|: the sign is in the staged weights
     bn[64 + tid] = shift[tid];
@@ -141,6 +161,7 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
         *reinterpret_cast<u32x4*>((h ? wll : wl) + (co * kStemPitch + ck * 8) * 2) = wv;
       }
     }
+  }
   }
 
   // input rows -> registers: row i0 + r (r < NR), group gk = 4 input columns 4 (gk - 1) .. + 3 of
@@ -304,6 +325,20 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
         }
       }
     }
+    if constexpr (RAW) {
+      // stem row r0 + rl, column sc, channels 16 j + 4 q .. + 3 (every row of an item is inside
+      // the image: items start at stem row 4 k)
+      T* __restrict__ zr = y + (static_cast<size_t>(n) * (H / 2) + r0) * (W / 2) * 64 + sc * 64 + 4 * q;
+#pragma unroll
+      for (int rl = 0; rl < M; ++rl)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint2 u = make_uint2(O::pack2(acc[rl][j][0], acc[rl][j][1]), O::pack2(acc[rl][j][2], acc[rl][j][3]));
+          if (kStemAbl & 4) asm volatile("" ::"v"(u.x), "v"(u.y));
+          else *reinterpret_cast<uint2*>(zr + static_cast<size_t>(rl) * (W / 2) * 64 + 16 * j) = u;
+        }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -397,13 +432,15 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
   load_rows(8 * k0 + 3, I8{}, xv[0]);
   store_rows(8 * k0 + 3, I8{}, xv[0]);
   __syncthreads();
-  stem_rows(4 * k0 - 1, I5{}, carry, vm);
+  if constexpr (RAW) stem_rows(4 * k0, I4{}, carry, vm);
+  else stem_rows(4 * k0 - 1, I5{}, carry, vm);
   // item k0 + d's new rows into set d % PFD, during item k0's pool
   if constexpr (PF) {
     if (k0 + 1 < k1) load_rows(8 * k0 + 10, I8{}, xv[PFD - 1]);
     if (PFD == 2 && k0 + 2 < k1) load_rows(8 * k0 + 18, I8{}, xv[0]);
   }
-  pool(k0, vm);
+  if constexpr (RAW) __syncthreads();   // item k0 + 1's ring writes follow every wave's reads
+  else pool(k0, vm);
   // item k: its rows are in set S = (k - k0) % PFD (a compile-time index: a register set picked
   // at run time would live in scratch); once stored, the set takes item k + PFD's
   auto item = [&](int k, auto sidx) __attribute__((always_inline)) {
@@ -417,7 +454,13 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     if (PF && k + PFD < k1) load_rows(8 * (k + PFD) + 2, I8{}, xv[S]);
     if constexpr (PF) stem_rows(4 * k, I4{}, carry, vm);
     else stem_rows(4 * k - 1, I5{}, carry, vm);
-    pool(k, vm);
+    if constexpr (RAW) {
+      // the next item's ring writes wait for every wave's window reads (the pool's barrier does
+      // this in the pooled kernel)
+      __syncthreads();
+    } else {
+      pool(k, vm);
+    }
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, PFD - 1>;
@@ -429,6 +472,185 @@ __global__ __launch_bounds__(NW * 64, 1) void stem_pool_kernel(StemViews xs, int
     }
   }
   for (; k < k1; ++k) item(k, S1{});   // PFD 2: at most one item left, its rows in set 1
+}
+
+
+// ---- the training stem's weight gradient (round 5; lib/models/pose_resnet.py:192 under autograd):
+//   dW[co][ci][kh][kw] = sum over (n, oy, ox) of dz[n][oy][ox][co] * x[n][ci][2 oy - 3 + kh][2 ox - 3 + kw]
+// as MFMAs over the pixels (K) of one stem row at a time: D[co][f] with f = kw * 4 + ci (kw < 8,
+// ci < 4: tap 7 and channel 3 are dropped by the reduction).  A block walks a strip of stem rows
+// of one image; wave w = kernel row kh.  Per stem row:
+//   * dz row [128 px][64 co] in LDS (16-B chunks XOR-swizzled by pixel: conflict-free transposed
+//     reads), A = dz^T by ds_read_b64_tr_b16 (4 pixel rows x 16 channels per 16-lane group);
+//   * the input window as the inference stem stages it ([input row][col + 3][3 ch + 0] bf16 in a
+//     16-row ring, read straight from the caller's NCHW f32 views): the im2col row of pixel px at
+//     kernel row kh is the 64 contiguous bytes at 16 px of ring row 2 oy - 3 + kh, so B = X is a
+//     transposed read with a 16-B row stride;
+//   * the next row's dz and its two new input rows are loaded into registers while this row's
+//     MFMAs run, then written to the other dz buffer / free ring slots (one barrier per row).
+// Each block writes its partial [7 kh][32 f][64 co] f32; posu_stem_wgrad sums the partials in block
+// order (deterministic) into the parameter's [64][3][7][7] layout.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+constexpr int kWgThreads = 448;          // 7 waves
+constexpr int kWgRing = 16;
+constexpr int kWgCols = 264;             // window columns: input cols -3 .. 260
+constexpr int kWgRB = kWgCols * 8;
+constexpr int kWgDz = 128 * 128;         // one dz row: 128 px x 64 ch x 2 B
+constexpr int kWgGroups = 66;            // 4-column input groups per row
+constexpr int kWgPart = 7 * 32 * 64;     // floats per block partial
+
+__device__ __forceinline__ int wg_sw(int px) { return (((px >> 1) & 1) << 1) | (((px >> 3) & 1) << 2); }
+
+__device__ __forceinline__ uint4 tr_pair(const char* p0, const char* p1) {
+  const s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p0));
+  const s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p1));
+  const uint2 u0 = __builtin_bit_cast(uint2, v0), u1 = __builtin_bit_cast(uint2, v1);
+  return make_uint4(u0.x, u0.y, u1.x, u1.y);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kWgThreads, 2) void stem_wgrad_kernel(StemViews xs, int Nv, int H, int strips,
+                                                                   const T* __restrict__ dz, float* __restrict__ part) {
+  using O = StemOp<T>;
+  constexpr int W = 256, Wo = 128;
+  __shared__ __attribute__((aligned(16))) char smem[kWgRing * kWgRB + 2 * kWgDz];
+  char* ring = smem;
+  char* dzb = smem + kWgRing * kWgRB;
+  const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
+  const int q = lane >> 4, a = (lane >> 2) & 3, p = lane & 3;
+  const int Ho = H / 2, rows = Ho / strips;
+  const int n = blockIdx.x / strips;
+  const int ya = (blockIdx.x - n * strips) * rows, yb = ya + rows;
+  const float* __restrict__ xn = xs.x[n / Nv] + static_cast<size_t>(n % Nv) * 3 * H * W;
+  const size_t plane = static_cast<size_t>(H) * W;
+  const T* __restrict__ dzn = dz + static_cast<size_t>(n) * Ho * Wo * 64;
+
+  // input rows iy0 .. iy0 + nr - 1 -> registers (item i: row i / 66, group i % 66 = input cols
+  // 4 (g - 1) .. + 3 of each plane) and -> ring slots (window cols 4 g - 1 .. 4 g + 2)
+  auto load_x = [&](int iy0, int nr, int it, float4 (&xv)[3]) {
+    const int i = tid + it * kWgThreads;
+    const int r = i / kWgGroups, g = i - r * kWgGroups;
+    const int iy = iy0 + r, c0 = 4 * (g - 1);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) xv[pl] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < nr * kWgGroups && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
+        static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) xv[pl] = *reinterpret_cast<const float4*>(xn + pl * plane + static_cast<size_t>(iy) * W + c0);
+    }
+  };
+  auto store_x = [&](int iy0, int nr, int it, const float4 (&xv)[3]) {
+    const int i = tid + it * kWgThreads;
+    if (i >= nr * kWgGroups) return;
+    const int r = i / kWgGroups, g = i - r * kWgGroups;
+    char* row = ring + ((iy0 + r) & (kWgRing - 1)) * kWgRB;
+    const float a0[4] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w};
+    const float a1[4] = {xv[1].x, xv[1].y, xv[1].z, xv[1].w};
+    const float a2[4] = {xv[2].x, xv[2].y, xv[2].z, xv[2].w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int wc = 4 * g - 1 + e;
+      if (wc >= 0 && wc < kWgCols)
+        *reinterpret_cast<uint2*>(row + wc * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
+    }
+  };
+  // dz row oy: 1024 16-B chunks, chunk i = pixel i / 8, channels 8 (i % 8) ..
+  auto load_dz = [&](int oy, uint4 (&dv)[3]) {
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int i = tid + it * kWgThreads;
+      dv[it] = i < 1024 ? *reinterpret_cast<const uint4*>(dzn + (static_cast<size_t>(oy) * Wo) * 64 + i * 8)
+                        : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_dz = [&](int buf, const uint4 (&dv)[3]) {
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+      const int i = tid + it * kWgThreads;
+      if (i < 1024) {
+        const int px = i >> 3, c = i & 7;
+        *reinterpret_cast<uint4*>(dzb + buf * kWgDz + px * 128 + ((c ^ wg_sw(px)) << 4)) = dv[it];
+      }
+    }
+  };
+
+  {  // prologue: input rows 2 ya - 3 .. 2 ya + 3, dz row ya
+    float4 xv[3];
+#pragma unroll
+    for (int it = 0; it < (7 * kWgGroups + kWgThreads - 1) / kWgThreads; ++it) {
+      load_x(2 * ya - 3, 7, it, xv);
+      store_x(2 * ya - 3, 7, it, xv);
+    }
+    uint4 dv[3];
+    load_dz(ya, dv);
+    store_dz(0, dv);
+  }
+  __syncthreads();
+
+  f32x4 acc[4][2];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) acc[mt][hf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int oy = ya; oy < yb; ++oy) {
+    const bool more = oy + 1 < yb;
+    float4 xv[3];
+    uint4 dv[3];
+    if (more) {   // two new input rows (132 items: threads 0 .. 131) and the next dz row
+      load_x(2 * oy + 4, 2, 0, xv);
+      load_dz(oy + 1, dv);
+    }
+    const char* dzr = dzb + (oy & 1) * kWgDz;
+    const char* xr = ring + ((2 * oy - 3 + kh) & (kWgRing - 1)) * kWgRB;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      // pixel rows of this lane's two 4-row blocks: 32 s + 8 q + 4 t + a
+      const int px0 = 32 * s + 8 * q + a, px1 = px0 + 4;
+      uint4 af[4], bf[2];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        const int chunk = 2 * mt + (p >> 1), within = (p & 1) * 8;
+        af[mt] = tr_pair(dzr + px0 * 128 + ((chunk ^ wg_sw(px0)) << 4) + within,
+                         dzr + px1 * 128 + ((chunk ^ wg_sw(px1)) << 4) + within);
+      }
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+        bf[hf] = tr_pair(xr + 16 * px0 + 32 * hf + 8 * p, xr + 16 * px1 + 32 * hf + 8 * p);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          if (kStemAbl & 1) acc[mt][hf][0] += __uint_as_float(af[mt].x ^ bf[hf].y);
+          else O::mma(acc[mt][hf], af[mt], bf[hf]);
+        }
+    }
+    if (more) {
+      store_x(2 * oy + 4, 2, 0, xv);
+      store_dz((oy + 1) & 1, dv);
+    }
+    __syncthreads();
+  }
+  // partial [kh][f][co]: lane (col f = 16 hf + (lane & 15), rows co = 16 mt + 4 q + r)
+  float* dst = part + static_cast<size_t>(blockIdx.x) * kWgPart + kh * 32 * 64;
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+      *reinterpret_cast<float4*>(dst + (16 * hf + (lane & 15)) * 64 + 16 * mt + 4 * q) =
+          make_float4(acc[mt][hf][0], acc[mt][hf][1], acc[mt][hf][2], acc[mt][hf][3]);
+}
+
+// dw[co][ci][kh][kw] (the parameter's layout) = sum over blocks b (in order) of part[b][kh][kw * 4 + ci][co]
+__global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblocks,
+                                                                 float* __restrict__ dw) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= 64 * 147) return;
+  const int co = t & 63, rest = t >> 6;          // rest = (kh * 7 + kw) * 3 + ci
+  const int ci = rest % 3, tap = rest / 3, kh = tap / 7, kw = tap - 7 * kh;
+  const float* p = part + (kh * 32 + kw * 4 + ci) * 64 + co;
+  float s = 0.f;
+  for (int b = 0; b < nblocks; ++b) s += p[static_cast<size_t>(b) * kWgPart];
+  dw[((co * 3 + ci) * 7 + kh) * 7 + kw] = s;
 }
 
 }  // namespace
@@ -489,4 +711,77 @@ extern "C" int posu_stem_pool_views_fwd(int dtype, const float* const* views, in
                                         int hflip, const void* w, const float* scale, const float* shift, void* y,
                                         void* stream) {
   return stem_launch(dtype, views, nviews, Nv, H, W, hflip, w, scale, shift, y, stream, "posu_stem_pool_views_fwd");
+}
+
+// ---- training stem (round 5, ABI 14)
+namespace {
+int stem_train_views(const char* what, int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                     StemViews& xs) {
+  const std::string wh(what);
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, wh + ": dtype must be BF16 or F16");
+  POSU_REQUIRE(views && nviews >= 1 && nviews <= kMaxViews, wh + ": 1 .. 8 views");
+  for (int v = 0; v < nviews; ++v) POSU_REQUIRE(views[v], wh + ": null view pointer");
+  POSU_REQUIRE(Nv > 0 && H > 0 && H % 8 == 0 && W == 256, wh + ": built for W = 256 and H % 8 == 0");
+  POSU_REQUIRE(static_cast<long long>(Nv) * 3 * H * W < (1LL << 40), wh + ": input too large");
+  for (int v = 0; v < nviews; ++v) {
+    POSU_REQUIRE((reinterpret_cast<size_t>(views[v]) & 15) == 0, wh + ": views must be 16-byte aligned");
+    xs.x[v] = views[v];
+  }
+  return 0;
+}
+
+int wgrad_strips(int N, int H) {
+  int strips = 1;   // about two blocks per CU
+  while (N * strips * 2 <= 512 && (H / 2) % (strips * 2) == 0 && (H / 2) / (strips * 2) >= 8) strips *= 2;
+  return strips;
+}
+}  // namespace
+
+extern "C" int posu_stem_conv_views_fwd(int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                                        const float* w, void* z, void* stream) {
+  StemViews xs{};
+  const int rc = stem_train_views("posu_stem_conv_views_fwd", dtype, views, nviews, Nv, H, W, xs);
+  if (rc) return rc;
+  POSU_REQUIRE(w && z, "posu_stem_conv_views_fwd: null pointer");
+  const int N = Nv * nviews, pairs = H / 8;
+  int strips = 1;
+  while (N * strips * 2 <= 256 && pairs % (strips * 2) == 0) strips *= 2;
+  hipStream_t s = as_stream(stream);
+  const dim3 grid(static_cast<unsigned>(N * strips));
+  if (dtype == POSU_BF16)
+    hipLaunchKernelGGL((stem_pool_kernel<uint16_t, 8, false, true>), grid, dim3(512), 0, s, xs, Nv, N, H, W, 0, strips,
+                       static_cast<const void*>(w), nullptr, nullptr, static_cast<uint16_t*>(z));
+  else
+    hipLaunchKernelGGL((stem_pool_kernel<f16_t, 8, false, true>), grid, dim3(512), 0, s, xs, Nv, N, H, W, 0, strips,
+                       static_cast<const void*>(w), nullptr, nullptr, static_cast<f16_t*>(z));
+  return check_launch("posu_stem_conv_views_fwd");
+}
+
+extern "C" long long posu_stem_wgrad_workspace(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || H % 8 != 0 || W != 256) return -1;
+  return static_cast<long long>(N) * wgrad_strips(N, H) * kWgPart * 4;
+}
+
+extern "C" int posu_stem_wgrad_views(int dtype, const float* const* views, int nviews, int Nv, int H, int W,
+                                     const void* dz, float* dw, void* workspace, long long workspace_bytes,
+                                     void* stream) {
+  StemViews xs{};
+  const int rc = stem_train_views("posu_stem_wgrad_views", dtype, views, nviews, Nv, H, W, xs);
+  if (rc) return rc;
+  POSU_REQUIRE(dz && dw && workspace, "posu_stem_wgrad_views: null pointer");
+  POSU_REQUIRE((reinterpret_cast<size_t>(dz) & 15) == 0 && (reinterpret_cast<size_t>(workspace) & 15) == 0,
+               "posu_stem_wgrad_views: dz / workspace must be 16-byte aligned");
+  const int N = Nv * nviews, strips = wgrad_strips(N, H);
+  POSU_REQUIRE(workspace_bytes >= posu_stem_wgrad_workspace(N, H, W), "posu_stem_wgrad_views: workspace too small");
+  hipStream_t s = as_stream(stream);
+  float* part = static_cast<float*>(workspace);
+  const dim3 grid(static_cast<unsigned>(N * strips));
+  if (dtype == POSU_BF16)
+    hipLaunchKernelGGL(stem_wgrad_kernel<uint16_t>, grid, dim3(kWgThreads), 0, s, xs, Nv, H, strips,
+                       static_cast<const uint16_t*>(dz), part);
+  else
+    hipLaunchKernelGGL(stem_wgrad_kernel<f16_t>, grid, dim3(kWgThreads), 0, s, xs, Nv, H, strips,
+                       static_cast<const f16_t*>(dz), part);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((64 * 147 + 255) / 256), dim3(256), 0, s, part, N * strips, dw);
+  return check_launch("posu_stem_wgrad_views");
 }

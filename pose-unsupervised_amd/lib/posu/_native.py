@@ -82,6 +82,9 @@ _SIGNATURES = {
     'posu_bn_train_bwd_mask': [_i, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_bn_relu_maxpool3x3s2_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
     'posu_maxpool3x3s2_bwd_idx': [_i, _p, _p, _i, _i, _i, _i, _p, _p],
+    'posu_stem_conv_views_fwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p],
+    'posu_stem_wgrad_workspace': [_i, _i, _i],
+    'posu_stem_wgrad_views': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _ll, _p],
     'posu_bn_apply': [_i, _p, _i, _i, _i, _p, _p, _p, _i, _p, _p],
     'posu_bn_train_bwd': [_i, _p, _p, _p, _p, _p, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _ll, _p],
     'posu_channel_sum': [_i, _p, _i, _i, _p, _p, _ll, _p],
@@ -90,7 +93,8 @@ _SIGNATURES = {
 }
 _RESTYPES = {'posu_last_error': ctypes.c_char_p, 'posu_conv2d_wgrad_workspace': ctypes.c_longlong,
              'posu_pack_job_blocks': ctypes.c_longlong,
-             'posu_bn_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong}
+             'posu_bn_workspace': ctypes.c_longlong, 'posu_maxpool3x3s2_bwd_workspace': ctypes.c_longlong,
+             'posu_stem_wgrad_workspace': ctypes.c_longlong}
 
 
 def library_path():

@@ -184,3 +184,51 @@ def maxpool3x3s2_bwd_idx(idx, gy, hw):
     call('posu_maxpool3x3s2_bwd_idx', nat.dtype_code_of(gy), ptr(idx), ptr(gy), n, h, w, c, ptr(gx),
          stream_of(gy.device))
     return gx
+
+
+def _views_arg(views):
+    """A list of NCHW f32 [Nv, 3, H, W] cuda views of one shape -> (ctypes pointer array, Nv, H, W); the
+    array object must stay alive until the call returns (the kernel arguments are copied at launch)."""
+    import ctypes
+    if not views or not all(v.is_cuda and v.dtype == torch.float32 and v.is_contiguous() for v in views):
+        raise TypeError('stem views: contiguous f32 cuda tensors expected')
+    n, c, h, w = views[0].shape
+    if c != 3 or any(tuple(v.shape) != (n, c, h, w) for v in views):
+        raise ValueError('stem views: views of one shape [N, 3, H, W] expected')
+    arr = (ctypes.c_void_p * len(views))(*[v.data_ptr() for v in views])
+    return arr, n, h, w
+
+
+def stem_conv(views, weight, code):
+    """The training stem's raw 7x7 / s2 / p3 convolution of the views (stacked view-major) from the f32
+    parameter itself: z [V * Nv, H/2, W/2, 64] in the compute dtype (posu_stem_conv_views_fwd)."""
+    import ctypes
+    arr, n, h, w = _views_arg(views)
+    require_cuda(weight)
+    if weight.dtype != torch.float32 or tuple(weight.shape) != (64, 3, 7, 7) or not weight.is_contiguous():
+        raise ValueError('stem_conv: a contiguous f32 [64, 3, 7, 7] weight expected')
+    z = torch.empty((n * len(views), h // 2, w // 2, 64), dtype=nat_dtype(code), device=views[0].device)
+    call('posu_stem_conv_views_fwd', code, ctypes.cast(arr, ctypes.c_void_p), len(views), n, h, w, ptr(weight),
+         ptr(z), stream_of(z.device))
+    return z
+
+
+def stem_wgrad(views, dz, code, out=None):
+    """dW [64, 3, 7, 7] f32 of the stem convolution from its output gradient dz (posu_stem_wgrad_views)."""
+    import ctypes
+    arr, n, h, w = _views_arg(views)
+    require_cuda(dz)
+    need = nat.load().posu_stem_wgrad_workspace(n * len(views), h, w)
+    if need <= 0:
+        raise ValueError('stem_wgrad: unsupported shape')
+    ws = workspace(dz.device, need, 'stem_wgrad')
+    if out is None:
+        out = torch.empty((64, 3, 7, 7), dtype=torch.float32, device=dz.device)
+    call('posu_stem_wgrad_views', code, ctypes.cast(arr, ctypes.c_void_p), len(views), n, h, w, ptr(dz), ptr(out),
+         ptr(ws), ws.numel(), stream_of(dz.device))
+    return out
+
+
+def nat_dtype(code):
+    from . import ops
+    return ops.torch_dtype(code)

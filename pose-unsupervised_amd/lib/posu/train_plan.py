@@ -38,6 +38,9 @@ HEAD_CPAD = 64   # heatmap-gradient channels padded to one 64-channel tile
 # (the activation before the pool is never written, the backward needs no argmax pass)
 RELU_BITMASK = True
 FUSED_STEM_POOL = True
+# round 5: the stem's convolution and weight gradient as their own kernels, straight from the NCHW
+# f32 views (no NHWC pack; the generic 8-channel-padded conv / weight gradient took 260 / 477 us)
+STEM_KERNELS = True
 
 
 def _conv_tuned(x, w, cout, k, stride, pad, code):
@@ -133,8 +136,12 @@ class _ConvBN:
 
     def forward_pooled(self, x, nseg, code):
         """The stem: conv -> BN (train) -> ReLU -> max-pool 3x3 / s2 in one pass after the
-        statistics (T.bn_relu_maxpool); returns (pooled, saved, argmax taps)."""
-        z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
+        statistics (T.bn_relu_maxpool); returns (pooled, saved, argmax taps).  x: the packed NHWC
+        input, or the list of NCHW f32 views (the stem's own convolution kernel, T.stem_conv)."""
+        if isinstance(x, (list, tuple)):
+            z = T.stem_conv(x, self.conv.weight.detach(), code)
+        else:
+            z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
         bn = self.bn
         mean, rstd, sc, sh = T.bn_train_fwd(z, nseg, bn.weight, bn.bias, bn.eps, bn.momentum, bn.running_mean,
                                             bn.running_var)
@@ -150,8 +157,11 @@ class _ConvBN:
         relu_from = (sc, sh) if (self.relu and not has_res) else None
         dz, gres, dgam, dbet = T.bn_train_bwd(gy, mask_y, z, nseg, mean, rstd, self.bn.weight, want_gres=want_gres,
                                               relu_from=relu_from, mask=mask)
-        grads.wgrad(self.conv.weight, lambda: T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride, self.pad,
-                                                             code), dz, x)
+        if isinstance(x, (list, tuple)):   # the stem from the NCHW views (stem_conv): its own kernel
+            grads.wgrad(self.conv.weight, lambda: T.stem_wgrad(x, dz, code), dz, *x)
+        else:
+            grads.wgrad(self.conv.weight, lambda: T.conv2d_wgrad(dz, x, self.cin, self.k, self.k, self.stride,
+                                                                 self.pad, code), dz, x)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
         dx = None
@@ -317,9 +327,12 @@ class TrainPlan:
         if i == 0:
             self.pack()
             n, _, h, w = x[0].shape
-            xin = torch.empty((n * len(x), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(code), device=x[0].device)
-            for k, v in enumerate(x):
-                ops.pack_nchw_to_nhwc(v, code, STEM_CIN_PAD, out=xin[k * n:(k + 1) * n])
+            if FUSED_STEM_POOL and self._stem_kernels(x):
+                xin = [v.contiguous().float() for v in x]
+            else:
+                xin = torch.empty((n * len(x), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(code), device=x[0].device)
+                for k, v in enumerate(x):
+                    ops.pack_nchw_to_nhwc(v, code, STEM_CIN_PAD, out=xin[k * n:(k + 1) * n])
             if FUSED_STEM_POOL:
                 y, s0, idx = self.stem.forward_pooled(xin, nseg, code)
                 saved = {'stem': s0, 'pool_idx': idx, 'blocks': []}
@@ -395,6 +408,16 @@ class TrainPlan:
             self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
             g = None
         return g, grads.close()
+
+    def _stem_kernels(self, views):
+        """The stem's own conv / weight-gradient kernels apply: 2-byte compute dtype, 3-channel 7x7 /
+        s2 / p3 conv1 without bias, 1..8 views of [N, 3, H, 256] with H % 8 == 0."""
+        from ._native import BF16, F16
+        c = self.stem.conv
+        n, ch, h, w = views[0].shape
+        return (STEM_KERNELS and self.code in (BF16, F16) and 1 <= len(views) <= 8 and ch == 3 and w == 256
+                and h % 8 == 0 and tuple(c.weight.shape) == (64, 3, 7, 7) and c.stride == (2, 2)
+                and c.padding == (3, 3) and c.bias is None)
 
     def _bns(self):
         out = [u.bn for u in self.units()] + [d.bn for d in self.deconvs]

@@ -237,6 +237,29 @@ def test_fused_stem_bn_relu_maxpool_equals_the_two_pass_path(cuda, code, shape):
     assert torch.equal(gx, gx_ref)
 
 
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('nv,n,h', [(1, 2, 16), (4, 2, 24), (3, 1, 8), (2, 3, 64)])
+def test_training_stem_conv_and_weight_gradient(cuda, code, nv, n, h):
+    """ABI 14: the training stem's own kernels straight from NCHW f32 views -- the raw 7x7 / s2 / p3
+    convolution and its weight gradient -- against torch autograd on the dtype-rounded operands."""
+    g = torch.Generator().manual_seed(43)
+    views = [torch.randn(n, 3, h, 256, generator=g) for _ in range(nv)]
+    wt = torch.randn(64, 3, 7, 7, generator=g) * 0.1
+    dt = ops.torch_dtype(code)
+    x = torch.cat([v.to(dt).float() for v in views])   # the kernels round the input to the dtype
+    wr = wt.to(dt).float().requires_grad_(True)
+    y = F.conv2d(x, wr, stride=2, padding=3)
+    dy = torch.randn(y.shape, generator=g).to(dt).float()
+    (dw_ref,) = torch.autograd.grad(y, wr, dy)
+    vd = [v.to(cuda) for v in views]
+    z = T.stem_conv(vd, wt.to(cuda), code)
+    dw = T.stem_wgrad(vd, _nhwc(dy, cuda, dt), code)
+    torch.cuda.synchronize()
+    assert z.shape == (nv * n, h // 2, 128, 64) and dw.shape == (64, 3, 7, 7)
+    _close_lowp(_nchw(z), y.detach(), 0.01)
+    torch.testing.assert_close(dw.cpu(), dw_ref, atol=2e-3 * dw_ref.abs().max().item(), rtol=1e-3)
+
+
 def test_channel_sum(cuda):
     g = torch.Generator().manual_seed(15)
     x = torch.randn(3, 17, 11, 64, generator=g)

@@ -44,6 +44,8 @@ def main():
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--first', default='pack_weights', help='substring of the first kernel of a step')
     ap.add_argument('--launches', action='store_true')
+    ap.add_argument('--gaps', type=float, default=0.0,
+                    help='also list the idle intervals (no kernel on any stream) longer than this many us')
     a = ap.parse_args()
     rows = []
     with open(a.csv) as f:
@@ -77,8 +79,23 @@ def main():
     for c, v in sorted(cat.items(), key=lambda x: -x[1]):
         print('  %-18s %9.1f us' % (c, v / k))
     if a.launches:
+        t0 = steps[-1][0][0]
         for s, e, n in steps[-1]:
-            print('%9.1f us  %s' % ((e - s) / 1e3, short(n)))
+            print('%9.1f us  %s  @%.1f' % ((e - s) / 1e3, short(n), (s - t0) / 1e3))
+    if a.gaps > 0:
+        st = sorted(steps[-1])
+        end, prev, total = None, None, 0.0
+        print('idle intervals > %.1f us in the last step:' % a.gaps)
+        for s, e, n in st:
+            if end is not None and s > end:
+                g = (s - end) / 1e3
+                total += g
+                if g > a.gaps:
+                    print('  %8.1f us idle @%.1f after %s, before %s' % (g, (end - st[0][0]) / 1e3, short(prev),
+                                                                      short(n)))
+            if end is None or e > end:
+                end, prev = e, n
+        print('  idle total %.1f us' % total)
 
 
 if __name__ == '__main__':
