@@ -640,17 +640,28 @@ __global__ __launch_bounds__(kWgThreads, 2) void stem_wgrad_kernel(StemViews xs,
           make_float4(acc[mt][hf][0], acc[mt][hf][1], acc[mt][hf][2], acc[mt][hf][3]);
 }
 
-// dw[co][ci][kh][kw] (the parameter's layout) = sum over blocks b (in order) of part[b][kh][kw * 4 + ci][co]
+// dw[co][ci][kh][kw] (the parameter's layout) = sum over the blocks' partials in a fixed order: a
+// 256-thread block owns 16 consecutive co of one (kh, kw, ci); lane sl of an output sums blocks
+// sl, sl + 16, .. (loads in flight together), then the 16 lanes combine in lane order via LDS
+constexpr int kWrLanes = 16;
 __global__ __launch_bounds__(256) void stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblocks,
                                                                  float* __restrict__ dw) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= 64 * 147) return;
-  const int co = t & 63, rest = t >> 6;          // rest = (kh * 7 + kw) * 3 + ci
+  __shared__ float red[kWrLanes][17];
+  const int c = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int rest = blockIdx.x >> 2, co = (blockIdx.x & 3) * 16 + c;   // rest = (kh * 7 + kw) * 3 + ci
   const int ci = rest % 3, tap = rest / 3, kh = tap / 7, kw = tap - 7 * kh;
   const float* p = part + (kh * 32 + kw * 4 + ci) * 64 + co;
   float s = 0.f;
-  for (int b = 0; b < nblocks; ++b) s += p[static_cast<size_t>(b) * kWgPart];
-  dw[((co * 3 + ci) * 7 + kh) * 7 + kw] = s;
+#pragma unroll 4
+  for (int b = sl; b < nblocks; b += kWrLanes) s += p[static_cast<size_t>(b) * kWgPart];
+  red[sl][c] = s;
+  __syncthreads();
+  if (threadIdx.x < 16) {
+    float t = 0.f;
+#pragma unroll
+    for (int l = 0; l < kWrLanes; ++l) t += red[l][threadIdx.x];
+    dw[((co * 3 + ci) * 7 + kh) * 7 + kw] = t;
+  }
 }
 
 }  // namespace
@@ -782,6 +793,6 @@ extern "C" int posu_stem_wgrad_views(int dtype, const float* const* views, int n
   else
     hipLaunchKernelGGL(stem_wgrad_kernel<f16_t>, grid, dim3(kWgThreads), 0, s, xs, Nv, H, strips,
                        static_cast<const f16_t*>(dz), part);
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3((64 * 147 + 255) / 256), dim3(256), 0, s, part, N * strips, dw);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(147 * 4), dim3(256), 0, s, part, N * strips, dw);
   return check_launch("posu_stem_wgrad_views");
 }
