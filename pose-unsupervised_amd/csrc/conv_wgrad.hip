@@ -114,6 +114,17 @@ __device__ __forceinline__ void wg_barrier() {
 #define POSU_WG_SLOTS 2
 #endif
 constexpr int kWgSlots = POSU_WG_SLOTS;
+// pixel-stage groups per block (round 5): KG groups of four waves take alternate pixel stages,
+// each through its own S-slot ring, and add their f32 tiles in LDS at the end -- twice the waves
+// issuing MFMAs and DMAs per CU at the same partial traffic (one partial tile per block)
+#ifndef POSU_WG_KG
+#define POSU_WG_KG 2
+#endif
+constexpr int kWgKG = POSU_WG_KG;
+// pixels per LDS stage of the 2-byte kernels (A/B knob)
+#ifndef POSU_WG_BP2
+#define POSU_WG_BP2 64
+#endif
 
 // chunk swizzle of LDS row `row` for rows of CG 16-byte chunks (see the header)
 template <int ES, int CG>
@@ -174,12 +185,13 @@ __device__ __forceinline__ float frag_f32(const char* tile, int ks, int c0, int 
   return *reinterpret_cast<const float*>(tile + r * ROWB + ((chunk ^ swz_row<4, CG>(r)) << 4) + (col & 3) * 4);
 }
 
-// BM x BN tile of dW, 4 waves in a 2 x 2 grid, BP pixels per LDS stage, S-slot ring
-template <typename T, int BM, int BN, int S>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
+// BM x BN tile of dW, 4 waves in a 2 x 2 grid, BP pixels per LDS stage, S-slot ring; KG such
+// groups take pixel stages kg, kg + KG, .. (lockstep: one workgroup barrier per round)
+template <typename T, int BM, int BN, int S, int KG>
+__global__ __launch_bounds__(256 * KG) void conv_wgrad_kernel(WgradGeom g) {
   constexpr int ES = static_cast<int>(sizeof(T));
   constexpr int E = 16 / ES;
-  constexpr int BP = ES == 2 ? 64 : 32;
+  constexpr int BP = ES == 2 ? POSU_WG_BP2 : 32;
   constexpr int RG = BM * ES, RX = BN * ES;  // LDS row bytes
   constexpr int CGG = RG / 16, CGX = RX / 16;
   constexpr int G_BYTES = BP * RG, STAGE = BP * (RG + RX);
@@ -188,9 +200,11 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
   constexpr int KSTEP = WOp<T>::KSTEP;
   static_assert(DG >= 1 && DX >= 1 && DG * 4096 == G_BYTES && DX * 4096 == BP * RX, "tile / DMA split");
   static_assert(S >= 2 && S <= 4 && (DG + DX) * (S - 2) < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) char smem[S * STAGE];
+  static_assert(KG == 1 || KG * S * STAGE >= 4 * BM * BN, "the groups' tiles fit in the rings");
+  __shared__ __attribute__((aligned(16))) char smem[KG * S * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int kg = __builtin_amdgcn_readfirstlane(tid >> 8), wid = (tid >> 6) & 3;
   const int wm = wid >> 1, wn = wid & 1;
 
   // XCD-aware order: consecutive tile ids on one XCD (its L2 holds the shared G rows)
@@ -207,7 +221,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
 
   const u32x4 grs = make_srd(g.g, g.P * g.M * ES);
   const u32x4 xrs = make_srd(g.x, g.N * g.H * g.W * g.C * ES);
-  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)smem));
+  // this group's ring
+  char* const ring = smem + kg * S * STAGE;
+  const unsigned lds0 = static_cast<unsigned>(reinterpret_cast<size_t>((__attribute__((address_space(3))) char*)ring));
   const unsigned wid_u = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(wid));
 
   // per-thread DMA slots: G slot d covers tile bytes (4d + wid) KiB + 16 lane
@@ -239,11 +255,14 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
     }
   }
 
-  const int nst = (pend - pbeg + BP - 1) / BP;
+  const int nst_all = (pend - pbeg + BP - 1) / BP;
+  // this group's stages: kg, kg + KG, ..; local stage i is global stage kg + KG i
+  const int nst = nst_all > kg ? (nst_all - kg + KG - 1) / KG : 0;
+  const int rounds = (nst_all + KG - 1) / KG;
 
 #define POSU_WG_DMA(ST, BUF)                                                                        \
   {                                                                                                 \
-    const int pb = pbeg + (ST) * BP;                                                                \
+    const int pb = pbeg + (kg + KG * (ST)) * BP;                                                    \
     const unsigned Gs_ = lds0 + (BUF) * STAGE + wid_u * 1024;                                       \
     const unsigned Xs_ = lds0 + (BUF) * STAGE + G_BYTES + wid_u * 1024;                             \
     _Pragma("unroll") for (int d = 0; d < DG; ++d) {                                                \
@@ -275,11 +294,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
   // S-slot ring: stages st+1 .. st+S-2 stay in flight while stage st is consumed; the
   // barrier publishes stage st and frees slot (st - 1) % S for stage st + S - 1
   for (int s0 = 0; s0 < S - 1 && s0 < nst; ++s0) POSU_WG_DMA(s0, s0);
-  for (int st = 0; st < nst; ++st) {
-    vm_wait_stages<DG + DX>(min(S - 2, nst - 1 - st));
+  for (int st = 0; st < rounds; ++st) {
+    // a group with no stage left this round still joins the round's barrier
+    if (st < nst) vm_wait_stages<DG + DX>(min(S - 2, nst - 1 - st));
     wg_barrier();
+    if (st >= nst) continue;
     if (st + S - 1 < nst) POSU_WG_DMA(st + S - 1, (st + S - 1) % S);
-    const char* Gs = smem + (st % S) * STAGE;
+    const char* Gs = ring + (st % S) * STAGE;
     const char* Xs = Gs + G_BYTES;
 #pragma unroll
     for (int ks = 0; ks < BP; ks += KSTEP) {
@@ -308,6 +329,34 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(WgradGeom g) {
   }
 #undef POSU_WG_DMA
 
+  if constexpr (KG > 1) {
+    // groups 1 .. KG-1 hand their tiles to group 0 through the (now idle) rings, lane-major per
+    // wave (16-B per lane and fragment); group 0 adds them in group order
+    wg_barrier();
+    float4* xch = reinterpret_cast<float4*>(smem);
+    if (kg > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          xch[(((kg - 1) * 4 + wid) * TM * TN + i * TN + j) * 64 + lane] =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    wg_barrier();
+    if (kg > 0) return;
+#pragma unroll
+    for (int h = 1; h < KG; ++h)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float4 v = xch[(((h - 1) * 4 + wid) * TM * TN + i * TN + j) * 64 + lane];
+          acc[i][j][0] += v.x;
+          acc[i][j][1] += v.y;
+          acc[i][j][2] += v.z;
+          acc[i][j][3] += v.w;
+        }
+  }
   // lane holds dW[m0 + .. + (lane & 15)][n .. n+3]: one 16-B store per fragment
   float* out = g.part + static_cast<size_t>(split) * g.Mpad * g.Npad;
 #pragma unroll
@@ -373,12 +422,15 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 // f32 partial tile, so more blocks cost partial traffic (2 x 67 MB at 1024 blocks); measured
 // per training step (weight gradients on the side stream): 128 blocks 23.06 ms, 192 22.21,
 // 256 21.97, 384 22.03, 512 22.12, 1024 22.76, 2048 23.69
-constexpr int kWgradBlocks = 256;
+#ifndef POSU_WG_BLOCKS
+#define POSU_WG_BLOCKS 128
+#endif
+constexpr int kWgradBlocks = POSU_WG_BLOCKS;
 
 template <typename T, int BM, int BN>
 void launch_wgrad(WgradGeom& g, hipStream_t s) {
   constexpr int ES = static_cast<int>(sizeof(T));
-  constexpr int BP = ES == 2 ? 64 : 32;
+  constexpr int BP = ES == 2 ? POSU_WG_BP2 : 32;
   g.mtiles = (g.M + BM - 1) / BM;
   g.ntiles = (g.K + BN - 1) / BN;
   g.Mpad = g.mtiles * BM;
@@ -390,7 +442,8 @@ void launch_wgrad(WgradGeom& g, hipStream_t s) {
   const int stages_per_split = (pst + splits - 1) / splits;
   g.pps = stages_per_split * BP;
   g.splits = (g.P + g.pps - 1) / g.pps;
-  hipLaunchKernelGGL((conv_wgrad_kernel<T, BM, BN, kWgSlots>), dim3(tiles * g.splits), dim3(256), 0, s, g);
+  hipLaunchKernelGGL((conv_wgrad_kernel<T, BM, BN, kWgSlots, kWgKG>), dim3(tiles * g.splits), dim3(256 * kWgKG), 0, s,
+                     g);
 }
 
 template <typename T>

@@ -1,0 +1,21 @@
+#!/bin/bash
+# weight-gradient variants (KG pixel-stage groups, blocks per launch, pixels per stage): micro + step
+OUT=gpurun_out/r5ap
+mkdir -p $OUT
+VS="main b96 b160 bp32b192 kg1b128"
+for v in $VS; do
+  if [ $v = main ]; then L=""; else L="--lib pose-unsupervised_amd/build/ab7/libposeu_$v.so"; fi
+  echo "== $v" >> $OUT/micro.txt
+  timeout -k 10 200 python -u tools/wgrad_micro.py $L >> $OUT/micro.txt 2> $OUT/micro_$v.err || exit $?
+done
+for r in 1 2; do
+  for v in $VS; do
+    if [ $v = main ]; then L=""; else L="tools/with_lib.py pose-unsupervised_amd/build/ab7/libposeu_$v.so"; fi
+    timeout -k 10 300 python -u $L bench.py --mode train --steps 20 --warmup 3 > $OUT/${v}_$r.json 2> $OUT/${v}_$r.err || exit $?
+    python - "$OUT/${v}_$r.json" "$v run $r" <<'PY' | tee -a $OUT/ab.txt
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], 'ms_per_step', d['ms_per_step'], 'value', d['value'])
+PY
+  done
+done
