@@ -77,13 +77,16 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     """{class: (read_bytes, write_bytes)} of one training step of n frames (posu.train_plan's launch
     classes): per conv + BatchNorm unit -- conv: x (a stride-2 1x1 only its stride-2 pixels) and the
     packed weight read, z written; BN statistics: z read; BN apply: z (+ the residual) read, y
-    written; backward: BN partial sums and BN apply each read gy and z (+ y where the ReLU follows a
-    residual add), the apply writing dz (+ the residual branch's gradient); weight gradient: dz and x
+    written; backward: BN partial sums and BN apply each read gy and z (+ the ReLU bit mask, 1/16 of
+    y, where the ReLU follows a residual add: written by that unit's forward apply), the apply writing
+    dz (+ the residual branch's gradient); weight gradient: dz and x
     read, the f32 weight gradient written; data gradient: dz and the packed weight read, dx written
     (+ read where it accumulates into the identity branch's gradient).  Max-pool, the 1x1 head,
     packing (f32 parameters read, forward + data-gradient packs written) and Adam (parameters,
-    gradients and both moments read, parameters and moments written) complete it.  Every tensor
-    once per launch: the floor the kernels' PMC traffic is compared with."""
+    gradients and both moments read, parameters and moments written) complete it.  The stem (round
+    5): its conv and weight gradient read the f32 NCHW views; BN + ReLU + max-pool is one pass (z
+    read, the pooled activation and its argmax taps written) and the max-pool backward reads the taps.
+    Every tensor once per launch: the floor the kernels' PMC traffic is compared with."""
     cls = {k: [0, 0] for k in ('conv fwd / dgrad', 'conv wgrad', 'batchnorm', 'maxpool', 'weight packing',
                                  'adam (torch)', 'heads / losses')}
 
@@ -95,26 +98,31 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     nparam = [0]
 
     def unit(hw_in, cin, hw_out, cout, k, stride, residual=False, want_gres=False, dx=True, dx_acc=False,
-             relu_after_res=False):
+             relu_after_res=False, stem=False):
         wts = cout * cin * k * k
         nparam[0] += wts + 2 * cout
         xin = act(hw_out, cin) if (k == 1 and stride == 2) else act(hw_in, cin)
+        if stem:
+            xin = n * cin * hw_in * hw_in * 4                             # the f32 NCHW views
         z = act(hw_out, cout)
-        add('conv fwd / dgrad', xin + wts * es, z)                        # conv
+        mask = z // 16 if relu_after_res else 0                           # ReLU bits of y
+        add('conv fwd / dgrad', xin + wts * (4 if stem else es), z)       # conv
         add('batchnorm', z, 0)                                            # statistics
-        add('batchnorm', z + (z if residual else 0), z)                   # apply (+ residual)
-        extra = z if relu_after_res else 0                                # the mask read from y
+        if not stem:                                                      # (the stem: fused with the pool)
+            add('batchnorm', z + (z if residual else 0), z + mask)        # apply (+ residual, + mask)
+        extra = mask                                                      # the mask bits
         add('batchnorm', 2 * z + extra, 0)                                # backward partial sums
         add('batchnorm', 2 * z + extra, z + (z if want_gres else 0))      # backward apply
         add('conv wgrad', z + xin, wts * 4)
         if dx:
             add('conv fwd / dgrad', z + wts * es + (act(hw_in, cin) if dx_acc else 0), act(hw_in, cin))
-        add('weight packing', wts * 4, wts * es * (2 if dx else 1))
+        if not stem:
+            add('weight packing', wts * 4, wts * es * (2 if dx else 1))
 
-    # stem (direct 7x7 over the 8-channel packed input) + max-pool
-    unit(256, 8, 128, 64, 7, 2, dx=False)
-    add('maxpool', act(128, 64), act(64, 64))                            # forward
-    add('maxpool', act(128, 64) + act(64, 64), act(128, 64))             # backward (x, gy -> gx)
+    # stem (7x7 from the f32 views) + BN / ReLU / max-pool in one pass (taps: 1 byte per output)
+    unit(256, 3, 128, 64, 7, 2, dx=False, stem=True)
+    add('maxpool', act(128, 64), act(64, 64) + act(64, 64) // 2)         # forward: z -> pooled + taps
+    add('maxpool', act(64, 64) // 2 + act(64, 64), act(128, 64))         # backward (taps, gy -> gx)
     hw = 64
     for blocks, planes, cin, cout, hw_in in _R50:
         for b in range(blocks):

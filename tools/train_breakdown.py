@@ -50,8 +50,14 @@ def main():
     rows = []
     with open(a.csv) as f:
         for r in csv.DictReader(f):
-            rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name']))
+            rows.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), r['Kernel_Name'],
+                         r.get('Stream_Id') or r.get('Queue_Id') or '?'))
     rows.sort()
+    streams = {}
+    for r in rows:
+        streams.setdefault(r[3], 0)
+    rows_s = rows
+    rows = [r[:3] for r in rows]
     starts = [i for i, r in enumerate(rows) if a.first in r[2]]
     if len(starts) < 2:
         raise SystemExit('fewer than two steps found (first-kernel marker %r)' % a.first)
@@ -78,6 +84,15 @@ def main():
           '%d launches per step' % (k, span / k, busy / k, union / k, len(steps[-1])))
     for c, v in sorted(cat.items(), key=lambda x: -x[1]):
         print('  %-18s %9.1f us' % (c, v / k))
+    # per stream (rocprofv3's Stream_Id / Queue_Id): kernel time and categories of the last steps
+    lo, hi = steps[0][0][0], steps[-1][-1][1]
+    per = collections.defaultdict(lambda: collections.defaultdict(float))
+    for s_, e_, n_, sid in rows_s:
+        if lo <= s_ <= hi:
+            per[sid][category(n_)] += (e_ - s_) / 1e3
+    for sid, cats in sorted(per.items(), key=lambda x: -sum(x[1].values())):
+        print('  stream %s: %.1f us per step (%s)' % (sid, sum(cats.values()) / k,
+              ', '.join('%s %.0f' % (c, v / k) for c, v in sorted(cats.items(), key=lambda x: -x[1]))))
     if a.launches:
         t0 = steps[-1][0][0]
         for s, e, n in steps[-1]:
