@@ -185,6 +185,15 @@ def init_ranks(args, backend, device=None):
     return rank, local, world, dist
 
 
+def rank_device(local):
+    """(this rank's GPU, process-group backend): cuda:LOCAL_RANK over RCCL ('nccl').  Rehearsal of
+    the N-rank path on a box with fewer GPUs (POSU_SHARED_GPU_REHEARSAL=1, never the measured
+    line): ranks share the GPUs round-robin and talk over gloo (RCCL refuses two ranks on one GPU)."""
+    if os.environ.get('POSU_SHARED_GPU_REHEARSAL') == '1':
+        return torch.device('cuda', local % max(1, torch.cuda.device_count())), 'gloo'
+    return torch.device('cuda', local), 'nccl'
+
+
 def gather_per_rank(values, dist, device='cpu'):
     """All ranks' small float vectors (rank order), e.g. [frames, seconds]."""
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
@@ -701,9 +710,9 @@ def time_configs4(args, dev, rank, world, dist):
 def infer_main(args):
     from posu import dist as pdist
     _, local, world = pdist.env_rank()
-    dev = torch.device('cuda', local)
+    dev, backend = rank_device(local)
     torch.cuda.set_device(dev)
-    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
+    rank, local, world, dist = init_ranks(args, backend, device=dev)
     frames = 4 * args.groups
     res = time_pipeline(args, args.precision, dev, rank, args.steps, args.warmup, args.batches,
                         not args.no_autotune, dist, world)
@@ -836,6 +845,8 @@ def infer_main(args):
         'configs1': c1, 'configs4': c4, 'control': control, 'train_mode': train,
         'roofline': roof, 'cpu_baseline': cpu,
     }
+    if os.environ.get('POSU_SHARED_GPU_REHEARSAL') == '1':
+        line['shared_gpu_rehearsal'] = 'ranks share GPUs over gloo: a plumbing rehearsal, not a measurement'
     print(json.dumps(line, default=_json_default))
     if dist is not None:
         dist.destroy_process_group()
@@ -991,9 +1002,9 @@ def train_main(args):
     """`--mode train`: the configs[3] training step as the bench line."""
     from posu import dist as pdist
     _, local, _ = pdist.env_rank()
-    dev = torch.device('cuda', local)
+    dev, backend = rank_device(local)
     torch.cuda.set_device(dev)
-    rank, local, world, dist = init_ranks(args, 'nccl', device=dev)
+    rank, local, world, dist = init_ranks(args, backend, device=dev)
     line = run_training(args, dev, rank, world, dist, args.steps, args.warmup)
     if rank == 0:
         print(json.dumps(line, default=_json_default))
