@@ -650,10 +650,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const uint8_t* __restr
         const long long o = ((n * Ho + oy) * Wo + ox) * C + ch * E;
         float g[E];
         Vec<T>::unpack(*reinterpret_cast<const uint4*>(gy + o), g);
-        const int tap = dy * 3 + dx;
+        const unsigned tap = dy * 3 + dx;
+        // the chunk's E taps in one 4- / 8-byte load (o is a multiple of E)
+        unsigned long long tv;
+        if constexpr (E == 8) tv = *reinterpret_cast<const unsigned long long*>(idx + o);
+        else tv = *reinterpret_cast<const unsigned*>(idx + o);
 #pragma unroll
         for (int e = 0; e < E; ++e)
-          if (idx[o + e] == tap) acc[e] += g[e];
+          if (((tv >> (8 * e)) & 0xffu) == tap) acc[e] += g[e];
       }
     }
     *reinterpret_cast<uint4*>(gx + pix * C + ch * E) = Vec<T>::pack(acc);
@@ -932,6 +936,7 @@ extern "C" int posu_bn_relu_maxpool3x3s2_fwd(int dtype, const void* z, int nseg,
 extern "C" int posu_maxpool3x3s2_bwd_idx(int dtype, const void* idx, const void* gy, int N, int H, int W, int C,
                                          void* gx, void* stream) {
   POSU_REQUIRE(idx && gy && gx, "posu_maxpool3x3s2_bwd_idx: null pointer");
+  POSU_REQUIRE((reinterpret_cast<size_t>(idx) & 7) == 0, "posu_maxpool3x3s2_bwd_idx: idx must be 8-byte aligned");
   POSU_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_maxpool3x3s2_bwd_idx: bad shape");
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipStream_t s = as_stream(stream);

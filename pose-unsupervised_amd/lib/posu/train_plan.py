@@ -41,6 +41,9 @@ FUSED_STEM_POOL = True
 # round 5: the stem's convolution and weight gradient as their own kernels, straight from the NCHW
 # f32 views (no NHWC pack; the generic 8-channel-padded conv / weight gradient took 260 / 477 us)
 STEM_KERNELS = True
+# round 5: with the stem's own kernels (which read the f32 parameter) the step's weight packing
+# runs on the side stream beside the stem's forward; layer1 waits for it
+PACK_BESIDE_STEM = True
 
 
 def _conv_tuned(x, w, cout, k, stride, pad, code):
@@ -325,9 +328,24 @@ class TrainPlan:
         (heatmaps NCHW f32, deconv output NHWC)."""
         code = self.code
         if i == 0:
-            self.pack()
             n, _, h, w = x[0].shape
-            if FUSED_STEM_POOL and self._stem_kernels(x):
+            stem_own = FUSED_STEM_POOL and self._stem_kernels(x)
+            packed = None
+            if stem_own and PACK_BESIDE_STEM and SIDE_STREAM_WGRAD:
+                # the side stream takes the pack after everything before it on this stream (Adam);
+                # the stem needs no packed weight, layer1 waits for the pack below
+                dev = x[0].device
+                if self.side is None:
+                    self.side = torch.cuda.Stream(dev)
+                main = torch.cuda.current_stream(dev)
+                self.side.wait_stream(main)
+                with torch.cuda.stream(self.side):
+                    self.pack()
+                packed = torch.cuda.Event()
+                packed.record(self.side)
+            else:
+                self.pack()
+            if stem_own:
                 xin = [v.contiguous().float() for v in x]
             else:
                 xin = torch.empty((n * len(x), h, w, STEM_CIN_PAD), dtype=ops.torch_dtype(code), device=x[0].device)
@@ -340,6 +358,8 @@ class TrainPlan:
                 a0, s0 = self.stem.forward(xin, nseg, code)
                 y = ops.maxpool3x3s2_nhwc(a0, code)
                 saved = {'stem': s0, 'pool_in': a0, 'blocks': []}
+            if packed is not None:
+                torch.cuda.current_stream(x[0].device).wait_event(packed)
             for b in self.layers[0]:
                 y, sb = b.forward(y, nseg, code)
                 saved['blocks'].append(sb)
