@@ -44,6 +44,9 @@ STEM_KERNELS = True
 # round 5: with the stem's own kernels (which read the f32 parameter) the step's weight packing
 # runs on the side stream beside the stem's forward; layer1 waits for it
 PACK_BESIDE_STEM = True
+# round 5: a first block's downsample unit (conv + BN statistics + apply) runs on the side stream
+# beside its conv1 / conv2 units in the forward (the side stream is idle until the backward)
+DOWN_BESIDE = True
 
 
 def _conv_tuned(x, w, cout, k, stride, pad, code):
@@ -187,15 +190,34 @@ class _Block:
     def all_units(self):
         return self.units + ([self.down] if self.down is not None else [])
 
-    def forward(self, x, nseg, code):
+    def forward(self, x, nseg, code, side=None):
         saved = []
         res, sd = x, None
+        joined = None
         if self.down is not None:
-            res, sd = self.down.forward(x, nseg, code)
+            if side is not None:
+                # the downsample unit beside conv1 / conv2: the side stream starts after x exists; its
+                # tensors are used on the main stream (conv3's residual add, the backward), so the
+                # allocator is told (record_stream), and x is read on the side stream
+                main = torch.cuda.current_stream(x.device)
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    res, sd = self.down.forward(x, nseg, code)
+                joined = torch.cuda.Event()
+                joined.record(side)
+                x.record_stream(side)
+                for t in sd[1:]:
+                    if torch.is_tensor(t):
+                        t.record_stream(main)
+                res.record_stream(main)
+            else:
+                res, sd = self.down.forward(x, nseg, code)
         y = x
         for u in self.units[:-1]:
             y, s = u.forward(y, nseg, code)
             saved.append(s)
+        if joined is not None:
+            torch.cuda.current_stream(x.device).wait_event(joined)
         y, s = self.units[-1].forward(y, nseg, code, residual=res)
         saved.append(s)
         return y, (saved, sd)
@@ -361,7 +383,7 @@ class TrainPlan:
             if packed is not None:
                 torch.cuda.current_stream(x[0].device).wait_event(packed)
             for b in self.layers[0]:
-                y, sb = b.forward(y, nseg, code)
+                y, sb = b.forward(y, nseg, code, self._down_side(y))
                 saved['blocks'].append(sb)
             # num_batches_tracked += nseg for every BatchNorm (the reference's V backbone calls
             # each add 1): one multi-tensor launch instead of one tiny kernel per layer
@@ -373,7 +395,7 @@ class TrainPlan:
             saved = []
             y = x
             for b in self.layers[i]:
-                y, sb = b.forward(y, nseg, code)
+                y, sb = b.forward(y, nseg, code, self._down_side(y))
                 saved.append(sb)
             return y, saved
         saved = []
@@ -428,6 +450,15 @@ class TrainPlan:
             self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
             g = None
         return g, grads.close()
+
+    def _down_side(self, x):
+        """The side stream for DOWN_BESIDE (created on first use), or None."""
+        from .plan import _Tuner
+        if not (DOWN_BESIDE and SIDE_STREAM_WGRAD) or _Tuner.active:   # (tile trials time alone)
+            return None
+        if self.side is None:
+            self.side = torch.cuda.Stream(x.device)
+        return self.side
 
     def _stem_kernels(self, views):
         """The stem's own conv / weight-gradient kernels apply: 2-byte compute dtype, 3-channel 7x7 /
