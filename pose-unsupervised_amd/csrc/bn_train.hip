@@ -49,6 +49,19 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
   return r;
 }
 
+// 16 B at p + off when `ok`, else zeros; a byte of m at i when `ok`, else 0.  Loaded from a valid
+// address (`alt` when not ok) and selected by value: a select between *p and a local zero becomes
+// a select of addresses, which puts the zero in scratch (the f16 / f32 kernels had 32 B of it)
+template <typename T>
+__device__ __forceinline__ uint4 ld16_if(bool ok, const T* p, const T* alt, size_t off) {
+  const uint4 v = *reinterpret_cast<const uint4*>((ok ? p : alt) + off);
+  return ok ? v : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ unsigned ld8_if(bool ok, const uint8_t* m, const void* alt, size_t i) {
+  const unsigned v = (ok ? m : static_cast<const uint8_t*>(alt))[i];
+  return ok ? v : 0u;
+}
+
 // MODE 0: (sum (z - K), sum (z - K)^2) -- forward statistics / channel sums; K = the
 //         segment's first pixel when kout is non-null (shifted sums: a channel whose
 //         mean is large against its spread keeps its variance in the f32 partials),
@@ -150,8 +163,8 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
         const size_t off = sbase + static_cast<size_t>(p + u * rs.PL) * C;
         zq[u] = *reinterpret_cast<const uint4*>(z + off);
         gq[u] = MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero;
-        yq[u] = MODE == 1 && y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero;
-        mq[u] = MODE == 1 && ym ? ym[off / E] : 0u;
+        yq[u] = ld16_if(MODE == 1 && y && !ym, y, z, off);
+        mq[u] = ld8_if(MODE == 1 && ym, ym, z, off / E);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) acc(zq[u], gq[u], yq[u], mq[u]);
@@ -159,7 +172,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
     for (; p < pend; p += rs.PL) {
       const size_t off = sbase + static_cast<size_t>(p) * C;
       acc(*reinterpret_cast<const uint4*>(z + off), MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero,
-          MODE == 1 && y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero, MODE == 1 && ym ? ym[off / E] : 0u);
+          ld16_if(MODE == 1 && y && !ym, y, z, off), ld8_if(MODE == 1 && ym, ym, z, off / E));
     }
   }
 #pragma unroll
@@ -373,21 +386,20 @@ __global__ __launch_bounds__(256) void bn_apply_seg_kernel(const T* __restrict__
       ms[i] = pos_bits<T>(v);
     }
   };
-  const uint4 zero = make_uint4(0, 0, 0, 0);
   int i = blockIdx.x * 256 + threadIdx.x;
   for (; i + (U - 1) * stride < n; i += U * stride) {
     uint4 zq[U], rq[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       zq[u] = *reinterpret_cast<const uint4*>(zs + static_cast<size_t>(i + u * stride) * E);
-      rq[u] = rs ? *reinterpret_cast<const uint4*>(rs + static_cast<size_t>(i + u * stride) * E) : zero;
+      rq[u] = ld16_if(rs != nullptr, rs, zs, static_cast<size_t>(i + u * stride) * E);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) one(i + u * stride, zq[u], rq[u]);
   }
   for (; i < n; i += stride)
     one(i, *reinterpret_cast<const uint4*>(zs + static_cast<size_t>(i) * E),
-        rs ? *reinterpret_cast<const uint4*>(rs + static_cast<size_t>(i) * E) : zero);
+        ld16_if(rs != nullptr, rs, zs, static_cast<size_t>(i) * E));
 }
 
 template <typename T>
@@ -442,7 +454,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
     }
     *reinterpret_cast<uint4*>(dz + off) = Vec<T>::pack(v);
   };
-  const uint4 zero = make_uint4(0, 0, 0, 0);
   int i = blockIdx.x * 256 + threadIdx.x;
   for (; i + (U - 1) * stride < n; i += U * stride) {
     uint4 gq[U], zq[U], yq[U];
@@ -452,8 +463,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
       const size_t off = sb + static_cast<size_t>(i + u * stride) * E;
       gq[u] = *reinterpret_cast<const uint4*>(gy + off);
       zq[u] = *reinterpret_cast<const uint4*>(z + off);
-      yq[u] = y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero;
-      mq[u] = ym ? ym[off / E] : 0u;
+      yq[u] = ld16_if(y && !ym, y, z, off);
+      mq[u] = ld8_if(ym != nullptr, ym, z, off / E);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) one(i + u * stride, gq[u], zq[u], yq[u], mq[u]);
@@ -461,7 +472,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_seg_kernel(const T* __restri
   for (; i < n; i += stride) {
     const size_t off = sb + static_cast<size_t>(i) * E;
     one(i, *reinterpret_cast<const uint4*>(gy + off), *reinterpret_cast<const uint4*>(z + off),
-        y && !ym ? *reinterpret_cast<const uint4*>(y + off) : zero, ym ? ym[off / E] : 0u);
+        ld16_if(y && !ym, y, z, off), ld8_if(ym != nullptr, ym, z, off / E));
   }
 }
 

@@ -531,12 +531,15 @@ __global__ __launch_bounds__(kWgThreads, 2) void stem_wgrad_kernel(StemViews xs,
     const int i = tid + it * kWgThreads;
     const int r = i / kWgGroups, g = i - r * kWgGroups;
     const int iy = iy0 + r, c0 = 4 * (g - 1);
+    // a load from a valid address (the image's first pixels when outside) and a value select: a
+    // conditional load into zeros made the compiler keep the zeros in scratch
+    const bool ok = i < nr * kWgGroups && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
+                    static_cast<unsigned>(c0) < static_cast<unsigned>(W);
+    const size_t o = ok ? static_cast<size_t>(iy) * W + c0 : 0;
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl) xv[pl] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (i < nr * kWgGroups && static_cast<unsigned>(iy) < static_cast<unsigned>(H) &&
-        static_cast<unsigned>(c0) < static_cast<unsigned>(W)) {
-#pragma unroll
-      for (int pl = 0; pl < 3; ++pl) xv[pl] = *reinterpret_cast<const float4*>(xn + pl * plane + static_cast<size_t>(iy) * W + c0);
+    for (int pl = 0; pl < 3; ++pl) {
+      const float4 v = *reinterpret_cast<const float4*>(xn + pl * plane + o);
+      xv[pl] = ok ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
   auto store_x = [&](int iy0, int nr, int it, const float4 (&xv)[3]) {
@@ -544,14 +547,14 @@ __global__ __launch_bounds__(kWgThreads, 2) void stem_wgrad_kernel(StemViews xs,
     if (i >= nr * kWgGroups) return;
     const int r = i / kWgGroups, g = i - r * kWgGroups;
     char* row = ring + ((iy0 + r) & (kWgRing - 1)) * kWgRB;
-    const float a0[4] = {xv[0].x, xv[0].y, xv[0].z, xv[0].w};
-    const float a1[4] = {xv[1].x, xv[1].y, xv[1].z, xv[1].w};
-    const float a2[4] = {xv[2].x, xv[2].y, xv[2].z, xv[2].w};
+    // (components by compile-time index: arrays of them went to scratch)
+    auto cmp = [](const float4& v, int e) { return e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w; };
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int wc = 4 * g - 1 + e;
       if (wc >= 0 && wc < kWgCols)
-        *reinterpret_cast<uint2*>(row + wc * 8) = make_uint2(O::pack2(a0[e], a1[e]), O::pack2(a2[e], 0.f));
+        *reinterpret_cast<uint2*>(row + wc * 8) =
+            make_uint2(O::pack2(cmp(xv[0], e), cmp(xv[1], e)), O::pack2(cmp(xv[2], e), 0.f));
     }
   };
   // dz row oy: 1024 16-B chunks, chunk i = pixel i / 8, channels 8 (i % 8) ..
