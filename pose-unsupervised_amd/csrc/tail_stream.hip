@@ -57,6 +57,13 @@ struct TailSGeom {
 #define POSU_TS_ABLATE 0
 #endif
 constexpr int kAbl = POSU_TS_ABLATE;
+// cache-policy bits of the residual loads / y stores (A/B knobs; 0 = default)
+#ifndef POSU_TS_LD_AUX
+#define POSU_TS_LD_AUX 0
+#endif
+#ifndef POSU_TS_ST_AUX
+#define POSU_TS_ST_AUX 0
+#endif
 
 #ifndef POSU_TS_KD
 #define POSU_TS_KD 4
@@ -324,7 +331,8 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       if (kAbl & 72) {
         rv[i] = make_uint4(i, c0, 0, 0);
       } else {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, 0);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0,
+                                                             POSU_TS_LD_AUX);
         rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
       }
     }
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
       else
         __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, yrs,
-                                               lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, 0);
+                                               lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, POSU_TS_ST_AUX);
       // NEXT: the chunk's y, laid out like t2 ([pixel][P] rows, column-keyed swizzle)
       if constexpr (NEXT)
         *reinterpret_cast<uint4*>(smem + K::kYC + swzp<K::kRowB>(tpix(i), r16, (32 * cq + cpair) >> 3)) = o;
