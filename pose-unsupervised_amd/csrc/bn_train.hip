@@ -6,7 +6,7 @@
 // backward, the bias-gradient channel sum and the stem max-pool backward.
 //
 // Reductions are deterministic: per-block partial sums in f64 written to a workspace,
-// then a data-independent order (lanes over blocks, a fixed xor butterfly) per channel.  Running statistics
+// then a data-independent order (lanes over blocks, then the lanes in order) per channel.  Running statistics
 // follow torch.nn.BatchNorm2d: biased variance for normalisation, unbiased variance in
 // running_var, running = (1 - momentum) * running + momentum * batch, updated once per
 // segment in segment (= view) order like the reference's four backbone calls.
@@ -19,6 +19,9 @@ namespace {
 
 #ifndef POSU_BN_U1
 #define POSU_BN_U1 4    // pixels in flight per thread in the backward partial pass
+#endif
+#ifndef POSU_BN_FIN2
+#define POSU_BN_FIN2 1  // the second finalize form (block per 16 channels, lane sums met in LDS)
 #endif
 #ifndef POSU_BN_SEGU
 #define POSU_BN_SEGU 4  // chunks in flight per thread in the segment-major apply passes
@@ -589,6 +592,174 @@ __global__ __launch_bounds__(256) void channel_sum_finalize_kernel(const double*
   if (ln == 0 && c < C) out[c] = static_cast<float>(s[0]);
 }
 
+// ---- finalize, second form (POSU_BN_FIN2, the default): the passes above took 12 us per launch
+// in the training step (112 launches, 1.3 ms of the main stream) for a few hundred KiB of
+// partials: half-waves of one channel gather 32 scattered lines per load, under per-segment
+// branches.  Here a block serves FC2 consecutive channels: lane ln of channel cl sums the partial
+// blocks ln, ln + FL2, .. (FIT2 of them per pass, for up to FSEG segments: every load of a pass
+// issued before the first add), a wave's loads covering 4 blocks x 16 channels = 4 lines of
+// 128 B; the FL2 lane sums meet in LDS and thread (k, cl) of wave 0 adds them in lane order (a
+// fixed association), then does segment k's arithmetic -- the segments in parallel, not one
+// lane's serial chain.
+constexpr int FC2 = 16, FL2 = 16, FIT2 = 4;
+constexpr int kFinLds = 2 * FSEG * FL2 * FC2;  // doubles
+
+// returns, in thread t < FSEG * FC2 (segment seg0 + t / FC2, channel c0 + t % FC2), the sums
+// over the partial blocks; zeros elsewhere.  Every thread of the block calls it.
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ part, int seg0, int ns, int NB, int C,
+                                                int c0, double* __restrict__ lds, double& s, double& q) {
+  const int t = threadIdx.x, cl = t % FC2, ln = t / FC2;
+  const int c = c0 + cl;
+  const bool cv = c < C;
+  double a[FSEG], b[FSEG];
+#pragma unroll
+  for (int k = 0; k < FSEG; ++k) a[k] = b[k] = 0.0;
+  for (int base = 0; base < NB; base += FL2 * FIT2) {
+    double va[FSEG][FIT2], vb[FSEG][FIT2];
+#pragma unroll
+    for (int k = 0; k < FSEG; ++k)
+#pragma unroll
+      for (int j = 0; j < FIT2; ++j) {
+        const int blk = base + ln + FL2 * j;
+        const bool ok = cv && k < ns && blk < NB;
+        // a valid address either way, the value selected (no select of a load against a zero)
+        const double* p = part + (ok ? static_cast<size_t>((seg0 + k) * NB + blk) * 2 * C + c : 0);
+        const double x = p[0], y = p[ok ? C : 0];
+        va[k][j] = ok ? x : 0.0;
+        vb[k][j] = ok ? y : 0.0;
+      }
+#pragma unroll
+    for (int k = 0; k < FSEG; ++k)
+#pragma unroll
+      for (int j = 0; j < FIT2; ++j) {
+        a[k] += va[k][j];
+        b[k] += vb[k][j];
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < FSEG; ++k) {
+    lds[((0 * FSEG + k) * FL2 + ln) * FC2 + cl] = a[k];
+    lds[((1 * FSEG + k) * FL2 + ln) * FC2 + cl] = b[k];
+  }
+  __syncthreads();
+  s = q = 0.0;
+  if (t < FSEG * FC2) {
+    const int k = t / FC2;
+#pragma unroll
+    for (int l = 0; l < FL2; ++l) {
+      s += lds[((0 * FSEG + k) * FL2 + l) * FC2 + cl];
+      q += lds[((1 * FSEG + k) * FL2 + l) * FC2 + cl];
+    }
+  }
+  __syncthreads();  // lds is reused by the next call
+}
+
+__global__ __launch_bounds__(256) void bn_stats_finalize2_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                                 int Pseg, int C, const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float eps,
+                                                                 float momentum, const float* __restrict__ kshift,
+                                                                 float* __restrict__ running_mean,
+                                                                 float* __restrict__ running_var,
+                                                                 float* __restrict__ mean, float* __restrict__ rstd,
+                                                                 float* __restrict__ scale,
+                                                                 float* __restrict__ shift) {
+  __shared__ double lds[kFinLds];
+  __shared__ float mus[FSEG][FC2], vus[FSEG][FC2];
+  const int t = threadIdx.x, k = t / FC2, cl = t % FC2;
+  const int c0 = blockIdx.x * FC2, c = c0 + cl;
+  const bool mine = t < FSEG * FC2 && c < C;  // thread (segment k, channel c) of wave 0
+  const double n = static_cast<double>(Pseg);
+  const int cc = c < C ? c : 0;
+  const float gm = gamma ? gamma[cc] : 1.f, bt = beta ? beta[cc] : 0.f;
+  float rm = 0.f, rv = 0.f;
+  if (t < FC2 && c < C) {
+    rm = running_mean ? running_mean[c] : 0.f;
+    rv = running_var ? running_var[c] : 0.f;
+  }
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    const int ns = min(FSEG, nseg - seg0);
+    const bool act = mine && k < ns;
+    const int seg = seg0 + (act ? k : 0);
+    const float ks = kshift[seg * C + cc];  // issued beside the partials
+    double sum, sq;
+    reduce_partials(part, seg0, ns, NB, C, c0, lds, sum, sq);
+    if (act) {
+      const double dm = sum / n;  // shifted by K = kshift[seg][c]
+      const double mu = static_cast<double>(ks) + dm;
+      const double var = fmax(sq / n - dm * dm, 0.0);
+      const double r = 1.0 / sqrt(var + static_cast<double>(eps));
+      mean[seg * C + c] = static_cast<float>(mu);
+      rstd[seg * C + c] = static_cast<float>(r);
+      scale[seg * C + c] = static_cast<float>(gm * r);
+      shift[seg * C + c] = static_cast<float>(bt - mu * gm * r);
+      mus[k][cl] = static_cast<float>(mu);
+      vus[k][cl] = static_cast<float>(Pseg > 1 ? var * n / (n - 1.0) : var);
+    }
+    __syncthreads();
+    if (t < FC2 && c < C)
+      for (int j = 0; j < ns; ++j) {  // in segment order: running stats compose like V calls
+        rm = (1.f - momentum) * rm + momentum * mus[j][t];
+        rv = (1.f - momentum) * rv + momentum * vus[j][t];
+      }
+    __syncthreads();
+  }
+  if (t < FC2 && c < C) {
+    if (running_mean) running_mean[c] = rm;
+    if (running_var) running_var[c] = rv;
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __restrict__ part, int nseg, int NB,
+                                                               int Pseg, int C, const float* __restrict__ gamma,
+                                                               const float* __restrict__ rstd,
+                                                               float* __restrict__ coef, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta) {
+  __shared__ double lds[kFinLds];
+  __shared__ double sgs[FSEG][FC2], sgxs[FSEG][FC2];
+  const int t = threadIdx.x, k = t / FC2, cl = t % FC2;
+  const int c0 = blockIdx.x * FC2, c = c0 + cl;
+  const bool mine = t < FSEG * FC2 && c < C;
+  const double n = static_cast<double>(Pseg);
+  const int cc = c < C ? c : 0;
+  const float gm = gamma ? gamma[cc] : 1.f;
+  double tg = 0.0, tgx = 0.0;
+  for (int seg0 = 0; seg0 < nseg; seg0 += FSEG) {
+    const int ns = min(FSEG, nseg - seg0);
+    const bool act = mine && k < ns;
+    const int seg = seg0 + (act ? k : 0);
+    const float rs = rstd[seg * C + cc];
+    double sg, sgx;
+    reduce_partials(part, seg0, ns, NB, C, c0, lds, sg, sgx);
+    if (act) {
+      coef[(seg * 3 + 0) * C + c] = gm * rs;
+      coef[(seg * 3 + 1) * C + c] = static_cast<float>(sg / n);
+      coef[(seg * 3 + 2) * C + c] = static_cast<float>(sgx / n);
+      sgs[k][cl] = sg;
+      sgxs[k][cl] = sgx;
+    }
+    __syncthreads();
+    if (t < FC2 && c < C)
+      for (int j = 0; j < ns; ++j) {  // segment order
+        tg += sgs[j][t];
+        tgx += sgxs[j][t];
+      }
+    __syncthreads();
+  }
+  if (t < FC2 && c < C) {
+    if (dgamma) dgamma[c] = static_cast<float>(tgx);
+    if (dbeta) dbeta[c] = static_cast<float>(tg);
+  }
+}
+
+__global__ __launch_bounds__(256) void channel_sum_finalize2_kernel(const double* __restrict__ part, int NB, int C,
+                                                                    float* __restrict__ out) {
+  __shared__ double lds[kFinLds];
+  const int t = threadIdx.x, c = blockIdx.x * FC2 + t % FC2;
+  double s, q;
+  reduce_partials(part, 0, 1, NB, C, blockIdx.x * FC2, lds, s, q);
+  if (t < FC2 && c < C) out[c] = static_cast<float>(s);
+}
+
 // ---- max-pool 3x3 / s2 / p1 backward (PyTorch's tie rule: the first maximum in
 // window scan order, pool.h max_pool2d `val > maxval || isnan(val)`).
 // pass 1: argmax tap (0..8) per output element; pass 2: every input element gathers
@@ -778,8 +949,12 @@ extern "C" int posu_bn_train_fwd(int dtype, const void* z, int nseg, int Pseg, i
                        kshift, nullptr);
   });
   POSU_REQUIRE(ok, "posu_bn_train_fwd: unsupported dtype");
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
-                     gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
+  if (POSU_BN_FIN2)
+    hipLaunchKernelGGL(bn_stats_finalize2_kernel, dim3((C + FC2 - 1) / FC2), dim3(256), 0, s, part, nseg, rs.NB, Pseg,
+                       C, gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
+  else
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg,
+                       C, gamma, beta, eps, momentum, kshift, running_mean, running_var, mean, rstd, scale, shift);
   return check_launch("posu_bn_train_fwd");
 }
 
@@ -830,8 +1005,12 @@ int bn_bwd_impl(const char* name, int dtype, const void* gy, const void* y, cons
                        relu_shift, mean, rstd, Pseg, C, rs, part, nullptr, ym);
   });
   POSU_REQUIRE(ok, what + ": unsupported dtype");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C, gamma,
-                     rstd, coef, dgamma, dbeta);
+  if (POSU_BN_FIN2)
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3((C + FC2 - 1) / FC2), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+                       gamma, rstd, coef, dgamma, dbeta);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, nseg, rs.NB, Pseg, C,
+                       gamma, rstd, coef, dgamma, dbeta);
   with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     const int E = chunk_elems(dtype);
@@ -895,7 +1074,10 @@ extern "C" int posu_channel_sum(int dtype, const void* x, int P, int C, float* o
                        nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, P, C, rs, part, nullptr, nullptr);
   });
   POSU_REQUIRE(ok, "posu_channel_sum: unsupported dtype");
-  hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);
+  if (POSU_BN_FIN2)
+    hipLaunchKernelGGL(channel_sum_finalize2_kernel, dim3((C + FC2 - 1) / FC2), dim3(256), 0, s, part, rs.NB, C, out);
+  else
+    hipLaunchKernelGGL(channel_sum_finalize_kernel, dim3((C + FCH - 1) / FCH), dim3(256), 0, s, part, rs.NB, C, out);
   return check_launch("posu_channel_sum");
 }
 
