@@ -68,7 +68,8 @@ const char* posu_last_error(void);
  * bit mask (posu_bn_apply_mask / posu_bn_train_bwd_mask) and the fused stem BN + ReLU + max-pool
  * with stored argmax taps (posu_bn_relu_maxpool3x3s2_fwd / posu_maxpool3x3s2_bwd_idx), the training
  * stem's convolution and weight gradient from the NCHW f32 views (posu_stem_conv_views_fwd /
- * posu_stem_wgrad_views).  The
+ * posu_stem_wgrad_views); 15 (training) the data gradient on a chosen tile
+ * (posu_conv2d_dgrad_tile: the training step autotunes it like the forward convolutions).  The
  * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
@@ -100,10 +101,13 @@ int posu_pack_s2d_nchw(int dtype, const float* x, int N, int C, int H, int W,
  *                     k = tap * pitch + co, value w[co][ci][kh-1-th][kw-1-tw] (co < cout only;
  *                     posu_conv2d_dgrad's weight);
  *   POSU_PACK_DECONV: ConvTranspose2d [cin][cout][4][4] -> [4 classes][rows][kpad],
- *                     k = (ty*2 + tx) * cin + ci (posu_deconv4x4s2_fwd's w).
+ *                     k = (ty*2 + tx) * cin + ci (posu_deconv4x4s2_fwd's w).  ABI 15: also a
+ *                     [cin][cout][3][3] source (kh = kw = 3), read as its 4x4 zero-padding (tap
+ *                     index 3 = 0) -- a Conv2d(3, s2, p1) weight [co][ci][3][3] packed this way
+ *                     makes posu_deconv4x4s2_fwd the conv's data gradient (even H, W).
  * Zero outside the source.  block_start: the job's first block; blocks per job =
  * posu_pack_job_blocks(the job's mode .. kpad fields) (-1: kpad not a multiple of 8, a
- * deconv other than 4x4, or a non-positive size); total_blocks = their sum. */
+ * deconv other than 4x4 / 3x3, or a non-positive size); total_blocks = their sum. */
 #define POSU_PACK_CONV 0
 #define POSU_PACK_DGRAD 1
 #define POSU_PACK_DECONV 2
@@ -490,6 +494,12 @@ int posu_reproject(const double* M, const double* intr, const double* xy, const 
 int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
                       int Cin, int KH, int KW, int stride, int pad, const void* residual,
                       void* dx, int H, int W, void* stream);
+/* ABI 15: the same on tile configuration `tile` (posu_conv2d_fwd's table; -1 = the built-in
+ * heuristic, which posu_conv2d_dgrad runs).  Every tile except 39 accumulates in the same K order,
+ * so the choice changes speed, not results.  Refused: an unknown tile. */
+int posu_conv2d_dgrad_tile(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
+                           int Cin, int KH, int KW, int stride, int pad, const void* residual,
+                           void* dx, int H, int W, int tile, void* stream);
 
 /* Weight gradient dW[Cout][Creal][KH][KW] (f32, the nn.Conv2d weight layout) of a
  * conv over x[N,H,W,C] (C >= Creal, padded channels ignored) with output gradient

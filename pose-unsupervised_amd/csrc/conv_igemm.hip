@@ -1845,10 +1845,22 @@ extern "C" int posu_head1x1_nchw_fwd(int dtype, const void* x, int N, int H, int
 // zero-upsampled image when stride == 2 (g.up), so strided layers run through the same
 // MFMA kernel as the forward.  `residual` (optional, [N,H,W,Cin]) is added in the
 // epilogue: the identity-branch gradient of a residual block.
+extern "C" int posu_conv2d_dgrad_tile(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
+                                      int Cin, int KH, int KW, int stride, int pad, const void* residual, void* dx,
+                                      int H, int W, int tile, void* stream);
+
 extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
                                  int Cin, int KH, int KW, int stride, int pad, const void* residual, void* dx, int H,
                                  int W, void* stream) {
+  return posu_conv2d_dgrad_tile(dtype, dy, N, Ho, Wo, Cout, wt, Cin, KH, KW, stride, pad, residual, dx, H, W, -1,
+                                stream);
+}
+
+extern "C" int posu_conv2d_dgrad_tile(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
+                                      int Cin, int KH, int KW, int stride, int pad, const void* residual, void* dx,
+                                      int H, int W, int tile, void* stream) {
   POSU_REQUIRE(dtype != POSU_F16X3, "posu_conv2d_dgrad: the split dtype is inference-only");
+  POSU_REQUIRE(tile_ok(tile), "posu_conv2d_dgrad: unknown tile configuration");
   if (int st = common_checks(dtype, dy, wt, dx, N, Ho, Wo, Cout, Cin, "posu_conv2d_dgrad")) return st;
   POSU_REQUIRE(Cin % (16 / esz_of(dtype)) == 0, "posu_conv2d_dgrad: Cin must be a multiple of 16 bytes");
   POSU_REQUIRE(stride == 1 || stride == 2, "posu_conv2d_dgrad: stride 1 or 2");
@@ -1876,7 +1888,7 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
     g.out_H = H;
     g.out_W = W;
     g.ostride = 2;
-    return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
+    return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad", tile);
   }
   g.Ho = H;
   g.Wo = W;
@@ -1891,7 +1903,7 @@ extern "C" int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int W
   g.up = stride == 2 ? 1 : 0;
   g.out_H = H;
   g.out_W = W;
-  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad");
+  return dispatch<false>(dtype, g, 1, stream, "posu_conv2d_dgrad", tile);
 }
 
 // Plain GEMM on the conv kernel (1x1 window over M "pixels" of K channels):

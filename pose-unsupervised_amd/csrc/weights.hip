@@ -70,7 +70,7 @@ __host__ __device__ inline long long ceil_div(long long a, long long b) { return
 __host__ __device__ inline bool tiled(int mode, int cin, int ntap, int pitch) {
   if (mode == POSU_PACK_CONV) return conv_rows_per_block(cin, ntap) > 0;
   if (mode == POSU_PACK_DGRAD) return dgrad_ci_per_block(ntap) > 0 && pitch % 8 == 0;
-  return ntap == 16 && cin % 8 == 0;
+  return (ntap == 16 || ntap == 9) && cin % 8 == 0;
 }
 
 template <typename T>
@@ -101,7 +101,9 @@ __device__ void pack_generic(const posu_pack_job& j, long long b) {
       const int t = k / j.cin, ci = k - t * j.cin;
       if (row < j.cout && t < 4) {
         const int py = c >> 1, px = c & 1, ty = t >> 1, tx = t & 1;
-        v = src[((static_cast<long long>(ci) * j.cout + row) * 4 + (3 - py - 2 * ty)) * 4 + (3 - px - 2 * tx)];
+        const int kh = 3 - py - 2 * ty, kw = 3 - px - 2 * tx;  // kh / kw = 3 of a 3x3 source: a zero tap
+        if (kh < j.kh && kw < j.kw)
+          v = src[((static_cast<long long>(ci) * j.cout + row) * j.kh + kh) * j.kw + kw];
       }
     }
     dst[e] = cvt<T>(v);
@@ -207,15 +209,18 @@ __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_
       }
     }
   } else {
-    // deconv class c = py*2+px: out[c][row = co][k = (ty*2+tx) * cin + ci] = w[ci][co][3-py-2ty][3-px-2tx]
+    // deconv class c = py*2+px: out[c][row = co][k = (ty*2+tx) * cin + ci] = w[ci][co][3-py-2ty][3-px-2tx];
+    // a 3x3 source (round 5: the data gradient of a 3x3 / s2 / p1 conv is this transposed conv with the
+    // kernel zero-padded to 4x4) reads its taps kh, kw < 3 and zeros at index 3
+    const int KK = ntap;  // 16 or 9 source taps per (ci, co)
     const int cit = static_cast<int>(ceil_div(j.cin, kTileC));
     const int o0 = static_cast<int>(b / cit) * kDcCo, i0 = static_cast<int>(b % cit) * kTileC;
-    const int str = kDcCo * 16 + 1;
+    const int str = kDcCo * KK + 1;
     const int ci_n = max(0, min(kTileC, j.cin - i0)), co_n = max(0, min(kDcCo, j.cout - o0));
-    const int run = co_n * 16;
+    const int run = co_n * KK;
     if (run > 0) {
-      const float* __restrict__ s0 = src + (static_cast<long long>(i0) * j.cout + o0) * 16;
-      const long long cs = static_cast<long long>(j.cout) * 16;  // source stride between ci
+      const float* __restrict__ s0 = src + (static_cast<long long>(i0) * j.cout + o0) * KK;
+      const long long cs = static_cast<long long>(j.cout) * KK;  // source stride between ci
       stage(lds, s0, ci_n * run, [=](int i) { return (i / run) * cs + i % run; },
             [=](int i) { return (i / run) * str + i % run; });
     }
@@ -229,12 +234,14 @@ __global__ __launch_bounds__(kThreads) void pack_weights_kernel(const posu_pack_
       const int ci = i0 + 8 * ig;
       if (ci >= j.cin) continue;
       const int py = cls >> 1, px = cls & 1, ty = t >> 1, tx = t & 1;
-      const int tap = (3 - py - 2 * ty) * 4 + (3 - px - 2 * tx);
+      const int kh = 3 - py - 2 * ty, kw = 3 - px - 2 * tx;
+      const bool tv = kh < j.kh && kw < j.kw;
+      const int tap = tv ? kh * j.kw + kw : 0;
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int c = 8 * ig + e;
-        v[e] = (o < co_n && c < ci_n) ? lds[c * str + o * 16 + tap] : 0.f;
+        v[e] = (tv && o < co_n && c < ci_n) ? lds[c * str + o * KK + tap] : 0.f;
       }
       store8(dst + cls * per_cls + static_cast<long long>(o0 + o) * j.kpad + t * j.cin + ci, v);
     }
@@ -258,7 +265,7 @@ extern "C" long long posu_pack_job_blocks(int mode, int cout, int cin, int kh, i
                                          int kpad) {
   if (rows <= 0 || kpad <= 0 || kpad % 8 || cout <= 0 || cin <= 0 || kh <= 0 || kw <= 0 || pitch <= 0) return -1;
   if (mode != POSU_PACK_CONV && mode != POSU_PACK_DGRAD && mode != POSU_PACK_DECONV) return -1;
-  if (mode == POSU_PACK_DECONV && (kh != 4 || kw != 4)) return -1;
+  if (mode == POSU_PACK_DECONV && !(kh == kw && (kh == 4 || kh == 3))) return -1;
   const int ntap = kh * kw;
   if (!tiled(mode, cin, ntap, pitch))
     return ceil_div(static_cast<long long>(rows) * kpad * (mode == POSU_PACK_DECONV ? 4 : 1),

@@ -18,7 +18,7 @@ F16 = 3
 F16X3 = 4   # split fp16 (hi + lo pairs, three MFMAs per product): include/posu.h
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -74,6 +74,7 @@ _SIGNATURES = {
     'posu_flip_back': [_p, _p, _p, _i, _i, _i, _i, _i, _p, _p],
     # training path
     'posu_conv2d_dgrad': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _p],
+    'posu_conv2d_dgrad_tile': [_i, _p, _i, _i, _i, _i, _p, _i, _i, _i, _i, _i, _p, _p, _i, _i, _i, _p],
     'posu_conv2d_wgrad_workspace': [_i, _i, _i, _i, _i, _i, _i, _i, _i, _i],
     'posu_conv2d_wgrad': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _ll, _p],
     'posu_bn_workspace': [_i, _i],

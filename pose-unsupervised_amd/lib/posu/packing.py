@@ -183,10 +183,15 @@ def pack_dual_1x1_weight(w_a, scale_a, w_b, scale_b, dtype):
 
 
 def pack_deconv4x4_weight(w, bk, dtype):
+    """ConvTranspose2d(4, s2, p1) weight [Cin][Cout][4][4] -> [4 classes][CoutPad][Kpad].  A 3x3
+    weight [Cin][Cout][3][3] packs as its 4x4 zero-padding (tap index 3 = 0): a Conv2d(3, s2, p1)
+    weight [co][ci][3][3] packed so makes the sub-pixel deconv that conv's data gradient."""
     cin, cout, kh, kw = w.shape
-    if (kh, kw) != (4, 4):
-        raise NotImplementedError('sub-pixel deconv kernel supports kernel 4 / stride 2 / padding 1 only')
     wf = w.detach().float()
+    if (kh, kw) == (3, 3):
+        wf = torch.nn.functional.pad(wf, (0, 1, 0, 1))
+    elif (kh, kw) != (4, 4):
+        raise NotImplementedError('sub-pixel deconv kernel supports kernel 4 / stride 2 / padding 1 only')
     k = 4 * cin
     out = torch.zeros((4, round_up(cout, COUT_ALIGN), round_up(k, bk)), dtype=torch.float32, device=w.device)
     for py in range(2):
@@ -296,8 +301,10 @@ class BatchedPacker:
         return self.add(PACK_DGRAD, w, cout, cin, kh, kw, pitch, round_up(cin, COUT_ALIGN), round_up(kh * kw * pitch, bk))
 
     def deconv(self, w, bk):
-        cin, cout = w.shape[:2]
-        return self.add(PACK_DECONV, w, cout, cin, 4, 4, cin, round_up(cout, COUT_ALIGN), round_up(4 * cin, bk))
+        """A ConvTranspose2d(4, s2, p1) weight [cin][cout][4][4], or a 3x3 one read as its 4x4
+        zero-padding (a Conv2d(3, s2, p1) weight: its data gradient, train_plan)."""
+        cin, cout, kh, kw = w.shape
+        return self.add(PACK_DECONV, w, cout, cin, kh, kw, cin, round_up(cout, COUT_ALIGN), round_up(4 * cin, bk))
 
     def _build(self):
         arr = np.zeros(len(self.jobs), dtype=_JOB)

@@ -28,10 +28,12 @@ def workspace(device, nbytes, slot='default'):
     return buf
 
 
-def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=None, out=None, inplace=False):
+def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=None, out=None, inplace=False,
+                 tile=None):
     """dx [N, H, W, cin] of a conv x -> dy; `hw` = (H, W) of x; optional residual added.
     inplace=True (1x1 / stride-2 convolutions with a residual only) accumulates into `residual`
-    itself and returns it -- the caller gives up that tensor; otherwise nothing is mutated."""
+    itself and returns it -- the caller gives up that tensor; otherwise nothing is mutated.
+    tile: a conv tile configuration (posu_conv2d_dgrad_tile, ABI 15), None = the heuristic."""
     require_cuda(dy)
     n, ho, wo, cout = dy.shape
     h, w = hw
@@ -40,8 +42,12 @@ def conv2d_dgrad(dy, wt_packed, cin, kh, kw, stride, pad, hw, code, residual=Non
         out = residual  # accumulated in place over dy's pixels (posu_conv2d_dgrad)
     if out is None:
         out = torch.empty((n, h, w, cin), dtype=dy.dtype, device=dy.device)
-    call('posu_conv2d_dgrad', code, ptr(dy), n, ho, wo, cout, ptr(wt_packed), cin, kh, kw, stride, pad,
-         ptr(residual), ptr(out), h, w, stream_of(dy.device))
+    if tile is None:
+        call('posu_conv2d_dgrad', code, ptr(dy), n, ho, wo, cout, ptr(wt_packed), cin, kh, kw, stride, pad,
+             ptr(residual), ptr(out), h, w, stream_of(dy.device))
+    else:
+        call('posu_conv2d_dgrad_tile', code, ptr(dy), n, ho, wo, cout, ptr(wt_packed), cin, kh, kw, stride, pad,
+             ptr(residual), ptr(out), h, w, int(tile), stream_of(dy.device))
     return out
 
 

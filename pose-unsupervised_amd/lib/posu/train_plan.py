@@ -47,6 +47,14 @@ PACK_BESIDE_STEM = True
 # round 5: a first block's downsample unit (conv + BN statistics + apply) runs on the side stream
 # beside its conv1 / conv2 units in the forward (the side stream is idle until the backward)
 DOWN_BESIDE = True
+# round 5: the data-gradient convolutions on autotuned tiles (posu_conv2d_dgrad_tile, ABI 15), like the
+# forward ones (_conv_tuned); the in-place 1x1 / stride-2 ones keep the heuristic (a tuning trial
+# would accumulate into its output more than once)
+TUNE_DGRAD = True
+# round 5: a 3x3 / s2 / p1 conv's data gradient (each layer's first block, conv2) as the sub-pixel
+# transposed conv -- its 3x3 kernel zero-padded to 4x4 on the deconv layers' kernel: 16 taps per 2x2
+# output quad instead of 36 over the zero-upsampled gradient (even input sizes, no residual)
+S2_DGRAD_SUBPIXEL = True
 
 
 def _conv_tuned(x, w, cout, k, stride, pad, code):
@@ -64,6 +72,20 @@ def _conv_tuned(x, w, cout, k, stride, pad, code):
     key = ('train_conv', code, tuple(x.shape), cout, k, stride, pad)
     return _tuned(key, cout, lambda t: ops.conv2d_nhwc(x, w, cout, k, k, stride, pad, None, None, None, False, code,
                                                       out=z, tile=t))
+
+
+def _dgrad_tuned(dy, wt, cin, k, stride, pad, hw, code, residual=None, inplace=False):
+    """T.conv2d_dgrad on the tile the autotuner picked for its geometry (TUNE_DGRAD; every
+    admissible tile gives the same result)."""
+    from .plan import _tuned
+    will_inplace = (inplace and T.INPLACE_S2_DGRAD and residual is not None and k == 1 and stride == 2
+                    and pad == 0)
+    if not TUNE_DGRAD or will_inplace or dy.shape[3] % 64 or cin % 64:
+        return T.conv2d_dgrad(dy, wt, cin, k, k, stride, pad, hw, code, residual=residual, inplace=inplace)
+    out = torch.empty((dy.shape[0], hw[0], hw[1], cin), dtype=dy.dtype, device=dy.device)
+    key = ('train_dgrad', code, tuple(dy.shape), cin, k, stride, pad, tuple(hw), residual is not None)
+    return _tuned(key, cin, lambda t: T.conv2d_dgrad(dy, wt, cin, k, k, stride, pad, hw, code, residual=residual,
+                                                     out=out, tile=t))
 
 
 class _Grads(dict):
@@ -128,6 +150,14 @@ class _ConvBN:
     def pack(self, packer, bk, need_dgrad=True):
         self.w = packer.conv(self.conv.weight, self.cin_pad, bk)
         self.wt = packer.dgrad(self.conv.weight, bk) if need_dgrad else None
+        # a 3x3 / s2 / p1 conv's data gradient as the sub-pixel transposed conv (S2_DGRAD_SUBPIXEL)
+        self.wdc = (packer.deconv(self.conv.weight, bk)
+                    if need_dgrad and S2_DGRAD_SUBPIXEL and self._subpixel_dgrad() else None)
+
+    def _subpixel_dgrad(self):
+        c = self.conv
+        return (c.kernel_size == (3, 3) and c.stride == (2, 2) and c.padding == (1, 1) and c.dilation == (1, 1)
+                and c.groups == 1 and self.cout % 8 == 0 and (self.cout & (self.cout - 1)) == 0 and self.cin % 8 == 0)
 
     def forward(self, x, nseg, code, residual=None):
         z = _conv_tuned(x, self.w, self.cout, self.k, self.stride, self.pad, code)
@@ -171,9 +201,18 @@ class _ConvBN:
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
         dx = None
-        if need_dx:
-            dx = T.conv2d_dgrad(dz, self.wt, self.cin, self.k, self.k, self.stride, self.pad, x.shape[1:3], code,
-                                residual=dx_residual, inplace=inplace)
+        if need_dx and getattr(self, 'wdc', None) is not None and dx_residual is None and x.shape[1] % 2 == 0 \
+                and x.shape[2] % 2 == 0:
+            # dx of a 3x3 / s2 / p1 conv = ConvTranspose2d(4, s2, p1) of dz with the 3x3 kernel
+            # zero-padded to 4x4: four 2x2 sub-pixel classes (16 taps per output quad) instead of the
+            # 3x3 conv over the zero-upsampled dz (36), same kernel as the deconv layers
+            from .plan import _tuned
+            key = ('train_dgrad_s2', code, tuple(dz.shape), self.cin)
+            dx = _tuned(key, self.cin, lambda t: ops.deconv4x4s2_nhwc(dz, self.wdc, self.cin, None, None, False, code,
+                                                                      tile=t))
+        elif need_dx:
+            dx = _dgrad_tuned(dz, self.wt, self.cin, self.k, self.stride, self.pad, tuple(x.shape[1:3]), code,
+                              residual=dx_residual, inplace=inplace)
         return dx, gres
 
 

@@ -67,6 +67,58 @@ def test_conv_dgrad_matches_autograd(cuda, case, code):
         _close_lowp(_nchw(dx_r), dx_ref + res.to(dt).float())
 
 
+@pytest.mark.parametrize('case', [DGRAD_CASES[0], DGRAD_CASES[1], DGRAD_CASES[4], (2, 64, 16, 16, 256, 1, 1, 0)])
+@pytest.mark.parametrize('code', [BF16, F32])
+def test_conv_dgrad_every_tile_equals_the_heuristic(cuda, case, code):
+    """ABI 15 (posu_conv2d_dgrad_tile): every tile the training step's autotuner may pick for a data
+    gradient (posu.plan._tile_candidates of its output channels) gives the heuristic's dx bit for
+    bit, with and without the residual; an unknown tile is refused."""
+    from posu import plan as pl
+    n, cin, h, w, cout, k, s, p = case
+    g = torch.Generator().manual_seed(12)
+    dt = ops.torch_dtype(code)
+    wt = torch.randn(cout, cin, k, k, generator=g) * (2.0 / (cin * k * k)) ** 0.5
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    dy = torch.randn(n, ho, wo, cout, generator=g).to(cuda, dt)
+    res = torch.randn(n, h, w, cin, generator=g).to(cuda, dt)
+    wpk = packing.pack_conv_dgrad_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    for r in (None, res):
+        ref = T.conv2d_dgrad(dy, wpk, cin, k, k, s, p, (h, w), code, residual=r)
+        for t in pl._tile_candidates(cin, code):
+            got = T.conv2d_dgrad(dy, wpk, cin, k, k, s, p, (h, w), code, residual=r, tile=t)
+            assert torch.equal(got, ref), (t, r is None)
+    with pytest.raises(RuntimeError, match='unknown tile'):
+        T.conv2d_dgrad(dy, wpk, cin, k, k, s, p, (h, w), code, tile=13)
+
+
+@pytest.mark.parametrize('code', [F32, BF16])
+@pytest.mark.parametrize('n,cin,h,w,cout', [(2, 64, 16, 16, 128), (2, 128, 8, 12, 256), (1, 40, 6, 10, 64)])
+def test_s2_conv_data_gradient_as_subpixel_deconv(cuda, code, n, cin, h, w, cout):
+    """ABI 15 (the training step's first-block conv2 backward): the data gradient of a 3x3 / s2 / p1
+    conv as posu_deconv4x4s2_fwd over dz with the conv weight packed as a 3x3 deconv source (its
+    4x4 zero-padding) -- four 2x2 sub-pixel classes instead of the 3x3 conv over the zero-upsampled
+    gradient -- against autograd, and against posu_conv2d_dgrad (the upsampled form)."""
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(n, cin, h, w, generator=g, requires_grad=True)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (2.0 / (cin * 9)) ** 0.5
+    y = F.conv2d(x, wt, stride=2, padding=1)
+    dy = torch.randn_like(y)
+    (dx_ref,) = torch.autograd.grad(y, x, dy)
+    dt = ops.torch_dtype(code)
+    wdc = packing.pack_deconv4x4_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    dx = ops.deconv4x4s2_nhwc(_nhwc(dy, cuda, dt), wdc, cin, None, None, False, code)
+    wpk = packing.pack_conv_dgrad_weight(wt.to(cuda), ops.conv_bk(code), dt)
+    dx_up = T.conv2d_dgrad(_nhwc(dy, cuda, dt), wpk, cin, 3, 3, 2, 1, (h, w), code)
+    torch.cuda.synchronize()
+    assert dx.shape == dx_up.shape == (n, h, w, cin)
+    if code == F32:
+        torch.testing.assert_close(_nchw(dx), dx_ref, **FP32_TOL)
+        torch.testing.assert_close(dx, dx_up, atol=1e-5, rtol=1e-5)
+    else:
+        _close_lowp(_nchw(dx), dx_ref)
+        _close_lowp(_nchw(dx), _nchw(dx_up), 0.01)
+
+
 WGRAD_CASES = [
     # n, cin, cin_pad, h, w, cout, k, stride, pad
     (2, 3, 8, 32, 30, 64, 7, 2, 3),      # direct stem (channels padded to 8)
@@ -322,6 +374,9 @@ def test_batched_weight_packing_equals_the_torch_packs(cuda, code):
         (pk.dgrad(w1, bk), packing.pack_conv_dgrad_weight(w1, bk, dt)),
         (pk.deconv(wdc, bk), packing.pack_deconv4x4_weight(wdc, bk, dt)),
         (pk.conv(wdc, 48, bk), packing.pack_conv_weight(wdc, 48, bk, dt)),
+        # ABI 15: a 3x3 conv weight as a deconv source (zero-padded to 4x4), LDS-tiled and element-wise
+        (pk.deconv(w3, bk), packing.pack_deconv4x4_weight(w3, bk, dt)),
+        (pk.deconv(w3[:44, :24].contiguous(), bk), packing.pack_deconv4x4_weight(w3[:44, :24], bk, dt)),
     ]
     wpad = torch.zeros(64, 256, 1, 1, device=cuda)
     wpad[:17] = wh
@@ -355,6 +410,7 @@ def test_batched_weight_packing_network_sizes(cuda, code):
         (pk.dgrad(w1, bk), packing.pack_conv_dgrad_weight(w1, bk, dt)),
         (pk.deconv(wdc, bk), packing.pack_deconv4x4_weight(wdc, bk, dt)),
         (pk.conv(wdc, 256, bk), packing.pack_conv_weight(wdc, 256, bk, dt)),
+        (pk.deconv(w3, bk), packing.pack_deconv4x4_weight(w3, bk, dt)),
     ]
     pk.run()
     torch.cuda.synchronize()
