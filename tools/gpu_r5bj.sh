@@ -1,0 +1,21 @@
+#!/bin/bash
+# max-pool backward, 2x2-block form vs the first form: tests, training step A/B
+OUT=gpurun_out/r5bj
+mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_train_kernels.py tests/test_gpu_train.py > $OUT/tests.log 2>&1
+rc=$?; tail -2 $OUT/tests.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+  for v in pool2 pool1; do
+    if [ $v = pool2 ]; then L=""; else L="tools/with_lib.py pose-unsupervised_amd/build/ab14/libposeu_$v.so"; fi
+    timeout -k 10 300 python -u $L bench.py --mode train --steps 20 --warmup 3 > $OUT/${v}_$r.json 2> $OUT/${v}_$r.err || exit $?
+    python - "$OUT/${v}_$r.json" "$v run $r" <<'PY' | tee -a $OUT/ab.txt
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], 'ms_per_step', d['ms_per_step'], 'value', d['value'], 'loss', d['loss'])
+PY
+  done
+done
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --mode train --steps 3 --warmup 1 > $OUT/prof.log 2>&1 || exit 1
+grep -h "maxpool_bwd" $OUT/prof/run_kernel_stats.csv | cut -c1-200 | tee -a $OUT/ab.txt
+rm -f $OUT/prof/run_kernel_trace.csv
