@@ -206,23 +206,37 @@ extern "C" int posu_argmax2d_fwd(const float* hm, int N, int J, int H, int W, in
 namespace posu {
 namespace {
 
-__global__ __launch_bounds__(256) void mse_partial_kernel(const float* __restrict__ pred,
-                                                          const float* __restrict__ gt,
-                                                          const float* __restrict__ w, int NJ, int HW,
-                                                          float* __restrict__ ws) {
-  const int map = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (map >= NJ) return;
+// one 64-lane block per heatmap: 16-B loads, four independent partial sums per lane (a fixed
+// association: lane l adds elements 4l.., chunk j into sum j % 4), then the wave sum.  (Round 2 ran
+// a wave per map at four maps per block with 4-B loads: 128 blocks, 28 us per call for 32 x 16
+// maps of 64 x 64 -- latency-bound on half the CUs.)
+__global__ __launch_bounds__(64) void mse_partial_kernel(const float* __restrict__ pred,
+                                                         const float* __restrict__ gt,
+                                                         const float* __restrict__ w, int NJ, int HW,
+                                                         float* __restrict__ ws) {
+  const int map = blockIdx.x;
+  const int lane = threadIdx.x;
   const float* p = pred + static_cast<size_t>(map) * HW;
   const float* t = gt + static_cast<size_t>(map) * HW;
   const float wt = w ? w[map] : 1.f;
-  float acc = 0.f;
-  for (int i = lane; i < HW; i += 64) {
-    const float d = p[i] * wt - t[i] * wt;
-    acc += d * d;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if ((HW & 3) == 0 && ((reinterpret_cast<size_t>(p) | reinterpret_cast<size_t>(t)) & 15) == 0) {
+    const int n4 = HW >> 2;
+#pragma unroll 4
+    for (int j = lane; j < n4; j += 64) {
+      const float4 a = reinterpret_cast<const float4*>(p)[j], b = reinterpret_cast<const float4*>(t)[j];
+      const float d0 = a.x * wt - b.x * wt, d1 = a.y * wt - b.y * wt, d2 = a.z * wt - b.z * wt,
+                  d3 = a.w * wt - b.w * wt;
+      acc[(j >> 6) & 3] += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+    }
+  } else {
+    for (int i = lane; i < HW; i += 64) {
+      const float d = p[i] * wt - t[i] * wt;
+      acc[(i >> 6) & 3] += d * d;
+    }
   }
-  acc = wave_sum(acc);
-  if (lane == 0) ws[map] = acc;
+  const float s = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+  if (lane == 0) ws[map] = s;
 }
 
 __global__ __launch_bounds__(256) void mse_final_kernel(const float* __restrict__ ws, int NJ, float denom,
@@ -242,6 +256,14 @@ __global__ __launch_bounds__(256) void mse_bwd_kernel(const float* __restrict__ 
                                                       float* __restrict__ gpred) {
   const long long total = static_cast<long long>(NJ) * HW;
   const float g = 2.f * gloss[0] / denom;
+  if (total < (1LL << 31)) {   // 32-bit index math (the map of element i: an unsigned 32-bit division)
+    const unsigned tot = static_cast<unsigned>(total), hw = static_cast<unsigned>(HW);
+    for (unsigned i = blockIdx.x * 256u + threadIdx.x; i < tot; i += gridDim.x * 256u) {
+      const float wt = w ? w[i / hw] : 1.f;
+      gpred[i] = g * wt * (pred[i] * wt - gt[i] * wt);
+    }
+    return;
+  }
   for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<long long>(gridDim.x) * 256) {
     const int map = static_cast<int>(i / HW);
     const float wt = w ? w[map] : 1.f;
@@ -258,7 +280,7 @@ extern "C" int posu_joints_mse_fwd(const float* pred, const float* gt, const flo
   POSU_REQUIRE(N > 0 && J > 0 && HW > 0, "posu_joints_mse_fwd: bad shape");
   const int NJ = N * J;
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(mse_partial_kernel, dim3((NJ + 3) / 4), dim3(256), 0, s, pred, gt, w, NJ, HW, ws);
+  hipLaunchKernelGGL(mse_partial_kernel, dim3(NJ), dim3(64), 0, s, pred, gt, w, NJ, HW, ws);
   hipLaunchKernelGGL(mse_final_kernel, dim3(1), dim3(256), 0, s, ws, NJ,
                      static_cast<float>(static_cast<long long>(N) * HW), loss);
   return check_launch("posu_joints_mse_fwd");
