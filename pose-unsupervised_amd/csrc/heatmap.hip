@@ -29,11 +29,13 @@ __device__ __forceinline__ void online_add(float t, float col, float row, float&
   sy += e * row;
 }
 
-__global__ __launch_bounds__(256) void softargmax_fwd_kernel(const float* __restrict__ hm, int NJ, int J, int H,
-                                                             int W, float beta, const float* __restrict__ aff,
-                                                             float* __restrict__ out, float* __restrict__ stats) {
-  const int map = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+// one 64-lane block per map (round 5: was four maps per 256-thread block -- NJ / 4 blocks, half the
+// CUs idle at the training step's 512 maps; the per-map arithmetic is unchanged)
+__global__ __launch_bounds__(64) void softargmax_fwd_kernel(const float* __restrict__ hm, int NJ, int J, int H,
+                                                            int W, float beta, const float* __restrict__ aff,
+                                                            float* __restrict__ out, float* __restrict__ stats) {
+  const int map = blockIdx.x;
+  const int lane = threadIdx.x;
   if (map >= NJ) return;
   const int HW = H * W;
   const float* h = hm + static_cast<size_t>(map) * HW;
@@ -80,14 +82,14 @@ __global__ __launch_bounds__(256) void softargmax_fwd_kernel(const float* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void softargmax_bwd_kernel(const float* __restrict__ hm,
-                                                             const float* __restrict__ stats, int NJ, int J,
-                                                             int H, int W, float beta,
-                                                             const float* __restrict__ aff,
-                                                             const float* __restrict__ gout,
-                                                             float* __restrict__ ghm) {
-  const int map = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
+__global__ __launch_bounds__(64) void softargmax_bwd_kernel(const float* __restrict__ hm,
+                                                            const float* __restrict__ stats, int NJ, int J,
+                                                            int H, int W, float beta,
+                                                            const float* __restrict__ aff,
+                                                            const float* __restrict__ gout,
+                                                            float* __restrict__ ghm) {
+  const int map = blockIdx.x;
+  const int lane = threadIdx.x;
   if (map >= NJ) return;
   const int HW = H * W;
   const float M = stats[4 * map], inv_s = 1.f / stats[4 * map + 1];
@@ -102,10 +104,24 @@ __global__ __launch_bounds__(256) void softargmax_bwd_kernel(const float* __rest
   }
   const float* h = hm + static_cast<size_t>(map) * HW;
   float* gh = ghm + static_cast<size_t>(map) * HW;
+  auto one = [&](float hv, int row, int col) {
+    const float p = __expf(beta * hv - M) * inv_s;
+    return beta * p * ((col - x) * gx + (row - y) * gy);
+  };
+  if ((HW & 3) == 0 && (W & 3) == 0) {   // 16-B loads / stores, the same per-element arithmetic
+    const float4* h4 = reinterpret_cast<const float4*>(h);
+    float4* g4 = reinterpret_cast<float4*>(gh);
+#pragma unroll 4
+    for (int i = lane; i < HW / 4; i += 64) {
+      const float4 v = h4[i];
+      const int row = (i * 4) / W, col = i * 4 - row * W;
+      g4[i] = make_float4(one(v.x, row, col), one(v.y, row, col + 1), one(v.z, row, col + 2), one(v.w, row, col + 3));
+    }
+    return;
+  }
   for (int i = lane; i < HW; i += 64) {
     const int row = i / W, col = i - row * W;
-    const float p = __expf(beta * h[i] - M) * inv_s;
-    gh[i] = beta * p * ((col - x) * gx + (row - y) * gy);
+    gh[i] = one(h[i], row, col);
   }
 }
 
@@ -175,7 +191,7 @@ extern "C" int posu_softargmax2d_fwd(const float* hm, int N, int J, int H, int W
   POSU_REQUIRE(N >= 0 && J > 0 && H > 0 && W > 0, "posu_softargmax2d_fwd: bad shape");
   if (N == 0) return POSU_OK;
   const int NJ = N * J;
-  hipLaunchKernelGGL(softargmax_fwd_kernel, dim3((NJ + 3) / 4), dim3(256), 0, as_stream(stream), hm, NJ, J, H, W,
+  hipLaunchKernelGGL(softargmax_fwd_kernel, dim3(NJ), dim3(64), 0, as_stream(stream), hm, NJ, J, H, W,
                      beta, affine, out, stats);
   return check_launch("posu_softargmax2d_fwd");
 }
@@ -186,7 +202,7 @@ extern "C" int posu_softargmax2d_bwd(const float* hm, const float* stats, int N,
   POSU_REQUIRE(N >= 0 && J > 0 && H > 0 && W > 0, "posu_softargmax2d_bwd: bad shape");
   if (N == 0) return POSU_OK;
   const int NJ = N * J;
-  hipLaunchKernelGGL(softargmax_bwd_kernel, dim3((NJ + 3) / 4), dim3(256), 0, as_stream(stream), hm, stats, NJ,
+  hipLaunchKernelGGL(softargmax_bwd_kernel, dim3(NJ), dim3(64), 0, as_stream(stream), hm, stats, NJ,
                      J, H, W, beta, affine, gout, ghm);
   return check_launch("posu_softargmax2d_bwd");
 }
