@@ -1210,7 +1210,6 @@ extern "C" int posu_maxpool3x3s2_bwd_idx(int dtype, const void* idx, const void*
   POSU_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && C % chunk_elems(dtype) == 0, "posu_maxpool3x3s2_bwd_idx: bad shape");
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   hipStream_t s = as_stream(stream);
-  const int E = chunk_elems(dtype);
   const bool ok = with_storage(dtype, [&](auto tag) {
     using T = decltype(tag);
     pool_bwd_launch<T>(static_cast<const uint8_t*>(idx), static_cast<const T*>(gy), N, H, W, C, Ho, Wo,
