@@ -82,8 +82,9 @@ def parse():
     ap.add_argument('--serial-geo', action='store_true',
                     help='run each batch\'s decode + geometry after its network on one stream (default: on a '
                          'second stream, overlapping the next batch\'s network)')
-    ap.add_argument('--adam', default='fused', choices=['fused', 'foreach'],
-                    help="train mode: torch.optim.Adam's fused kernel (default) or its foreach launches")
+    ap.add_argument('--adam', default='posu', choices=['posu', 'fused', 'foreach'],
+                    help="train mode: posu.optim.Adam (default: posu_adam_step, every parameter in a few "
+                         "launches) or torch.optim.Adam's fused kernel / foreach launches")
     ap.add_argument('--no-autotune', action='store_true', help='keep the built-in conv tile heuristic')
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
@@ -913,7 +914,11 @@ def run_training(args, dev, rank, world, dist, steps, warmup):
     # the reference's optimizer (utils.py:79-83: optim.Adam, same hyper-parameters); fused=True
     # runs the update as one kernel per parameter group instead of torch's foreach multi-tensor
     # launches (same math): 26.3 -> 22.8 ms per step measured A/B
-    opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
+    if args.adam == 'posu':   # the same update on the HIP kernel (posu_adam_step), state layout unchanged
+        from posu.optim import Adam as PosuAdam
+        opt = PosuAdam(net.parameters(), lr=1e-3)
+    else:
+        opt = torch.optim.Adam(net.parameters(), lr=1e-3, fused=args.adam == 'fused')
 
     def step():
         loss = tb['loss']()

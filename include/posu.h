@@ -69,7 +69,9 @@ const char* posu_last_error(void);
  * with stored argmax taps (posu_bn_relu_maxpool3x3s2_fwd / posu_maxpool3x3s2_bwd_idx), the training
  * stem's convolution and weight gradient from the NCHW f32 views (posu_stem_conv_views_fwd /
  * posu_stem_wgrad_views); 15 (training) the data gradient on a chosen tile
- * (posu_conv2d_dgrad_tile: the training step autotunes it like the forward convolutions).  The
+ * (posu_conv2d_dgrad_tile: the training step autotunes it like the forward convolutions), 3x3
+ * sources of the batched deconv packing (the strided 3x3 convs' sub-pixel data gradient), the
+ * Adam step (posu_adam_step).  The
  * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
@@ -500,6 +502,21 @@ int posu_conv2d_dgrad(int dtype, const void* dy, int N, int Ho, int Wo, int Cout
 int posu_conv2d_dgrad_tile(int dtype, const void* dy, int N, int Ho, int Wo, int Cout, const void* wt,
                            int Cin, int KH, int KW, int stride, int pad, const void* residual,
                            void* dx, int H, int W, int tile, void* stream);
+
+/* ABI 15: the Adam step (torch.optim.Adam, utils/utils.py:79-83; core/function.py:366) over a
+ * table of f32 parameter tensors: per element g' = g (+ weight_decay p), m = b1 m + (1-b1) g',
+ * v = b2 v + (1-b2) g'^2, p -= lr / (1 - b1^step) * m / (sqrt(v) / sqrt(1 - b2^step) + eps),
+ * in f32 (within rounding of torch's kernels).  p, m, v updated in place; `step` = the step being
+ * taken (>= 1).  The table is host memory, read during the call (the launches carry it). */
+typedef struct posu_adam_tensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long long n;
+} posu_adam_tensor;
+int posu_adam_step(const posu_adam_tensor* tensors, int ntensors, double lr, double beta1, double beta2,
+                   double eps, double weight_decay, long long step, void* stream);
 
 /* Weight gradient dW[Cout][Creal][KH][KW] (f32, the nn.Conv2d weight layout) of a
  * conv over x[N,H,W,C] (C >= Creal, padded channels ignored) with output gradient

@@ -91,6 +91,7 @@ _SIGNATURES = {
     'posu_channel_sum': [_i, _p, _i, _i, _p, _p, _ll, _p],
     'posu_maxpool3x3s2_bwd_workspace': [_i, _i, _i, _i],
     'posu_maxpool3x3s2_bwd': [_i, _p, _i, _i, _i, _i, _p, _p, _p, _ll, _p],
+    'posu_adam_step': [_p, _i, _d, _d, _d, _d, _d, _ll, _p],
 }
 _RESTYPES = {'posu_last_error': ctypes.c_char_p, 'posu_conv2d_wgrad_workspace': ctypes.c_longlong,
              'posu_pack_job_blocks': ctypes.c_longlong,
