@@ -31,6 +31,8 @@ def category(n):
         return 'weight packing'
     if 'softargmax' in n or 'epipolar' in n or 'mse' in n:
         return 'heads / losses'
+    if 'adam_kernel' in n:
+        return 'adam (posu)'
     if 'multi_tensor_apply' in n:
         return 'adam (torch)'
     if 'nccl' in n.lower() or 'rccl' in n.lower():
