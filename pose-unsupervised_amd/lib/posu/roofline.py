@@ -88,7 +88,7 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     read, the pooled activation and its argmax taps written) and the max-pool backward reads the taps.
     Every tensor once per launch: the floor the kernels' PMC traffic is compared with."""
     cls = {k: [0, 0] for k in ('conv fwd / dgrad', 'conv wgrad', 'batchnorm', 'maxpool', 'weight packing',
-                                 'adam (torch)', 'heads / losses')}
+                                 'adam', 'heads / losses')}
 
     def add(c, r, w):
         cls[c][0] += r
@@ -146,7 +146,7 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     add('conv fwd / dgrad', hm + 256 * 64 * es, act(64, 256))
     add('conv wgrad', hm + act(64, 256), 256 * joints * 4)
     nparam[0] += 256 * joints + joints
-    add('adam (torch)', 4 * nparam[0] * 4, 3 * nparam[0] * 4)
+    add('adam', 4 * nparam[0] * 4, 3 * nparam[0] * 4)
     return {k: tuple(v) for k, v in cls.items()}
 
 

@@ -30,7 +30,7 @@ def test_training_classes():
     # activations dominate: doubling the frames nearly doubles the bytes (weights / Adam fixed)
     assert 1.95 < R.r50_256_train_algorithmic_bytes(256) / total < 2.0
     # Adam: 7 f32 words per parameter (PoseResNet-50: ~34M parameters)
-    nparam = sum(c['adam (torch)']) / 28
+    nparam = sum(c['adam']) / 28
     assert 3.3e7 < nparam < 3.5e7
 
 

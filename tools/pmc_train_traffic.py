@@ -40,7 +40,7 @@ def last_step(rows):
 def category(n):
     for key, cat in (('wgrad', 'conv wgrad'), ('conv_igemm', 'conv fwd / dgrad'), ('conv_persist', 'conv fwd / dgrad'),
                      ('bn_', 'batchnorm'), ('channel_sum', 'batchnorm'), ('maxpool', 'maxpool'),
-                     ('pack', 'weight packing'), ('multi_tensor_apply', 'adam (torch)')):
+                     ('pack', 'weight packing'), ('adam_kernel', 'adam'), ('multi_tensor_apply', 'adam')):
         if key in n:
             return cat
     return 'heads / losses'
