@@ -601,8 +601,9 @@ def _json_default(o):
 
 
 def peaked_parity(args, dev):
-    """tools/peaked.py: fit R50@256 to peaked targets through the training path, then the bf16 and
-    fp32 chains against the CPU oracle chain on those weights (the checker leg; N = 1)."""
+    """tools/peaked.py: fit R50@256 to peaked targets through the (fp32) training path, then the fp32,
+    fp16x3 (also with its tiles autotuned on the task, as the parity_mode leg tunes them), bf16 and
+    fp16 chains against the CPU oracle chain on those weights (the checker leg; N = 1)."""
     sys.path.insert(0, os.path.join(REPO, 'tools'))
     import peaked
     t0 = time.perf_counter()
@@ -614,7 +615,8 @@ def peaked_parity(args, dev):
     # fp32 (the parity mode) first, then both 2-byte modes (same MFMA rate), the benched one included
     for prec in dict.fromkeys(('fp32', args.precision, 'fp16x3', 'bf16', 'fp16')):
         out[prec], ref = peaked.parity(net, task, dev, prec, ref)
-    out['fit'] = {'steps': args.peaked_steps, 'seconds': round(fit_s, 2), 'groups': task['groups'],
+    out['fp16x3_autotuned'], _ = peaked.parity(net, task, dev, 'fp16x3', ref, autotune=True)
+    out['fit'] = {'steps': args.peaked_steps, 'seconds': round(fit_s, 2), 'groups': task['groups'], 'precision': 'fp32',
                   'heatmap_peak_mean': out['fp32']['heatmap_peak_mean'],
                   'oracle_mpjpe_vs_gt_mm': out['fp32']['oracle_mpjpe_vs_gt_mm']}
     return out
@@ -820,8 +822,13 @@ def infer_main(args):
                          'details in peaked_parity' % (args.precision, peaked['fit']['heatmap_peak_mean']))
         if par is not None:
             par['peaked_parity'] = {k: peaked['fp16x3'][k] for k in ('heatmap_abs_err', 'mpjpe_vs_ref_mm')}
-            par['within_baseline_bars'] = bool(peaked['fp16x3']['heatmap_abs_err']['max'] < 1e-3 and
-                                               peaked['fp16x3']['mpjpe_vs_ref_mm']['max'] < 1e-2)
+            par['peaked_parity_autotuned'] = {k: peaked['fp16x3_autotuned'][k]
+                                              for k in ('heatmap_abs_err', 'mpjpe_vs_ref_mm')}
+            # BASELINE.json's bars (heatmaps 1e-3; triangulated joints 1e-2 mm, mean and max), with the
+            # heuristic tiles and with the tuned ones
+            par['within_baseline_bars'] = all(
+                r['heatmap_abs_err']['max'] < 1e-3 and r['mpjpe_vs_ref_mm']['max'] < 1e-2 and
+                r['mpjpe_vs_ref_mm']['mean'] < 1e-2 for r in (peaked['fp16x3'], peaked['fp16x3_autotuned']))
     line = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
@@ -854,15 +861,19 @@ def infer_main(args):
 
 
 # ------------------------------------------------------------------ training
-TRAIN_FUND_WEIGHT = 1e-3   # the benched step's weight of the epipolar (FundamentalLoss) term
+# the benched step's weight of the epipolar (FundamentalLoss) term: the reference config's default
+# config.LOSS.FUNDAMENTAL_LOSS_WEIGHT (lib/core/config.py:102; function.py:308-309 multiplies by it)
+TRAIN_FUND_WEIGHT = 1.0
 
 
-def train_batch(args, dev, rank=0, world=1, dist=None):
+def train_batch(args, dev, rank=0, world=1, dist=None, fund_weight=None):
     """The configs[3] training batch of this rank and its loss (tests/test_gpu_train_full.py checks
     exactly this step): the bench's calibrated R50 (train mode, per-view BN) wrapped in
     MultiViewPose (DDP when dist is given), the rank's 4-view shard of synthetic crops, Gaussian
-    targets at seeded positions, loss() = sum over views of JointsMSELoss + TRAIN_FUND_WEIGHT x the
-    epipolar loss of the soft-argmax joints (core/function.py:154-366).  Returns a dict."""
+    targets at seeded positions, loss() = sum over views of JointsMSELoss + TRAIN_FUND_WEIGHT (or
+    fund_weight) x the epipolar loss of the soft-argmax joints weighted by the target weights, as the
+    reference's USE_TARGET_WEIGHT_FUND (core/function.py:154-366, 296-310).  Returns a dict."""
+    fw = TRAIN_FUND_WEIGHT if fund_weight is None else fund_weight
     from posu import synthetic as syn
     from core.loss import JointsMSELoss, FundamentalLoss
     from models.multiview_pose_resnet import get_multiview_pose_net
@@ -885,6 +896,7 @@ def train_batch(args, dev, rank=0, world=1, dist=None):
     target = torch.exp(-((ys - c[..., 1, None, None]) ** 2 + (xs - c[..., 0, None, None]) ** 2) / 8.0).to(dev)
     target = target.view(nv, nb, 16, hs, hs)
     weight = torch.ones(nb, 16, 1, device=dev)
+    fweight = weight.view(1, nb, 16).expand(nv, nb, 16).contiguous()   # the views' target weights [V, N, J]
     mse = JointsMSELoss(use_target_weight=True)
     fund = FundamentalLoss(cfg, fundamental_matrix_dict=syn.fundamental_dict(), device=dev)
     out = {'net': net, 'model': model, 'views': views, 'target': target, 'weight': weight, 'meta': meta,
@@ -896,9 +908,9 @@ def train_batch(args, dev, rank=0, world=1, dist=None):
         for v in range(nv):
             loss = loss + mse(raw[v], target[v], weight)
         coords = integral_preds_image_th(torch.cat(raw, 0), meta.affines).view(nv, nb, 16, 2)
-        epi = ops.epipolar_loss(coords, None, fund.F, meta.subj)
+        epi = ops.epipolar_loss(coords, fweight, fund.F, meta.subj)
         out['last'] = (raw, loss, epi)
-        return loss + TRAIN_FUND_WEIGHT * epi
+        return loss + fw * epi
     out['loss'] = loss_fn
     return out
 

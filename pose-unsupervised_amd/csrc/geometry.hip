@@ -192,20 +192,47 @@ __device__ __forceinline__ void dlt_point(double (&A)[ROWS][4], double* out) {
   out[2] = v2 / v3;
 }
 
+// R (4 x 4 upper triangular) <- the R factor of [R; a]: Givens rotations fold the row a into R, so
+// A^T A = R^T R over every row folded so far and R has A's right singular vectors and values (an
+// orthogonal transformation of the rows; nothing is squared).  Up to 4 + 4 doubles live per row
+// instead of the whole 2V x 4 matrix.
+__device__ __forceinline__ void givens_fold(double (&R)[4][4], double (&a)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    if (a[c] == 0.0) continue;
+    const double r = hypot(R[c][c], a[c]);
+    const double cs = R[c][c] / r, sn = a[c] / r;
+#pragma unroll
+    for (int j = c; j < 4; ++j) {
+      const double t = R[c][j];
+      R[c][j] = cs * t + sn * a[j];
+      a[j] = cs * a[j] - sn * t;
+    }
+  }
+}
+
 // Rows of invisible views are zero: a zero row adds nothing to A^T A, so the right
 // singular vectors of the remaining rows are unchanged.  ROWS is a compile-time
-// bound, so A lives in registers (no scratch) for the 4-view case.
+// bound, so A lives in registers (no scratch) for the 4-view case; above 4 views the rows are
+// folded into a 4 x 4 R factor as they are formed (givens_fold: A = 32 x 4 doubles spilled 32 VGPRs).
 template <int VMAX>
 __global__ __launch_bounds__(64) void triangulate_kernel(const double* __restrict__ Mall,
                                                          const double* __restrict__ intr,
                                                          const void* __restrict__ xyv, int xy_dtype, int sg,
                                                          int sv, const unsigned char* __restrict__ vis, int G, int V,
                                                          int J, int undistort, double* __restrict__ X) {
-  constexpr int ROWS = 2 * VMAX;
+  constexpr bool FOLD = VMAX > 4;
+  constexpr int ROWS = FOLD ? 4 : 2 * VMAX;
   const int t = blockIdx.x * 64 + threadIdx.x;
   if (t >= G * J) return;
   const int g = t / J, k = t - g * J;
   double A[ROWS][4];
+  if constexpr (FOLD) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) A[r][c] = 0.0;
+  }
   int nvis = 0;
 #pragma unroll
   for (int v = 0; v < VMAX; ++v) {
@@ -225,10 +252,23 @@ __global__ __launch_bounds__(64) void triangulate_kernel(const double* __restric
       ++nvis;
     }
     const double* M = Mall + gv * 12;
+    if constexpr (FOLD) {
+      if (on) {
+        double a0[4], a1[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      A[2 * v][c] = on ? u * M[8 + c] - M[c] : 0.0;
-      A[2 * v + 1][c] = on ? vv * M[8 + c] - M[4 + c] : 0.0;
+        for (int c = 0; c < 4; ++c) {
+          a0[c] = u * M[8 + c] - M[c];
+          a1[c] = vv * M[8 + c] - M[4 + c];
+        }
+        givens_fold(A, a0);
+        givens_fold(A, a1);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        A[2 * v][c] = on ? u * M[8 + c] - M[c] : 0.0;
+        A[2 * v + 1][c] = on ? vv * M[8 + c] - M[4 + c] : 0.0;
+      }
     }
   }
   double* out = X + static_cast<size_t>(t) * 3;
@@ -384,11 +424,14 @@ __global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ M
   int best_mask = 0, best_n = 0;
   double best_err = 10000.0;
   if (p.nvis >= 2) {
-    // itertools.combinations over the visible views, in view order
+    // itertools.combinations over the visible views, in view order (loops unrolled: the view
+    // indices are compile-time, so p's arrays stay in registers -- a run-time index put them in
+    // 144 B of scratch)
+#pragma unroll
     for (int a = 0; a < kPairViews; ++a) {
-      if (!p.on[a]) continue;
+#pragma unroll
       for (int b = a + 1; b < kPairViews; ++b) {
-        if (!p.on[b]) continue;
+        if (!p.on[a] || !p.on[b]) continue;
         double A[4][4];
         const int pv[2] = {a, b};
 #pragma unroll
@@ -404,7 +447,9 @@ __global__ __launch_bounds__(64) void ransac_kernel(const double* __restrict__ M
         dlt_point<4>(A, X);
         int mask = 0, n = 0;
         double err = 0.0;
-        for (int v = 0; v < V; ++v) {
+#pragma unroll
+        for (int v = 0; v < kPairViews; ++v) {
+          if (v >= V) break;
           const size_t gv = static_cast<size_t>(g) * V + v;
           double u, w;
           project_px(Mall + gv * 12, intr + gv * 9, X, u, w);

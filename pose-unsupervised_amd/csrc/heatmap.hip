@@ -108,7 +108,9 @@ __global__ __launch_bounds__(64) void softargmax_bwd_kernel(const float* __restr
     const float p = __expf(beta * hv - M) * inv_s;
     return beta * p * ((col - x) * gx + (row - y) * gy);
   };
-  if ((HW & 3) == 0 && (W & 3) == 0) {   // 16-B loads / stores, the same per-element arithmetic
+  // 16-B loads / stores (the same per-element arithmetic) when both maps are 16-B aligned: a view with
+  // a storage offset that is not a multiple of 4 floats takes the scalar loop
+  if ((HW & 3) == 0 && (W & 3) == 0 && ((reinterpret_cast<size_t>(h) | reinterpret_cast<size_t>(gh)) & 15) == 0) {
     const float4* h4 = reinterpret_cast<const float4*>(h);
     float4* g4 = reinterpret_cast<float4*>(gh);
 #pragma unroll 4

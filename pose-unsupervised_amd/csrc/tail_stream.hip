@@ -86,7 +86,7 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, int CM = 1>
 struct TailCfg {
   static constexpr int kRows = ROWS;               // image rows per workgroup
   static constexpr int kNW = NW;                   // waves per workgroup
@@ -94,13 +94,14 @@ struct TailCfg {
   static constexpr int kPx = kRows * W;            // tile pixels
   static constexpr int kNPG = kPx / (16 * MT);     // pixel groups of 16 MT px
   static constexpr int kNCQ = NW / kNPG;           // channel groups of 32
-  static constexpr int kRowB = P * 2;              // LDS bytes per pixel (bf16 / fp16)
+  static constexpr int kCM = CM;                   // stored halves per logical channel (2: split fp16 pairs)
+  static constexpr int kRowB = P * 2 * CM;         // LDS bytes per pixel (bf16 / fp16 / split pairs)
   static constexpr int kWinCols = W + 2;
   static constexpr int kWinPix = (kRows + 2) * kWinCols;
   static constexpr int kBN2 = kWinPix * kRowB;     // s2 b2 f32 behind the window
   static constexpr int kLds = kBN2 + 2 * P * 4;
   static constexpr int kS3 = kPx * kRowB;          // s3 b3 f32 behind t2 (over the window)
-  static constexpr int kKT = P / 32;               // k-steps per tap / per conv3 chunk
+  static constexpr int kKT = CM * P / 32;          // k-steps per tap / per conv3 chunk (split: hi, lo per 32 ch)
   static constexpr int kChunk = 32 * kNCQ;         // conv3 output channels per chunk
   static constexpr int kNC = C / kChunk;           // conv3 chunks
   static constexpr int kBlk3 = NEXT ? 2 : 1;       // stream blocks per conv3 chunk (+ the next conv1's K slice)
@@ -126,6 +127,7 @@ struct TailCfg {
   static_assert(kLdsAll <= 160 * 1024, "LDS");
   static_assert(!NEXT || kChunk == P, "the next conv1 takes one y chunk per K slice of P channels");
   static_assert(kKT % kD == 0, "the ring slot of a k-step is static inside a block");
+  static_assert(CM == 1 || (kD % 2 == 0 && kNB == 2 && W % 16 == 0), "split pairs: even stream depth, two fragment sets");
 };
 
 // P-channel LDS row of pixel `pix`, 16-B chunk `chunk`: the chunk index XOR `key` = the pixel's
@@ -148,9 +150,16 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 #define POSU_TS_MT4_WAVES 12
 #endif
 template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
-__global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
+__global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
-  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT>;
+  // split fp16 (POSU_F16X3, round 6): every pixel row holds [hi 32 | lo 32] per 32 channels, i.e. the
+  // kernel is the same GEMM over twice the K, whose k-step pairs (2c, 2c + 1) -- the hi and the lo
+  // halves of the same 32 channels, in the weight stream too -- are multiplied as hi.hi +
+  // lo(w).hi(x) + hi(w).lo(x) (the conv kernel's order per accumulator: bit-identical to it); the
+  // epilogues join residual pairs and split their outputs
+  constexpr bool SPL = O::SPLIT;
+  constexpr int CM = SPL ? 2 : 1;
+  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT, CM>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
   __shared__ __attribute__((aligned(16))) char smem[K::kLdsAll];
@@ -175,7 +184,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
     constexpr int kPixPerInst = 1024 / K::kRowB, kInst = K::kWinPix / kPixPerInst;
     static_assert(K::kWinPix % kPixPerInst == 0, "whole instructions");
     constexpr int kChunks = K::kRowB / 16;
-    const u32x4 t1s = make_srd(g.t1, g.N * H * W * P * ES);
+    const u32x4 t1s = make_srd(g.t1, g.N * H * W * P * CM * ES);
     const int sub = lane / kChunks, pc = lane % kChunks;
 #pragma unroll
     for (int k = 0; k < (kInst + NW - 1) / NW; ++k) {
@@ -186,7 +195,7 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
         const int yy = y0 + wr - 1, xx = wc - 1;
         const int lc = pc ^ wkey<W>(wr, wc);
         const bool ok = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < W;
-        dma16(t1s, ok ? (((n * H + yy) * W + xx) * P + 8 * lc) * ES : kOOB, lds0 + static_cast<unsigned>(m) * 1024u);
+        dma16(t1s, ok ? (((n * H + yy) * W + xx) * P * CM + 8 * lc) * ES : kOOB, lds0 + static_cast<unsigned>(m) * 1024u);
       }
     }
   }
@@ -229,10 +238,12 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
     }
   };
   const int cpair = 16 * (q & 1) + 8 * (q >> 1);
-  // relu(v * sc + sh (+ r)) over this lane's 8 values
+  // relu(v * sc + sh (+ r)) over this lane's 8 values; the multiply-add as an explicit fma, the conv
+  // epilogue's contraction: left to the compiler, the split variants' epilogues were vectorised into
+  // v_mul + v_pk_add (two roundings) and differed from the conv launches in the last f32 bit
   auto bn_relu = [&](float* v, const float* sc, const float* sh, const float* r) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] * sc[e] + sh[e] + (r ? r[e] : 0.f), 0.f);
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(__builtin_fmaf(v[e], sc[e], sh[e]) + (r ? r[e] : 0.f), 0.f);
   };
   // m-tile i's tile pixel (row-major in the tile) for this lane
   auto tpix = [&](int i) { return 16 * MT * pg + 16 * i + r16; };
@@ -241,8 +252,8 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
   // with `cols` pixels per row at 16-B chunk 4 d + q, swizzled by the lane's key (column & 15).
   // The pixel fragments of k-step d + 1 are read while k-step d's MFMAs run (two register
   // sets); the scheduling barriers keep the compiler from hoisting more of them.
-  // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 4 (d & 4) + (q ^ (key & 3)): four base
-  // pointers per (lane pixel, key), the k-step's 16 B at kb[d & 3] + (d & 4) * 64
+  // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 16 (d >> 2) + (q ^ (key & 3)): four base
+  // pointers per (lane pixel, key), the k-step's 16 B at kb[d & 3] + (d >> 2) * 256
   auto bases = [&](const char* (&kb)[4], int base, int lpix, int key) {
     const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
 #pragma unroll
@@ -268,9 +279,9 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
     auto rd = [&](int i, int d) -> uint4 {
       if (kAbl & 4) return make_uint4(i, d, lane, blk);
       if constexpr (W24)
-        return *reinterpret_cast<const uint4*>(kc[i % 3][d & 3] + (i / 3) * 2 * K::kWinCols * K::kRowB + (d & 4) * 64);
+        return *reinterpret_cast<const uint4*>(kc[i % 3][d & 3] + (i / 3) * 2 * K::kWinCols * K::kRowB + (d >> 2) * 256);
       else
-        return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d & 4) * 64);
+        return *reinterpret_cast<const uint4*>(kb[d & 3] + coff(i) * K::kRowB + (d >> 2) * 256);
     };
 #pragma unroll
     for (int i = 0; i < MT; ++i) b[0][i] = rd(i, 0);
@@ -281,20 +292,43 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
         for (int i = 0; i < MT; ++i) b[(d + 1) % NB][i] = rd(i, d + 1);
       }
       const int s = d % kD;
+      if constexpr (SPL) {
+        // the hi step (d even) issues both uses of its pixel fragments, hi.hi then lo(w).hi(x) (the
+        // lo weights of step d + 1 are in their slot already), the lo step hi(w).lo(x); then the slot
+        // used for the last time is refilled: the lo weights' after the hi step, the hi weights'
+        // after the lo step (a slot keeps its k-steps mod kD)
+        const int s2 = (d & 1) ? s - 1 : s + 1;
+        if ((d & 1) == 0) {
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
+          for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d % NB][i].y);
-          else O::mma(acc[i][j], wa[s][j], b[d % NB][i]);
+            for (int j = 0; j < 2; ++j) O::mma(acc[i][j], wa[s][j], b[d % NB][i]);
         }
-        // one set: m-tile i's fragment of the next k-step once its MFMAs are issued
-        if (NB == 1 && d + 1 < K::kKT) b[0][i] = rd(i, d + 1);
-      }
-      const int p = K::kKT * blk + d + kD;
-      if (!(kAbl & 2)) {
-        wa[s][0] = *frag(p, 0);
-        wa[s][1] = *frag(p, 1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) O::mma(acc[i][j], wa[s2][j], b[d % NB][i]);
+        const int p = K::kKT * blk + ((d & 1) ? d - 1 : d + 1) + kD;
+        if (!(kAbl & 2)) {
+          wa[s2][0] = *frag(p, 0);
+          wa[s2][1] = *frag(p, 1);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            if (kAbl & 1) acc[i][j][0] += __uint_as_float(wa[s][j].x ^ b[d % NB][i].y);
+            else O::mma(acc[i][j], wa[s][j], b[d % NB][i]);
+          }
+          // one set: m-tile i's fragment of the next k-step once its MFMAs are issued
+          if (NB == 1 && d + 1 < K::kKT) b[0][i] = rd(i, d + 1);
+        }
+        const int p = K::kKT * blk + d + kD;
+        if (!(kAbl & 2)) {
+          wa[s][0] = *frag(p, 0);
+          wa[s][1] = *frag(p, 1);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -313,28 +347,62 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
             [&](int i) { return (16 * i / W) * K::kWinCols + (16 * i) % W; });
     }
   }
-  const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C;
-  T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C;
+  const T* xg = reinterpret_cast<const T*>(g.x) + static_cast<size_t>(n * H + y0) * W * C * CM;
+  T* yg = reinterpret_cast<T*>(g.y) + static_cast<size_t>(n * H + y0) * W * C * CM;
   // the tile's x / y (/ t1n) through buffer descriptors: a lane's 32-bit byte offset plus
   // compile-time per-m-tile / per-chunk steps, instead of a 64-bit address per m-tile (the
   // chained layer3 tail spilled such addresses: 34 VGPRs, round 4); stores keep soffset 0 (the
   // store-data hazard)
   const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xg), 0, K::kPx * C * ES, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yg, 0, K::kPx * C * ES, 0x00020000);
-  const int lane_xy = ((16 * MT * pg + r16) * C + 32 * cq + cpair) * ES;   // m-tile 0, chunk 0
-  // conv3 chunk nc's residual in the epilogue's lane layout
-  auto res_load = [&](int nc, uint4 (&rv)[MT]) {
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(xg), 0, K::kPx * C * CM * ES, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(yg, 0, K::kPx * C * CM * ES, 0x00020000);
+  // m-tile 0, chunk 0 (split: the hi half; the lo half 32 elements = 64 B further)
+  const int lane_xy = ((16 * MT * pg + r16) * C * CM + (SPL ? split_ch(32 * cq + cpair) : 32 * cq + cpair)) * ES;
+  auto xy_off = [&](int i, int nc) { return lane_xy + (16 * i * C + K::kChunk * nc) * CM * ES; };
+  // conv3 chunk nc's residual in the epilogue's lane layout (rl: the split pairs' lo halves)
+  auto res_load = [&](int nc, uint4 (&rv)[MT], uint4 (&rl)[MT]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       if (kAbl & 72) {
         rv[i] = make_uint4(i, c0, 0, 0);
+        rl[i] = rv[i];
       } else {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0,
-                                                             POSU_TS_LD_AUX);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xrs, xy_off(i, nc), 0, POSU_TS_LD_AUX);
         rv[i] = make_uint4(v[0], v[1], v[2], v[3]);
+        if constexpr (SPL) {
+          const auto l = __builtin_amdgcn_raw_buffer_load_b128(xrs, xy_off(i, nc) + 64, 0, POSU_TS_LD_AUX);
+          rl[i] = make_uint4(l[0], l[1], l[2], l[3]);
+        }
       }
+    }
+  };
+  // 16-B store of the 8 values of this lane (split: the hi and the lo halves, 64 B apart)
+  auto st8 = [&](__amdgpu_buffer_rsrc_t rs, int off, const float* v) {
+    if constexpr (SPL) {
+      uint4 h, l;
+      split8(v, h, l);
+      __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){h.x, h.y, h.z, h.w}, rs,
+                                             off, 0, POSU_TS_ST_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){l.x, l.y, l.z, l.w}, rs,
+                                             off + 64, 0, POSU_TS_ST_AUX);
+    } else {
+      const uint4 o = O::store_vals(v);
+      __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, rs,
+                                             off, 0, POSU_TS_ST_AUX);
+    }
+  };
+  // the same 8 values into an LDS image of P-channel rows (t2, the NEXT y chunk): chunk c8 (the
+  // logical 8-channel chunk in the row), split: hi and lo chunks
+  auto lds8 = [&](int base, int pix, int c8, const float* v) {
+    if constexpr (SPL) {
+      uint4 h, l;
+      split8(v, h, l);
+      const int ch = split_ch(8 * c8) >> 3;
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, ch)) = h;
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, ch + 4)) = l;
+    } else {
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, c8)) = O::store_vals(v);
     }
   };
   // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
@@ -354,19 +422,19 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       float v[8];
       pair(acc, i, v);
       bn_relu(v, sc, sh, nullptr);
-      *reinterpret_cast<uint4*>(smem + swzp<K::kRowB>(tpix(i), r16, c0 >> 3)) = O::store_vals(v);
+      lds8(0, tpix(i), c0 >> 3, v);
     }
   }
   lds_barrier();
 
   // ---- conv3: output chunk nc (kChunk channels; this wave's 32), kKT channel steps over t2
   const float* b3l = reinterpret_cast<const float*>(smem + K::kS3);
-  auto chunk = [&](int nc, uint4 (&rv)[MT]) {
+  auto chunk = [&](int nc, uint4 (&rv)[MT], uint4 (&rl)[MT]) {
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
     zero(acc);
     block(acc, 9 + K::kBlk3 * nc, 0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers)
-    if constexpr (NEXT) res_load(nc, rv);
+    if constexpr (NEXT) res_load(nc, rv, rl);
     float sc[8], sh[8];
     ld8(b3l + c0, sc);
     ld8(b3l + C + c0, sh);
@@ -377,16 +445,13 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
     for (int i = 0; i < MT; ++i) {
       float v[8], r[8];
       pair(acc, i, v);
-      O::load_vals(rv[i], r);
+      if constexpr (SPL) join8(rv[i], rl[i], r);
+      else O::load_vals(rv[i], r);
       bn_relu(v, sc, sh, r);
-      const uint4 o = O::store_vals(v);
-      if (kAbl & 40) asm volatile("" ::"v"(o.x), "v"(o.y), "v"(o.z), "v"(o.w));
-      else
-        __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, yrs,
-                                               lane_xy + (16 * i * C + K::kChunk * nc) * ES, 0, POSU_TS_ST_AUX);
+      if (kAbl & 40) asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
+      else st8(yrs, xy_off(i, nc), v);
       // NEXT: the chunk's y, laid out like t2 ([pixel][P] rows, column-keyed swizzle)
-      if constexpr (NEXT)
-        *reinterpret_cast<uint4*>(smem + K::kYC + swzp<K::kRowB>(tpix(i), r16, (32 * cq + cpair) >> 3)) = o;
+      if constexpr (NEXT) lds8(K::kYC, tpix(i), (32 * cq + cpair) >> 3, v);
     }
     if constexpr (NEXT) {
       // the next block's conv1 over this K slice (y channels kChunk nc ..): same k order as a
@@ -402,14 +467,14 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
   for (int nc = 0; nc < K::kNC; ++nc) {
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
     // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
-    uint4 rv[MT];
-    if constexpr (!NEXT) res_load(nc, rv);
-    chunk(nc, rv);
+    uint4 rv[MT], rl[MT];
+    if constexpr (!NEXT) res_load(nc, rv, rl);
+    chunk(nc, rv, rl);
   }
   if constexpr (NEXT) {
     // t1n = relu(conv1n * s1n + b1n), this lane's 8 channels of each m-tile's pixel
-    T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * P;
-    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(tg, 0, K::kPx * P * ES, 0x00020000);
+    T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * P * CM;
+    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(tg, 0, K::kPx * P * CM * ES, 0x00020000);
     const int c0 = 32 * cq + cpair;
     float sc[8], sh[8];
     ld8(g.s1n + c0, sc);
@@ -419,11 +484,18 @@ __global__ __launch_bounds__(NW * 64, (MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVE
       float v[8];
       pair(acc1, i, v);
       bn_relu(v, sc, sh, nullptr);
-      const uint4 o = O::store_vals(v);
-      __builtin_amdgcn_raw_buffer_store_b128((__attribute__((ext_vector_type(4))) unsigned){o.x, o.y, o.z, o.w}, trs,
-                                             (tpix(i) * P + c0) * ES, 0, 0);
+      st8(trs, (tpix(i) * P * CM + (SPL ? split_ch(c0) : c0)) * ES, v);
     }
   }
+}
+
+// split fp16 instances (round 6): layer1 (W = 64, planes 64: 2 rows x 64 px, four waves as 2 pixel x 2
+// channel groups), layer2 (2 rows x 32 px, four waves), layer3 (4 rows x 16 px, eight waves) -- the
+// pairs double the t1 window, so the tiles are the bf16 ones' small variants (68 / 69 / 110 KB of LDS)
+template <int W, int P, int C, int ROWS, int NW, bool NEXT, int MT>
+void launch_tail_split(const TailSGeom& g, hipStream_t s) {
+  hipLaunchKernelGGL((tail_stream_kernel<f16s_t, W, P, C, ROWS, NW, NEXT, MT>), dim3(static_cast<unsigned>(g.N * (g.H / ROWS))),
+                     dim3(NW * 64), 0, s, g);
 }
 
 template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
@@ -465,7 +537,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                      void* stream) {
   const std::string what = name;
   const bool next = t1n != nullptr;
-  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16, what + ": dtype must be BF16 or F16");
+  const bool spl = dtype == POSU_F16X3;
+  POSU_REQUIRE(dtype == POSU_BF16 || dtype == POSU_F16 || spl, what + ": dtype must be BF16, F16 or F16X3");
   POSU_REQUIRE(t1 && x && wstream && s2 && b2 && s3 && b3 && y, what + ": null pointer");
   POSU_REQUIRE(x != y && t1 != y, what + ": the output must not alias an input");
   POSU_REQUIRE(!next || (s1n && b1n && t1n != y && t1n != x && t1n != t1),
@@ -473,12 +546,17 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   const bool l3 = W == 16 && C == 1024 && P == 256, l2 = W == 32 && C == 512 && P == 128;
   const bool l3w = W == 24 && C == 1024 && P == 256;   // layer3 at 384x384 (R152 configs[4])
   const bool l2w = W == 48 && C == 512 && P == 128;    // layer2 at 384x384
-  POSU_REQUIRE(l2 || l3 || l3w || l2w, what + ": built for layer2 (W = 32 or 48, C = 512, planes = 128) and layer3 "
-                                              "(W = 16 or 24, C = 1024, planes = 256) of PoseResNet at 256x256 / 384x384");
+  const bool l1 = W == 64 && C == 256 && P == 64;      // layer1 at 256x256 (the split dtype only)
+  POSU_REQUIRE(l2 || l3 || l3w || l2w || (spl && l1),
+               what + ": built for layer2 (W = 32 or 48, C = 512, planes = 128) and layer3 (W = 16 or 24, C = 1024, "
+                      "planes = 256) of PoseResNet at 256x256 / 384x384, and (split fp16) layer1 (W = 64, C = 256, "
+                      "planes = 64)");
+  POSU_REQUIRE(!spl || !(l3w || l2w), what + ": the split dtype runs the 256x256 tails (W = 64, 32, 16)");
+  const int cm = spl ? 2 : 1;   // stored halves per logical channel
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
-    // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream)
-    const long long kt = P / 32, nc = C / P;
+    // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream); split: KT = 2 P / 32
+    const long long kt = cm * P / 32, nc = C / P;
     const long long need = (P / 32) * (9 * kt + (next ? 2 : 1) * nc * kt) * 2 * 64 * 8 * 2;
     POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
@@ -488,10 +566,10 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   // workgroup, else 4-row tiles (64 px, 4 m-tiles per wave): at batch 64 (BASELINE configs[1]) the
   // 8-row grid left half the CUs idle (128 workgroups)
   const bool l3h = l3 && N > 0 && H % 4 == 0 && static_cast<long long>(N) * (H / 8) < POSU_TS_L3_SMALL_GRID;
-  const int rows = l3 ? (l3h ? 4 : 8) : l3w ? 6 : l2w ? 2 : kL2Rows;
+  const int rows = spl ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? 6 : l2w ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
-  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 < (1LL << 31) - 256,
+  POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 * cm < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
   for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(s3),
                         static_cast<const void*>(b3), next ? t1n : t1, static_cast<const void*>(next ? s1n : s3),
@@ -514,7 +592,18 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   g.wseg = wstream_bytes / 64;
   g.warm = warm_wgs(wstream_bytes);
   hipStream_t s = as_stream(stream);
-  if (l3h) {
+  if (spl) {
+    if (l1) {
+      if (next) launch_tail_split<64, 64, 256, 2, 4, true, 4>(g, s);
+      else launch_tail_split<64, 64, 256, 2, 4, false, 4>(g, s);
+    } else if (l2) {
+      if (next) launch_tail_split<32, 128, 512, 2, 4, true, 4>(g, s);
+      else launch_tail_split<32, 128, 512, 2, 4, false, 4>(g, s);
+    } else {
+      if (next) launch_tail_split<16, 256, 1024, 4, 8, true, 4>(g, s);
+      else launch_tail_split<16, 256, 1024, 4, 8, false, 4>(g, s);
+    }
+  } else if (l3h) {
     if (next) launch_tail<16, 256, 1024, 4, 8, true, 4>(dtype, g, s);
     else launch_tail<16, 256, 1024, 4, 8, false, 4>(dtype, g, s);
   } else if (l3) {

@@ -21,12 +21,10 @@ def calc_dists(preds, target, normalize):
 
 
 def dist_acc(dists, thr=0.5):
-    """Fraction below `thr` ignoring -1 entries; -1 if there are none (evaluate.py:32-39)."""
-    dist_cal = np.not_equal(dists, -1)
-    num_dist_cal = dist_cal.sum()
-    if num_dist_cal > 0:
-        return np.less(dists[dist_cal], thr).sum() * 1.0 / num_dist_cal
-    return -1
+    """Fraction of the entries != -1 below `thr`; -1 when every entry is -1 (evaluate.py:32-39)."""
+    valid = dists != -1
+    n = int(np.count_nonzero(valid))
+    return np.count_nonzero(dists[valid] < thr) * 1.0 / n if n else -1
 
 
 def _np(x):
@@ -34,26 +32,25 @@ def _np(x):
 
 
 def accuracy(output, target, hm_type='gaussian', thr=0.5):
-    """evaluate.py:42-73 (output / target: [N, J, h, w] numpy or cuda tensors)."""
-    idx = list(range(output.shape[1]))
-    norm = 1.0
-    if hm_type == 'gaussian':
-        pred, _ = get_max_preds(output)
-        target, _ = get_max_preds(target)
-        pred, target = _np(pred), _np(target)
-        h = output.shape[2]
-        w = output.shape[3]
-        norm = np.ones((pred.shape[0], 2)) * np.array([h, w]) / 10
-    dists = calc_dists(pred, target, norm)
-    acc = np.zeros((len(idx) + 1))
+    """evaluate.py:42-73 (output / target: [N, J, h, w] numpy or cuda tensors) -> (acc [J+1],
+    avg_acc, cnt, pred): both argmaxes from the HIP kernel, then every joint's PCK at once over the
+    [J, N] distance table (acc[0] = the mean over the joints that have a valid target)."""
+    if hm_type != 'gaussian':
+        raise NotImplementedError("accuracy: hm_type 'gaussian' only (the reference defines pred for it alone)")
+    pred, tgt = (_np(get_max_preds(t)[0]) for t in (output, target))
+    norm = np.tile(np.array([output.shape[2], output.shape[3]], dtype=np.float64) / 10, (pred.shape[0], 1))
+    dists = calc_dists(pred, tgt, norm)                      # [J, N], -1: target outside the map
+    valid = dists != -1
+    nval = valid.sum(axis=1)
+    hits = np.logical_and(dists < thr, valid).sum(axis=1)
+    per_joint = np.where(nval > 0, hits * 1.0 / np.maximum(nval, 1), -1.0)
+    acc = np.concatenate([[0.0], per_joint])
+    counted = per_joint[per_joint >= 0]
+    cnt = len(counted)
     avg_acc = 0
-    cnt = 0
-    for i in range(len(idx)):
-        acc[i + 1] = dist_acc(dists[idx[i]])
-        if acc[i + 1] >= 0:
-            avg_acc = avg_acc + acc[i + 1]
-            cnt += 1
-    if cnt != 0:
+    for a in counted:   # accumulated joint by joint, as the reference does
+        avg_acc = avg_acc + a
+    if cnt:
         avg_acc = avg_acc / cnt
         acc[0] = avg_acc
     return acc, avg_acc, cnt, pred

@@ -127,12 +127,13 @@ def bottleneck_nhwc(x, w1, s1, b1, w2, s2, b2, w3, s3, b3, code, out=None):
 
 def bottleneck_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, out=None):
     """conv2 + conv3 (+ residual) of a layer2 / layer3 identity Bottleneck with the weights
-    streamed into registers (posu_bottleneck_tail_stream_fwd, csrc/tail_stream.hip);
-    wstream = packing.pack_tail_stream(conv2 pack, conv3 pack)."""
+    streamed into registers (posu_bottleneck_tail_stream_fwd, csrc/tail_stream.hip; the split dtype
+    also at layer1's shape); wstream = packing.pack_tail_stream(conv2 pack, conv3 pack)."""
     n, h, w, c = x.shape
     if out is None:
         out = torch.empty_like(x)
-    call('posu_bottleneck_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3], ptr(wstream),
+    call('posu_bottleneck_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c // cmul(code), t1.shape[3] // cmul(code),
+         ptr(wstream),
          wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), stream_of(x.device))
     return out
 
@@ -177,7 +178,8 @@ def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, c
         out = torch.empty_like(x)
     if t1n is None:
         t1n = torch.empty((n, h, w, p), dtype=x.dtype, device=x.device)
-    call('posu_bottleneck_tail_stream_next_fwd', code, ptr(t1), ptr(x), n, h, w, c, p, ptr(wstream),
+    cm = cmul(code)
+    call('posu_bottleneck_tail_stream_next_fwd', code, ptr(t1), ptr(x), n, h, w, c // cm, p // cm, ptr(wstream),
          wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n),
          ptr(t1n), stream_of(x.device))
     return out, t1n

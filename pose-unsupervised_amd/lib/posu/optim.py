@@ -32,22 +32,25 @@ class Adam(torch.optim.Adam):
         for group in self.param_groups:
             if group.get('amsgrad') or group.get('maximize') or group.get('differentiable'):
                 raise NotImplementedError('posu.optim.Adam: amsgrad / maximize / differentiable are not supported')
-            by_step = {}
-            for p in group['params']:
-                if p.grad is None:
-                    continue
+            # every parameter is checked before any state changes: a refusal leaves the optimizer as it was
+            params = [p for p in group['params'] if p.grad is not None]
+            for p in params:
                 if p.grad.is_sparse or p.is_complex() or p.dtype != torch.float32:
                     raise NotImplementedError('posu.optim.Adam: dense f32 parameters only')
                 nat.require_cuda(p, p.grad)
                 st = self.state[p]
+                if not p.is_contiguous() or (len(st) and not (st['exp_avg'].is_contiguous() and
+                                                              st['exp_avg_sq'].is_contiguous())):
+                    raise NotImplementedError('posu.optim.Adam: contiguous parameters and state only')
+            by_step = {}
+            for p in params:
+                st = self.state[p]
                 if len(st) == 0:   # torch.optim.Adam's state (step on the host, as its non-fused form)
                     st['step'] = torch.tensor(0.0)
-                    st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st['exp_avg'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 st['step'] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                if not (p.is_contiguous() and st['exp_avg'].is_contiguous() and st['exp_avg_sq'].is_contiguous()):
-                    raise NotImplementedError('posu.optim.Adam: contiguous parameters and state only')
                 by_step.setdefault((int(st['step'].item()), p.device), []).append((p, g, st))
             beta1, beta2 = group['betas']
             for (step, dev), items in by_step.items():

@@ -73,17 +73,22 @@ def pack_tail_stream(w2pk, w3pk, w1n=None):
     w1n (the next identity block's conv1 pack [P][C], posu_bottleneck_tail_stream_next_fwd):
     after conv3 chunk nc come the next conv1's KT k-steps over that chunk's channels -- p =
     9 KT + 2 KT nc + c: conv3 as above; p = 9 KT + 2 KT nc + KT + c: conv1n n-tile 2 cq + j,
-    k-step KT nc + c."""
+    k-step KT nc + c.
+
+    Split fp16 packs (to_split: K' = 2 K, [hi 32 | lo 32] per 32 k) give KT = 2 P / 32: every pair of
+    k-steps is the hi and the lo half of the same 32 channels, which the split tail multiplies as
+    hi.hi + lo(w).hi(x) + hi(w).lo(x)."""
     planes, c = w2pk.shape[0], w3pk.shape[0]
-    ncq, kt, nc = planes // 32, planes // 32, c // planes
+    ncq, kt, nc = planes // 32, w3pk.shape[1] // 32, c // planes
+    cm = kt * 32 // planes   # stored halves per logical channel (2: split packs)
     f2 = mfma_fragments(w2pk)                                    # [2 ncq][9 kt][64][8]
     f3 = mfma_fragments(w3pk)                                    # [2 ncq nc][kt][64][8]
     s2 = f2.reshape(ncq, 2, 9 * kt, 64, 8).permute(0, 2, 1, 3, 4)
     s3 = f3.reshape(nc, ncq, 2, kt, 64, 8).permute(1, 0, 3, 2, 4, 5)              # [ncq][nc][kt][2][64][8]
     if w1n is None:
         return torch.cat([s2, s3.reshape(ncq, nc * kt, 2, 64, 8)], dim=1).contiguous()
-    if tuple(w1n.shape) != (planes, c):
-        raise ValueError('pack_tail_stream: the next conv1 pack must be [%d][%d]' % (planes, c))
+    if tuple(w1n.shape) != (planes, c * cm):
+        raise ValueError('pack_tail_stream: the next conv1 pack must be [%d][%d]' % (planes, c * cm))
     f1 = mfma_fragments(w1n)                                     # [2 ncq][nc kt][64][8]
     s1 = f1.reshape(ncq, 2, nc, kt, 64, 8).permute(0, 2, 3, 1, 4, 5)              # [ncq][nc][kt][2][64][8]
     s31 = torch.stack([s3, s1], dim=2).reshape(ncq, nc * 2 * kt, 2, 64, 8)

@@ -257,6 +257,9 @@ S2_CHAIN = True
 # the identity Bottlenecks at 384x384 (R152, BASELINE configs[4]) as conv1 + the streamed tail
 # (round 5): layer3 at W = 24 (not chained), layer2 at W = 48 (chained)
 TAIL_W24 = True
+# the split dtype's identity Bottlenecks of layer1 / layer2 / layer3 as conv1 + the streamed tail
+# (chained), round 6; False: three conv launches each
+SPLIT_TAILS = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -269,7 +272,7 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l1', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -278,6 +281,7 @@ class _Block:
         self.dual = None
         self.w1f = self.w3f = None   # conv1 / conv3 packed for the fused kernel (permuted K)
         self.w3d = None              # the fused first block's [w3*s3 | wd*sd] (permuted conv3 K)
+        self.l1 = False              # a layer1 identity block on the streamed tail (the split dtype, round 6)
         self.l2 = False              # a layer2 identity block (fused kernel, the convs' own packs)
         self.l3 = False              # a layer3 identity block (conv1, then the fused conv2 + conv3 tail)
         self.wst = None              # layer2 / layer3: the tail's per-wave weight streams (pack_tail_stream)
@@ -310,16 +314,20 @@ class _Block:
         elif code in (ops.BF16, ops.F16) and len(names) == 3 and self._fusable_shape():
             self.w1f = pack_bottleneck_conv1_weight(blk.conv1.weight, ops.torch_dtype(code))
             self.w3f = pack_bottleneck_conv3_weight(blk.conv3.weight, ops.torch_dtype(code))
-        elif code in (ops.BF16, ops.F16) and len(names) == 3:
-            self.l2 = self._layer2_shape()
-            self.l3 = self._layer3_shape()
-            if self.l2 or self.l3:
+        elif code in (ops.BF16, ops.F16, ops.F16X3) and len(names) == 3:
+            # (the split dtype: its packs hold 2 K halves per row; layer1 too -- the fused layer1 kernel
+            # does not hold pairs -- on the streamed tail, round 6)
+            cm = ops.cmul(code)
+            self.l1 = code == ops.F16X3 and SPLIT_TAILS and self._layer1_shape(cm)
+            self.l2 = (code != ops.F16X3 or SPLIT_TAILS) and self._layer2_shape(cm)
+            self.l3 = (code != ops.F16X3 or SPLIT_TAILS) and self._layer3_shape(cm)
+            if self.l1 or self.l2 or self.l3:
                 self.wst = pack_tail_stream(self.convs[1].w, self.convs[2].w)
 
     def link_next(self, nxt):
         """Chain this identity block's streamed tail with the next block's conv1 (same layer, same
         kind of tail)."""
-        if (self.l2 and nxt.l2) or (self.l3 and nxt.l3):
+        if (self.l1 and nxt.l1) or (self.l2 and nxt.l2) or (self.l3 and nxt.l3):
             self.chain = nxt.convs[0]
             self.wsn = pack_tail_stream(self.convs[1].w, self.convs[2].w, self.chain.w)
         elif self.ws2 is not None and nxt.l2:   # layer2's strided tail and block 1's conv1
@@ -330,6 +338,8 @@ class _Block:
         """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
         if not FUSED_BOTTLENECK or not _fused_fits(x, self.cout):
             return None
+        if self.l1 and x.shape[2] == 64 and x.shape[1] % 2 == 0:   # split fp16: 2-row tiles
+            return 'l1'
         if self.l2 and x.shape[2] == 32 and x.shape[1] % 4 == 0:
             return 'l2'
         if self.l3 and x.shape[2] == 16 and x.shape[1] % 8 == 0:
@@ -369,17 +379,22 @@ class _Block:
         return (self.ws2 is not None and S2_TAIL and FUSED_BOTTLENECK and _fused_fits(x, self.cout) and
                 x.shape[2] == 64 and x.shape[1] % 8 == 0)
 
-    def _layer2_shape(self):
+    def _tail_shape(self, c, p, cm):
+        """An identity Bottleneck C -> P -> P -> C (1x1, 3x3 / 1 / pad 1, 1x1) whose packs hold cm
+        stored halves per logical k."""
         c1, c2, c3 = self.convs
-        return (c1.k == 1 and c1.stride == 1 and c1.w.shape == (128, 512) and
-                c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (128, 1152) and
-                c3.k == 1 and c3.stride == 1 and c3.w.shape == (512, 128))
+        return (c1.k == 1 and c1.stride == 1 and tuple(c1.w.shape) == (p, c * cm) and
+                c2.k == 3 and c2.stride == 1 and c2.pad == 1 and tuple(c2.w.shape) == (p, 9 * p * cm) and
+                c3.k == 1 and c3.stride == 1 and tuple(c3.w.shape) == (c, p * cm))
 
-    def _layer3_shape(self):
-        c1, c2, c3 = self.convs
-        return (c1.k == 1 and c1.stride == 1 and c1.w.shape == (256, 1024) and
-                c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (256, 2304) and
-                c3.k == 1 and c3.stride == 1 and c3.w.shape == (1024, 256))
+    def _layer1_shape(self, cm=1):
+        return self._tail_shape(256, 64, cm)
+
+    def _layer2_shape(self, cm=1):
+        return self._tail_shape(512, 128, cm)
+
+    def _layer3_shape(self, cm=1):
+        return self._tail_shape(1024, 256, cm)
 
     def _fusable_shape(self):
         c1, c2, c3 = self.convs

@@ -392,7 +392,11 @@ class TrainPlan:
             n, _, h, w = x[0].shape
             stem_own = FUSED_STEM_POOL and self._stem_kernels(x)
             packed = None
-            if stem_own and PACK_BESIDE_STEM and SIDE_STREAM_WGRAD:
+            # (the first pack, which allocates the packer's persistent buffers and job table, runs on
+            # the main stream: allocated on the side stream they would return to its pool when the
+            # packer is rebuilt, while main-stream kernels may still read them)
+            built = self.packer is not None and self.packer.device == self.head.weight.device
+            if stem_own and PACK_BESIDE_STEM and SIDE_STREAM_WGRAD and built:
                 # the side stream takes the pack after everything before it on this stream (Adam);
                 # the stem needs no packed weight, layer1 waits for the pack below
                 dev = x[0].device

@@ -484,3 +484,94 @@ def test_plan_with_chained_tails_matches_unchained_plan(cuda, precision):
         P.CHAINED_TAILS = saved
     torch.cuda.synchronize()
     assert torch.equal(hm1, hm0) and torch.equal(f1, f0)
+
+
+def _split_pack(w, cin):
+    """A conv weight -> (split fp16 pack [Cout][2 K], its power-of-two exponent e) as the fp16x3 plan
+    packs it (the epilogue scale carries 2^-e)."""
+    pk = packing.pack_conv_weight(w, cin, 32, torch.float32)
+    e = packing.split_exponent(pk)
+    return packing.to_split(pk, e), e
+
+
+@pytest.mark.parametrize('layer,n,h', [('layer1', 2, 64), ('layer1', 1, 2), ('layer1', 3, 10), ('layer1', 128, 64),
+                                       ('layer2', 2, 32), ('layer2', 1, 2), ('layer2', 3, 12), ('layer2', 128, 32),
+                                       ('layer3', 2, 16), ('layer3', 1, 4), ('layer3', 3, 12), ('layer3', 128, 16)])
+def test_split_tails_match_conv_launches(cuda, layer, n, h):
+    """Split fp16 (POSU_F16X3) streamed tails, round 6: the plain tail against the conv2 + conv3
+    (+ residual) launches, the chained tail against the plain tail + a conv launch of the next conv1 --
+    bit-identical (per accumulator the conv kernel's K order and its hi.hi, lo.hi, hi.lo sequence; the
+    same epilogue arithmetic and (hi, lo) split), every output starting as a NaN sentinel; and the
+    tail within the split dtype's f32-level error of an fp64 torch block.  (128, ..): the
+    production grids."""
+    c, p, w = {'layer1': (256, 64, 64), 'layer2': (512, 128, 32), 'layer3': (1024, 256, 16)}[layer]
+    S = ops.F16X3
+    g = torch.Generator().manual_seed(131 + h + n + p)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
+    w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1n = (torch.rand(p, generator=g) + 0.5, torch.randn(p, generator=g) * 0.1)
+    x = torch.randn(n, h, w, c, generator=g, dtype=torch.float64)
+    xd = packing.to_split(x).to(cuda)
+    (p1, e1), (p2, e2), (p3, e3), (p1n, e1n) = (_split_pack(t.to(cuda), t.shape[1]) for t in (w1, w2, w3, w1n))
+    def sc(bn, e):
+        return (bn[0].double() * 2.0 ** -e).float().to(cuda), bn[1].to(cuda)
+    s1, b1 = sc(bn1, e1)
+    s2, b2 = sc(bn2, e2)
+    s3, b3 = sc(bn3, e3)
+    s1n, b1n = sc(bn1n, e1n)
+    t1 = ops.conv2d_nhwc(xd, p1, p, 1, 1, 1, 0, s1, b1, None, True, S)
+    y = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s2, b2, s3, b3, S,
+                                        out=_sentinel(xd))
+    t2 = ops.conv2d_nhwc(t1, p2, p, 3, 3, 1, 1, s2, b2, None, True, S)
+    two = ops.conv2d_nhwc(t2, p3, c, 1, 1, 1, 0, s3, b3, xd, True, S)
+    yc, t1n = ops.bottleneck_tail_stream_next_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1n), s2, b2, s3, b3, s1n,
+                                                   b1n, S, out=_sentinel(xd), t1n=_sentinel(t1))
+    t1n_ref = ops.conv2d_nhwc(two, p1n, p, 1, 1, 1, 0, s1n, b1n, None, True, S)
+    torch.cuda.synchronize()
+    dy = int((y.view(torch.int16) != two.view(torch.int16)).sum())
+    dyc = int((yc.view(torch.int16) != two.view(torch.int16)).sum())
+    dt1 = int((t1n.view(torch.int16) != t1n_ref.view(torch.int16)).sum())
+    print('split %s tail n=%d h=%d: y differing %d, chained y %d, t1n %d' % (layer, n, h, dy, dyc, dt1))
+    assert dy == 0 and dyc == 0 and dt1 == 0
+    if n >= 128:
+        return
+    # fp64 torch on the values the device holds: within the f32 level of sum |w x|
+    xq = ops.widen(xd, S).double().cpu().permute(0, 3, 1, 2)
+    wq = [t.float().double() for t in (w1, w2, w3)]
+    a = [t.double() for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1])]
+    r1 = F.relu(F.conv2d(xq, wq[0]) * a[0].view(1, -1, 1, 1) + a[1].view(1, -1, 1, 1))
+    r2 = F.relu(F.conv2d(r1, wq[1], padding=1) * a[2].view(1, -1, 1, 1) + a[3].view(1, -1, 1, 1))
+    ref = F.relu(F.conv2d(r2, wq[2]) * a[4].view(1, -1, 1, 1) + a[5].view(1, -1, 1, 1) + xq)
+    got = ops.widen(y, S).double().cpu().permute(0, 3, 1, 2)
+    err = float((got - ref).abs().max())
+    assert err <= 1e-5 * (1.0 + float(ref.abs().max())), err
+
+
+def test_split_plan_tails_are_bit_identical_to_conv_launches(cuda):
+    """The R50@256 fp16x3 plan with its identity Bottlenecks of layer1-3 on the split streamed tails
+    (chained; plan.SPLIT_TAILS) gives the heatmaps and features of the plan that runs every
+    convolution as its own launch, bit for bit."""
+    import posu.plan as P
+    from models.pose_resnet import get_pose_net
+    net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision='fp16x3')
+    net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
+    net = net.to(cuda).eval()
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=14)]
+    saved = P.SPLIT_TAILS
+    try:
+        with torch.no_grad():
+            P.SPLIT_TAILS = True
+            plan = P.PoseResNetPlan(net, ops.F16X3)
+            assert [b.l1 for b in plan.layers[0]] == [False, True, True]
+            assert [b.l2 for b in plan.layers[1]] == [False, True, True, True]
+            assert [b.l3 for b in plan.layers[2]] == [False] + [True] * 5
+            assert [b.chain is not None for b in plan.layers[0]] == [False, True, False]
+            hm1, x11, f1 = plan.run(plan.pack_input(views))
+            P.SPLIT_TAILS = False
+            plan0 = P.PoseResNetPlan(net, ops.F16X3)
+            assert not any(b.l1 or b.l2 or b.l3 for layer in plan0.layers for b in layer)
+            hm0, x10, f0 = plan0.run(plan0.pack_input(views))
+    finally:
+        P.SPLIT_TAILS = saved
+    torch.cuda.synchronize()
+    assert torch.equal(x11, x10) and torch.equal(hm1, hm0) and torch.equal(f1, f0)

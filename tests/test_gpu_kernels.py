@@ -232,6 +232,29 @@ def test_triangulate_one_point_api(cuda, golden):
     np.testing.assert_allclose(X, g['poses3d'][0, 4], atol=1e-6)
 
 
+@pytest.mark.parametrize('nviews', [5, 8, 12])
+def test_triangulation_more_than_four_views(cuda, golden, nviews):
+    """More than 4 views (posu_triangulate_dlt's 16-view kernel, rows folded into a 4 x 4 R factor by
+    Givens rotations, round 6): exact on noise-free pinhole projections, and the oracle's numpy-SVD
+    restatement of pymvg find3d on noisy distorted ones."""
+    from multiviews.triangulate import build_multi_camera_system
+    g = golden('cameras.npz')
+    cams = syn.group_cameras(3, distortion=True)[:nviews]   # two subject rigs: up to 12 distinct cameras
+    r = np.random.default_rng(nviews)
+    for nodist in (True, False):
+        system = build_multi_camera_system([('c%d' % i, c) for i, c in enumerate(cams)], no_distortion=nodist)
+        oc = [G._camera(c, nodist) for c in cams]
+        for X in g['poses3d'][0, :6]:
+            pts = [system.find2d('c%d' % i, X, distorted=not nodist) for i in range(nviews)]
+            if not nodist:
+                pts = [p + r.normal(0, 2.0, size=2) for p in pts]
+            got = system.find3d([('c%d' % i, p) for i, p in enumerate(pts)])
+            ref = G.find3d([c[0] for c in oc], [c[1] for c in oc], [c[2] for c in oc], pts)
+            if nodist:
+                np.testing.assert_allclose(got, X, atol=1e-6, rtol=0)
+            np.testing.assert_allclose(got, ref, atol=1e-6, rtol=0)
+
+
 @pytest.mark.parametrize('code,tol', [(F32, 1e-4), (BF16, 0.05), (F16, 0.01)])
 def test_s2d_stem_matches_torch(cuda, code, tol):
     g = torch.Generator().manual_seed(6)

@@ -4,14 +4,16 @@ not product code).
 With random synthetic weights the heatmaps are flat noise, and the reference's soft-argmax
 (softmax of 100 x heatmap, lib/utils/transforms.py:149-171) turns a 0.02 heatmap difference
 into a jump between noise maxima -- a joint deviation that measures nothing about the kernels.
-Here the network is first fitted, on the GPU through the product training path (bf16, per-view
-BatchNorm, Adam lr 1e-3 as in the reference), to Gaussian targets (sigma 2, NETWORK.SIGMA of
+Here the network is first fitted, on the GPU through the product training path (fp32 since round 6 --
+the fitted net then does not move when the bf16 training kernels' summation order changes, which
+moved the 2-byte chains' heavy-tailed max-over-joints in round 5; per-view BatchNorm, Adam lr 1e-3 as
+in the reference), to Gaussian targets (sigma 2, NETWORK.SIGMA of
 the reference config) at the projections of synthetic 3-D poses into the four cameras of each
 group; its heatmaps then peak where the poses project, like a trained network's, and the
 benched bf16 / fp32 chains can be compared with the CPU oracle chain on them (heatmaps, image-px
 joints, triangulated joints in mm).
 
-    fit_peaked(dev, groups=8, steps=300) -> (net [eval mode, precision bf16], task dict)
+    fit_peaked(dev, groups=8, steps=300, precision='fp32') -> (net [eval mode], task dict)
 """
 import os
 import sys
@@ -67,7 +69,7 @@ def make_task(groups, dev, seed=0, size=256, njoints=16):
             'joints_hm': joints_hm, 'groups': groups}
 
 
-def fit_peaked(dev, groups=8, steps=300, seed=0, lr=1e-3, log=None):
+def fit_peaked(dev, groups=8, steps=300, seed=0, lr=1e-3, log=None, precision='fp32'):
     """Fit R50@256 (synthetic init, calibrated BN statistics) to the task's targets; returns the
     network in eval mode and the task."""
     from core.loss import JointsMSELoss
@@ -76,7 +78,7 @@ def fit_peaked(dev, groups=8, steps=300, seed=0, lr=1e-3, log=None):
     from posu import synthetic as syn
     torch.manual_seed(seed)
     cfg = syn.make_cfg(num_layers=50, image_size=256)
-    net = get_pose_net(cfg, is_train=False, precision='bf16')
+    net = get_pose_net(cfg, is_train=False, precision=precision)
     net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=syn.calibrated_seed(50, 256),
                                                  bn_stats=syn.load_bn_stats(50, 256)))
     net = net.to(dev).train()
@@ -98,11 +100,13 @@ def fit_peaked(dev, groups=8, steps=300, seed=0, lr=1e-3, log=None):
     return net, task
 
 
-def parity(net, task, dev, precision, ref=None):
+def parity(net, task, dev, precision, ref=None, autotune=False):
     """The benched chain on the task's views (eval-mode plan in `precision`: forward -> soft-argmax +
     crop affine -> fp64 DLT triangulation) against the CPU oracle chain on the same weights (fp32
-    reference forward -> soft-argmax -> transform_back -> triangulate_poses).  Returns (metrics
-    dict, the oracle outputs for reuse)."""
+    reference forward -> soft-argmax -> transform_back -> triangulate_poses).  autotune: the plan's
+    tiles autotuned on these views first (as bench.py does), so the tiles the tuner picks -- the split
+    dtype's two-K-group tile among them -- are the ones measured.  Returns (metrics dict, the oracle
+    outputs for reuse)."""
     from oracle import geometry_ref as G
     from oracle import pose_resnet_ref as PR
     from posu import ops
@@ -121,6 +125,8 @@ def parity(net, task, dev, precision, ref=None):
         net.precision = precision
         with torch.no_grad():
             plan = net.plan(dev)
+            if autotune:
+                plan.autotune(plan.pack_input(task['views']), keep_features=False, reps=2)
             hm = plan.run(plan.pack_input(task['views']), keep_features=False)[0]
             coords = ops.softargmax2d(hm, beta=100.0, affine=meta.affines).view(4, groups, hm.shape[1], 2)
             X = ops.triangulate_dlt(meta.M, meta.intr, coords, None, undistort=True, view_major=True)
@@ -133,7 +139,7 @@ def parity(net, task, dev, precision, ref=None):
     gt = mpjpe_stats(ref['X'], host['poses3d'])
     r6 = lambda v: float('%.6g' % float(v))  # noqa: E731
     peak = hm.amax(dim=(2, 3))
-    return ({'precision': precision, 'heatmap_peak_mean': r6(peak.mean()), 'heatmap_peak_min': r6(peak.min()),
+    return ({'precision': precision, 'autotuned': bool(autotune), 'heatmap_peak_mean': r6(peak.mean()), 'heatmap_peak_min': r6(peak.min()),
              'heatmap_abs_err': {'max': r6(hm_err.max()), 'mean': r6(hm_err.mean())},
              'joints_px_err': {'mean': r6(jerr.mean()), 'max': r6(jerr.max())},
              'mpjpe_vs_ref_mm': {'mean': r6(st['mean']), 'std': r6(st['std']), 'max': r6(st['max'])},
@@ -155,7 +161,8 @@ if __name__ == '__main__':
     mx = hm.amax(dim=(2, 3))
     print('eval heatmap peak: mean %.3f min %.3f' % (float(mx.mean()), float(mx.min())))
     t1 = time.time()
-    res, ref = parity(net, task, dev, 'bf16')
+    res, ref = parity(net, task, dev, 'fp32')
     print(res)
-    print(parity(net, task, dev, 'fp32', ref)[0])
+    for p, tune in (('fp16x3', False), ('fp16x3', True), ('fp16', False), ('bf16', False)):
+        print(parity(net, task, dev, p, ref, autotune=tune)[0])
     print('parity in %.1f s' % (time.time() - t1))
