@@ -71,7 +71,9 @@ const char* posu_last_error(void);
  * posu_stem_wgrad_views); 15 (training) the data gradient on a chosen tile
  * (posu_conv2d_dgrad_tile: the training step autotunes it like the forward convolutions), 3x3
  * sources of the batched deconv packing (the strided 3x3 convs' sub-pixel data gradient), the
- * Adam step (posu_adam_step).  The
+ * Adam step (posu_adam_step); 16 (round 6) the split-fp16 dtype in the streamed Bottleneck tails
+ * (posu_bottleneck_tail_stream_fwd / _next_fwd, layer1 / layer2 / layer3 at 256x256) and the
+ * downsampling first-block tail (posu_bottleneck_down_tail_stream_fwd).  The
  * ctypes binding refuses a library of another revision. */
 int posu_abi_version(void);
 
@@ -245,6 +247,27 @@ int posu_bottleneck_tail_stream_fwd(int dtype, const void* t1, const void* x, in
  * BN; t1n [N, H, W, P] out (aliasing no other operand).  y and t1n are bit-identical to this
  * tail followed by posu_conv2d_fwd(next conv1, ReLU) over y. */
 int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                         int P, const void* wstream, long long wstream_bytes, const float* s2,
+                                         const float* b2, const float* s3, const float* b3, void* y,
+                                         const float* s1n, const float* b1n, void* t1n, void* stream);
+
+/* (ABI 16) Both tails above also take POSU_F16X3 (split fp16 pairs, [N, H, W, 2 C] storage, C and P
+ * logical), at layer1 (W = 64, C = 256, P = 64; 2-row tiles), layer2 (W = 32; 2-row tiles) and
+ * layer3 (W = 16; 4-row tiles) of PoseResNet at 256x256: every k-step pair multiplied as hi.hi +
+ * lo(w).hi(x) + hi(w).lo(x), bit-identical to the split posu_conv2d_fwd launches they replace;
+ * wstream = packing.pack_tail_stream of the split packs (K' = 2 K).
+ *
+ * The FIRST Bottleneck of layer1 (lib/models/pose_resnet.py:61-99 with its stride-1 downsample,
+ * pose_resnet.py:136-141; eval BN folded), split fp16 only: conv2 + the [conv3 | downsample] dual
+ * GEMM + ReLU in one launch,
+ *   y = relu( [w3*s3 | wd*sd] . [ relu(bn2(conv2_3x3(t1))) ; x ] * s3 + b3 ),
+ * = posu_conv2d_fwd(conv2) then posu_conv1x1_dual_fwd(t2, x, stride 1), bit for bit.  t1 [N, H, 64, P]
+ * (conv1's output), x [N, H, 64, P] (the block input), y [N, H, 64, C] with C = 256, P = 64
+ * (logical channels), H even.  s3 / b3: the dual GEMM's scale (the split weight exponent's 2^-e) and
+ * shift (b3 + bd).  s1n / b1n / t1n: optional (all null, or all given) -- the next identity block's
+ * conv1 + BN1 + ReLU over y, as posu_bottleneck_tail_stream_next_fwd.  wstream =
+ * packing.pack_down_tail_stream(conv2 pack, dual pack[, next conv1 pack]). */
+int posu_bottleneck_down_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
                                          int P, const void* wstream, long long wstream_bytes, const float* s2,
                                          const float* b2, const float* s3, const float* b3, void* y,
                                          const float* s1n, const float* b1n, void* t1n, void* stream);

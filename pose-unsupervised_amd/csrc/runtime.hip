@@ -20,4 +20,4 @@ int check_launch(const char* what) {
 
 extern "C" const char* posu_last_error(void) { return posu::g_last_error.c_str(); }
 
-extern "C" int posu_abi_version(void) { return 15; }
+extern "C" int posu_abi_version(void) { return 16; }

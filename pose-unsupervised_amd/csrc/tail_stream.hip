@@ -86,7 +86,7 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, int CM = 1>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, int CM = 1, bool DOWN = false>
 struct TailCfg {
   static constexpr int kRows = ROWS;               // image rows per workgroup
   static constexpr int kNW = NW;                   // waves per workgroup
@@ -104,10 +104,15 @@ struct TailCfg {
   static constexpr int kKT = CM * P / 32;          // k-steps per tap / per conv3 chunk (split: hi, lo per 32 ch)
   static constexpr int kChunk = 32 * kNCQ;         // conv3 output channels per chunk
   static constexpr int kNC = C / kChunk;           // conv3 chunks
-  static constexpr int kBlk3 = NEXT ? 2 : 1;       // stream blocks per conv3 chunk (+ the next conv1's K slice)
+  // stream blocks per conv3 chunk (+ DOWN: the downsample's K slice over x; + NEXT: the next conv1's)
+  static constexpr int kBlk3 = 1 + DOWN + NEXT;
   static constexpr int kSteps = 9 * kKT + kNC * kKT * kBlk3;
   static constexpr int kYC = kS3 + 2 * C * 4;      // NEXT: the y chunk [kPx][P] behind BN3
-  static constexpr int kLdsAll = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
+  static constexpr int kLdsN = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
+  // DOWN: the tile's block-input pixels (the downsample's B operand, P channels) behind everything
+  // else, staged by LDS-DMA at the start beside the window
+  static constexpr int kX0 = kLdsN;
+  static constexpr int kLdsAll = DOWN ? kX0 + kPx * kRowB : kLdsN;
   // weight prefetch depth (k-steps); NEXT keeps a second accumulator set live, so its stream
   // runs POSU_TS_KD_NEXT deep
   // (W = 24: nine m-tiles per wave, one fragment set and a two-deep stream -- 256 VGPRs, no
@@ -118,6 +123,9 @@ struct TailCfg {
   static constexpr int kDW = W == 24 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
   static constexpr int kNB = W == 24 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
+  // swizzle keys stay inside a pixel row: 16 chunks or more take (column & 15), the 8-chunk rows of
+  // 64-channel 2-byte images (layer1 at 384x384) (column & 7)
+  static constexpr int kKM = kRowB / 16 >= 16 ? 15 : kRowB / 16 - 1;
   static_assert(kNPG * kNCQ == NW && kNPG >= 1 && kPx % (16 * MT) == 0 && (16 * MT) % W == 0,
                 "every wave: 16 MT px (whole image rows) x 32 channels");
   // W = 24 (R152@384's layer3, round 5): m-tiles straddle image rows -- m-tile i = 3 m + c holds
@@ -149,8 +157,12 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 #ifndef POSU_TS_MT4_WAVES
 #define POSU_TS_MT4_WAVES 12
 #endif
-template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
-__global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
+// DOWN (round 6, layer1's first block in split fp16): the Bottleneck with a stride-1 1x1 downsample
+// (pose_resnet.py:136-141) -- no residual; each conv3 chunk also runs the downsample over the block
+// input x (P channels, staged in LDS) into the same accumulators, [w3*s3 | wd*sd] with shift = b3 + bd
+// (posu_conv1x1_dual_fwd's K order: bit-identical to it)
+template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false>
+__global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   // split fp16 (POSU_F16X3, round 6): every pixel row holds [hi 32 | lo 32] per 32 channels, i.e. the
   // kernel is the same GEMM over twice the K, whose k-step pairs (2c, 2c + 1) -- the hi and the lo
@@ -159,7 +171,7 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
   // epilogues join residual pairs and split their outputs
   constexpr bool SPL = O::SPLIT;
   constexpr int CM = SPL ? 2 : 1;
-  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT, CM>;
+  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT, CM, DOWN>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
   __shared__ __attribute__((aligned(16))) char smem[K::kLdsAll];
@@ -193,9 +205,26 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
         const int pix = kPixPerInst * m + sub;
         const int wr = pix / K::kWinCols, wc = pix - wr * K::kWinCols;
         const int yy = y0 + wr - 1, xx = wc - 1;
-        const int lc = pc ^ wkey<W>(wr, wc);
+        const int lc = pc ^ (wkey<W>(wr, wc) & K::kKM);
         const bool ok = static_cast<unsigned>(yy) < static_cast<unsigned>(H) && static_cast<unsigned>(xx) < W;
         dma16(t1s, ok ? (((n * H + yy) * W + xx) * P * CM + 8 * lc) * ES : kOOB, lds0 + static_cast<unsigned>(m) * 1024u);
+      }
+    }
+    if constexpr (DOWN) {
+      // the block input's tile pixels (x: [N][H][W][P], the rows y0 .. y0 + kRows - 1 contiguous),
+      // pixel p's chunks keyed by its column & 15 (the t2 image's layout)
+      constexpr int kXInst = K::kPx / kPixPerInst;
+      static_assert(K::kPx % kPixPerInst == 0, "whole instructions");
+      const u32x4 xs = make_srd(g.x, g.N * H * W * P * CM * ES);
+#pragma unroll
+      for (int k = 0; k < (kXInst + NW - 1) / NW; ++k) {
+        const int m = wid + NW * k;
+        if (m < kXInst) {
+          const int pix = kPixPerInst * m + sub;
+          const int lc = pc ^ ((pix % W) & K::kKM);
+          dma16(xs, ((n * H + y0) * W * P * CM + pix * P * CM + 8 * lc) * ES,
+                lds0 + static_cast<unsigned>(K::kX0 + m * 1024));
+        }
       }
     }
   }
@@ -255,6 +284,7 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
   // chunk (4 d + q) ^ key = 4 ((d & 3) ^ (key >> 2)) + 16 (d >> 2) + (q ^ (key & 3)): four base
   // pointers per (lane pixel, key), the k-step's 16 B at kb[d & 3] + (d >> 2) * 256
   auto bases = [&](const char* (&kb)[4], int base, int lpix, int key) {
+    key &= K::kKM;
     const char* lb = smem + base + lpix * K::kRowB + ((q ^ (key & 3)) << 4);
 #pragma unroll
     for (int k = 0; k < 4; ++k) kb[k] = lb + ((k ^ (key >> 2)) << 6);
@@ -399,10 +429,10 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
       uint4 h, l;
       split8(v, h, l);
       const int ch = split_ch(8 * c8) >> 3;
-      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, ch)) = h;
-      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, ch + 4)) = l;
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16 & K::kKM, ch)) = h;
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16 & K::kKM, ch + 4)) = l;
     } else {
-      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16, c8)) = O::store_vals(v);
+      *reinterpret_cast<uint4*>(smem + base + swzp<K::kRowB>(pix, r16 & K::kKM, c8)) = O::store_vals(v);
     }
   };
   // BN2 + ReLU -> t2 over the window (every wave is done reading it first), BN3 beside it
@@ -433,8 +463,10 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
     const int c0 = K::kChunk * nc + 32 * cq + cpair;
     zero(acc);
     block(acc, 9 + K::kBlk3 * nc, 0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
+    // DOWN: the downsample's K slice over the block input into the same accumulators
+    if constexpr (DOWN) block(acc, 9 + K::kBlk3 * nc + 1, K::kX0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers)
-    if constexpr (NEXT) res_load(nc, rv, rl);
+    if constexpr (NEXT && !DOWN) res_load(nc, rv, rl);
     float sc[8], sh[8];
     ld8(b3l + c0, sc);
     ld8(b3l + C + c0, sh);
@@ -445,9 +477,13 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
     for (int i = 0; i < MT; ++i) {
       float v[8], r[8];
       pair(acc, i, v);
-      if constexpr (SPL) join8(rv[i], rl[i], r);
-      else O::load_vals(rv[i], r);
-      bn_relu(v, sc, sh, r);
+      if constexpr (DOWN) {
+        bn_relu(v, sc, sh, nullptr);   // no residual: the downsample is in the accumulators
+      } else {
+        if constexpr (SPL) join8(rv[i], rl[i], r);
+        else O::load_vals(rv[i], r);
+        bn_relu(v, sc, sh, r);
+      }
       if (kAbl & 40) asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]));
       else st8(yrs, xy_off(i, nc), v);
       // NEXT: the chunk's y, laid out like t2 ([pixel][P] rows, column-keyed swizzle)
@@ -457,7 +493,7 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
       // the next block's conv1 over this K slice (y channels kChunk nc ..): same k order as a
       // conv launch over y, so t1n is bit-identical to it
       lds_barrier();
-      block(acc1, 9 + K::kBlk3 * nc + 1, K::kYC, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
+      block(acc1, 9 + K::kBlk3 * nc + 1 + DOWN, K::kYC, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     }
   };
   // unrolled: hipcc's wait counts at a loop head merge both paths and made every chunk's first
@@ -468,7 +504,7 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
     // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
     uint4 rv[MT], rl[MT];
-    if constexpr (!NEXT) res_load(nc, rv, rl);
+    if constexpr (!NEXT && !DOWN) res_load(nc, rv, rl);
     chunk(nc, rv, rl);
   }
   if constexpr (NEXT) {
@@ -492,19 +528,19 @@ __global__ __launch_bounds__(NW * 64, (Op<T>::SPLIT || MT == 8 || W == 48 ? 8 : 
 // split fp16 instances (round 6): layer1 (W = 64, planes 64: 2 rows x 64 px, four waves as 2 pixel x 2
 // channel groups), layer2 (2 rows x 32 px, four waves), layer3 (4 rows x 16 px, eight waves) -- the
 // pairs double the t1 window, so the tiles are the bf16 ones' small variants (68 / 69 / 110 KB of LDS)
-template <int W, int P, int C, int ROWS, int NW, bool NEXT, int MT>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT, int MT, bool DOWN = false>
 void launch_tail_split(const TailSGeom& g, hipStream_t s) {
-  hipLaunchKernelGGL((tail_stream_kernel<f16s_t, W, P, C, ROWS, NW, NEXT, MT>), dim3(static_cast<unsigned>(g.N * (g.H / ROWS))),
-                     dim3(NW * 64), 0, s, g);
+  hipLaunchKernelGGL((tail_stream_kernel<f16s_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>),
+                     dim3(static_cast<unsigned>(g.N * (g.H / ROWS))), dim3(NW * 64), 0, s, g);
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false>
 void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(g.N * (g.H / ROWS)));
   if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT, MT>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>), grid, dim3(NW * 64), 0, s, g);
   else
-    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // layer3's 4-row tiles below this many 8-row workgroups (A/B builds: 0 never, a large value always)
@@ -534,7 +570,7 @@ namespace {
 int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
                      const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
                      const float* s3, const float* b3, void* y, const float* s1n, const float* b1n, void* t1n,
-                     void* stream) {
+                     void* stream, bool down = false) {
   const std::string what = name;
   const bool next = t1n != nullptr;
   const bool spl = dtype == POSU_F16X3;
@@ -547,17 +583,21 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   const bool l3w = W == 24 && C == 1024 && P == 256;   // layer3 at 384x384 (R152 configs[4])
   const bool l2w = W == 48 && C == 512 && P == 128;    // layer2 at 384x384
   const bool l1 = W == 64 && C == 256 && P == 64;      // layer1 at 256x256 (the split dtype only)
-  POSU_REQUIRE(l2 || l3 || l3w || l2w || (spl && l1),
+  const bool l1w = W == 96 && C == 256 && P == 64;     // layer1 at 384x384 (R152 configs[4]; bf16 / fp16)
+  POSU_REQUIRE(l2 || l3 || l3w || l2w || (spl && l1) || (!spl && l1w),
                what + ": built for layer2 (W = 32 or 48, C = 512, planes = 128) and layer3 (W = 16 or 24, C = 1024, "
-                      "planes = 256) of PoseResNet at 256x256 / 384x384, and (split fp16) layer1 (W = 64, C = 256, "
-                      "planes = 64)");
+                      "planes = 256) of PoseResNet at 256x256 / 384x384, layer1 at 384x384 (W = 96, C = 256, planes "
+                      "64; BF16 / F16) and (split fp16) layer1 at 256x256 (W = 64)");
   POSU_REQUIRE(!spl || !(l3w || l2w), what + ": the split dtype runs the 256x256 tails (W = 64, 32, 16)");
+  POSU_REQUIRE(!down || (spl && l1) || (!spl && l1w),
+               what + ": built for layer1's first Bottleneck (x 64 -> y 256 channels, planes 64) at W = 64 in split "
+                      "fp16 and at W = 96 in BF16 / F16");
   const int cm = spl ? 2 : 1;   // stored halves per logical channel
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream); split: KT = 2 P / 32
     const long long kt = cm * P / 32, nc = C / P;
-    const long long need = (P / 32) * (9 * kt + (next ? 2 : 1) * nc * kt) * 2 * 64 * 8 * 2;
+    const long long need = (P / 32) * (9 * kt + (1 + down + next) * nc * kt) * 2 * 64 * 8 * 2;
     POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
@@ -566,9 +606,10 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   // workgroup, else 4-row tiles (64 px, 4 m-tiles per wave): at batch 64 (BASELINE configs[1]) the
   // 8-row grid left half the CUs idle (128 workgroups)
   const bool l3h = l3 && N > 0 && H % 4 == 0 && static_cast<long long>(N) * (H / 8) < POSU_TS_L3_SMALL_GRID;
-  const int rows = spl ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? 6 : l2w ? 2 : kL2Rows;
+  const int rows = spl ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? 6 : (l2w || l1w) ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
+  POSU_REQUIRE(!down || x != t1n, what + ": t1n must not alias x");
   POSU_REQUIRE(static_cast<long long>(N) * H * W * C * 2 * cm < (1LL << 31) - 256,
                what + ": activation exceeds the 2 GiB addressing range");
   for (const void* p : {t1, x, static_cast<const void*>(y), wstream, static_cast<const void*>(s3),
@@ -592,7 +633,10 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   g.wseg = wstream_bytes / 64;
   g.warm = warm_wgs(wstream_bytes);
   hipStream_t s = as_stream(stream);
-  if (spl) {
+  if (spl && down) {
+    if (next) launch_tail_split<64, 64, 256, 2, 4, true, 4, true>(g, s);
+    else launch_tail_split<64, 64, 256, 2, 4, false, 4, true>(g, s);
+  } else if (spl) {
     if (l1) {
       if (next) launch_tail_split<64, 64, 256, 2, 4, true, 4>(g, s);
       else launch_tail_split<64, 64, 256, 2, 4, false, 4>(g, s);
@@ -602,6 +646,14 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     } else {
       if (next) launch_tail_split<16, 256, 1024, 4, 8, true, 4>(g, s);
       else launch_tail_split<16, 256, 1024, 4, 8, false, 4>(g, s);
+    }
+  } else if (l1w) {   // 2 rows x 96 px = 192 px, 6 m-tiles per wave (one image row), 4 waves
+    if (down) {
+      if (next) launch_tail<96, 64, 256, 2, 4, true, 6, true>(dtype, g, s);
+      else launch_tail<96, 64, 256, 2, 4, false, 6, true>(dtype, g, s);
+    } else {
+      if (next) launch_tail<96, 64, 256, 2, 4, true, 6>(dtype, g, s);
+      else launch_tail<96, 64, 256, 2, 4, false, 6>(dtype, g, s);
     }
   } else if (l3h) {
     if (next) launch_tail<16, 256, 1024, 4, 8, true, 4>(dtype, g, s);
@@ -645,4 +697,17 @@ extern "C" int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, c
   }
   return tail_stream_impl("posu_bottleneck_tail_stream_next_fwd", dtype, t1, x, N, H, W, C, P, wstream,
                           wstream_bytes, s2, b2, s3, b3, y, s1n, b1n, t1n, stream);
+}
+
+// Layer1's first Bottleneck (split fp16, round 6): conv2 + [conv3 | downsample] dual GEMM + ReLU in one
+// launch (the downsample over the block input x [N, H, 64, P] staged in LDS), optionally chained with
+// the next block's conv1 (t1n != nullptr).  s3 / b3: the dual GEMM's scale / shift (b3 + bd);
+// wstream = packing.pack_down_tail_stream(conv2 pack, dual pack[, next conv1 pack]).
+extern "C" int posu_bottleneck_down_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W,
+                                                    int C, int P, const void* wstream, long long wstream_bytes,
+                                                    const float* s2, const float* b2, const float* s3,
+                                                    const float* b3, void* y, const float* s1n, const float* b1n,
+                                                    void* t1n, void* stream) {
+  return tail_stream_impl("posu_bottleneck_down_tail_stream_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes,
+                          s2, b2, s3, b3, y, s1n, b1n, t1n, stream, true);
 }

@@ -18,7 +18,7 @@ F16 = 3
 F16X3 = 4   # split fp16 (hi + lo pairs, three MFMAs per product): include/posu.h
 
 # the ABI revision this binding declares (include/posu.h); load() refuses any other library
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'libposeu.so')
 _lock = threading.Lock()
@@ -46,6 +46,8 @@ _SIGNATURES = {
     'posu_bottleneck_fwd': [_i, _p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p],
     'posu_bottleneck_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p],
     'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
+                                             _p, _p],
+    'posu_bottleneck_down_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _p],
     'posu_bottleneck_s2_tail_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p],
     'posu_bottleneck_s2_tail_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p, _p, _p, _p],

@@ -185,6 +185,24 @@ def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, c
     return out, t1n
 
 
+def bottleneck_down_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, s1n=None, b1n=None, out=None, t1n=None):
+    """Layer1's first Bottleneck after its conv1 in split fp16 (posu_bottleneck_down_tail_stream_fwd):
+    conv2 + the [conv3 | downsample] dual GEMM (scale s3, shift b3) + ReLU in one launch, t1 / x
+    [N, H, 64, 64] -> y [N, H, 64, 256] (logical channels); with s1n / b1n also the next identity block's
+    conv1 + BN1 + ReLU over y.  Returns (y, t1n or None)."""
+    n, h, w, _ = x.shape
+    cm = cmul(code)
+    c = s3.numel()
+    if out is None:
+        out = torch.empty((n, h, w, c * cm), dtype=x.dtype, device=x.device)
+    if s1n is not None and t1n is None:
+        t1n = torch.empty_like(t1)
+    call('posu_bottleneck_down_tail_stream_fwd', code, ptr(t1), ptr(x), n, h, w, c, t1.shape[3] // cm, ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n),
+         ptr(t1n if s1n is not None else None), stream_of(x.device))
+    return out, (t1n if s1n is not None else None)
+
+
 def bottleneck_down_nhwc(x, w1, s1, b1, w2, s2, b2, w3d, shift3, code, out=None):
     """Fused first Bottleneck of layer1 with its downsample (posu_bottleneck_down_fwd):
     x [N, H, W, C] -> y [N, H, W, w3d.shape[0]]."""

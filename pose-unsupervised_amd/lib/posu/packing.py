@@ -95,6 +95,32 @@ def pack_tail_stream(w2pk, w3pk, w1n=None):
     return torch.cat([s2, s31], dim=1).contiguous()
 
 
+def pack_down_tail_stream(w2pk, wdual, w1n=None):
+    """The per-wave weight streams of posu_bottleneck_down_tail_stream_fwd (layer1's first Bottleneck,
+    split fp16): conv2 [P][9 P'] as pack_tail_stream, then per output chunk nc (P channels) the dual
+    GEMM's KT k-steps over t2 followed by its KT k-steps over the block input (pack_dual_1x1_weight's
+    K order [conv3 | downsample], split: [C][2 P' ]), then (w1n) the next conv1's KT k-steps over the
+    chunk -- [P/32][9 KT + NC (2 + (w1n given)) KT][2][64][8], KT = P' / 32 (P' the stored halves of P)."""
+    planes, c = w2pk.shape[0], wdual.shape[0]
+    ncq, kt2, nc = planes // 32, wdual.shape[1] // 32, c // planes
+    kt = kt2 // 2
+    if w2pk.shape[1] != 9 * kt * 32:
+        raise ValueError('pack_down_tail_stream: conv2 pack [%d][%d] and dual pack [%d][%d] disagree on the planes'
+                         % (tuple(w2pk.shape) + tuple(wdual.shape)))
+    f2 = mfma_fragments(w2pk)
+    s2 = f2.reshape(ncq, 2, 9 * kt, 64, 8).permute(0, 2, 1, 3, 4)
+    fd = mfma_fragments(wdual)                                                    # [C/16][2 kt][64][8]
+    sd = fd.reshape(nc, ncq, 2, kt2, 64, 8).permute(1, 0, 3, 2, 4, 5)            # [ncq][nc][2 kt][2][64][8]
+    if w1n is not None:
+        if tuple(w1n.shape) != (planes, c * kt * 32 // planes):
+            raise ValueError('pack_down_tail_stream: the next conv1 pack must be [%d][%d]'
+                             % (planes, c * kt * 32 // planes))
+        f1 = mfma_fragments(w1n)
+        s1 = f1.reshape(ncq, 2, nc, kt, 64, 8).permute(0, 2, 3, 1, 4, 5)          # [ncq][nc][kt][2][64][8]
+        sd = torch.cat([sd, s1], dim=2)
+    return torch.cat([s2, sd.reshape(ncq, -1, 2, 64, 8)], dim=1).contiguous()
+
+
 def bottleneck_conv3_order(planes):
     """Input-channel order of the fused Bottleneck's conv3 K (csrc/bottleneck.hip): column
     32 b + 8 q + e reads channel 32 b + 16 (e >> 2) + 4 q + (e & 3) -- the order in which

@@ -18,7 +18,7 @@ import torch
 
 from . import ops
 from .packing import (fold_bn, pack_bottleneck_conv1_weight, pack_bottleneck_conv3_weight, pack_bottleneck_down_weight,
-                      pack_conv_weight, pack_deconv4x4_weight,
+                      pack_conv_weight, pack_deconv4x4_weight, pack_down_tail_stream,
                       pack_dual_1x1_weight, pack_s2_tail_stream, pack_stem_fused_weight, pack_stem_s2d_weight,
                       pack_tail_stream, split_exponent, to_split)
 
@@ -258,8 +258,12 @@ S2_CHAIN = True
 # (round 5): layer3 at W = 24 (not chained), layer2 at W = 48 (chained)
 TAIL_W24 = True
 # the split dtype's identity Bottlenecks of layer1 / layer2 / layer3 as conv1 + the streamed tail
-# (chained), round 6; False: three conv launches each
+# (chained), layer1's first block as conv1 + the down tail (chained), round 6; False: the conv launches
 SPLIT_TAILS = True
+# layer1 at 384x384 (96-wide maps, R152 configs[4]) in bf16 / fp16 plans on the streamed tails (round 6):
+# the first block as conv1 + the down tail, the identity blocks as the (chained) tail; False: three
+# conv launches per block (the fused layer1 kernel is built for 64-wide maps)
+TAIL_W96 = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -272,7 +276,8 @@ def _fused_fits(x, cout):
 
 
 class _Block:
-    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l1', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n')
+    __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l1', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n',
+                 'wsd', 'wsdn', 'dscale', 'code')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -289,6 +294,10 @@ class _Block:
         self.wsn = None              # the streams with that conv1 appended (pack_tail_stream(.., w1n))
         self.ws2 = None              # layer2 block 0: the strided tail's weight streams (pack_s2_tail_stream)
         self.ws2n = None             # ... with the next block's conv1 appended (the chained strided tail)
+        self.wsd = None              # split layer1 block 0: the down tail's streams (pack_down_tail_stream)
+        self.wsdn = None             # ... with the next block's conv1 appended
+        self.dscale = None           # ... the dual GEMM's epilogue scale (2^-e)
+        self.code = code
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -301,6 +310,19 @@ class _Block:
                     c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c2.w.shape == (64, 576) and \
                     self.dual.w.shape[1] >= 128:
                 self.w3d = pack_bottleneck_down_weight(self.dual.w, 64)
+            if code == ops.F16X3 and SPLIT_TAILS and self.dual.stride2 == 1 and self.dual.cout == 256 and \
+                    c1.k == 1 and c1.stride == 1 and tuple(c1.w.shape) == (64, 128) and \
+                    c2.k == 3 and c2.stride == 1 and c2.pad == 1 and tuple(c2.w.shape) == (64, 1152) and \
+                    tuple(self.dual.w.shape) == (256, 256):
+                self.wsd = pack_down_tail_stream(c2.w, self.dual.w)
+                self.dscale = (self.dual.scale if self.dual.scale is not None else
+                               torch.ones(256, device=self.dual.shift.device))
+            if code in (ops.BF16, ops.F16) and TAIL_W96 and self.dual.stride2 == 1 and self.dual.cout == 256 and \
+                    c1.k == 1 and c1.stride == 1 and tuple(c1.w.shape) == (64, 64) and \
+                    c2.k == 3 and c2.stride == 1 and c2.pad == 1 and tuple(c2.w.shape) == (64, 576) and \
+                    tuple(self.dual.w.shape) == (256, 128):
+                self.wsd = pack_down_tail_stream(c2.w, self.dual.w)
+                self.dscale = torch.ones(256, device=self.dual.shift.device)
             if code in (ops.BF16, ops.F16) and self.dual.stride2 == 2 and self.dual.cout == 512 and \
                     c1.k == 1 and c1.stride == 1 and c1.w.shape == (128, 256) and \
                     c2.k == 3 and c2.stride == 2 and c2.pad == 1 and c2.w.shape == (128, 1152) and \
@@ -314,6 +336,10 @@ class _Block:
         elif code in (ops.BF16, ops.F16) and len(names) == 3 and self._fusable_shape():
             self.w1f = pack_bottleneck_conv1_weight(blk.conv1.weight, ops.torch_dtype(code))
             self.w3f = pack_bottleneck_conv3_weight(blk.conv3.weight, ops.torch_dtype(code))
+            # (the same blocks at 96-wide maps run conv1 + the streamed tail: 'l1' at W = 96)
+            self.l1 = TAIL_W96 and self._layer1_shape()
+            if self.l1:
+                self.wst = pack_tail_stream(self.convs[1].w, self.convs[2].w)
         elif code in (ops.BF16, ops.F16, ops.F16X3) and len(names) == 3:
             # (the split dtype: its packs hold 2 K halves per row; layer1 too -- the fused layer1 kernel
             # does not hold pairs -- on the streamed tail, round 6)
@@ -330,6 +356,9 @@ class _Block:
         if (self.l1 and nxt.l1) or (self.l2 and nxt.l2) or (self.l3 and nxt.l3):
             self.chain = nxt.convs[0]
             self.wsn = pack_tail_stream(self.convs[1].w, self.convs[2].w, self.chain.w)
+        elif self.wsd is not None and nxt.l1:   # split layer1: the down tail and block 1's conv1
+            self.chain = nxt.convs[0]
+            self.wsdn = pack_down_tail_stream(self.convs[1].w, self.dual.w, self.chain.w)
         elif self.ws2 is not None and nxt.l2:   # layer2's strided tail and block 1's conv1
             self.chain = nxt.convs[0]
             self.ws2n = pack_s2_tail_stream(self.convs[1].w, self.dual.w, self.chain.w)
@@ -338,7 +367,7 @@ class _Block:
         """'l2' / 'l3' when this block runs as conv1 + the register-streamed tail, else None."""
         if not FUSED_BOTTLENECK or not _fused_fits(x, self.cout):
             return None
-        if self.l1 and x.shape[2] == 64 and x.shape[1] % 2 == 0:   # split fp16: 2-row tiles
+        if self.l1 and x.shape[2] == (64 if self.code == ops.F16X3 else 96) and x.shape[1] % 2 == 0:   # 2-row tiles
             return 'l1'
         if self.l2 and x.shape[2] == 32 and x.shape[1] % 4 == 0:
             return 'l2'
@@ -358,6 +387,11 @@ class _Block:
         if kind is None:
             if t1 is not None:
                 raise RuntimeError('a chained conv1 output handed to a block without a streamed tail')
+            if self.wsdn is not None and CHAINED_TAILS and self._down_tail_ok(x):
+                c1, c2 = self.convs
+                n1 = self.chain
+                return ops.bottleneck_down_tail_stream_nhwc(c1(x, code), x, self.wsdn, c2.scale, c2.shift, self.dscale,
+                                                            self.dual.shift, code, s1n=n1.scale, b1n=n1.shift, out=out)
             if self.ws2n is not None and CHAINED_TAILS and S2_CHAIN and self._s2_tail_ok(x):
                 c1, c2 = self.convs
                 n1 = self.chain
@@ -373,6 +407,12 @@ class _Block:
                                                         n1.scale, n1.shift, code, out=out)
         return ops.bottleneck_tail_stream_nhwc(t1, x, self.wst, c2.scale, c2.shift, c3.scale, c3.shift, code,
                                                out=out), None
+
+    def _down_tail_ok(self, x):
+        """Split layer1's first block runs conv1 + the down tail (SPLIT_TAILS)."""
+        return (self.wsd is not None and FUSED_BOTTLENECK and _fused_fits(x, self.cout) and x.shape[1] % 2 == 0 and
+                (x.shape[2] == 64 and self.code == ops.F16X3 and SPLIT_TAILS or
+                 x.shape[2] == 96 and self.code != ops.F16X3 and TAIL_W96))
 
     def _s2_tail_ok(self, x):
         """layer2's first block runs conv1 + the strided tail (S2_TAIL)."""
@@ -413,6 +453,10 @@ class _Block:
             c1, c2 = self.convs
             return ops.bottleneck_down_nhwc(x, c1.w, c1.scale, c1.shift, c2.w, c2.scale, c2.shift, self.w3d,
                                             self.dual.shift, code, out=out)
+        if self._down_tail_ok(x):
+            c1, c2 = self.convs
+            return ops.bottleneck_down_tail_stream_nhwc(c1(x, code), x, self.wsd, c2.scale, c2.shift, self.dscale,
+                                                        self.dual.shift, code, out=out)[0]
         if self._s2_tail_ok(x):
             c1, c2 = self.convs
             return ops.bottleneck_s2_tail_nhwc(c1(x, code), x, self.ws2, c2.scale, c2.shift, self.dual.shift, code,

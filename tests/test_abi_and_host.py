@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert sorted(declared) == _native.exported_symbols()
-    assert lib.posu_abi_version() == _native.ABI_VERSION == 15
+    assert lib.posu_abi_version() == _native.ABI_VERSION == 16
     assert lib.posu_conv_bk(_native.BF16) == 64 and lib.posu_conv_bk(_native.F32) == 32
     assert lib.posu_conv_bk(_native.F16X3) == 64   # halves: 32 logical k per K-tile
 

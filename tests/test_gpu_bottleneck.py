@@ -565,7 +565,8 @@ def test_split_plan_tails_are_bit_identical_to_conv_launches(cuda):
             assert [b.l1 for b in plan.layers[0]] == [False, True, True]
             assert [b.l2 for b in plan.layers[1]] == [False, True, True, True]
             assert [b.l3 for b in plan.layers[2]] == [False] + [True] * 5
-            assert [b.chain is not None for b in plan.layers[0]] == [False, True, False]
+            assert plan.layers[0][0].wsdn is not None      # layer1 block 0 on the down tail, chained
+            assert [b.chain is not None for b in plan.layers[0]] == [True, True, False]
             hm1, x11, f1 = plan.run(plan.pack_input(views))
             P.SPLIT_TAILS = False
             plan0 = P.PoseResNetPlan(net, ops.F16X3)
@@ -575,3 +576,101 @@ def test_split_plan_tails_are_bit_identical_to_conv_launches(cuda):
         P.SPLIT_TAILS = saved
     torch.cuda.synchronize()
     assert torch.equal(x11, x10) and torch.equal(hm1, hm0) and torch.equal(f1, f0)
+
+
+@pytest.mark.parametrize('n,h', [(2, 64), (1, 2), (3, 10), (128, 64)])
+def test_split_down_tail_matches_conv_launches(cuda, n, h):
+    """Layer1's first Bottleneck in split fp16 (posu_bottleneck_down_tail_stream_fwd, round 6): conv2 +
+    the [conv3 | downsample] dual GEMM in one launch, against the conv2 launch + posu_conv1x1_dual_fwd
+    (stride 1) -- bit-identical -- and, chained, its t1n against a conv launch of the next conv1 over
+    y; NaN-sentinel outputs."""
+    S = ops.F16X3
+    c, p, w = 256, 64, 64
+    g = torch.Generator().manual_seed(151 + h + n)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=64, p=p)
+    w3 = torch.randn(c, p, 1, 1, generator=g) * (2.0 / p) ** 0.5 * 0.3
+    bn3 = (torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1)
+    wd = torch.randn(c, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5 * 0.3
+    bnd = (torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1)
+    w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1n = (torch.rand(p, generator=g) + 0.5, torch.randn(p, generator=g) * 0.1)
+    x = torch.randn(n, h, w, 64, generator=g, dtype=torch.float64).abs()   # a max-pool output of ReLUs
+    xd = packing.to_split(x).to(cuda)
+    (p1, e1), (p2, e2), (p1n, e1n) = (_split_pack(t.to(cuda), t.shape[1]) for t in (w1, w2, w1n))
+    dual = packing.pack_dual_1x1_weight(w3.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), torch.float64)
+    ed = packing.split_exponent(dual)
+    pdual = packing.to_split(dual, ed)
+    dsc = torch.full((c,), 2.0 ** -ed, device=cuda)
+    shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
+    def sc(bn, e):
+        return (bn[0].double() * 2.0 ** -e).float().to(cuda), bn[1].to(cuda)
+    s1, b1 = sc(bn1, e1)
+    s2, b2 = sc(bn2, e2)
+    s1n, b1n = sc(bn1n, e1n)
+    t1 = ops.conv2d_nhwc(xd, p1, p, 1, 1, 1, 0, s1, b1, None, True, S)
+    ysent = _sentinel(xd, (n, h, w, 2 * c))
+    y, none = ops.bottleneck_down_tail_stream_nhwc(t1, xd, packing.pack_down_tail_stream(p2, pdual), s2, b2, dsc, shift,
+                                                   S, out=ysent)
+    t2 = ops.conv2d_nhwc(t1, p2, p, 3, 3, 1, 1, s2, b2, None, True, S)
+    ref = ops.conv1x1_dual_nhwc(t2, xd, 1, pdual, c, shift, True, S, scale=dsc)
+    yc, t1n = ops.bottleneck_down_tail_stream_nhwc(t1, xd, packing.pack_down_tail_stream(p2, pdual, p1n), s2, b2, dsc,
+                                                   shift, S, s1n=s1n, b1n=b1n, out=_sentinel(ysent),
+                                                   t1n=_sentinel(t1))
+    t1n_ref = ops.conv2d_nhwc(ref, p1n, p, 1, 1, 1, 0, s1n, b1n, None, True, S)
+    torch.cuda.synchronize()
+    assert none is None
+    dy = int((y.view(torch.int16) != ref.view(torch.int16)).sum())
+    dyc = int((yc.view(torch.int16) != ref.view(torch.int16)).sum())
+    dt1 = int((t1n.view(torch.int16) != t1n_ref.view(torch.int16)).sum())
+    print('split down tail n=%d h=%d: y differing %d, chained y %d, t1n %d' % (n, h, dy, dyc, dt1))
+    assert dy == 0 and dyc == 0 and dt1 == 0
+
+
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('n,h', [(2, 96), (1, 2), (3, 10), (64, 96)])
+def test_w96_layer1_tails_match_conv_launches(cuda, code, n, h):
+    """Layer1 at 384x384 (96-wide maps, R152 configs[4]; round 6): the identity blocks' streamed tail
+    (plain and chained) and the first block's down tail (conv2 + [conv3 | downsample], plain and
+    chained) against the conv launches they replace -- bit-identical (64-channel 2-byte LDS rows: 8
+    chunks, swizzle keys column & 7); NaN-sentinel outputs.  (64, 96): the production grid."""
+    c, p, w = 256, 64, 96
+    dt = ops.torch_dtype(code)
+    bk = ops.conv_bk(code)
+    g = torch.Generator().manual_seed(171 + h + n)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
+    w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1n = (torch.rand(p, generator=g) + 0.5, torch.randn(p, generator=g) * 0.1)
+    xd = torch.randn(n, h, w, c, generator=g).to(cuda, dt)
+    p1, p2, p3, p1n = (packing.pack_conv_weight(t.to(cuda), t.shape[1], bk, dt) for t in (w1, w2, w3, w1n))
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1], bn1n[0], bn1n[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, p, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    y = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5], code,
+                                        out=_sentinel(xd))
+    t2 = ops.conv2d_nhwc(t1, p2, p, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    two = ops.conv2d_nhwc(t2, p3, c, 1, 1, 1, 0, s[4], s[5], xd, True, code)
+    yc, t1n = ops.bottleneck_tail_stream_next_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1n), s[2], s[3], s[4],
+                                                   s[5], s[6], s[7], code, out=_sentinel(xd), t1n=_sentinel(t1))
+    t1n_ref = ops.conv2d_nhwc(two, p1n, p, 1, 1, 1, 0, s[6], s[7], None, True, code)
+    # the first block: 64 input channels, downsample 1x1 + BN beside conv3
+    x0 = torch.randn(n, h, w, 64, generator=g).abs().to(cuda, dt)
+    w3d = torch.randn(c, p, 1, 1, generator=g) * (2.0 / p) ** 0.5 * 0.3
+    wd = torch.randn(c, 64, 1, 1, generator=g) * (2.0 / 64) ** 0.5 * 0.3
+    bnd = (torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1)
+    pdual = packing.pack_dual_1x1_weight(w3d.to(cuda), bn3[0].to(cuda), wd.to(cuda), bnd[0].to(cuda), dt)
+    shift = (bn3[1].double() + bnd[1].double()).float().to(cuda)
+    ones = torch.ones(c, device=cuda)
+    p1d = packing.pack_conv_weight(w1[:, :64].contiguous().to(cuda), 64, bk, dt)
+    t1d = ops.conv2d_nhwc(x0, p1d, p, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    yd, _ = ops.bottleneck_down_tail_stream_nhwc(t1d, x0, packing.pack_down_tail_stream(p2, pdual), s[2], s[3], ones,
+                                                 shift, code, out=_sentinel(xd))
+    t2d = ops.conv2d_nhwc(t1d, p2, p, 3, 3, 1, 1, s[2], s[3], None, True, code)
+    dref = ops.conv1x1_dual_nhwc(t2d, x0, 1, pdual, c, shift, True, code)
+    ydc, t1nd = ops.bottleneck_down_tail_stream_nhwc(t1d, x0, packing.pack_down_tail_stream(p2, pdual, p1n), s[2], s[3],
+                                                     ones, shift, code, s1n=s[6], b1n=s[7], out=_sentinel(xd),
+                                                     t1n=_sentinel(t1))
+    t1nd_ref = ops.conv2d_nhwc(dref, p1n, p, 1, 1, 1, 0, s[6], s[7], None, True, code)
+    torch.cuda.synchronize()
+    diff = lambda a, b: int((a.view(torch.int16) != b.view(torch.int16)).sum())  # noqa: E731
+    res = [diff(y, two), diff(yc, two), diff(t1n, t1n_ref), diff(yd, dref), diff(ydc, dref), diff(t1nd, t1nd_ref)]
+    print('W = 96 tails n=%d h=%d: y / chained y / t1n / down y / chained down y / its t1n differing %s' % (n, h, res))
+    assert res == [0] * 6
