@@ -125,12 +125,16 @@ def parse():
     return ap.parse_args()
 
 
-# the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
-# line's `control` leg times it in the same process, so a gain shows on the driver's own box
-# (round 5: the two-K-group tile 39 among the inference tile candidates)
+# the plan switches the recent rounds added (posu.plan): off, the plan is the earlier round's -- the
+# line's `control` legs time it in the same process, so a gain shows on the driver's own box.
+# headline (bf16 R50@256): round 5's two-K-group tile 39 among the inference tile candidates;
+# parity_mode (fp16x3): round 6's split streamed tails (layer1-3, layer1's down tail);
+# configs4 (R152@384 fp16): round 6's layer1 tails at 96-wide maps.
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
-# control leg compares the plans at the same numerics)
+# control legs compare the plans at the same numerics)
 CONTROL_FLAGS = ('TILES_KSPLIT',)
+CONTROL_FLAGS_PARITY = ('SPLIT_TAILS',)
+CONTROL_FLAGS_C4 = ('TAIL_W96',)
 
 
 def apply_plan_flags(flags):
@@ -666,45 +670,51 @@ def time_configs1(args, dev, rank, world, dist):
                          'frac': round(tf / PEAK_BF16_TFLOPS, 4)}}
 
 
-def time_control(args, dev, rank, world, dist):
-    """The benched pipeline with CONTROL_FLAGS off (the previous round's plan), same process and
-    box: its network_ms beside the line's."""
+def _flags_off(flags, fn):
+    """fn() with the posu.plan switches `flags` off; the plan switches and the autotuner's tables
+    (the control plan re-tunes geometries it shares with the measured plan) restored afterwards."""
     from posu import plan as pl
-    saved = {f: getattr(pl, f) for f in CONTROL_FLAGS}
-    # the control plan re-tunes geometries it shares with the headline plan: keep the headline's
-    # tile table (and its tuning records) as they were, for later captures and the tile dump
+    saved = {f: getattr(pl, f) for f in flags}
     tables = [(t, dict(t)) for t in (pl._TUNE_CACHE, pl._TUNE_TIMES, pl._REFINE_TIMES)]
     try:
-        for f in CONTROL_FLAGS:
+        for f in flags:
             setattr(pl, f, False)
-        r = time_pipeline(args, args.precision, dev, rank, args.control_steps, 3, args.batches,
-                          not args.no_autotune, dist, world)
+        return fn()
     finally:
         for f, v in saved.items():
             setattr(pl, f, v)
         for t, snap in tables:
             t.clear()
             t.update(snap)
-    return {'flags_off': list(CONTROL_FLAGS), 'network_ms': round(r['net_ms'], 4), 'steps': args.control_steps,
-            'ms_per_step': round(r['elapsed'] / args.control_steps * 1e3, 4)}
 
 
-def time_configs4(args, dev, rank, world, dist):
+def time_control(args, dev, rank, world, dist, precision=None, flags=CONTROL_FLAGS):
+    """The benched pipeline (precision: the headline's, or another leg's) with `flags` off (the earlier
+    round's plan), same process and box: its network_ms beside the leg's."""
+    prec = precision or args.precision
+    r = _flags_off(flags, lambda: time_pipeline(args, prec, dev, rank, args.control_steps, 3, args.batches,
+                                                not args.no_autotune, dist, world))
+    return {'flags_off': list(flags), 'precision': prec, 'network_ms': round(r['net_ms'], 4),
+            'steps': args.control_steps, 'ms_per_step': round(r['elapsed'] / args.control_steps * 1e3, 4)}
+
+
+def time_configs4(args, dev, rank, world, dist, steps=None):
     """BASELINE configs[4]'s per-GPU pipeline: R152 backbone at 384x384, fp16 compute, fp64
     triangulation, 16 groups x 4 views per GPU (the 8-GPU job's shard), tiles autotuned, the same
     two-stage replay as the line: frames/s and the fraction of the fp16 (= bf16) MFMA peak."""
     import argparse as _ap
     a4 = _ap.Namespace(**vars(args))
     a4.layers, a4.size, a4.groups, a4.precision, a4.tune_file = 152, 384, 16, 'fp16', ''
-    r = time_pipeline(a4, 'fp16', dev, rank, args.c4_steps, 3, 2, not args.no_autotune, dist, world)
+    steps = steps or args.c4_steps
+    r = time_pipeline(a4, 'fp16', dev, rank, steps, 3, 2, not args.no_autotune, dist, world)
     from posu import dist as pdist
     el = pdist.max_over_ranks(r['elapsed'], device=dev)
     frames = 4 * a4.groups
     tf = GFLOP_PER_FRAME[(152, 384)] * frames / (r['net_ms'] * 1e-3) / 1e3
     return {'metric': '4-view 384x384 frames/sec (fwd+triangulate), R152 fp16 (BASELINE configs[4], per-GPU shard '
-                      'of 16 groups x 4 views)', 'value': round(pdist.throughput(frames, args.c4_steps, world, el), 2),
-            'unit': 'frames/s', 'n_gpus': world, 'steps': args.c4_steps, 'network_ms': round(r['net_ms'], 4),
-            'ms_per_step': round(el / args.c4_steps * 1e3, 4), 'dtype': 'fp16',
+                      'of 16 groups x 4 views)', 'value': round(pdist.throughput(frames, steps, world, el), 2),
+            'unit': 'frames/s', 'n_gpus': world, 'steps': steps, 'network_ms': round(r['net_ms'], 4),
+            'ms_per_step': round(el / steps * 1e3, 4), 'dtype': 'fp16',
             'roofline': {'bound': 'mfma', 'achieved': round(tf, 2), 'peak': PEAK_BF16_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': round(tf / PEAK_BF16_TFLOPS, 4),
                          'flop_per_launch': '%.2f GFLOP/frame x %d frames' % (GFLOP_PER_FRAME[(152, 384)], frames)}}
@@ -787,9 +797,15 @@ def infer_main(args):
             par['roofline'] = {'bound': 'mfma', 'achieved': round(tfp, 2), 'peak': PEAK_BF16_TFLOPS,
                                'unit': 'TFLOP/s', 'frac': round(tfp / PEAK_BF16_TFLOPS, 4),
                                'mfma_frac': round(3 * tfp / PEAK_BF16_TFLOPS, 4)}
+        if args.control_steps > 0:
+            par['control'] = time_control(args, dev, rank, world, dist, 'fp16x3', CONTROL_FLAGS_PARITY)
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
     control = time_control(args, dev, rank, world, dist) if args.control_steps > 0 else None
     c4 = time_configs4(args, dev, rank, world, dist) if args.c4_steps > 0 else None
+    if c4 is not None and args.control_steps > 0:
+        cc = _flags_off(CONTROL_FLAGS_C4, lambda: time_configs4(args, dev, rank, world, dist,
+                                                                 steps=min(args.c4_steps, args.control_steps)))
+        c4['control'] = {'flags_off': list(CONTROL_FLAGS_C4), 'network_ms': cc['network_ms'], 'value': cc['value']}
     if args.train_steps > 0 and args.train_last:
         train = train_leg()
     if rank != 0:

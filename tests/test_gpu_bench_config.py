@@ -125,8 +125,9 @@ def test_bench_configuration_matches_the_oracle_chain(cuda, oracle_run, precisio
 def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda, monkeypatch):
     """configs[4]'s per-GPU pipeline at its per-GPU shape: R152 backbone at 384x384, fp16 compute,
     fp64 triangulation, 16 groups x 4 views, per-layer AUTOTUNED tiles, bench's replay path
-    (hipGraph, fused stem; layer1 unfused at 96x96 maps; layer3's 35 identity blocks as conv1 + the
-    W = 24 streamed tail -- asserted taken).
+    (hipGraph, fused stem; layer1 at 96x96 maps as conv1 + the chained down tail, the chained tail and
+    the plain tail (round 6); layer3's 35 identity blocks as conv1 + the W = 24 streamed tail -- both
+    asserted taken).
       * oracle subset (CPU-feasible): groups 0-1 against the fp32 CPU oracle chain;
       * full size, property checks: every output finite; the device triangulation of all 16
         groups against the oracle's DLT on the same device joints (BASELINE's 1e-2 mm); the
@@ -142,20 +143,27 @@ def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda, monkeypatch):
                                   bn_stats=syn.load_bn_stats(layers, size))
     from posu import ops, plan as P
     calls = []
-    tail = ops.bottleneck_tail_stream_nhwc
 
-    def counted(t1, x, *a, **k):
-        calls.append(tuple(x.shape))
-        return tail(t1, x, *a, **k)
-    monkeypatch.setattr(ops, 'bottleneck_tail_stream_nhwc', counted)
+    def counting(fn, tag):
+        def counted(t1, x, *a, **k):
+            calls.append((tag,) + tuple(x.shape))
+            return fn(t1, x, *a, **k)
+        return counted
+    for name in ('bottleneck_tail_stream_nhwc', 'bottleneck_tail_stream_next_nhwc', 'bottleneck_down_tail_stream_nhwc'):
+        monkeypatch.setattr(ops, name, counting(getattr(ops, name), name))
     # (the two-K-group tile 39 sums K in another order: kept out of this bit-for-bit batch
     # invariance check)
     monkeypatch.setattr(P, 'TILES_KSPLIT', False)
     full = _bench_plan_outputs(cuda, 'fp16', True, layers=layers, size=size, groups=groups)
-    n_full = sum(1 for c in calls if c == (64, 24, 24, 1024))
+    n_full = sum(1 for c in calls if c == ('bottleneck_tail_stream_nhwc', 64, 24, 24, 1024))
+    # layer1 (96x96): per eager forward one down tail, one chained tail, one plain tail
+    l1 = [sum(1 for c in calls if c == (nm, 64, 96, 96, ch)) for nm, ch in
+          (('bottleneck_down_tail_stream_nhwc', 64), ('bottleneck_tail_stream_next_nhwc', 256),
+           ('bottleneck_tail_stream_nhwc', 256))]
     small = _bench_plan_outputs(cuda, 'fp16', False, layers=layers, size=size, groups=sub)
     # every eager forward of the plan runs layer3's 35 identity blocks on the W = 24 tail
     assert n_full > 0 and n_full % 35 == 0, n_full
+    assert l1[0] > 0 and l1[0] == l1[1] == l1[2] == n_full // 35, (l1, n_full)
     _, host = synthetic_meta(groups, 'cpu', image_size=size)
     # full size: triangulation and loss consistency of every group
     V, J = 4, full['coords0'].shape[2]

@@ -15,6 +15,7 @@
 #   pmc@NAME:ARGS       HBM traffic per forward launch (FETCH_SIZE, WRITE_SIZE passes) -> OUTDIR/NAME_pmc_traffic.txt
 #   profile:COMMIT      tools/profile_round.sh (the HEAD profile set)
 #   ab@NAME:FLAG:ARGS   bench ARGS with --plan-flag FLAG=1 and =0, twice each, alternating -> OUTDIR/NAME_ab.txt
+#   run@NAME:ARGS       python3 -u ARGS (a tool script and its arguments) -> OUTDIR/NAME.txt
 set -o pipefail
 OUT=${1:?usage: gpu_call.sh OUTDIR STEP...}
 shift
@@ -99,6 +100,9 @@ for step in "$@"; do
           summ "$OUT/${name}_${v}_$r.json" "$flag=$v run $r" | tee -a "$OUT/${name}_ab.txt"
         done
       done ;;
+    run)
+      timeout -k 10 600 python3 -u "${argv[@]}" > "$OUT/$name.txt" 2>&1 || fail "$step" $?
+      tail -5 "$OUT/$name.txt" ;;
     *)
       echo "unknown step kind: $kind"; exit 2 ;;
   esac
