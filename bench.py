@@ -125,14 +125,14 @@ def parse():
     return ap.parse_args()
 
 
-# the plan switches the recent rounds added (posu.plan): off, the plan is the earlier round's -- the
+# the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` legs time it in the same process, so a gain shows on the driver's own box.
-# headline (bf16 R50@256): round 5's two-K-group tile 39 among the inference tile candidates;
-# parity_mode (fp16x3): round 6's split streamed tails (layer1-3, layer1's down tail);
-# configs4 (R152@384 fp16): round 6's layer1 tails at 96-wide maps.
+# headline (bf16 R50@256): none this round (round 5's two-K-group tile 39 showed no gain in its control
+# leg and is off, plan.TILES_KSPLIT); parity_mode (fp16x3): round 6's split streamed tails (layer1-3,
+# layer1's down tail); configs4 (R152@384 fp16): round 6's layer1 tails at 96-wide maps.
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control legs compare the plans at the same numerics)
-CONTROL_FLAGS = ('TILES_KSPLIT',)
+CONTROL_FLAGS = ()
 CONTROL_FLAGS_PARITY = ('SPLIT_TAILS',)
 CONTROL_FLAGS_C4 = ('TAIL_W96',)
 
@@ -800,7 +800,11 @@ def infer_main(args):
         if args.control_steps > 0:
             par['control'] = time_control(args, dev, rank, world, dist, 'fp16x3', CONTROL_FLAGS_PARITY)
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None
-    control = time_control(args, dev, rank, world, dist) if args.control_steps > 0 else None
+    control = None
+    if args.control_steps > 0:
+        control = (time_control(args, dev, rank, world, dist) if CONTROL_FLAGS else
+                   {'flags_off': [], 'note': 'no switch of the headline plan added this round; parity_mode.control '
+                                             'and configs4.control time the legs whose plans changed'})
     c4 = time_configs4(args, dev, rank, world, dist) if args.c4_steps > 0 else None
     if c4 is not None and args.control_steps > 0:
         cc = _flags_off(CONTROL_FLAGS_C4, lambda: time_configs4(args, dev, rank, world, dist,

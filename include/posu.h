@@ -155,7 +155,10 @@ int posu_nhwc_to_nchw_f32(int dtype, const void* x, int N, int H, int W, int C,
  *     7 / 15 (bf16 / f16, ABI 11): 128x128 with eight staggered waves (2x4 / 4x2 wave grids);
  *     39 (bf16 / f16, ABI 13, NHWC outputs): 128x128 with two K groups of four waves (each group
  *        sums every other K-tile over the whole tile, the halves added in LDS at the end: a
- *        different K order, so not bit-identical to the other tiles).
+ *        different K order, so not bit-identical to the other tiles);
+ *     split fp16 (POSU_F16X3): 7 / 15 unstaggered; 31 (ABI 16) staggered, the lagging waves holding a
+ *        K-tile's third product hi(w).lo(x) across the barrier; 47 / 55 (ABI 16) the staggered
+ *        128x128 eight-wave tiles (2x4 / 4x2 wave grids).
  *   The tile only changes speed (every configuration but 39 computes the same sums in the same
  *   K order); the Python plan picks it per layer by timing every admissible
  *   configuration once (PoseResNetPlan.autotune).  The library keeps no mutable state:

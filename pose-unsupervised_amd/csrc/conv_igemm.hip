@@ -120,7 +120,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
   // split fp16: K-tiles of [hi 32 | lo 32] halves, three MFMAs per K-tile and fragment pair;
   // outputs / residuals are (hi, lo) pairs, ocs halves per output pixel
   constexpr bool SPL = O::SPLIT;
-  static_assert(!(SPL && SG), "split fp16 runs the unstaggered loops");
+  // (round 6: the split dtype staggers too -- the lagging waves hold a K-tile's third product, hi(w).lo(x))
   constexpr int BK = 8 * E;                   // 128-byte LDS rows
   static_assert(!KS || (NW == 8 && S == 2 && !SG && !HD && E == 8), "K groups: eight waves, two slots of pairs");
   constexpr int NWG = KS ? NW / 2 : NW;       // waves per K group
@@ -509,6 +509,34 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
     if constexpr (!(ABL & 4)) POSU_DMA_TILE(0, 0);
     warm_done();
     if (lag) __builtin_amdgcn_s_setprio(1);  // the lagging half wins issue arbitration (-2..-7 %)
+    if constexpr (SPL) {
+      // split fp16 (round 6): a K-tile's products are hi.hi and lo(w).hi(x) over the hi pixel
+      // fragments, then hi(w).lo(x); the lagging waves keep the last one's operands (the lo pixel and
+      // the hi weight fragments) and issue it after the next barrier, before the next K-tile's hi.hi
+      // -- per accumulator the plain loop's sequence, so the results are bit-identical to it
+      for (int kt = 0; kt < nk; ++kt) {
+        vm_wait<0>();
+        __syncthreads();
+        if (kt + 1 < nk) POSU_DMA_TILE(kt + 1, (kt + 1) & 1);
+        const char* As_ = smem + (kt & 1) * STAGE;
+        const char* Bs_ = As_ + A_BYTES;
+        if (lag && kt > 0) mma(hA, hB);
+        uint4 af[TM], bfr[TN];
+        read(As_, Bs_, 0, af, bfr);
+        mma(af, bfr);
+        {
+          uint4 bl[TN];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bl[j] = *reinterpret_cast<const uint4*>(Bs_ + swz(wn * WTN + j * 16 + r16, 4 + q));
+          mma(af, bl);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) hA[i] = *reinterpret_cast<const uint4*>(As_ + swz(wm * WTM + i * 16 + r16, 4 + q));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) hB[j] = bfr[j];
+        if (!lag) mma(hA, hB);
+      }
+    } else {
     for (int kt = 0; kt < nk; ++kt) {
       if constexpr (!(ABL & 2)) vm_wait<0>();
       __syncthreads();
@@ -522,6 +550,7 @@ __global__ __launch_bounds__(NW * 64) void conv_igemm_kernel(ConvGeom g) {
       mmx(af, bfr);
       rdx(As_, Bs_, 1, hA, hB);
       if (!lag) mmx(hA, hB);
+    }
     }
     if (lag) mmx(hA, hB);
     if constexpr (ABL & 2) vm_wait<0>();
@@ -1482,12 +1511,16 @@ void launch_cfg(const ConvGeom& g, int blocks, int stages, hipStream_t s) {
 //   block, and eight waves two per SIMD);
 //   -1: the built-in heuristic.
 bool tile_ok(int tile) {
-  if (tile == -1 || tile == 23 || tile == 31 || tile == 7 || tile == 15 || tile == 39) return true;
+  if (tile == -1 || tile == 23 || tile == 31 || tile == 7 || tile == 15 || tile == 39 || tile == 47 || tile == 55)
+    return true;
   if (tile < 0 || tile >= 64) return false;
   const int c = tile & 7, v = (tile >> 3) & 3;
   return c <= 6 && v <= 2 && !(v == 1 && c > 4) && !(v == 2 && c == 5);
 }
 
+#ifndef POSU_SPLIT_SG_HEAD
+#define POSU_SPLIT_SG_HEAD 0   // (the staggered split 256x256 head instance spills 23 VGPRs)
+#endif
 template <typename T, bool DUAL>
 int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
   // the split dtype runs the plain (unstaggered, non-persistent) loops: its K-tiles pair two
@@ -1504,8 +1537,9 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       g.ntiles = 1;
       g.mtiles = (g.M + 255) / 256;
       if constexpr (SPL) {
-        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, false, true>), dim3(g.mtiles * nclass),
-                           dim3(512), 0, s, g);
+        // (round 6: the staggered loop in split fp16 too, POSU_SPLIT_SG_HEAD; bit-identical either way)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, POSU_SPLIT_SG_HEAD != 0, true>),
+                           dim3(g.mtiles * nclass), dim3(512), 0, s, g);
       } else {
         // staggered two-slot loop (waves 4-7 half a K-tile behind; bit-exact with tile 5)
         hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 256, 8, 2, 2, DUAL, true, true>), dim3(g.mtiles * nclass),
@@ -1547,7 +1581,8 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
     }
   } else if (tile == 23 || tile == 31) {
     const int c = tile == 23 ? 5 : 6;
-    if (FAST2 && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
+    // (split fp16: 31 only -- its staggered 256x256 instance spills 56 VGPRs)
+    if ((FAST2 || (SPL && c == 6)) && g.CoutPad % (c == 5 ? 256 : 128) == 0) {
       cfg = c;
       sg = true;
     }
@@ -1557,6 +1592,12 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
       sg = FAST2;
       w8 = SPL;
       wg4 = tile == 15;
+    }
+  } else if (tile == 47 || tile == 55) {   // split fp16: the staggered 128x128 eight-wave tiles (round 6)
+    if (SPL && g.CoutPad % 128 == 0) {
+      cfg = 7;
+      sg = true;
+      wg4 = tile == 55;
     }
   } else if (tile >= 0) {
     const int c = tile & 7, v = (tile >> 3) & 3;
@@ -1588,6 +1629,15 @@ int launch(ConvGeom g, int nclass, hipStream_t s, const char* what, int tile) {
         hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL>), dim3(nb), dim3(512), 0, s, g);
       else
         hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL>), dim3(nb), dim3(512), 0, s, g);
+      return check_launch(what);
+    }
+    if (sg) {   // round 6: the staggered eight-wave tiles in split fp16: 256x128 (31), 128x128 (47 / 55)
+      if (cfg == 7 && wg4)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
+      else if (cfg == 7)
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 128, 128, 8, 2, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
+      else
+        hipLaunchKernelGGL((conv_igemm_kernel<T, 256, 128, 8, 4, 2, DUAL, true>), dim3(nb), dim3(512), 0, s, g);
       return check_launch(what);
     }
   }

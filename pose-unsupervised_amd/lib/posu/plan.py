@@ -87,8 +87,12 @@ class RawViews:
 # the 128x128 eight-wave staggered conv tiles (7 / 15, round 4) among the autotuner's candidates
 TILES_128X8 = True
 # the 128x128 tile with two K groups of four waves (39, round 5; inference plans only: its K order
-# differs from the other tiles', and the training plan relies on every candidate summing alike)
-TILES_KSPLIT = True
+# differs from the other tiles', and the training plan relies on every candidate summing alike).
+# Off since round 6: no network-level gain on the driver's box (control leg 2.2622 vs 2.2641 ms,
+# BENCH_r05; fp16x3 5.780 / 5.847 vs 5.782 / 5.784 ms, profiles/r06/ksplit_fp16x3_ab_r6e.txt), and
+# without it every candidate tile computes the same sums -- the results no longer depend on which tile
+# the autotuner picks (bitwise reproducible without a fixed --tune-file)
+TILES_KSPLIT = False
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -125,10 +129,11 @@ def _tile_candidates(cout, code=None, ksplit=False):
     sg = [23 + 8 * (t == 6) for t in c if t in (5, 6)] + ([7, 15] if cpad % 128 == 0 and TILES_128X8 else [])
     # (tile 32, the persistent 256x64 four-wave instance, is left out: it spills 928 B per lane to
     # scratch and took ~1.2 ms per launch in the tuning trials, 10x the other tiles)
-    if code == ops.F16X3:   # the split dtype: plain rings only (no stagger, no persistent stream), the
-        # unstaggered eight-wave 128x128 tiles (7 / 15) and the two-K-group tile (39)
+    if code == ops.F16X3:   # the split dtype: plain rings (no persistent stream), the unstaggered (7 / 15)
+        # and (round 6) staggered (47 / 55) eight-wave 128x128 tiles, the staggered 256x128 tile (31) and the
+        # two-K-group tile (39)
         return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + (
-            [7, 15] + ([39] if ksplit else []) if cpad % 128 == 0 else [])
+            [7, 15, 47, 55, 31] + ([39] if ksplit else []) if cpad % 128 == 0 else [])
     if ksplit and code in (ops.BF16, ops.F16) and cpad % 128 == 0:
         sg = sg + [39]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg

@@ -31,7 +31,7 @@ def rel_err(got, ref, absref):
 
 @pytest.mark.parametrize('cin,cout,k,stride,n,hw', [(64, 128, 3, 1, 2, 16), (256, 64, 1, 1, 3, 8),
                                                     (128, 256, 3, 2, 2, 16), (32, 64, 1, 1, 1, 5)])
-@pytest.mark.parametrize('tile', [-1, 0, 3, 5, 9, 18, 7, 15, 39])
+@pytest.mark.parametrize('tile', [-1, 0, 3, 5, 9, 18, 7, 15, 39, 31, 47, 55])
 def test_split_conv_matches_fp64(cuda, cin, cout, k, stride, n, hw, tile):
     torch.manual_seed(cin + cout + k + tile)
     pad = k // 2
@@ -57,6 +57,11 @@ def test_split_conv_matches_fp64(cuda, cin, cout, k, stride, n, hw, tile):
     got = from_split(y)
     # f32 accumulation over K products + the operands' 2^-22 split error: well under 1e-5 of sum |w x|
     assert rel_err(got, ref, mag) < 2e-6
+    if tile in (31, 47, 55):   # the staggered split tiles: bit-identical to their unstaggered twins
+        twin = {31: 6, 47: 7, 55: 15}[tile]
+        y2 = ops.conv2d_nhwc(xs, ws, cout, k, k, stride, pad, (scale.double() * 2.0 ** -e).float(), shift, rs, True, S,
+                             tile=twin)
+        assert torch.equal(y, y2)
 
 
 def test_split_dual_and_deconv_head_match_fp64(cuda):

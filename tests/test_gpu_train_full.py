@@ -105,8 +105,9 @@ def test_full_step_fp32_forward_matches_oracle(full_step):
 # (1e-3 x epipolar, MSE-dominated) measured cosine 0.999923 (gated at 1 - 2e-4), per-tensor norm
 # deviation median 0.0045 / max 0.094 (layer1.1.bn2.weight)
 FULL_BF16 = {'hm': 0.45, 'mse': 6e-4, 'epi': 0.03, 'cos': 1 - 2e-4, 'norm_median': 0.01, 'norm_max': 0.2}
-# the benched loss (FundamentalLoss x 1 on flat heatmaps): about half the measured cosine
-FULL_BF16_FUND = {'cos': 0.0}
+# the benched loss (FundamentalLoss x 1 on flat heatmaps): round 6 (call r6e) measured cosine 0.9285 against
+# the fp32 step's gradients (JointsMSE only: 0.999922); gated at twice its distance from 1
+FULL_BF16_FUND = {'cos': 0.85}
 
 
 def _grad_cmp(a, b):
