@@ -270,6 +270,17 @@ int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* 
  * shift (b3 + bd).  s1n / b1n / t1n: optional (all null, or all given) -- the next identity block's
  * conv1 + BN1 + ReLU over y, as posu_bottleneck_tail_stream_next_fwd.  wstream =
  * packing.pack_down_tail_stream(conv2 pack, dual pack[, next conv1 pack]). */
+/* (ABI 16) The LAST identity block of a layer chained with the NEXT layer's first conv1 + BN1 + ReLU
+ * (1x1 / stride 1 over y, C -> Pn = 2 P at this map size: layer2 / 3 / 4 block 0's conv1,
+ * lib/models/pose_resnet.py:79-81), split fp16 at 256x256 only; Pn = P is
+ * posu_bottleneck_tail_stream_next_fwd.  Each y chunk's next-conv1 k-steps run twice, once per half
+ * of the Pn outputs (two accumulator sets); t1n [N, H, W, Pn] (logical), s1n / b1n [Pn] f32, wstream =
+ * packing.pack_tail_stream(conv2, conv3, next conv1 [Pn][C']).  Bit-identical to the tail followed by
+ * posu_conv2d_fwd(next conv1) over y. */
+int posu_bottleneck_tail_stream_chain_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
+                                          int P, int Pn, const void* wstream, long long wstream_bytes,
+                                          const float* s2, const float* b2, const float* s3, const float* b3,
+                                          void* y, const float* s1n, const float* b1n, void* t1n, void* stream);
 int posu_bottleneck_down_tail_stream_fwd(int dtype, const void* t1, const void* x, int N, int H, int W, int C,
                                          int P, const void* wstream, long long wstream_bytes, const float* s2,
                                          const float* b2, const float* s3, const float* b3, void* y,

@@ -86,7 +86,8 @@ __device__ __forceinline__ void ld8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, int CM = 1, bool DOWN = false>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, int CM = 1, bool DOWN = false,
+          int NX = 1>
 struct TailCfg {
   static constexpr int kRows = ROWS;               // image rows per workgroup
   static constexpr int kNW = NW;                   // waves per workgroup
@@ -105,7 +106,8 @@ struct TailCfg {
   static constexpr int kChunk = 32 * kNCQ;         // conv3 output channels per chunk
   static constexpr int kNC = C / kChunk;           // conv3 chunks
   // stream blocks per conv3 chunk (+ DOWN: the downsample's K slice over x; + NEXT: the next conv1's)
-  static constexpr int kBlk3 = 1 + DOWN + NEXT;
+  // (NX: the next conv1's output channels in units of P -- 2 when it opens the next layer, round 6)
+  static constexpr int kBlk3 = 1 + DOWN + NEXT * NX;
   static constexpr int kSteps = 9 * kKT + kNC * kKT * kBlk3;
   static constexpr int kYC = kS3 + 2 * C * 4;      // NEXT: the y chunk [kPx][P] behind BN3
   static constexpr int kLdsN = NEXT && kYC + kPx * kRowB > kLds ? kYC + kPx * kRowB : kLds;
@@ -161,7 +163,11 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 // (pose_resnet.py:136-141) -- no residual; each conv3 chunk also runs the downsample over the block
 // input x (P channels, staged in LDS) into the same accumulators, [w3*s3 | wd*sd] with shift = b3 + bd
 // (posu_conv1x1_dual_fwd's K order: bit-identical to it)
-template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false>
+// NX = 2 (round 6, split fp16): the next conv1 has 2 P outputs -- the first block of the NEXT layer
+// (layer2 / 3 / 4 block 0's conv1, C -> 2 P at this map size) -- so the last identity block of a layer
+// chains it too: two accumulator sets, each over the same y chunk image
+template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false,
+          int NX = 1>
 __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   // split fp16 (POSU_F16X3, round 6): every pixel row holds [hi 32 | lo 32] per 32 channels, i.e. the
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
   // epilogues join residual pairs and split their outputs
   constexpr bool SPL = O::SPLIT;
   constexpr int CM = SPL ? 2 : 1;
-  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT, CM, DOWN>;
+  using K = TailCfg<W, P, C, ROWS, NW, NEXT, MT, CM, DOWN, NX>;
   constexpr int kRows = ROWS, kThreads = NW * 64;
   constexpr int ES = 2, kD = K::kD;
   __shared__ __attribute__((aligned(16))) char smem[K::kLdsAll];
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
   lds_barrier();
 
   f32x4 acc[MT][2];   // [m-tile i: tile pixels 16 MT pg + 16 i ..][n-tile j]
-  f32x4 acc1[MT][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
+  f32x4 acc1[NX][MT][2];  // NEXT: the next conv1's accumulators over the whole chunk loop
   auto zero = [&](f32x4 (&a)[MT][2]) {
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -493,12 +499,17 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
       // the next block's conv1 over this K slice (y channels kChunk nc ..): same k order as a
       // conv launch over y, so t1n is bit-identical to it
       lds_barrier();
-      block(acc1, 9 + K::kBlk3 * nc + 1 + DOWN, K::kYC, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
+#pragma unroll
+      for (int h = 0; h < NX; ++h)
+        block(acc1[h], 9 + K::kBlk3 * nc + 1 + DOWN + h, K::kYC, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     }
   };
   // unrolled: hipcc's wait counts at a loop head merge both paths and made every chunk's first
   // weight wait also wait for the previous chunk's y stores (layer2 tail 90.7 -> 86.7 us)
-  if constexpr (NEXT) zero(acc1);
+  if constexpr (NEXT) {
+#pragma unroll
+    for (int h = 0; h < NX; ++h) zero(acc1[h]);
+  }
 #pragma unroll
   for (int nc = 0; nc < K::kNC; ++nc) {
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
@@ -508,19 +519,23 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
     chunk(nc, rv, rl);
   }
   if constexpr (NEXT) {
-    // t1n = relu(conv1n * s1n + b1n), this lane's 8 channels of each m-tile's pixel
-    T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * P * CM;
-    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(tg, 0, K::kPx * P * CM * ES, 0x00020000);
-    const int c0 = 32 * cq + cpair;
-    float sc[8], sh[8];
-    ld8(g.s1n + c0, sc);
-    ld8(g.b1n + c0, sh);
+    // t1n = relu(conv1n * s1n + b1n) [.., NX P], this lane's 8 channels (of each half) of each m-tile's pixel
+    constexpr int PN = NX * P;
+    T* tg = reinterpret_cast<T*>(g.t1n) + static_cast<size_t>(n * H + y0) * W * PN * CM;
+    const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(tg, 0, K::kPx * PN * CM * ES, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      float v[8];
-      pair(acc1, i, v);
-      bn_relu(v, sc, sh, nullptr);
-      st8(trs, (tpix(i) * P * CM + (SPL ? split_ch(c0) : c0)) * ES, v);
+    for (int h = 0; h < NX; ++h) {
+      const int c0 = h * P + 32 * cq + cpair;
+      float sc[8], sh[8];
+      ld8(g.s1n + c0, sc);
+      ld8(g.b1n + c0, sh);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        float v[8];
+        pair(acc1[h], i, v);
+        bn_relu(v, sc, sh, nullptr);
+        st8(trs, (tpix(i) * PN * CM + (SPL ? split_ch(c0) : c0)) * ES, v);
+      }
     }
   }
 }
@@ -528,9 +543,9 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
 // split fp16 instances (round 6): layer1 (W = 64, planes 64: 2 rows x 64 px, four waves as 2 pixel x 2
 // channel groups), layer2 (2 rows x 32 px, four waves), layer3 (4 rows x 16 px, eight waves) -- the
 // pairs double the t1 window, so the tiles are the bf16 ones' small variants (68 / 69 / 110 KB of LDS)
-template <int W, int P, int C, int ROWS, int NW, bool NEXT, int MT, bool DOWN = false>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT, int MT, bool DOWN = false, int NX = 1>
 void launch_tail_split(const TailSGeom& g, hipStream_t s) {
-  hipLaunchKernelGGL((tail_stream_kernel<f16s_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>),
+  hipLaunchKernelGGL((tail_stream_kernel<f16s_t, W, P, C, ROWS, NW, NEXT, MT, DOWN, NX>),
                      dim3(static_cast<unsigned>(g.N * (g.H / ROWS))), dim3(NW * 64), 0, s, g);
 }
 
@@ -570,7 +585,7 @@ namespace {
 int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x, int N, int H, int W, int C, int P,
                      const void* wstream, long long wstream_bytes, const float* s2, const float* b2,
                      const float* s3, const float* b3, void* y, const float* s1n, const float* b1n, void* t1n,
-                     void* stream, bool down = false) {
+                     void* stream, bool down = false, int nx = 1) {
   const std::string what = name;
   const bool next = t1n != nullptr;
   const bool spl = dtype == POSU_F16X3;
@@ -593,11 +608,13 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                what + ": built for layer1's first Bottleneck (x 64 -> y 256 channels, planes 64) at W = 64 in split "
                       "fp16 and at W = 96 in BF16 / F16");
   const int cm = spl ? 2 : 1;   // stored halves per logical channel
+  POSU_REQUIRE(nx == 1 || (nx == 2 && spl && next && !down && (l1 || l2 || l3)),
+               what + ": a next conv1 of 2 P outputs is chained by the split 256x256 identity tails only");
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream); split: KT = 2 P / 32
     const long long kt = cm * P / 32, nc = C / P;
-    const long long need = (P / 32) * (9 * kt + (1 + down + next) * nc * kt) * 2 * 64 * 8 * 2;
+    const long long need = (P / 32) * (9 * kt + (1 + down + (next ? nx : 0)) * nc * kt) * 2 * 64 * 8 * 2;
     POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
@@ -636,6 +653,10 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   if (spl && down) {
     if (next) launch_tail_split<64, 64, 256, 2, 4, true, 4, true>(g, s);
     else launch_tail_split<64, 64, 256, 2, 4, false, 4, true>(g, s);
+  } else if (spl && nx == 2) {
+    if (l1) launch_tail_split<64, 64, 256, 2, 4, true, 4, false, 2>(g, s);
+    else if (l2) launch_tail_split<32, 128, 512, 2, 4, true, 4, false, 2>(g, s);
+    else launch_tail_split<16, 256, 1024, 4, 8, true, 4, false, 2>(g, s);
   } else if (spl) {
     if (l1) {
       if (next) launch_tail_split<64, 64, 256, 2, 4, true, 4>(g, s);
@@ -710,4 +731,21 @@ extern "C" int posu_bottleneck_down_tail_stream_fwd(int dtype, const void* t1, c
                                                     void* t1n, void* stream) {
   return tail_stream_impl("posu_bottleneck_down_tail_stream_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes,
                           s2, b2, s3, b3, y, s1n, b1n, t1n, stream, true);
+}
+
+// The last identity block of a layer chained with the NEXT layer's first conv1 (1x1, C -> Pn = 2 P at this
+// map size; the strided block's conv2 / dual GEMM follow as their own launches), split fp16 only (round 6):
+// t1n [N, H, W, Pn] (logical), s1n / b1n [Pn]; wstream = packing.pack_tail_stream(conv2, conv3, next conv1
+// pack [Pn][C']).  Pn = P is posu_bottleneck_tail_stream_next_fwd.
+extern "C" int posu_bottleneck_tail_stream_chain_fwd(int dtype, const void* t1, const void* x, int N, int H, int W,
+                                                     int C, int P, int Pn, const void* wstream,
+                                                     long long wstream_bytes, const float* s2, const float* b2,
+                                                     const float* s3, const float* b3, void* y, const float* s1n,
+                                                     const float* b1n, void* t1n, void* stream) {
+  if (!t1n || P <= 0 || (Pn != P && Pn != 2 * P)) {
+    set_error("posu_bottleneck_tail_stream_chain_fwd: t1n must be given and Pn must be P or 2 P");
+    return POSU_ERR_ARG;
+  }
+  return tail_stream_impl("posu_bottleneck_tail_stream_chain_fwd", dtype, t1, x, N, H, W, C, P, wstream, wstream_bytes,
+                          s2, b2, s3, b3, y, s1n, b1n, t1n, stream, false, Pn / P);
 }

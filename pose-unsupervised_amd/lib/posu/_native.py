@@ -47,6 +47,8 @@ _SIGNATURES = {
     'posu_bottleneck_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p],
     'posu_bottleneck_tail_stream_next_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _p],
+    'posu_bottleneck_tail_stream_chain_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p,
+                                              _p, _p, _p],
     'posu_bottleneck_down_tail_stream_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _p, _p, _p, _p,
                                              _p, _p],
     'posu_bottleneck_s2_tail_fwd': [_i, _p, _p, _i, _i, _i, _i, _i, _p, _ll, _p, _p, _p, _i, _p, _p],

@@ -185,6 +185,22 @@ def bottleneck_tail_stream_next_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, c
     return out, t1n
 
 
+def bottleneck_tail_stream_chain_nhwc(t1, x, wstream, s2, b2, s3, b3, s1n, b1n, code, out=None, t1n=None):
+    """The last identity block's tail of a layer chained with the NEXT layer's first conv1 + BN1 + ReLU
+    (C -> Pn = s1n.numel() = 2 P; posu_bottleneck_tail_stream_chain_fwd, split fp16): (y, t1n [N, H, W, Pn])."""
+    n, h, w, c = x.shape
+    cm = cmul(code)
+    p, pn = t1.shape[3] // cm, s1n.numel()
+    if out is None:
+        out = torch.empty_like(x)
+    if t1n is None:
+        t1n = torch.empty((n, h, w, pn * cm), dtype=x.dtype, device=x.device)
+    call('posu_bottleneck_tail_stream_chain_fwd', code, ptr(t1), ptr(x), n, h, w, c // cm, p, pn, ptr(wstream),
+         wstream.numel() * wstream.element_size(), ptr(s2), ptr(b2), ptr(s3), ptr(b3), ptr(out), ptr(s1n), ptr(b1n),
+         ptr(t1n), stream_of(x.device))
+    return out, t1n
+
+
 def bottleneck_down_tail_stream_nhwc(t1, x, wstream, s2, b2, s3, b3, code, s1n=None, b1n=None, out=None, t1n=None):
     """Layer1's first Bottleneck after its conv1 in split fp16 (posu_bottleneck_down_tail_stream_fwd):
     conv2 + the [conv3 | downsample] dual GEMM (scale s3, shift b3) + ReLU in one launch, t1 / x

@@ -81,17 +81,20 @@ def pack_tail_stream(w2pk, w3pk, w1n=None):
     planes, c = w2pk.shape[0], w3pk.shape[0]
     ncq, kt, nc = planes // 32, w3pk.shape[1] // 32, c // planes
     cm = kt * 32 // planes   # stored halves per logical channel (2: split packs)
+    # (w1n may have 2 P rows: the next LAYER's first conv1, chained by a layer's last tail -- its k-steps
+    # come per chunk as two halves of P output channels, posu_bottleneck_tail_stream_chain_fwd)
     f2 = mfma_fragments(w2pk)                                    # [2 ncq][9 kt][64][8]
     f3 = mfma_fragments(w3pk)                                    # [2 ncq nc][kt][64][8]
     s2 = f2.reshape(ncq, 2, 9 * kt, 64, 8).permute(0, 2, 1, 3, 4)
     s3 = f3.reshape(nc, ncq, 2, kt, 64, 8).permute(1, 0, 3, 2, 4, 5)              # [ncq][nc][kt][2][64][8]
     if w1n is None:
         return torch.cat([s2, s3.reshape(ncq, nc * kt, 2, 64, 8)], dim=1).contiguous()
-    if tuple(w1n.shape) != (planes, c * cm):
-        raise ValueError('pack_tail_stream: the next conv1 pack must be [%d][%d]' % (planes, c * cm))
-    f1 = mfma_fragments(w1n)                                     # [2 ncq][nc kt][64][8]
-    s1 = f1.reshape(ncq, 2, nc, kt, 64, 8).permute(0, 2, 3, 1, 4, 5)              # [ncq][nc][kt][2][64][8]
-    s31 = torch.stack([s3, s1], dim=2).reshape(ncq, nc * 2 * kt, 2, 64, 8)
+    if w1n.shape[0] not in (planes, 2 * planes) or w1n.shape[1] != c * cm:
+        raise ValueError('pack_tail_stream: the next conv1 pack must be [%d or %d][%d]' % (planes, 2 * planes, c * cm))
+    nx = w1n.shape[0] // planes
+    f1 = mfma_fragments(w1n)                                     # [2 ncq nx][nc kt][64][8]
+    s1 = f1.reshape(nx, ncq, 2, nc, kt, 64, 8).permute(1, 3, 0, 4, 2, 5, 6)      # [ncq][nc][nx][kt][2][64][8]
+    s31 = torch.cat([s3.unsqueeze(2), s1], dim=2).reshape(ncq, nc * (1 + nx) * kt, 2, 64, 8)
     return torch.cat([s2, s31], dim=1).contiguous()
 
 

@@ -269,6 +269,9 @@ SPLIT_TAILS = True
 # the first block as conv1 + the down tail, the identity blocks as the (chained) tail; False: three
 # conv launches per block (the fused layer1 kernel is built for 64-wide maps)
 TAIL_W96 = True
+# split fp16: the last identity block of layers 1-3 chains the NEXT layer's first conv1 too (C -> 2 P,
+# posu_bottleneck_tail_stream_chain_fwd, round 6), so that block's conv1 is no launch of its own
+CHAIN_LAYERS = True
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -282,7 +285,7 @@ def _fused_fits(x, cout):
 
 class _Block:
     __slots__ = ('convs', 'down', 'dual', 'w1f', 'w3f', 'w3d', 'l1', 'l2', 'l3', 'wst', 'chain', 'wsn', 'ws2', 'ws2n',
-                 'wsd', 'wsdn', 'dscale', 'code')
+                 'wsd', 'wsdn', 'dscale', 'code', 'xchain', 'wsx')
 
     def __init__(self, blk, code, bk):
         names = ['conv1', 'conv2', 'conv3'] if hasattr(blk, 'conv3') else ['conv1', 'conv2']
@@ -303,6 +306,8 @@ class _Block:
         self.wsdn = None             # ... with the next block's conv1 appended
         self.dscale = None           # ... the dual GEMM's epilogue scale (2^-e)
         self.code = code
+        self.xchain = None           # split: the next layer's first conv1 (_Conv), chained by this last tail
+        self.wsx = None              # ... its tail stream (pack_tail_stream(.., that conv1): NX = 2)
         ds = blk.downsample
         if ds is not None and len(names) == 3 and ds[0].kernel_size == (1, 1) and \
                 blk.conv3.weight.shape[1] % bk == 0 and ds[0].weight.shape[1] % bk == 0:
@@ -378,20 +383,36 @@ class _Block:
             return 'l2'
         if self.l3 and x.shape[2] == 16 and x.shape[1] % 8 == 0:
             return 'l3'
-        if self.l3 and x.shape[2] == 24 and x.shape[1] % 6 == 0 and TAIL_W24:   # R152@384 (configs[4])
+        split = self.code == ops.F16X3   # (the split tails: 256x256 maps only)
+        if self.l3 and x.shape[2] == 24 and x.shape[1] % 6 == 0 and TAIL_W24 and not split:   # R152@384 (configs[4])
             return 'l3w'
-        if self.l2 and x.shape[2] == 48 and x.shape[1] % 2 == 0 and TAIL_W24:   # layer2 at 384x384
+        if self.l2 and x.shape[2] == 48 and x.shape[1] % 2 == 0 and TAIL_W24 and not split:   # layer2 at 384x384
             return 'l2w'
         return None
 
-    def run(self, x, code, out=None, t1=None):
+    def link_layer(self, first):
+        """Split fp16: chain this last identity block's tail with the next layer's first block's conv1
+        (1x1 / stride 1, C -> 2 P: posu_bottleneck_tail_stream_chain_fwd)."""
+        if not (self.code == ops.F16X3 and (self.l1 or self.l2 or self.l3) and first.dual is not None):
+            return
+        c1n = first.convs[0]
+        planes = self.convs[1].cout
+        if c1n.k == 1 and c1n.stride == 1 and c1n.cout == 2 * planes and tuple(c1n.w.shape)[1] == self.convs[0].w.shape[1]:
+            self.xchain = c1n
+            self.wsx = pack_tail_stream(self.convs[1].w, self.convs[2].w, c1n.w)
+
+    def run(self, x, code, out=None, t1=None, chain_out=False):
         """-> (y, t1n): t1n = the next block's conv1 output when this block's tail is chained
-        (CHAINED_TAILS), else None; t1 = this block's conv1 output from the previous block's
+        (CHAINED_TAILS; chain_out: the last block of a layer chaining the next layer's first conv1,
+        CHAIN_LAYERS), else None; t1 = this block's conv1 output from the previous block's
         chained tail (None: computed here)."""
         kind = self._tail_kind(x)
         if kind is None:
             if t1 is not None:
-                raise RuntimeError('a chained conv1 output handed to a block without a streamed tail')
+                if self.dual is None:
+                    raise RuntimeError('a chained conv1 output handed to a block without a streamed tail')
+                # the first block of a layer whose conv1 the previous layer's last tail computed
+                return self.dual(self.convs[1](t1, code), x, code, out=out), None
             if self.wsdn is not None and CHAINED_TAILS and self._down_tail_ok(x):
                 c1, c2 = self.convs
                 n1 = self.chain
@@ -406,6 +427,10 @@ class _Block:
         c1, c2, c3 = self.convs
         if t1 is None:
             t1 = c1(x, code)
+        if chain_out and self.xchain is not None and CHAINED_TAILS and CHAIN_LAYERS:
+            n1 = self.xchain
+            return ops.bottleneck_tail_stream_chain_nhwc(t1, x, self.wsx, c2.scale, c2.shift, c3.scale, c3.shift,
+                                                         n1.scale, n1.shift, code, out=out)
         if self.chain is not None and CHAINED_TAILS and kind != 'l3w':   # (no chained tail at W = 24)
             n1 = self.chain
             return ops.bottleneck_tail_stream_next_nhwc(t1, x, self.wsn, c2.scale, c2.shift, c3.scale, c3.shift,
@@ -524,6 +549,8 @@ class PoseResNetPlan:
         for layer in self.layers:
             for b0, b1 in zip(layer, layer[1:]):
                 b0.link_next(b1)
+        for la, lb in zip(self.layers, self.layers[1:]):
+            la[-1].link_layer(lb[0])
         mods = list(net.deconv_layers)
         self.deconvs = []
         for i in range(0, len(mods), 3):
@@ -717,10 +744,14 @@ class PoseResNetPlan:
         if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
             x = self.stem_pool(x)
             x1 = None
+            t1 = None   # a conv1 output handed across a layer boundary (CHAIN_LAYERS)
             for li, layer in enumerate(self.layers):
-                x = self._run_layer(layer, x, code)
+                for bi, blk in enumerate(layer):
+                    x, t1 = blk.run(x, code, t1=t1, chain_out=bi == len(layer) - 1 and li + 1 < len(self.layers))
                 if li == 0:
                     x1 = x
+            if t1 is not None:
+                raise RuntimeError('the last layer produced a chained conv1 output')
             for dc in self.deconvs[:-1]:
                 x = dc(x, code)
             hm, f = self._last_deconv_head(x, keep_features)

@@ -188,3 +188,43 @@ def test_r152_384_fp16_pipeline_matches_the_oracle_chain(cuda, monkeypatch):
     assert c['heatmap_abs_err']['mean'] < 0.05 and c['heatmap_abs_err']['max'] < 0.5
     assert c['triangulation_same_2d_mm']['max'] < 1e-2      # the DLT itself: BASELINE's 1e-2 mm
     assert c['epipolar_loss_rel_err'] < 0.1
+
+
+def test_configs1_batch64_plan_end_to_end(cuda):
+    """BASELINE configs[1]'s plan exactly as bench.time_configs1 runs it -- R50@256 bf16, ONE batch of 64
+    frames, autotuned tiles (layer3's 4-row streamed tails at this grid), captured in a hipGraph --
+    end to end: every heatmap finite, and rows 0-1 bit-identical to a 2-frame plan on the heuristic
+    tiles (since round 6 every candidate tile sums K in the same order: tile 39 is off), whose
+    heatmaps are checked against the fp32 CPU oracle at the bf16 band."""
+    from oracle import pose_resnet_ref as PR
+    net = bench.build_model(50, 256, 'bf16', cuda)
+    plan = net.plan(cuda)
+    views = [v.to(cuda) for v in syn.synthetic_views(1, 64, 256, seed=300)]
+    with torch.no_grad():
+        plan.autotune(plan.pack_input(views), keep_features=False, reps=2)
+        s = torch.cuda.Stream(cuda)
+        s.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(s):
+            plan.run(plan.pack_input(views), keep_features=False)
+        torch.cuda.current_stream(cuda).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            hm = plan.run(plan.pack_input(views), keep_features=False)[0]
+        g.replay()
+        torch.cuda.synchronize()
+        hm64 = hm.clone()
+        from posu import plan as P
+        saved = dict(P._TUNE_CACHE)
+        P._TUNE_CACHE.clear()
+        try:
+            hm2 = plan.run(plan.pack_input([v[:2] for v in views]), keep_features=False)[0]
+        finally:
+            P._TUNE_CACHE.update(saved)
+        torch.cuda.synchronize()
+    assert torch.isfinite(hm64).all()
+    assert torch.equal(hm64[:2], hm2)
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    ref, _, _ = PR.pose_resnet_forward(views[0][:2].cpu(), sd, 50)
+    err = (hm2.cpu() - ref).abs()
+    print('configs1 batch-64 plan: rows 0-1 vs the oracle, heatmaps max %.3g mean %.3g' % (err.max(), err.mean()))
+    assert float(err.max()) < BANDS['bf16']['hm_max'] and float(err.mean()) < BANDS['bf16']['hm_mean']

@@ -527,12 +527,24 @@ def test_split_tails_match_conv_launches(cuda, layer, n, h):
     yc, t1n = ops.bottleneck_tail_stream_next_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1n), s2, b2, s3, b3, s1n,
                                                    b1n, S, out=_sentinel(xd), t1n=_sentinel(t1))
     t1n_ref = ops.conv2d_nhwc(two, p1n, p, 1, 1, 1, 0, s1n, b1n, None, True, S)
+    # the layer's last tail chaining the NEXT layer's first conv1 (C -> 2 P, posu_bottleneck_tail_stream_chain_fwd)
+    w1x = torch.randn(2 * p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1x = (torch.rand(2 * p, generator=g) + 0.5, torch.randn(2 * p, generator=g) * 0.1)
+    p1x, e1x = _split_pack(w1x.to(cuda), c)
+    s1x, b1x = sc(bn1x, e1x)
+    yx, t1x = ops.bottleneck_tail_stream_chain_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1x), s2, b2, s3, b3, s1x,
+                                                    b1x, S, out=_sentinel(xd),
+                                                    t1n=_sentinel(t1, (n, h, w, 4 * p)))
+    t1x_ref = ops.conv2d_nhwc(two, p1x, 2 * p, 1, 1, 1, 0, s1x, b1x, None, True, S)
     torch.cuda.synchronize()
     dy = int((y.view(torch.int16) != two.view(torch.int16)).sum())
     dyc = int((yc.view(torch.int16) != two.view(torch.int16)).sum())
     dt1 = int((t1n.view(torch.int16) != t1n_ref.view(torch.int16)).sum())
-    print('split %s tail n=%d h=%d: y differing %d, chained y %d, t1n %d' % (layer, n, h, dy, dyc, dt1))
-    assert dy == 0 and dyc == 0 and dt1 == 0
+    dyx = int((yx.view(torch.int16) != two.view(torch.int16)).sum())
+    dt1x = int((t1x.view(torch.int16) != t1x_ref.view(torch.int16)).sum())
+    print('split %s tail n=%d h=%d: y differing %d, chained y %d, t1n %d; layer-chained y %d, t1n (2 P) %d'
+          % (layer, n, h, dy, dyc, dt1, dyx, dt1x))
+    assert dy == 0 and dyc == 0 and dt1 == 0 and dyx == 0 and dt1x == 0
     if n >= 128:
         return
     # fp64 torch on the values the device holds: within the f32 level of sum |w x|
@@ -566,6 +578,8 @@ def test_split_plan_tails_are_bit_identical_to_conv_launches(cuda):
             assert [b.l2 for b in plan.layers[1]] == [False, True, True, True]
             assert [b.l3 for b in plan.layers[2]] == [False] + [True] * 5
             assert plan.layers[0][0].wsdn is not None      # layer1 block 0 on the down tail, chained
+            # the last tail of layers 1-3 chains the next layer's first conv1 (CHAIN_LAYERS)
+            assert [layer[-1].xchain is not None for layer in plan.layers] == [True, True, True, False]
             assert [b.chain is not None for b in plan.layers[0]] == [True, True, False]
             hm1, x11, f1 = plan.run(plan.pack_input(views))
             P.SPLIT_TAILS = False

@@ -392,7 +392,8 @@ def test_every_tile_configuration_matches_torch(cuda, cfg, code):
 def test_invalid_tile_is_refused(cuda):
     x = torch.zeros(1, 8, 8, 64, device=cuda, dtype=torch.bfloat16)
     w = torch.zeros(64, 64, device=cuda, dtype=torch.bfloat16)
-    for bad in (47, 29, 64, 70, 40 + 5):   # (7 / 15: the 128x128 eight-wave tiles since round 4; 39 round 5)
+    # (7 / 15: the 128x128 eight-wave tiles since round 4; 39 round 5; 47 / 55 split fp16, round 6)
+    for bad in (63, 29, 64, 70, 40 + 5):
         with pytest.raises(RuntimeError, match='tile must be'):
             ops.conv2d_nhwc(x, w, 64, 1, 1, 1, 0, None, None, None, False, BF16, tile=bad)
 

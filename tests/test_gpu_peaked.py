@@ -102,8 +102,12 @@ def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
     net = net.to(cuda)
     groups = task['groups']
     host = task['host']
+    # targets 2 heatmap px right of the fitted ones: the net (fitted in fp32 to the unshifted targets) sits
+    # at the fp32 optimum of those, where the MSE gradient is rounding noise; against shifted targets
+    # the MSE gradient is a real signal for the bf16 backward to reproduce
+    targets = torch.roll(task['target'], shifts=2, dims=-1).cpu().numpy()
     g = {'num_layers': 50, 'image_size': 256, 'nviews': 4, 'batch': groups, 'seed': 0, 'fund_weight': fund_weight,
-         'targets': task['target'].cpu().numpy(), 'target_weight': np.ones((4, groups, 16, 1), np.float32),
+         'targets': targets, 'target_weight': np.ones((4, groups, 16, 1), np.float32),
          'centers': host['centers'], 'scales': host['scales'], 'subjects': np.asarray(host['subjects'])}
     sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
     net, hm, joints, mse, fund = _step(cuda, g, 'bf16', net=net, views=task['views'])
@@ -142,8 +146,14 @@ def test_bf16_train_step_on_peaked_network(fitted, cuda, fund_weight):
     assert np.median(rel) < b['norm_median'] and cos > b['cos']
 
 
-# about 2 x the round-5 measurement (call r5e): heatmaps 0.0351 max, MSE 1.3e-2 relative (a small
-# residual near the fit's optimum, so the bf16 heatmap rounding is a visible fraction of it);
-# gradients: with the FundamentalLoss median 0.059 / cosine 0.792, MSE only 0.030 / 0.970
-PEAKED_TRAIN_BF16 = {True: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.12, 'cos': 0.6},
-                     False: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.06, 'cos': 0.94}}
+# about 2 x the round-6 measurement (call r6g; the fp32-fitted net, targets shifted 2 px): heatmaps
+# 0.0351 max, MSE 1.8e-3 relative; gradients with the FundamentalLoss x 5 (the reference's fund5 config)
+# median 0.034 / cosine 0.751, JointsMSE only 0.0089 / 0.917 (the worst tensor: final_layer.bias, whose
+# gradient -- the heatmaps' summed residual -- nearly cancels).  Why the FundamentalLoss step stays near
+# 0.75: the oracle's own autograd of the FundamentalLoss w.r.t. the heatmaps, taken at the bf16
+# forward's heatmaps against the oracle's, agrees only to cosine 0.715 -- the soft-argmax at beta = 100
+# turns the bf16 forward's heatmap rounding (0.035 max) into a different gradient before any backward
+# kernel runs, so no backward precision can lift it (the faithful training step is the fp32 mode,
+# test_gpu_train.py)
+PEAKED_TRAIN_BF16 = {True: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.07, 'cos': 0.5},
+                     False: {'hm': 0.07, 'loss': 0.03, 'norm_median': 0.02, 'cos': 0.83}}
