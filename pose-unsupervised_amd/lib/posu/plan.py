@@ -93,6 +93,8 @@ TILES_128X8 = True
 # without it every candidate tile computes the same sums -- the results no longer depend on which tile
 # the autotuner picks (bitwise reproducible without a fixed --tune-file)
 TILES_KSPLIT = False
+# the split dtype's staggered eight-wave tiles (31, 47 / 55; round 6) among its autotuner candidates
+TILES_SPLIT_SG = True
 
 # ---- per-layer tile autotuning: geometry key -> conv tile configuration (process-wide,
 # shared by every plan, so a re-packed plan does not re-tune)
@@ -133,7 +135,7 @@ def _tile_candidates(cout, code=None, ksplit=False):
         # and (round 6) staggered (47 / 55) eight-wave 128x128 tiles, the staggered 256x128 tile (31) and the
         # two-K-group tile (39)
         return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + (
-            [7, 15, 47, 55, 31] + ([39] if ksplit else []) if cpad % 128 == 0 else [])
+            [7, 15] + ([47, 55, 31] if TILES_SPLIT_SG else []) + ([39] if ksplit else []) if cpad % 128 == 0 else [])
     if ksplit and code in (ops.BF16, ops.F16) and cpad % 128 == 0:
         sg = sg + [39]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
