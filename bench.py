@@ -279,11 +279,13 @@ def pmc_traffic_train(layers, size, precision, groups):
 def pmc_traffic(layers, size, precision, groups):
     """HBM bytes of one network forward from the newest committed PMC reduction
     (profiles/<round>/pmc_traffic_network.txt, written by tools/profile_round.sh with the
-    commit it was measured at), for the default workload; (None, None) otherwise."""
-    if (layers, size, precision, groups) != (50, 256, 'bf16', 32):
+    commit it was measured at; the fp16x3 plan's: pmc_traffic_network_fp16x3.txt, round 6), for the
+    default workload; (None, None) otherwise."""
+    if (layers, size, groups) != (50, 256, 32) or precision not in ('bf16', 'fp16x3'):
         return None, None
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*', 'pmc_traffic_network.txt')))
+    name = 'pmc_traffic_network.txt' if precision == 'bf16' else 'pmc_traffic_network_fp16x3.txt'
+    files = sorted(glob.glob(os.path.join(REPO, 'profiles', 'r*', name)))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -798,6 +800,10 @@ def infer_main(args):
             par['roofline'] = {'bound': 'mfma', 'achieved': round(tfp, 2), 'peak': PEAK_BF16_TFLOPS,
                                'unit': 'TFLOP/s', 'frac': round(tfp / PEAK_BF16_TFLOPS, 4),
                                'mfma_frac': round(3 * tfp / PEAK_BF16_TFLOPS, 4)}
+            ptr, psrc = pmc_traffic(args.layers, args.size, 'fp16x3', args.groups)
+            if ptr:
+                par['roofline']['traffic'] = ptr
+                par['roofline']['traffic_source'] = dict(psrc, counters='PMC FETCH_SIZE x2 + WRITE_SIZE, bytes per forward')
         if args.control_steps > 0:
             par['control'] = time_control(args, dev, rank, world, dist, 'fp16x3', CONTROL_FLAGS_PARITY)
     c1 = time_configs1(args, dev, rank, world, dist) if args.c1_steps > 0 else None

@@ -73,7 +73,9 @@ def main():
             'commit': os.environ.get('POSU_COMMIT')}
     alg = None
     from posu import roofline
-    if len(f) == len(roofline.r50_256_launches()):
+    split = any('f16s_t' in x[1] for x in f)   # the fp16x3 plan: its own launch list (no algorithmic table)
+    line['plan'] = 'fp16x3' if split else 'default (bf16 / fp16)'
+    if not split and len(f) == len(roofline.r50_256_launches()):
         alg = roofline.r50_256_launches()
         line['algorithmic_bytes'] = sum(r + wr for _, r, wr in alg)
         line['traffic_over_algorithmic'] = round(line['traffic_bytes'] / line['algorithmic_bytes'], 4)
