@@ -770,6 +770,8 @@ def infer_main(args):
         tr.update(metric=TRAIN_METRIC, n_gpus=world, frac=roof.get('frac'), traffic=roof.get('traffic'),
                   algorithmic_bytes=roof.get('algorithmic_bytes'),
                   traffic_over_algorithmic=roof.get('traffic_over_algorithmic'),
+                  algorithmic_bytes_fused_bn=roof.get('algorithmic_bytes_fused_bn'),
+                  traffic_over_fused_bn_ideal=roof.get('traffic_over_fused_bn_ideal'),
                   parallelism=t['config']['parallelism'], workload=t['config']['workload'],
                   optimizer=t['config']['optimizer'])
         return tr
@@ -1023,8 +1025,13 @@ def _train_loop(args, dev, dist, world, step, steps, warmup, nv, nb, stream):
             from posu import roofline as _rl
             alg = _rl.r50_256_train_algorithmic_bytes(frames, 2)
             roof['algorithmic_bytes'] = alg
+            # beside it the ideal step with BatchNorm fused into its neighbours (round 6): what the
+            # separate BN passes cost, in bytes
+            ideal = _rl.r50_256_train_algorithmic_bytes(frames, 2, fused_bn=True)
+            roof['algorithmic_bytes_fused_bn'] = ideal
             if traffic and nb == 32:
                 roof['traffic_over_algorithmic'] = round(traffic / alg, 4)
+                roof['traffic_over_fused_bn_ideal'] = round(traffic / ideal, 4)
     return {
         'metric': TRAIN_METRIC, 'value': round(value, 2), 'unit': 'frames/s', 'n_gpus': world,
         'steps': steps, 'warmup': warmup, 'ms_per_step': round(elapsed / steps * 1e3, 4),

@@ -73,7 +73,7 @@ def r50_256_algorithmic_bytes(n=128, es=2):
 
 
 # ---- the training step (bench.py --mode train / the train_mode leg): algorithmic bytes by class
-def r50_256_train_classes(n=128, es=2, joints=16):
+def r50_256_train_classes(n=128, es=2, joints=16, fused_bn=False):
     """{class: (read_bytes, write_bytes)} of one training step of n frames (posu.train_plan's launch
     classes): per conv + BatchNorm unit -- conv: x (a stride-2 1x1 only its stride-2 pixels) and the
     packed weight read, z written; BN statistics: z read; BN apply: z (+ the residual) read, y
@@ -86,7 +86,15 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     gradients and both moments read, parameters and moments written) complete it.  The stem (round
     5): its conv and weight gradient read the f32 NCHW views; BN + ReLU + max-pool is one pass (z
     read, the pooled activation and its argmax taps written) and the max-pool backward reads the taps.
-    Every tensor once per launch: the floor the kernels' PMC traffic is compared with."""
+    Every tensor once per launch: the floor the kernels' PMC traffic is compared with.
+
+    fused_bn (round 6): the IDEAL step with BatchNorm fused into its neighbours instead of passes of its
+    own -- the statistics in the producing conv's epilogue, BN + ReLU applied on the consumer's operand
+    load (the block outputs after a residual add still materialised: one pass, z + residual read, y
+    written), the backward sums in the epilogue of the kernel that writes gy (z read there), dz = f(gy, z)
+    formed on the data- and weight-gradient operand loads (z read by each; written only where the
+    residual branch needs it).  Its total against the launch-structure floor is what the separate BN
+    passes cost."""
     cls = {k: [0, 0] for k in ('conv fwd / dgrad', 'conv wgrad', 'batchnorm', 'maxpool', 'weight packing',
                                  'adam', 'heads / losses')}
 
@@ -107,12 +115,17 @@ def r50_256_train_classes(n=128, es=2, joints=16):
         z = act(hw_out, cout)
         mask = z // 16 if relu_after_res else 0                           # ReLU bits of y
         add('conv fwd / dgrad', xin + wts * (4 if stem else es), z)       # conv
-        add('batchnorm', z, 0)                                            # statistics
-        if not stem:                                                      # (the stem: fused with the pool)
-            add('batchnorm', z + (z if residual else 0), z + mask)        # apply (+ residual, + mask)
-        extra = mask                                                      # the mask bits
-        add('batchnorm', 2 * z + extra, 0)                                # backward partial sums
-        add('batchnorm', 2 * z + extra, z + (z if want_gres else 0))      # backward apply
+        if fused_bn:
+            if residual:                                                  # y materialised after the add
+                add('batchnorm', 2 * z, z + mask)
+            add('batchnorm', z + 2 * z, z if want_gres else 0)            # sums' z; dgrad / wgrad read z
+        else:
+            add('batchnorm', z, 0)                                        # statistics
+            if not stem:                                                  # (the stem: fused with the pool)
+                add('batchnorm', z + (z if residual else 0), z + mask)    # apply (+ residual, + mask)
+            extra = mask                                                  # the mask bits
+            add('batchnorm', 2 * z + extra, 0)                            # backward partial sums
+            add('batchnorm', 2 * z + extra, z + (z if want_gres else 0))  # backward apply
         add('conv wgrad', z + xin, wts * 4)
         if dx:
             add('conv fwd / dgrad', z + wts * es + (act(hw_in, cin) if dx_acc else 0), act(hw_in, cin))
@@ -150,5 +163,5 @@ def r50_256_train_classes(n=128, es=2, joints=16):
     return {k: tuple(v) for k, v in cls.items()}
 
 
-def r50_256_train_algorithmic_bytes(n=128, es=2):
-    return sum(r + w for r, w in r50_256_train_classes(n, es).values())
+def r50_256_train_algorithmic_bytes(n=128, es=2, fused_bn=False):
+    return sum(r + w for r, w in r50_256_train_classes(n, es, fused_bn=fused_bn).values())
