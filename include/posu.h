@@ -272,7 +272,8 @@ int posu_bottleneck_tail_stream_next_fwd(int dtype, const void* t1, const void* 
  * packing.pack_down_tail_stream(conv2 pack, dual pack[, next conv1 pack]). */
 /* (ABI 16) The LAST identity block of a layer chained with the NEXT layer's first conv1 + BN1 + ReLU
  * (1x1 / stride 1 over y, C -> Pn = 2 P at this map size: layer2 / 3 / 4 block 0's conv1,
- * lib/models/pose_resnet.py:79-81), split fp16 at 256x256 only; Pn = P is
+ * lib/models/pose_resnet.py:79-81) at 256x256: the split fp16 tails of layers 1-3 and the bf16 / fp16 tails of
+ * layers 2-3 (their 4-m-tile variants: layer2 2-row, layer3 4-row tiles); Pn = P is
  * posu_bottleneck_tail_stream_next_fwd.  Each y chunk's next-conv1 k-steps run twice, once per half
  * of the Pn outputs (two accumulator sets); t1n [N, H, W, Pn] (logical), s1n / b1n [Pn] f32, wstream =
  * packing.pack_tail_stream(conv2, conv3, next conv1 [Pn][C']).  Bit-identical to the tail followed by

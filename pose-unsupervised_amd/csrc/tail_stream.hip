@@ -122,8 +122,9 @@ struct TailCfg {
   // (round 5: with x / y / t1n behind buffer descriptors the chained variants fit the plain tail's
   // 4-deep stream and two fragment sets without spills -- network 2.3529 / 2.3514 vs 2.3991 / 2.3966
   // ms with round 4's 1-deep / one set (layer2) and 2-deep / two sets (layer3), profiles/r05)
-  static constexpr int kDW = W == 24 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
-  static constexpr int kNB = W == 24 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
+  // (round 6: the chained W = 24 tail runs 2-row tiles, three m-tiles per wave: the plain tail's depths)
+  static constexpr int kDW = W == 24 && MT == 9 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
+  static constexpr int kNB = W == 24 && MT == 9 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
   // swizzle keys stay inside a pixel row: 16 chunks or more take (column & 15), the 8-chunk rows of
   // 64-channel 2-byte images (layer1 at 384x384) (column & 7)
@@ -168,7 +169,7 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 // chains it too: two accumulator sets, each over the same y chunk image
 template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false,
           int NX = 1>
-__global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
+__global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 || NX == 2 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   // split fp16 (POSU_F16X3, round 6): every pixel row holds [hi 32 | lo 32] per 32 channels, i.e. the
   // kernel is the same GEMM over twice the K, whose k-step pairs (2c, 2c + 1) -- the hi and the lo
@@ -549,13 +550,14 @@ void launch_tail_split(const TailSGeom& g, hipStream_t s) {
                      dim3(static_cast<unsigned>(g.N * (g.H / ROWS))), dim3(NW * 64), 0, s, g);
 }
 
-template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false>
+template <int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false, int NX = 1>
 void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
   const dim3 grid(static_cast<unsigned>(g.N * (g.H / ROWS)));
   if (dtype == POSU_BF16)
-    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<uint16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN, NX>), grid, dim3(NW * 64), 0, s,
+                       g);
   else
-    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN>), grid, dim3(NW * 64), 0, s, g);
+    hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN, NX>), grid, dim3(NW * 64), 0, s, g);
 }
 
 // layer3's 4-row tiles below this many 8-row workgroups (A/B builds: 0 never, a large value always)
@@ -608,8 +610,8 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
                what + ": built for layer1's first Bottleneck (x 64 -> y 256 channels, planes 64) at W = 64 in split "
                       "fp16 and at W = 96 in BF16 / F16");
   const int cm = spl ? 2 : 1;   // stored halves per logical channel
-  POSU_REQUIRE(nx == 1 || (nx == 2 && spl && next && !down && (l1 || l2 || l3)),
-               what + ": a next conv1 of 2 P outputs is chained by the split 256x256 identity tails only");
+  POSU_REQUIRE(nx == 1 || (nx == 2 && next && !down && (l2 || l3 || (spl && l1))),
+               what + ": a next conv1 of 2 P outputs is chained by the 256x256 identity tails only (layer1: split)");
   {
     // the stream the selected variant reads: NCQ channel groups x (9 KT conv2 + NC KT conv3 [+ NC KT
     // next conv1]) k-steps x 2 n-tiles x 1 KB (packing.pack_tail_stream); split: KT = 2 P / 32
@@ -618,12 +620,15 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     POSU_REQUIRE(wstream_bytes == need, what + ": wstream holds " + std::to_string(wstream_bytes) + " bytes, the " +
                                             (next ? "chained" : "plain") + " tail reads " + std::to_string(need));
   }
-  POSU_REQUIRE(!(l3w && next), what + ": no chained variant at W = 24 (run the tail and a conv1 launch)");
+  // (W = 24 chained: 2-row tiles, round 6; the plain W = 24 tail keeps 6-row tiles)
   // layer3 at W = 16: 8-row tiles (128 px, 8 m-tiles per wave) while they give every CU a
   // workgroup, else 4-row tiles (64 px, 4 m-tiles per wave): at batch 64 (BASELINE configs[1]) the
   // 8-row grid left half the CUs idle (128 workgroups)
   const bool l3h = l3 && N > 0 && H % 4 == 0 && static_cast<long long>(N) * (H / 8) < POSU_TS_L3_SMALL_GRID;
-  const int rows = spl ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? 6 : (l2w || l1w) ? 2 : kL2Rows;
+  // (nx = 2, bf16 / fp16: the 4-m-tile variants -- layer2 2-row, layer3 4-row tiles -- whose second
+  // accumulator set fits twice)
+  const int rows = spl ? (l3 ? 4 : 2) : nx == 2 ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? (next ? 2 : 6) :
+                   (l2w || l1w) ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
   POSU_REQUIRE(!down || x != t1n, what + ": t1n must not alias x");
@@ -668,6 +673,9 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
       if (next) launch_tail_split<16, 256, 1024, 4, 8, true, 4>(g, s);
       else launch_tail_split<16, 256, 1024, 4, 8, false, 4>(g, s);
     }
+  } else if (nx == 2) {   // a layer's last tail chaining the next layer's first conv1 (2 P outputs)
+    if (l3) launch_tail<16, 256, 1024, 4, 8, true, 4, false, 2>(dtype, g, s);
+    else launch_tail<32, 128, 512, 2, 4, true, 4, false, 2>(dtype, g, s);
   } else if (l1w) {   // 2 rows x 96 px = 192 px, 6 m-tiles per wave (one image row), 4 waves
     if (down) {
       if (next) launch_tail<96, 64, 256, 2, 4, true, 6, true>(dtype, g, s);
@@ -682,8 +690,9 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   } else if (l3) {
     if (next) launch_tail<16, 256, 1024, 8, 8, true>(dtype, g, s);
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
-  } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave
-    launch_tail<24, 256, 1024, 6, 8, false, 9>(dtype, g, s);
+  } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave (chained: 2 rows x 24 px, 3 m-tiles)
+    if (next) launch_tail<24, 256, 1024, 2, 8, true, 3>(dtype, g, s);
+    else launch_tail<24, 256, 1024, 6, 8, false, 9>(dtype, g, s);
   } else if (l2w) {   // 2 rows x 48 px = 96 px, 6 m-tiles per wave, 4 waves
     if (next) launch_tail<48, 128, 512, 2, 4, true, 6>(dtype, g, s);
     else launch_tail<48, 128, 512, 2, 4, false, 6>(dtype, g, s);

@@ -264,6 +264,11 @@ S2_CHAIN = True
 # the identity Bottlenecks at 384x384 (R152, BASELINE configs[4]) as conv1 + the streamed tail
 # (round 5): layer3 at W = 24 (not chained), layer2 at W = 48 (chained)
 TAIL_W24 = True
+# layer3 at W = 24: the identity tails chained like the 256x256 ones (2-row tiles, three m-tiles per wave,
+# round 6).  Off: measured even with each conv1 a launch of its own after the plain 6-row tail (configs[4]
+# 9.82 / 10.01 vs 9.97 / 9.97 k frames/s, profiles/r06/w24_chain_ab_r6l.txt) -- the 2-row tiles' weight
+# stream (a third of the MFMAs per fragment) costs what the conv1 launches cost
+TAIL_W24_CHAIN = False
 # the split dtype's identity Bottlenecks of layer1 / layer2 / layer3 as conv1 + the streamed tail
 # (chained), layer1's first block as conv1 + the down tail (chained), round 6; False: the conv launches
 SPLIT_TAILS = True
@@ -393,9 +398,11 @@ class _Block:
         return None
 
     def link_layer(self, first):
-        """Split fp16: chain this last identity block's tail with the next layer's first block's conv1
-        (1x1 / stride 1, C -> 2 P: posu_bottleneck_tail_stream_chain_fwd)."""
-        if not (self.code == ops.F16X3 and (self.l1 or self.l2 or self.l3) and first.dual is not None):
+        """Chain this last identity block's tail with the next layer's first block's conv1 (1x1 / stride 1,
+        C -> 2 P: posu_bottleneck_tail_stream_chain_fwd): split fp16 layers 1-3, bf16 / fp16 layers 2-3."""
+        tails = (self.l1 or self.l2 or self.l3) if self.code == ops.F16X3 else (
+            self.code in (ops.BF16, ops.F16) and (self.l2 or self.l3))
+        if not (tails and first.dual is not None):
             return
         c1n = first.convs[0]
         planes = self.convs[1].cout
@@ -429,11 +436,12 @@ class _Block:
         c1, c2, c3 = self.convs
         if t1 is None:
             t1 = c1(x, code)
-        if chain_out and self.xchain is not None and CHAINED_TAILS and CHAIN_LAYERS:
+        if chain_out and self.xchain is not None and CHAINED_TAILS and CHAIN_LAYERS and \
+                kind in (('l1', 'l2', 'l3') if self.code == ops.F16X3 else ('l2', 'l3')):
             n1 = self.xchain
             return ops.bottleneck_tail_stream_chain_nhwc(t1, x, self.wsx, c2.scale, c2.shift, c3.scale, c3.shift,
                                                          n1.scale, n1.shift, code, out=out)
-        if self.chain is not None and CHAINED_TAILS and kind != 'l3w':   # (no chained tail at W = 24)
+        if self.chain is not None and CHAINED_TAILS and (kind != 'l3w' or TAIL_W24_CHAIN):
             n1 = self.chain
             return ops.bottleneck_tail_stream_next_nhwc(t1, x, self.wsn, c2.scale, c2.shift, c3.scale, c3.shift,
                                                         n1.scale, n1.shift, code, out=out)

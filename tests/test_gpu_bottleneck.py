@@ -415,13 +415,15 @@ def test_plan_strided_tail_is_bit_identical_to_two_launches(cuda, precision):
 @pytest.mark.parametrize('code', [BF16, F16])
 @pytest.mark.parametrize('layer,n,h', [('layer3', 2, 16), ('layer3', 1, 8), ('layer3', 3, 24), ('layer3', 128, 16),
                                        ('layer2', 2, 32), ('layer2', 1, 4), ('layer2', 3, 12), ('layer2', 128, 32),
-                                       ('layer2w', 2, 48), ('layer2w', 1, 2), ('layer2w', 3, 10), ('layer2w', 64, 48)])
+                                       ('layer2w', 2, 48), ('layer2w', 1, 2), ('layer2w', 3, 10), ('layer2w', 64, 48),
+                                       ('layer3w', 2, 24), ('layer3w', 1, 6), ('layer3w', 3, 18), ('layer3w', 64, 24)])
 def test_chained_tail_matches_tail_and_next_conv1(cuda, code, layer, n, h):
     """Chained streamed tail (posu_bottleneck_tail_stream_next_fwd): block i's tail computing block
     i+1's conv1 + BN1 + ReLU over its output y.  y and t1n are bit-identical to the plain tail
     followed by a conv launch of the next conv1 over y (the same K order per accumulator); both
     outputs start as NaN sentinels, so a store that never lands fails."""
-    c, p, w = {'layer3': (1024, 256, 16), 'layer2': (512, 128, 32), 'layer2w': (512, 128, 48)}[layer]
+    c, p, w = {'layer3': (1024, 256, 16), 'layer2': (512, 128, 32), 'layer2w': (512, 128, 48),
+               'layer3w': (1024, 256, 24)}[layer]
     g = torch.Generator().manual_seed(97 + h + n)
     w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
     w1n = torch.randn(p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
@@ -469,9 +471,11 @@ def test_plan_with_chained_tails_matches_unchained_plan(cuda, precision):
     net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
     net = net.to(cuda).eval()
     plan = net.plan(cuda)
-    # layer2: the strided tail chains block 1's conv1 too (round 4)
+    # layer2: the strided tail chains block 1's conv1 too (round 4); the last tails of layers 2-3 chain
+    # the next layer's first conv1 (CHAIN_LAYERS, round 6)
     assert [b.chain is not None for b in plan.layers[1]] == [True, True, True, False]
     assert [b.chain is not None for b in plan.layers[2]] == [False, True, True, True, True, False]
+    assert [layer[-1].xchain is not None for layer in plan.layers] == [False, True, True, False]
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=13)]
     saved = P.CHAINED_TAILS
     try:
@@ -688,3 +692,33 @@ def test_w96_layer1_tails_match_conv_launches(cuda, code, n, h):
     res = [diff(y, two), diff(yc, two), diff(t1n, t1n_ref), diff(yd, dref), diff(ydc, dref), diff(t1nd, t1nd_ref)]
     print('W = 96 tails n=%d h=%d: y / chained y / t1n / down y / chained down y / its t1n differing %s' % (n, h, res))
     assert res == [0] * 6
+
+
+@pytest.mark.parametrize('code', [BF16, F16])
+@pytest.mark.parametrize('layer,n,h', [('layer2', 2, 32), ('layer2', 3, 12), ('layer2', 128, 32),
+                                       ('layer3', 2, 16), ('layer3', 1, 8), ('layer3', 128, 16)])
+def test_layer_chained_tail_matches_tail_and_next_layer_conv1(cuda, code, layer, n, h):
+    """A layer's last identity tail chaining the NEXT layer's first conv1 (C -> 2 P,
+    posu_bottleneck_tail_stream_chain_fwd, round 6) in bf16 / fp16: y and the 2 P-channel t1n
+    bit-identical to the plain tail + a conv launch of that conv1 over y; NaN-sentinel outputs."""
+    c, p, w = {'layer3': (1024, 256, 16), 'layer2': (512, 128, 32)}[layer]
+    g = torch.Generator().manual_seed(211 + h + n)
+    w1, bn1, w2, bn2, w3, bn3 = _block_params(g, c=c, p=p)
+    w1x = torch.randn(2 * p, c, 1, 1, generator=g) * (2.0 / c) ** 0.5
+    bn1x = (torch.rand(2 * p, generator=g) + 0.5, torch.randn(2 * p, generator=g) * 0.1)
+    dt = ops.torch_dtype(code)
+    bk = ops.conv_bk(code)
+    xd = torch.randn(n, h, w, c, generator=g).to(cuda, dt)
+    p1, p2, p3, p1x = (packing.pack_conv_weight(t.to(cuda), t.shape[1], bk, dt) for t in (w1, w2, w3, w1x))
+    s = [t.to(cuda) for t in (bn1[0], bn1[1], bn2[0], bn2[1], bn3[0], bn3[1], bn1x[0], bn1x[1])]
+    t1 = ops.conv2d_nhwc(xd, p1, p, 1, 1, 1, 0, s[0], s[1], None, True, code)
+    y_ref = ops.bottleneck_tail_stream_nhwc(t1, xd, packing.pack_tail_stream(p2, p3), s[2], s[3], s[4], s[5], code)
+    t1x_ref = ops.conv2d_nhwc(y_ref, p1x, 2 * p, 1, 1, 1, 0, s[6], s[7], None, True, code)
+    y, t1x = ops.bottleneck_tail_stream_chain_nhwc(t1, xd, packing.pack_tail_stream(p2, p3, p1x), s[2], s[3], s[4],
+                                                   s[5], s[6], s[7], code, out=_sentinel(xd),
+                                                   t1n=_sentinel(t1, (n, h, w, 2 * p)))
+    torch.cuda.synchronize()
+    dy = int((y.view(torch.int16) != y_ref.view(torch.int16)).sum())
+    dt1 = int((t1x.view(torch.int16) != t1x_ref.view(torch.int16)).sum())
+    print('%s layer-chained tail n=%d h=%d: y differing %d, t1n (2 P) %d' % (layer, n, h, dy, dt1))
+    assert dy == 0 and dt1 == 0
