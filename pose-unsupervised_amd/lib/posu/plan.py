@@ -279,6 +279,10 @@ TAIL_W96 = True
 # split fp16: the last identity block of layers 1-3 chains the NEXT layer's first conv1 too (C -> 2 P,
 # posu_bottleneck_tail_stream_chain_fwd, round 6), so that block's conv1 is no launch of its own
 CHAIN_LAYERS = True
+# the same layer chain in bf16 / fp16 plans (layers 2-3, NX = 2 tails): bit-identical, but measured
+# 0.6 % slower on the headline (call r6m: 2.279 vs 2.264 ms; the 2-row NX = 2 tiles halve the layer's
+# last tail's rows per workgroup, which costs what the saved conv1 launch gains), so off
+CHAIN_LAYERS_2B = False
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -399,9 +403,10 @@ class _Block:
 
     def link_layer(self, first):
         """Chain this last identity block's tail with the next layer's first block's conv1 (1x1 / stride 1,
-        C -> 2 P: posu_bottleneck_tail_stream_chain_fwd): split fp16 layers 1-3, bf16 / fp16 layers 2-3."""
+        C -> 2 P: posu_bottleneck_tail_stream_chain_fwd): split fp16 layers 1-3, bf16 / fp16 layers 2-3
+        (CHAIN_LAYERS_2B)."""
         tails = (self.l1 or self.l2 or self.l3) if self.code == ops.F16X3 else (
-            self.code in (ops.BF16, ops.F16) and (self.l2 or self.l3))
+            CHAIN_LAYERS_2B and self.code in (ops.BF16, ops.F16) and (self.l2 or self.l3))
         if not (tails and first.dual is not None):
             return
         c1n = first.convs[0]

@@ -470,9 +470,14 @@ def test_plan_with_chained_tails_matches_unchained_plan(cuda, precision):
     net = get_pose_net(syn.make_cfg(num_layers=50, image_size=256), is_train=False, precision=precision)
     net.load_state_dict(syn.synthetic_state_dict(net.state_dict(), seed=0, bn_stats=syn.load_bn_stats(50, 256)))
     net = net.to(cuda).eval()
-    plan = net.plan(cuda)
+    saved2b = P.CHAIN_LAYERS_2B
+    P.CHAIN_LAYERS_2B = True   # (off in the benched plans: measured neutral-to-slower, plan.py)
+    try:
+        plan = net.plan(cuda)
+    finally:
+        P.CHAIN_LAYERS_2B = saved2b
     # layer2: the strided tail chains block 1's conv1 too (round 4); the last tails of layers 2-3 chain
-    # the next layer's first conv1 (CHAIN_LAYERS, round 6)
+    # the next layer's first conv1 (CHAIN_LAYERS + CHAIN_LAYERS_2B, round 6)
     assert [b.chain is not None for b in plan.layers[1]] == [True, True, True, False]
     assert [b.chain is not None for b in plan.layers[2]] == [False, True, True, True, True, False]
     assert [layer[-1].xchain is not None for layer in plan.layers] == [False, True, True, False]
