@@ -17,8 +17,20 @@
 namespace posu {
 namespace {
 
+// pixels in flight per thread in the partial passes (the sums do not depend on them: each thread
+// adds its pixels in order).  The launches are ~256 blocks of 4 waves, one wave per SIMD, so the
+// loads in flight per wave set the bandwidth (round 6: 4 / 8 -> 16)
 #ifndef POSU_BN_U1
-#define POSU_BN_U1 4    // pixels in flight per thread in the backward partial pass
+#define POSU_BN_U1 4    // the backward partial pass (z, gy and the mask per pixel)
+#endif
+#ifndef POSU_BN_U0
+#define POSU_BN_U0 8    // the forward statistics (z per pixel)
+#endif
+#ifndef POSU_BN_NBT
+#define POSU_BN_NBT 256  // partial-sum blocks per launch (target)
+#endif
+#ifndef POSU_BN_RED1
+#define POSU_BN_RED1 0   // 1: the block reduction through one [256][E] f64 array, sums then squares
 #endif
 #ifndef POSU_BN_FIN2
 #define POSU_BN_FIN2 1  // the second finalize form (block per 16 channels, lane sums met in LDS)
@@ -44,7 +56,7 @@ RedShape red_shape(int Pseg, int C, int E, int nseg) {
   r.CG = (r.CPR + r.CB - 1) / r.CB;
   // <= 64 partial blocks per view of 4 (one load round per finalize lane); per training step
   // measured 128 / 256 / 512 / 1024 total blocks: 22.61 / 21.93 / 22.09 / 22.43 ms
-  int nb = std::max(1, 256 / (r.CG * nseg));
+  int nb = std::max(1, POSU_BN_NBT / (r.CG * nseg));
   nb = std::min(nb, kMaxNB);
   nb = std::min(nb, std::max(1, Pseg / r.PL));
   // f64 partials of wide, short layers (layer4: 2048 channels x 2048 pixels per view) stay
@@ -84,7 +96,7 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
                                                          RedShape rs, double* __restrict__ part,
                                                          float* __restrict__ kout, const uint8_t* __restrict__ ym) {
   constexpr int E = Vec<T>::E;
-  __shared__ double red[2][256][E];
+  __shared__ double red[POSU_BN_RED1 ? 1 : 2][256][E];
   const int tid = threadIdx.x;
   const int pl = tid / rs.CB, cb = tid - pl * rs.CB;
   const int ch = blockIdx.y * rs.CB + cb;
@@ -157,9 +169,11 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
         }
       }
     };
-    // U pixels per step with all their loads issued first (memory-level parallelism)
-    constexpr int U = MODE == 0 ? 8 : POSU_BN_U1;
+    // U pixels per step with all their loads issued first (memory-level parallelism); the ReLU
+    // source's loads behind wave-uniform branches (a y or mask load only when that is the source)
+    constexpr int U = MODE == 0 ? POSU_BN_U0 : POSU_BN_U1;
     const uint4 zero = make_uint4(0, 0, 0, 0);
+    const bool use_y = MODE == 1 && y && !ym, use_m = MODE == 1 && ym;
     int p = pbeg + pl;
     for (; p + (U - 1) * rs.PL < pend; p += U * rs.PL) {
       uint4 zq[U], gq[U], yq[U];
@@ -169,8 +183,15 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
         const size_t off = sbase + static_cast<size_t>(p + u * rs.PL) * C;
         zq[u] = *reinterpret_cast<const uint4*>(z + off);
         gq[u] = MODE == 1 ? *reinterpret_cast<const uint4*>(gy + off) : zero;
-        yq[u] = ld16_if(MODE == 1 && y && !ym, y, z, off);
-        mq[u] = ld8_if(MODE == 1 && ym, ym, z, off / E);
+        yq[u] = zero;
+        mq[u] = 0u;
+      }
+      if (use_y) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) yq[u] = *reinterpret_cast<const uint4*>(y + sbase + static_cast<size_t>(p + u * rs.PL) * C);
+      } else if (use_m) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) mq[u] = ym[(sbase + static_cast<size_t>(p + u * rs.PL) * C) / E];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) acc(zq[u], gq[u], yq[u], mq[u]);
@@ -181,10 +202,35 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
           ld16_if(MODE == 1 && y && !ym, y, z, off), ld8_if(MODE == 1 && ym, ym, z, off / E));
     }
   }
+  double* dst = part + (static_cast<size_t>(seg) * rs.NB + blk) * 2 * C;
+  if constexpr (POSU_BN_RED1) {
+    // the same tree, one quantity at a time through a 16 KB array (the partial pass shares CUs
+    // with the weight-gradient kernels' 128 KB of LDS in the backward)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+#pragma unroll
+      for (int e = 0; e < E; ++e) red[0][tid][e] = k ? b[e] : a[e];
+      __syncthreads();
+      for (int s = rs.PL / 2; s > 0; s >>= 1) {
+        if (pl < s) {
+          const int o = tid + s * rs.CB;
+#pragma unroll
+          for (int e = 0; e < E; ++e) red[0][tid][e] += red[0][o][e];
+        }
+        __syncthreads();
+      }
+      if (pl == 0 && active) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) dst[k * C + ch * E + e] = red[0][tid][e];
+      }
+      __syncthreads();
+    }
+    return;
+  }
 #pragma unroll
   for (int e = 0; e < E; ++e) {
     red[0][tid][e] = a[e];
-    red[1][tid][e] = b[e];
+    red[POSU_BN_RED1 ? 0 : 1][tid][e] = b[e];
   }
   __syncthreads();
   for (int s = rs.PL / 2; s > 0; s >>= 1) {
@@ -193,17 +239,16 @@ __global__ __launch_bounds__(256) void bn_partial_kernel(const T* __restrict__ z
 #pragma unroll
       for (int e = 0; e < E; ++e) {
         red[0][tid][e] += red[0][o][e];
-        red[1][tid][e] += red[1][o][e];
+        red[POSU_BN_RED1 ? 0 : 1][tid][e] += red[POSU_BN_RED1 ? 0 : 1][o][e];
       }
     }
     __syncthreads();
   }
   if (pl == 0 && active) {
-    double* dst = part + (static_cast<size_t>(seg) * rs.NB + blk) * 2 * C;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       dst[ch * E + e] = red[0][tid][e];
-      dst[C + ch * E + e] = red[1][tid][e];
+      dst[C + ch * E + e] = red[POSU_BN_RED1 ? 0 : 1][tid][e];
     }
   }
 }

@@ -58,12 +58,15 @@ def main():
         nb = z.numel() * 2
         mean, rstd, sc, sh = T.bn_train_fwd(z, NSEG, gamma, beta, 1e-5, 0.1)
         y = T.bn_apply(z, NSEG, sc, sh, r, True)
+        _, mask = T.bn_apply_mask(z, NSEG, sc, sh, r)
         out = torch.empty_like(z)
         cases = [
             ('stats', lambda: T.bn_train_fwd(z, NSEG, gamma, beta, 1e-5, 0.1), 1),
             ('apply', lambda: T.bn_apply(z, NSEG, sc, sh, None, True, out=out), 2),
             ('apply+res', lambda: T.bn_apply(z, NSEG, sc, sh, r, True, out=out), 3),
             ('bwd(y,gres)', lambda: T.bn_train_bwd(gy, y, z, NSEG, mean, rstd, gamma, want_gres=True), 8),
+            ('bwd(mask,gres)', lambda: T.bn_train_bwd(gy, None, z, NSEG, mean, rstd, gamma, want_gres=True,
+                                                      mask=mask), 6),
             ('bwd(relu_from)', lambda: T.bn_train_bwd(gy, None, z, NSEG, mean, rstd, gamma, relu_from=(sc, sh)), 5),
         ]
         for name, fn, passes in cases:

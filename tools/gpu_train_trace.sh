@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r3q
+O=${1:-gpurun_out/r3q}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$O/train" -o run -- \
