@@ -47,6 +47,11 @@ PACK_BESIDE_STEM = True
 # round 5: a first block's downsample unit (conv + BN statistics + apply) runs on the side stream
 # beside its conv1 / conv2 units in the forward (the side stream is idle until the backward)
 DOWN_BESIDE = True
+# round 6: in the backward, a first block's downsample unit takes the block output's gradient and the
+# residual unit's ReLU mask itself (no g' = gy * mask tensor written for it) and runs its BatchNorm
+# backward + weight gradient on a third stream beside the main branch's units; only its data gradient
+# (accumulated into the main branch's) joins the main stream
+DOWN_BWD_BESIDE = True
 # round 5: the data-gradient convolutions on autotuned tiles (posu_conv2d_dgrad_tile, ABI 15), like the
 # forward ones (_conv_tuned); the in-place 1x1 / stride-2 ones keep the heuristic (a tuning trial
 # would accumulate into its output more than once)
@@ -184,13 +189,26 @@ class _ConvBN:
         y, idx = T.bn_relu_maxpool(z, nseg, sc, sh)
         return y, (x, z, None, mean, rstd, sc, sh, False, None), idx
 
-    def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None,
-                 inplace=False):
+    def relu_gate(self, saved):
+        """The ReLU mask of this (residual, ReLU) unit's output as bn_train_bwd takes it: (y, bits)."""
+        x, z, y, mean, rstd, sc, sh, has_res, mask = saved
+        if not (self.relu and has_res):
+            raise RuntimeError('relu_gate: a residual unit with ReLU only')
+        return (y if mask is None else None), mask
+
+    def backward_bn(self, gy, saved, nseg, code, grads, want_gres=False, gate=None):
+        """BatchNorm backward and the weight gradient: -> (dz, gres).  gate = another unit's
+        relu_gate(): gy is gated by that unit's ReLU mask first (the downsample unit of a first block,
+        whose gradient is the block output's gated by the residual unit's ReLU)."""
         x, z, y, mean, rstd, sc, sh, has_res, mask = saved
         # ReLU mask: the forward's bits, or y after a residual add, else recomputed from z (one
         # tensor read less)
         mask_y = y if (self.relu and has_res and mask is None) else None
         relu_from = (sc, sh) if (self.relu and not has_res) else None
+        if gate is not None:
+            if self.relu:
+                raise RuntimeError('a gated unit has no ReLU of its own')
+            mask_y, mask = gate
         dz, gres, dgam, dbet = T.bn_train_bwd(gy, mask_y, z, nseg, mean, rstd, self.bn.weight, want_gres=want_gres,
                                               relu_from=relu_from, mask=mask)
         if isinstance(x, (list, tuple)):   # the stem from the NCHW views (stem_conv): its own kernel
@@ -200,6 +218,15 @@ class _ConvBN:
                                                                  self.pad, code), dz, x)
         grads[self.bn.weight] = dgam
         grads[self.bn.bias] = dbet
+        return dz, gres
+
+    def backward(self, gy, saved, nseg, code, grads, want_gres=False, need_dx=True, dx_residual=None,
+                 inplace=False, gate=None, dz=None):
+        """-> (dx, gres); dz: the BatchNorm backward already run (backward_bn), only the data gradient."""
+        gres = None
+        if dz is None:
+            dz, gres = self.backward_bn(gy, saved, nseg, code, grads, want_gres=want_gres, gate=gate)
+        x = saved[0]
         dx = None
         if need_dx and getattr(self, 'wdc', None) is not None and dx_residual is None and x.shape[1] % 2 == 0 \
                 and x.shape[2] % 2 == 0:
@@ -261,9 +288,30 @@ class _Block:
         saved.append(s)
         return y, (saved, sd)
 
-    def backward(self, gy, saved, nseg, code, grads):
+    def backward(self, gy, saved, nseg, code, grads, beside=None):
+        """beside: a stream for the downsample unit's BatchNorm backward + weight gradient
+        (DOWN_BWD_BESIDE), or None."""
         su, sd = saved
-        g, gres = self.units[-1].backward(gy, su[-1], nseg, code, grads, want_gres=True)
+        u3 = self.units[-1]
+        gated = self.down is not None and DOWN_BWD_BESIDE and u3.relu and su[-1][7]
+        dz_d = joined = None
+        if gated and beside is not None:
+            # the downsample's BatchNorm backward from gy and the residual unit's ReLU mask, beside the
+            # main branch; gy, the mask and the saved tensors are read there (record_stream), its
+            # outputs are used on the main stream after `joined`
+            main = torch.cuda.current_stream(gy.device)
+            beside.wait_stream(main)
+            gate = u3.relu_gate(su[-1])
+            with torch.cuda.stream(beside):
+                dz_d, _ = self.down.backward_bn(gy, sd, nseg, code, grads, gate=gate)
+            joined = torch.cuda.Event()
+            joined.record(beside)
+            for t in (gy,) + tuple(t for t in gate if t is not None) + tuple(t for t in sd if torch.is_tensor(t)):
+                t.record_stream(beside)
+            for t in (dz_d, grads[self.down.bn.weight], grads[self.down.bn.bias], grads.get(self.down.conv.weight)):
+                if t is not None:
+                    t.record_stream(main)
+        g, gres = u3.backward(gy, su[-1], nseg, code, grads, want_gres=not gated)
         for u, s in zip(reversed(self.units[:-1]), reversed(su[:-1])):
             if u is self.units[0]:
                 break
@@ -275,7 +323,14 @@ class _Block:
         dx_main, _ = self.units[0].backward(g, su[0], nseg, code, grads)
         # dx_main is this block's own temporary: the downsample's 1x1 / stride-2 data gradient
         # accumulates into it in place
-        dx, _ = self.down.backward(gres, sd, nseg, code, grads, dx_residual=dx_main, inplace=True)
+        if joined is not None:
+            torch.cuda.current_stream(gy.device).wait_event(joined)
+            dx, _ = self.down.backward(None, sd, nseg, code, grads, dx_residual=dx_main, inplace=True, dz=dz_d)
+        elif gated:
+            dx, _ = self.down.backward(gy, sd, nseg, code, grads, dx_residual=dx_main, inplace=True,
+                                       gate=u3.relu_gate(su[-1]))
+        else:
+            dx, _ = self.down.backward(gres, sd, nseg, code, grads, dx_residual=dx_main, inplace=True)
         return dx
 
 
@@ -484,7 +539,7 @@ class TrainPlan:
         blocks = self.layers[i]
         sblocks = saved['blocks'] if i == 0 else saved
         for b, sb in zip(reversed(blocks), reversed(sblocks)):
-            g = b.backward(g, sb, nseg, code, grads)
+            g = b.backward(g, sb, nseg, code, grads, self._down_bwd_stream(g))
         if i == 0:
             if 'pool_idx' in saved:
                 g = T.maxpool3x3s2_bwd_idx(saved['pool_idx'], g, saved['stem'][1].shape[1:3])
@@ -493,6 +548,15 @@ class TrainPlan:
             self.stem.backward(g, saved['stem'], nseg, code, grads, need_dx=False)
             g = None
         return g, grads.close()
+
+    def _down_bwd_stream(self, g):
+        """The third stream for DOWN_BWD_BESIDE (created on first use), or None."""
+        from .plan import _Tuner
+        if not (DOWN_BWD_BESIDE and SIDE_STREAM_WGRAD) or _Tuner.active:
+            return None
+        if getattr(self, 'beside', None) is None:
+            self.beside = torch.cuda.Stream(g.device)
+        return self.beside
 
     def _down_side(self, x):
         """The side stream for DOWN_BESIDE (created on first use), or None."""
