@@ -123,8 +123,8 @@ struct TailCfg {
   // 4-deep stream and two fragment sets without spills -- network 2.3529 / 2.3514 vs 2.3991 / 2.3966
   // ms with round 4's 1-deep / one set (layer2) and 2-deep / two sets (layer3), profiles/r05)
   // (round 6: the chained W = 24 tail runs 2-row tiles, three m-tiles per wave: the plain tail's depths)
-  static constexpr int kDW = W == 24 && MT == 9 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
-  static constexpr int kNB = W == 24 && MT == 9 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
+  static constexpr int kDW = W == 24 && MT >= 6 ? 2 : !NEXT ? POSU_TS_KD : POSU_TS_KD_NEXT ? POSU_TS_KD_NEXT : 4;
+  static constexpr int kNB = W == 24 && MT >= 6 ? 1 : !NEXT ? 2 : POSU_TS_NB_NEXT ? POSU_TS_NB_NEXT : 2;
   static constexpr int kD = kDW < kKT ? kDW : kKT;
   // swizzle keys stay inside a pixel row: 16 chunks or more take (column & 15), the 8-chunk rows of
   // 64-channel 2-byte images (layer1 at 384x384) (column & 7)
@@ -169,7 +169,7 @@ __device__ __forceinline__ int wkey(int wr, int wc) {
 // chains it too: two accumulator sets, each over the same y chunk image
 template <typename T, int W, int P, int C, int ROWS, int NW, bool NEXT = false, int MT = 8, bool DOWN = false,
           int NX = 1>
-__global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 || NX == 2 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
+__global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : W == 24 && MT == 6 ? 32 : Op<T>::SPLIT || MT == 8 || W == 48 || W == 96 || NX == 2 ? 8 : POSU_TS_MT4_WAVES) / NW) void tail_stream_kernel(TailSGeom g) {
   using O = Op<T>;
   // split fp16 (POSU_F16X3, round 6): every pixel row holds [hi 32 | lo 32] per 32 channels, i.e. the
   // kernel is the same GEMM over twice the K, whose k-step pairs (2c, 2c + 1) -- the hi and the lo
@@ -274,6 +274,7 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
     }
   };
   const int cpair = 16 * (q & 1) + 8 * (q >> 1);
+  constexpr bool kLateRes = NEXT || (W == 24 && MT == 6);   // residual loads after a chunk's MFMAs
   // relu(v * sc + sh (+ r)) over this lane's 8 values; the multiply-add as an explicit fma, the conv
   // epilogue's contraction: left to the compiler, the split variants' epilogues were vectorised into
   // v_mul + v_pk_add (two roundings) and differed from the conv launches in the last f32 bit
@@ -472,8 +473,9 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
     block(acc, 9 + K::kBlk3 * nc, 0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
     // DOWN: the downsample's K slice over the block input into the same accumulators
     if constexpr (DOWN) block(acc, 9 + K::kBlk3 * nc + 1, K::kX0, 16 * MT * pg + r16, r16, [&](int i) { return 16 * i; });
-    // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers)
-    if constexpr (NEXT && !DOWN) res_load(nc, rv, rl);
+    // NEXT: the residual after the MFMAs (the next conv1's accumulators take its registers; so do
+    // the W = 24 4-row tiles' 128-register budget)
+    if constexpr (kLateRes && !DOWN) res_load(nc, rv, rl);
     float sc[8], sh[8];
     ld8(b3l + c0, sc);
     ld8(b3l + C + c0, sh);
@@ -516,7 +518,7 @@ __global__ __launch_bounds__(NW * 64, (DOWN && Op<T>::SPLIT ? 4 : Op<T>::SPLIT |
     // the chunk's residual, kKT k-steps ahead of its epilogue (the weight fragments consumed
     // meanwhile were loaded before it: the in-order vmcnt does not hold them back)
     uint4 rv[MT], rl[MT];
-    if constexpr (!NEXT && !DOWN) res_load(nc, rv, rl);
+    if constexpr (!kLateRes && !DOWN) res_load(nc, rv, rl);
     chunk(nc, rv, rl);
   }
   if constexpr (NEXT) {
@@ -560,6 +562,12 @@ void launch_tail(int dtype, const TailSGeom& g, hipStream_t s) {
     hipLaunchKernelGGL((tail_stream_kernel<f16_t, W, P, C, ROWS, NW, NEXT, MT, DOWN, NX>), grid, dim3(NW * 64), 0, s, g);
 }
 
+// layer3 at W = 24 (R152@384): the plain tail's rows per tile -- 6 (144 px, 9 m-tiles per wave, one
+// workgroup per CU) or 4 (96 px, 6 m-tiles per wave, 80 KB of LDS: two workgroups per CU, 128 registers
+// with the residual loaded after a chunk's MFMAs; measured slower: configs[4] 7.10 vs 6.71 ms, call r6s)
+#ifndef POSU_TS_L3W_ROWS
+#define POSU_TS_L3W_ROWS 6
+#endif
 // layer3's 4-row tiles below this many 8-row workgroups (A/B builds: 0 never, a large value always)
 #ifndef POSU_TS_L3_SMALL_GRID
 #define POSU_TS_L3_SMALL_GRID 256
@@ -627,7 +635,7 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
   const bool l3h = l3 && N > 0 && H % 4 == 0 && static_cast<long long>(N) * (H / 8) < POSU_TS_L3_SMALL_GRID;
   // (nx = 2, bf16 / fp16: the 4-m-tile variants -- layer2 2-row, layer3 4-row tiles -- whose second
   // accumulator set fits twice)
-  const int rows = spl ? (l3 ? 4 : 2) : nx == 2 ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? (next ? 2 : 6) :
+  const int rows = spl ? (l3 ? 4 : 2) : nx == 2 ? (l3 ? 4 : 2) : l3 ? (l3h ? 4 : 8) : l3w ? (next ? 2 : POSU_TS_L3W_ROWS) :
                    (l2w || l1w) ? 2 : kL2Rows;
   POSU_REQUIRE(N > 0 && H > 0 && H % rows == 0,
                what + ": H must be a positive multiple of " + std::to_string(rows) + " (the tile rows)");
@@ -692,7 +700,7 @@ int tail_stream_impl(const char* name, int dtype, const void* t1, const void* x,
     else launch_tail<16, 256, 1024, 8, 8>(dtype, g, s);
   } else if (l3w) {   // 6 rows x 24 px = 144 px, 9 m-tiles per wave (chained: 2 rows x 24 px, 3 m-tiles)
     if (next) launch_tail<24, 256, 1024, 2, 8, true, 3>(dtype, g, s);
-    else launch_tail<24, 256, 1024, 6, 8, false, 9>(dtype, g, s);
+    else launch_tail<24, 256, 1024, POSU_TS_L3W_ROWS, 8, false, POSU_TS_L3W_ROWS * 3 / 2>(dtype, g, s);
   } else if (l2w) {   // 2 rows x 48 px = 96 px, 6 m-tiles per wave, 4 waves
     if (next) launch_tail<48, 128, 512, 2, 4, true, 6>(dtype, g, s);
     else launch_tail<48, 128, 512, 2, 4, false, 6>(dtype, g, s);
