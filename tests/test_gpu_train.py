@@ -272,3 +272,30 @@ def test_train_step_r50_256_matches_oracle_autograd(cuda, precision, fund_weight
     for k, v in bufs.items():
         np.testing.assert_allclose(sd[k].cpu().numpy(), v.numpy(), atol=1e-4 if precision == 'fp32' else 2e-2,
                                    rtol=1e-4 if precision == 'fp32' else 2e-2, err_msg=k)
+
+
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+def test_downsample_backward_beside_is_bit_identical(cuda, golden, precision):
+    """train_plan.DOWN_BWD_BESIDE (round 6): the first blocks' downsample BatchNorm backward on a third
+    stream, reading the block output's gradient gated by the residual unit's ReLU mask instead of a
+    written g' tensor -- every parameter gradient and the running statistics exactly those of the
+    serial order."""
+    from posu import train_plan as TP
+    g = golden('train_step_r50_128.npz')
+    saved = TP.DOWN_BWD_BESIDE
+    out = {}
+    try:
+        for flag in (True, False):
+            TP.DOWN_BWD_BESIDE = flag
+            net, hm, _, mse, fund = _step(cuda, g, precision)
+            out[flag] = ({n: p.grad.detach().clone() for n, p in net.named_parameters()},
+                         {k: v.detach().clone() for k, v in net.state_dict().items()},
+                         torch.stack(hm).detach().clone())
+    finally:
+        TP.DOWN_BWD_BESIDE = saved
+    (ga, sa, ha), (gb, sb, hb) = out[True], out[False]
+    assert torch.equal(ha, hb)
+    for n in ga:
+        assert torch.equal(ga[n], gb[n]), n
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k

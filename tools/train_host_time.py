@@ -25,7 +25,11 @@ def main():
     dev = torch.device('cuda', 0)
     torch.cuda.set_device(dev)
     tb = bench.train_batch(args, dev)
-    opt = torch.optim.Adam(tb['net'].parameters(), lr=1e-3, fused=True)
+    if args.adam == 'posu':   # bench.py's default optimizer
+        from posu.optim import Adam as PosuAdam
+        opt = PosuAdam(tb['net'].parameters(), lr=1e-3)
+    else:
+        opt = torch.optim.Adam(tb['net'].parameters(), lr=1e-3, fused=args.adam == 'fused')
     from posu import plan as pplan
 
     def phases():
@@ -69,6 +73,17 @@ def main():
     print('free-running %d steps: host enqueue %.2f ms per step (median), wall %.2f ms per step, host ahead at '
           'the end by %.2f ms' % (args.steps, statistics.median(host), (t2 - t0) * 1e3 / args.steps,
                                   (t2 - t1) * 1e3))
+    if os.environ.get('POSU_HOST_PROFILE'):   # where the host time goes: cProfile over free-running steps
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(args.steps):
+            phases()
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats('tottime').print_stats(40)
+        pstats.Stats(pr).sort_stats('cumulative').print_stats(40)
 
 
 if __name__ == '__main__':
