@@ -89,8 +89,9 @@ def parse():
     ap.add_argument('--tune-file', default='',
                     help='per-layer tile table: loaded if it exists (no tuning trials run), else written '
                          'after autotuning -- profile runs load it so traces hold no trial launches')
-    ap.add_argument('--chunks', type=int, default=1,
-                    help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages')
+    ap.add_argument('--chunks', type=int, default=None,
+                    help='depth-first slices for the HBM-bound stem..layer2 / deconv2..head stages (default: the '
+                         'plan\'s per-dtype choice, plan.default_chunks(): 2 for fp16x3, else 1)')
     ap.add_argument('--cpu-baseline-seconds', type=float, default=12.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-mpjpe', action='store_true', help='skip the oracle-chain MPJPE check')
@@ -574,7 +575,7 @@ def time_pipeline(args, precision, dev, rank, steps, warmup, nbatch, autotune, d
     return {'elapsed': elapsed, 'net_ms': net_ms, 'geo_ms': geo_ms, 'X0': X.detach().cpu().numpy().copy(),
             'coords0': coords.detach().cpu().numpy().copy(), 'hm0': r.hm.detach().cpu().clone(),
             'use_graph': use_graph, 'tuned': tuned, 'loss0': float(loss), 'meta': r.meta, 'host': host,
-            'shard': shard}
+            'shard': shard, 'chunks': args.chunks if args.chunks is not None else plan.default_chunks()}
 
 
 def triangulation_parity_all_ranks(res, dev):
@@ -794,7 +795,7 @@ def infer_main(args):
         elp = pdist.max_over_ranks(rp['elapsed'], device=dev)
         par = {'precision': 'fp16x3', 'value': round(pdist.throughput(frames, args.parity_steps, world, elp), 2),
                'unit': 'frames/s', 'network_ms': round(rp['net_ms'], 4), 'steps': args.parity_steps,
-               'ms_per_step': round(elp / args.parity_steps * 1e3, 4)}
+               'ms_per_step': round(elp / args.parity_steps * 1e3, 4), 'chunks': rp['chunks']}
         if gf:
             tfp = gf * frames / (rp['net_ms'] * 1e-3) / 1e3
             # frac: the network's real flops against the dense fp16 peak; mfma_frac: the MFMA work
@@ -868,7 +869,7 @@ def infer_main(args):
                    'frames_per_gpu_step': frames, 'global_batch_frames': frames * world,
                    'parallelism': 'dp%d (the global batch of %d groups sharded by posu.dist.shard_groups, '
                                   'no data-path collective)' % (world, args.groups * world),
-                   'hipgraph': res['use_graph'], 'chunks': args.chunks, 'tiles': res['tuned'] or 'heuristic',
+                   'hipgraph': res['use_graph'], 'chunks': res['chunks'], 'tiles': res['tuned'] or 'heuristic',
                    'input_batches_rotated': args.batches,
                    'stages': ('network and decode+geometry in order on one stream' if args.serial_geo or args.batches < 2
                               else 'network on the main stream, decode+geometry of the same batch on a second '

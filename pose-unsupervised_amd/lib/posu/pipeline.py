@@ -33,7 +33,7 @@ class MultiViewBatchMeta:
 
 
 class MultiViewPipeline:
-    def __init__(self, model, nviews=4, chunks=1):
+    def __init__(self, model, nviews=4, chunks=None):
         self.model = model
         self.nviews = nviews
         self.chunks = chunks

@@ -283,6 +283,12 @@ CHAIN_LAYERS = True
 # 0.6 % slower on the headline (call r6m: 2.279 vs 2.264 ms; the 2-row NX = 2 tiles halve the layer's
 # last tail's rows per workgroup, which costs what the saved conv1 launch gains), so off
 CHAIN_LAYERS_2B = False
+# round 6: the split dtype's forward runs stem..layer2 and deconv2..head depth-first over two halves
+# of the batch by default (run(chunks=None)): its activations are twice the 2-byte ones, so a half
+# batch's layer1 / layer2 tensors stay in the 256 MiB Infinity Cache between launches -- 5.534 /
+# 5.540 vs 5.556 / 5.632 ms per forward at 32 x 4 (call r6v; 4 chunks 5.67-5.70: the halved grids
+# cost more).  The 2-byte plans measured slower chunked (round 3) and keep 1.
+CHUNKS_F16X3 = 2
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -650,11 +656,22 @@ class PoseResNetPlan:
         return self.stem(x, code)
 
     def _stage_early(self, x, out=None, keep=None):
-        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill)."""
+        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill); layer1's last
+        tail hands layer2's first block its conv1 output as in the whole-batch run (CHAIN_LAYERS)."""
         code = self.code
         x = self.stem_pool(x)
-        x1 = x = self._run_layer(self.layers[0], x, code, out=keep)
-        x = self._run_layer(self.layers[1], x, code, out=out)
+        t1 = None
+        x1 = None
+        for li in (0, 1):
+            layer = self.layers[li]
+            for bi, blk in enumerate(layer):
+                last = bi == len(layer) - 1
+                x, t1 = blk.run(x, code, out=((keep if li == 0 else out) if last else None), t1=t1,
+                                chain_out=last and li == 0)
+            if li == 0:
+                x1 = x
+        if t1 is not None:
+            raise RuntimeError('layer2 produced a chained conv1 output')
         return x, x1
 
     @staticmethod
@@ -691,7 +708,11 @@ class PoseResNetPlan:
     def _block_cout(blk):
         return blk.cout
 
-    def autotune(self, x, chunks=1, keep_features=True, reps=3):
+    def default_chunks(self):
+        """The depth-first slices run(chunks=None) takes: CHUNKS_F16X3 for the split dtype, else 1."""
+        return CHUNKS_F16X3 if self.code == ops.F16X3 else 1
+
+    def autotune(self, x, chunks=None, keep_features=True, reps=3):
         """Time every admissible tile configuration of every conv launch of this forward
         (on the packed input x) and keep the fastest per layer geometry; later runs (and
         hipGraph captures) use the tuned tiles."""
@@ -746,15 +767,18 @@ class PoseResNetPlan:
             _TUNE_CACHE[key] = min(cands, key=lambda t: (res[t], cands.index(t)))
             _REFINE_TIMES[key] = res
 
-    def run(self, x, chunks=1, keep_features=True):
+    def run(self, x, chunks=None, keep_features=True):
         """Packed input -> (heatmaps NCHW f32, layer1 out NHWC, deconv out NHWC).
 
         chunks > 1 runs the HBM-bound ends of the network (stem..layer2 and
         deconv2..head) depth-first over `chunks` slices of the batch, so their
         activations stay resident in the 256 MiB Infinity Cache between producer and
-        consumer; layer3..deconv1 run on the whole batch.  keep_features=False skips
-        materialising the full layer1 / deconv outputs (returned as None)."""
+        consumer; layer3..deconv1 run on the whole batch (None: default_chunks()).
+        keep_features=False skips materialising the full layer1 / deconv outputs
+        (returned as None)."""
         code = self.code
+        if chunks is None:
+            chunks = self.default_chunks()
         n = x.shape[0]
         if chunks <= 1 or n % chunks or len(self.deconvs) < 2:
             x = self.stem_pool(x)

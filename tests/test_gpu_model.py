@@ -124,6 +124,25 @@ def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks):
     torch.testing.assert_close(f1, f0, atol=1e-6, rtol=1e-6)
 
 
+def test_split_plan_runs_chunked_by_default_and_equals_whole_batch(cuda):
+    """fp16x3 (round 6): run() takes plan.CHUNKS_F16X3 = 2 depth-first halves by default, with layer1's
+    last tail chaining layer2's first conv1 inside each half -- heatmaps, layer1 output and deconv
+    features bit-identical to the whole-batch run (every kernel's per-pixel sums are the same)."""
+    from posu import plan as P
+    net = _model(50, 256, 0, 'fp16x3', cuda)
+    views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=6)]
+    plan = net.plan(cuda)
+    assert plan.default_chunks() == P.CHUNKS_F16X3 == 2
+    x = plan.pack_input(views)
+    with torch.no_grad():
+        hm0, x10, f0 = plan.run(x, chunks=1)
+        hm1, x11, f1 = plan.run(x)
+        hm2, _, _ = plan.run(x, keep_features=False)
+    torch.cuda.synchronize()
+    assert torch.equal(hm1, hm0) and torch.equal(hm2, hm0)
+    assert torch.equal(x11, x10) and torch.equal(f1, f0)
+
+
 def test_chunked_run_with_fused_stem_equals_whole_batch(cuda):
     """bf16 at 256x256 hands the views to the fused stem (RawViews); chunked runs slice
     them per chunk (a chunk may cover part of a view) and give the whole-batch result."""
