@@ -421,7 +421,7 @@ class _Block:
             self.xchain = c1n
             self.wsx = pack_tail_stream(self.convs[1].w, self.convs[2].w, c1n.w)
 
-    def run(self, x, code, out=None, t1=None, chain_out=False):
+    def run(self, x, code, out=None, t1=None, chain_out=False, t1n_out=None):
         """-> (y, t1n): t1n = the next block's conv1 output when this block's tail is chained
         (CHAINED_TAILS; chain_out: the last block of a layer chaining the next layer's first conv1,
         CHAIN_LAYERS), else None; t1 = this block's conv1 output from the previous block's
@@ -451,7 +451,7 @@ class _Block:
                 kind in (('l1', 'l2', 'l3') if self.code == ops.F16X3 else ('l2', 'l3')):
             n1 = self.xchain
             return ops.bottleneck_tail_stream_chain_nhwc(t1, x, self.wsx, c2.scale, c2.shift, c3.scale, c3.shift,
-                                                         n1.scale, n1.shift, code, out=out)
+                                                         n1.scale, n1.shift, code, out=out, t1n=t1n_out)
         if self.chain is not None and CHAINED_TAILS and (kind != 'l3w' or TAIL_W24_CHAIN):
             n1 = self.chain
             return ops.bottleneck_tail_stream_next_nhwc(t1, x, self.wsn, c2.scale, c2.shift, c3.scale, c3.shift,
@@ -655,9 +655,11 @@ class PoseResNetPlan:
                 out=out, out_hw=(x.shape[1], x.shape[2]), tile=t))
         return self.stem(x, code)
 
-    def _stage_early(self, x, out=None, keep=None):
-        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill); layer1's last
-        tail hands layer2's first block its conv1 output as in the whole-batch run (CHAIN_LAYERS)."""
+    def _stage_early(self, x, out=None, keep=None, t1_out=None):
+        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill); each layer's last
+        tail hands the next layer's first block its conv1 output as in the whole-batch run
+        (CHAIN_LAYERS): layer1's inside the slice, layer2's into t1_out (the slice of a whole-batch
+        buffer layer3 takes).  Returns (layer2 out, layer1 out, t1_out if layer2's tail filled it)."""
         code = self.code
         x = self.stem_pool(x)
         t1 = None
@@ -667,12 +669,11 @@ class PoseResNetPlan:
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
                 x, t1 = blk.run(x, code, out=((keep if li == 0 else out) if last else None), t1=t1,
-                                chain_out=last and li == 0)
+                                chain_out=last and (li == 0 or t1_out is not None),
+                                t1n_out=t1_out if li == 1 and last else None)
             if li == 0:
                 x1 = x
-        if t1 is not None:
-            raise RuntimeError('layer2 produced a chained conv1 output')
-        return x, x1
+        return x, x1, t1
 
     @staticmethod
     def _run_layer(layer, x, code, out=None):
@@ -808,12 +809,27 @@ class PoseResNetPlan:
         x2 = torch.empty((n, h2, w2, self._block_cout(self.layers[1][-1]) * cm), dtype=dt, device=dev)
         x1 = (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1]) * cm), dtype=dt, device=dev)
               if keep_features else None)
+        # layer3's first conv1, computed by layer2's last tail chunk by chunk (CHAIN_LAYERS), else None
+        l3c1 = self.layers[2][0].convs[0] if len(self.layers) > 2 and self.layers[2][0].convs else None
+        t1 = (torch.empty((n, h2, w2, l3c1.cout * cm), dtype=dt, device=dev)
+              if l3c1 is not None and self.layers[1][-1].xchain is not None else None)
+        chained = []
         for k in range(chunks):
             sl = slice(k * c, (k + 1) * c)
-            self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl])
+            _, _, t1k = self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl],
+                                          t1_out=None if t1 is None else t1[sl])
+            chained.append(t1k is not None)
+        if any(chained) != all(chained):
+            raise RuntimeError('the chunks of one batch took different layer2 tails')
+        t1 = t1 if all(chained) else None
         y = x2
-        for layer in self.layers[2:]:
-            y = self._run_layer(layer, y, code)
+        for li in range(2, len(self.layers)):
+            layer = self.layers[li]
+            for bi, blk in enumerate(layer):
+                last = bi == len(layer) - 1
+                y, t1 = blk.run(y, code, t1=t1, chain_out=last and li + 1 < len(self.layers))
+        if t1 is not None:
+            raise RuntimeError('the last layer produced a chained conv1 output')
         y = self.deconvs[0](y, code)
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)
