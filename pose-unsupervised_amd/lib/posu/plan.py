@@ -285,9 +285,11 @@ CHAIN_LAYERS = True
 CHAIN_LAYERS_2B = False
 # round 6: the split dtype's forward runs stem..layer2 and deconv2..head depth-first over two halves
 # of the batch by default (run(chunks=None)): its activations are twice the 2-byte ones, so a half
-# batch's layer1 / layer2 tensors stay in the 256 MiB Infinity Cache between launches -- 5.534 /
-# 5.540 vs 5.556 / 5.632 ms per forward at 32 x 4 (call r6v; 4 chunks 5.67-5.70: the halved grids
-# cost more).  The 2-byte plans measured slower chunked (round 3) and keep 1.
+# batch's layer1 / layer2 tensors stay in the 256 MiB Infinity Cache between launches; the layers stay
+# chained (layer1 -> layer2 inside a half, layer2 -> layer3 through a whole-batch buffer) -- 5.47-5.64
+# vs 5.60-5.75 ms per forward at 32 x 4 (profiles/r06/chunks_ab_r6vwx.txt; 4 chunks slower: the halved
+# grids cost more).  The bf16 headline measured slower chunked (2.376 / 2.378 vs 2.325 / 2.346 ms) and
+# keeps 1.
 CHUNKS_F16X3 = 2
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
