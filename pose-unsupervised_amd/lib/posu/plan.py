@@ -291,6 +291,10 @@ CHAIN_LAYERS_2B = False
 # grids cost more).  The bf16 headline measured slower chunked (2.376 / 2.378 vs 2.325 / 2.346 ms) and
 # keeps 1.
 CHUNKS_F16X3 = 2
+# which ends of the network a chunked run slices (A/B switches; both by default)
+CHUNK_EARLY = True   # stem..layer2 (EARLY_LAYERS = 1: stem..layer1)
+EARLY_LAYERS = 2
+CHUNK_LATE = True    # deconv2..head
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -657,22 +661,23 @@ class PoseResNetPlan:
                 out=out, out_hw=(x.shape[1], x.shape[2]), tile=t))
         return self.stem(x, code)
 
-    def _stage_early(self, x, out=None, keep=None, t1_out=None):
-        """stem -> maxpool -> layer1 -> layer2 (keep: layer1 output slice to fill); each layer's last
-        tail hands the next layer's first block its conv1 output as in the whole-batch run
-        (CHAIN_LAYERS): layer1's inside the slice, layer2's into t1_out (the slice of a whole-batch
-        buffer layer3 takes).  Returns (layer2 out, layer1 out, t1_out if layer2's tail filled it)."""
+    def _stage_early(self, x, out=None, keep=None, t1_out=None, nl=2):
+        """stem -> maxpool -> layer1 [-> layer2] (nl layers; out: the last one's output slice, keep: layer1
+        output slice to fill when nl = 2); each layer's last tail hands the next layer's first block its
+        conv1 output as in the whole-batch run (CHAIN_LAYERS): inside the slice, and the last early
+        layer's into t1_out (the slice of a whole-batch buffer the next layer takes).  Returns (last early
+        layer's out, layer1 out, t1_out if the last tail filled it)."""
         code = self.code
         x = self.stem_pool(x)
         t1 = None
         x1 = None
-        for li in (0, 1):
+        for li in range(nl):
             layer = self.layers[li]
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
-                x, t1 = blk.run(x, code, out=((keep if li == 0 else out) if last else None), t1=t1,
-                                chain_out=last and (li == 0 or t1_out is not None),
-                                t1n_out=t1_out if li == 1 and last else None)
+                x, t1 = blk.run(x, code, out=((out if li == nl - 1 else keep) if last else None), t1=t1,
+                                chain_out=last and (li < nl - 1 or t1_out is not None),
+                                t1n_out=t1_out if li == nl - 1 and last else None)
             if li == 0:
                 x1 = x
         return x, x1, t1
@@ -808,24 +813,29 @@ class PoseResNetPlan:
         hp, wp = (hs - 1) // 2 + 1, (ws - 1) // 2 + 1          # after maxpool = layer1 grid
         h2, w2 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1          # layer2 grid
         cm = ops.cmul(code)
-        x2 = torch.empty((n, h2, w2, self._block_cout(self.layers[1][-1]) * cm), dtype=dt, device=dev)
-        x1 = (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1]) * cm), dtype=dt, device=dev)
-              if keep_features else None)
-        # layer3's first conv1, computed by layer2's last tail chunk by chunk (CHAIN_LAYERS), else None
-        l3c1 = self.layers[2][0].convs[0] if len(self.layers) > 2 and self.layers[2][0].convs else None
-        t1 = (torch.empty((n, h2, w2, l3c1.cout * cm), dtype=dt, device=dev)
-              if l3c1 is not None and self.layers[1][-1].xchain is not None else None)
+        el = 1 if EARLY_LAYERS == 1 else 2                      # layers in the chunked early stage
+        he, we = (hp, wp) if el == 1 else (h2, w2)
+        x2 = torch.empty((n, he, we, self._block_cout(self.layers[el - 1][-1]) * cm), dtype=dt, device=dev)
+        x1 = x2 if el == 1 else (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1]) * cm), dtype=dt,
+                                             device=dev) if keep_features else None)
+        # the next layer's first conv1, computed by the last early layer's tail chunk by chunk
+        # (CHAIN_LAYERS), else None
+        nc1 = self.layers[el][0].convs[0] if len(self.layers) > el and self.layers[el][0].convs else None
+        t1 = (torch.empty((n, he, we, nc1.cout * cm), dtype=dt, device=dev)
+              if nc1 is not None and self.layers[el - 1][-1].xchain is not None else None)
         chained = []
-        for k in range(chunks):
+        ce = chunks if CHUNK_EARLY else 1
+        c = n // ce
+        for k in range(ce):
             sl = slice(k * c, (k + 1) * c)
-            _, _, t1k = self._stage_early(x[sl], out=x2[sl], keep=None if x1 is None else x1[sl],
-                                          t1_out=None if t1 is None else t1[sl])
+            _, _, t1k = self._stage_early(x[sl], out=x2[sl], keep=None if (x1 is None or el == 1) else x1[sl],
+                                          t1_out=None if t1 is None else t1[sl], nl=el)
             chained.append(t1k is not None)
         if any(chained) != all(chained):
-            raise RuntimeError('the chunks of one batch took different layer2 tails')
+            raise RuntimeError('the chunks of one batch took different tails')
         t1 = t1 if all(chained) else None
         y = x2
-        for li in range(2, len(self.layers)):
+        for li in range(el, len(self.layers)):
             layer = self.layers[li]
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
@@ -836,7 +846,9 @@ class PoseResNetPlan:
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)
         f = (torch.empty((n, hf, wf, self.deconvs[-1].cout * cm), dtype=dt, device=dev) if keep_features else None)
-        for k in range(chunks):
+        cl = chunks if CHUNK_LATE else 1
+        c = n // cl
+        for k in range(cl):
             sl = slice(k * c, (k + 1) * c)
             self._stage_late(y[sl], hm_out=hm[sl], f_out=None if f is None else f[sl], keep_f=f is not None)
-        return hm, x1, f
+        return hm, (x1 if keep_features else None), f

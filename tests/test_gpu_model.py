@@ -107,16 +107,22 @@ def test_pipeline_matches_cpu_oracle(cuda):
     np.testing.assert_allclose(X.cpu().numpy(), Xref, atol=1e-2, rtol=1e-9)
 
 
-@pytest.mark.parametrize('chunks', [2, 4])
-def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks):
+@pytest.mark.parametrize('chunks,early', [(2, 2), (4, 2), (2, 1)])
+def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks, early):
+    from posu import plan as P
     net = _model(50, 128, 0, 'fp32', cuda)
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 128, seed=4)]
     plan = net.plan(cuda)
     x = plan.pack_input(views)
-    with torch.no_grad():
-        hm0, x10, f0 = plan.run(x)
-        hm1, x11, f1 = plan.run(x, chunks=chunks)
-        hm2, x12, f2 = plan.run(x, chunks=chunks, keep_features=False)
+    saved = P.EARLY_LAYERS
+    try:
+        P.EARLY_LAYERS = early   # the chunked early stage: stem..layer2 (2) or stem..layer1 (1)
+        with torch.no_grad():
+            hm0, x10, f0 = plan.run(x)
+            hm1, x11, f1 = plan.run(x, chunks=chunks)
+            hm2, x12, f2 = plan.run(x, chunks=chunks, keep_features=False)
+    finally:
+        P.EARLY_LAYERS = saved
     assert x12 is None and f2 is None
     torch.testing.assert_close(hm1, hm0, atol=1e-6, rtol=1e-6)
     torch.testing.assert_close(hm2, hm0, atol=1e-6, rtol=1e-6)
@@ -124,20 +130,27 @@ def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks):
     torch.testing.assert_close(f1, f0, atol=1e-6, rtol=1e-6)
 
 
-def test_split_plan_runs_chunked_by_default_and_equals_whole_batch(cuda):
-    """fp16x3 (round 6): run() takes plan.CHUNKS_F16X3 = 2 depth-first halves by default, with layer1's
-    last tail chaining layer2's first conv1 inside each half -- heatmaps, layer1 output and deconv
-    features bit-identical to the whole-batch run (every kernel's per-pixel sums are the same)."""
+@pytest.mark.parametrize('early', [2, 1])
+def test_split_plan_runs_chunked_by_default_and_equals_whole_batch(cuda, early):
+    """fp16x3 (round 6): run() takes plan.CHUNKS_F16X3 = 2 depth-first halves by default, the layers'
+    last tails chaining the next layers' first conv1 inside each half and across into the whole-batch
+    part -- heatmaps, layer1 output and deconv features bit-identical to the whole-batch run (every
+    kernel's per-pixel sums are the same)."""
     from posu import plan as P
     net = _model(50, 256, 0, 'fp16x3', cuda)
     views = [v.to(cuda) for v in syn.synthetic_views(4, 2, 256, seed=6)]
     plan = net.plan(cuda)
     assert plan.default_chunks() == P.CHUNKS_F16X3 == 2
     x = plan.pack_input(views)
-    with torch.no_grad():
-        hm0, x10, f0 = plan.run(x, chunks=1)
-        hm1, x11, f1 = plan.run(x)
-        hm2, _, _ = plan.run(x, keep_features=False)
+    saved = P.EARLY_LAYERS
+    try:
+        P.EARLY_LAYERS = early
+        with torch.no_grad():
+            hm0, x10, f0 = plan.run(x, chunks=1)
+            hm1, x11, f1 = plan.run(x)
+            hm2, _, _ = plan.run(x, keep_features=False)
+    finally:
+        P.EARLY_LAYERS = saved
     torch.cuda.synchronize()
     assert torch.equal(hm1, hm0) and torch.equal(hm2, hm0)
     assert torch.equal(x11, x10) and torch.equal(f1, f0)
