@@ -64,13 +64,19 @@ for step in "$@"; do
     bench)
       timeout -k 10 600 python3 -u bench.py $args > "$OUT/$name.json" 2> "$OUT/$name.err" || fail "$step" $?
       summ "$OUT/$name.json" "$name" ;;
+    replay|pmc)
+      # stem runs per forward: --chunks N, else the plan's default (2 for the split dtype's halves)
+      spf=1
+      [[ " $args " == *" fp16x3 "* ]] && spf=2
+      if [[ " $args " =~ " --chunks "([0-9]+)" " ]]; then spf=${BASH_REMATCH[1]}; [ "$spf" -lt 1 ] && spf=1; fi
+      ;;&
     replay)
       timeout -k 10 300 python3 bench.py $LEAN --tune-file "$OUT/${name}_tiles.json" $args \
         > "$OUT/${name}_tune.json" 2> "$OUT/${name}_tune.err" || fail "$step" $?
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${name}_trace" -o run -- \
         python3 bench.py $LEAN --tune-file "$OUT/${name}_tiles.json" --steps 10 --warmup 3 $args \
         > "$OUT/${name}_traced.log" 2>&1 || fail "$step" $?
-      python3 tools/replay_breakdown.py "$OUT/${name}_trace/run_kernel_trace.csv" --last 5 --start stem_pool_kernel \
+      python3 tools/replay_breakdown.py "$OUT/${name}_trace/run_kernel_trace.csv" --last 5 --start stem_pool_kernel --per $spf \
         > "$OUT/${name}_replay_breakdown.txt" || fail "$step" $?
       cp "$OUT/${name}_trace/run_kernel_stats.csv" "$OUT/${name}_kernel_stats.csv" 2>/dev/null
       rm -rf "$OUT/${name}_trace"
@@ -84,7 +90,7 @@ for step in "$@"; do
           > "$OUT/${name}_pmc_$ctr.log" 2>&1 || fail "$step" $?
       done
       POSU_COMMIT=${POSU_COMMIT:-unknown} python3 tools/pmc_traffic.py "$OUT/${name}_pmc_FETCH_SIZE/run_counter_collection.csv" \
-        "$OUT/${name}_pmc_WRITE_SIZE/run_counter_collection.csv" > "$OUT/${name}_pmc_traffic.txt" || fail "$step" $?
+        "$OUT/${name}_pmc_WRITE_SIZE/run_counter_collection.csv" --stems $spf > "$OUT/${name}_pmc_traffic.txt" || fail "$step" $?
       rm -rf "$OUT/${name}_pmc_FETCH_SIZE" "$OUT/${name}_pmc_WRITE_SIZE"
       head -3 "$OUT/${name}_pmc_traffic.txt" ;;
     profile)

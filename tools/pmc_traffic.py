@@ -50,6 +50,9 @@ def main():
     ap.add_argument('write_csv')
     ap.add_argument('launches', nargs='?', type=int, help='launches per forward (default: from the last stem)')
     ap.add_argument('--stem-fetch-scale', type=float, default=2.0)
+    ap.add_argument('--stems', type=int, default=1,
+                    help='runs of stem / input-pack launches per forward (a forward run depth-first over N chunks '
+                         'has N: plan.CHUNKS_F16X3 = 2)')
     a = ap.parse_args()
     fetch = load(a.fetch_csv, 'FETCH_SIZE')
     write = load(a.write_csv, 'WRITE_SIZE')
@@ -57,11 +60,13 @@ def main():
         per_fwd = a.launches
     else:  # the last forward starts at the first input-pack launch of the final run of packs
         names = [x[1] for x in fetch]
-        i = len(names) - 1
-        while i >= 0 and not any(k in names[i] for k in ('pack', 'stem_pool')):
+        i = len(names)
+        for _ in range(a.stems):   # back over --stems runs of stem / pack launches
             i -= 1
-        while i > 0 and any(k in names[i - 1] for k in ('pack', 'stem_pool')):
-            i -= 1
+            while i >= 0 and not any(k in names[i] for k in ('pack', 'stem_pool')):
+                i -= 1
+            while i > 0 and any(k in names[i - 1] for k in ('pack', 'stem_pool')):
+                i -= 1
         per_fwd = len(names) - i
     f = fetch[-per_fwd:]
     w = write[-per_fwd:]

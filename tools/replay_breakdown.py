@@ -27,6 +27,9 @@ def main():
     ap.add_argument('--last', type=int, default=5, help='replays (from the end of the trace) to aggregate')
     ap.add_argument('--start', default='stem_pool_kernel',
                     help='kernel-name substring of a replay\'s first launch(es) (pack_split_kernel: the fp16x3 plan)')
+    ap.add_argument('--per', type=int, default=1,
+                    help='start launches per replay: a forward run depth-first over N chunks starts N stem runs '
+                         '(plan.CHUNKS_F16X3 = 2); each chunk\'s early segment is merged with what follows it')
     a = ap.parse_args()
     st = a.start
     rows = []
@@ -54,6 +57,20 @@ def main():
                 cur.append((s, e, n))
     if cur is not None:
         replays.append(cur)
+    if a.per > 1:
+        # chunked forwards: the early segments of chunks 1 .. N-1 (each shorter than the last chunk's
+        # segment, which runs on through the rest of the network) are merged with the segments after them
+        merged, i = [], 0
+        while i + a.per - 1 < len(replays):
+            grp = replays[i:i + a.per]
+            lens = [len(g) for g in grp]
+            contiguous = all(grp[j + 1][0][0] - grp[j][-1][1] <= 20000 for j in range(a.per - 1))
+            if contiguous and all(l == lens[0] for l in lens[:-1]) and lens[-1] > lens[0]:
+                merged.append([x for g in grp for x in g])
+                i += a.per
+            else:
+                i += 1
+        replays = merged
     if replays:   # complete replays: the most common length
         k = statistics.mode(len(r) for r in replays)
         replays = [r for r in replays if len(r) == k]
