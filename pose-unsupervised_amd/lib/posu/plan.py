@@ -295,6 +295,7 @@ CHUNKS_F16X3 = 2
 CHUNK_EARLY = True   # stem..layer2 (EARLY_LAYERS = 1: stem..layer1)
 EARLY_LAYERS = 2
 CHUNK_LATE = True    # deconv2..head
+LATE_CHUNKS = 0      # > 0: the late stage's own slice count (0: the run's chunks)
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
 
 
@@ -846,7 +847,7 @@ class PoseResNetPlan:
         hf, wf = y.shape[1] * 2 ** (len(self.deconvs) - 1), y.shape[2] * 2 ** (len(self.deconvs) - 1)
         hm = torch.empty((n, self.njoints, hf, wf), dtype=torch.float32, device=dev)
         f = (torch.empty((n, hf, wf, self.deconvs[-1].cout * cm), dtype=dt, device=dev) if keep_features else None)
-        cl = chunks if CHUNK_LATE else 1
+        cl = (LATE_CHUNKS if LATE_CHUNKS > 0 and n % LATE_CHUNKS == 0 else chunks) if CHUNK_LATE else 1
         c = n // cl
         for k in range(cl):
             sl = slice(k * c, (k + 1) * c)
