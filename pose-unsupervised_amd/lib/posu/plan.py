@@ -293,7 +293,7 @@ CHAIN_LAYERS_2B = False
 CHUNKS_F16X3 = 2
 # which ends of the network a chunked run slices (A/B switches; both by default)
 CHUNK_EARLY = True   # stem..layer2 (EARLY_LAYERS = 1: stem..layer1)
-EARLY_LAYERS = 2
+EARLY_LAYERS = 2     # layers in the chunked early stage (1 .. 3)
 CHUNK_LATE = True    # deconv2..head
 LATE_CHUNKS = 0      # > 0: the late stage's own slice count (0: the run's chunks)
 _FUSED_MAX_BYTES = (1 << 31) - 256   # the fused kernels address x / y with 32-bit byte offsets
@@ -676,7 +676,8 @@ class PoseResNetPlan:
             layer = self.layers[li]
             for bi, blk in enumerate(layer):
                 last = bi == len(layer) - 1
-                x, t1 = blk.run(x, code, out=((out if li == nl - 1 else keep) if last else None), t1=t1,
+                dst = out if li == nl - 1 else (keep if li == 0 else None)
+                x, t1 = blk.run(x, code, out=dst if last else None, t1=t1,
                                 chain_out=last and (li < nl - 1 or t1_out is not None),
                                 t1n_out=t1_out if li == nl - 1 and last else None)
             if li == 0:
@@ -812,10 +813,11 @@ class PoseResNetPlan:
         else:
             hs, ws = (x.shape[1] - 1) // 2 + 1, (x.shape[2] - 1) // 2 + 1
         hp, wp = (hs - 1) // 2 + 1, (ws - 1) // 2 + 1          # after maxpool = layer1 grid
-        h2, w2 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1          # layer2 grid
         cm = ops.cmul(code)
-        el = 1 if EARLY_LAYERS == 1 else 2                      # layers in the chunked early stage
-        he, we = (hp, wp) if el == 1 else (h2, w2)
+        el = max(1, min(EARLY_LAYERS, len(self.layers) - 1))   # layers in the chunked early stage
+        he, we = hp, wp
+        for _ in range(el - 1):                                  # layers 2.. halve the grid
+            he, we = (he - 1) // 2 + 1, (we - 1) // 2 + 1
         x2 = torch.empty((n, he, we, self._block_cout(self.layers[el - 1][-1]) * cm), dtype=dt, device=dev)
         x1 = x2 if el == 1 else (torch.empty((n, hp, wp, self._block_cout(self.layers[0][-1]) * cm), dtype=dt,
                                              device=dev) if keep_features else None)

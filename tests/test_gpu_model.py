@@ -107,7 +107,7 @@ def test_pipeline_matches_cpu_oracle(cuda):
     np.testing.assert_allclose(X.cpu().numpy(), Xref, atol=1e-2, rtol=1e-9)
 
 
-@pytest.mark.parametrize('chunks,early', [(2, 2), (4, 2), (2, 1)])
+@pytest.mark.parametrize('chunks,early', [(2, 2), (4, 2), (2, 1), (2, 3)])
 def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks, early):
     from posu import plan as P
     net = _model(50, 128, 0, 'fp32', cuda)
@@ -130,7 +130,7 @@ def test_chunked_depth_first_run_equals_whole_batch(cuda, chunks, early):
     torch.testing.assert_close(f1, f0, atol=1e-6, rtol=1e-6)
 
 
-@pytest.mark.parametrize('early', [2, 1])
+@pytest.mark.parametrize('early', [2, 1, 3])
 def test_split_plan_runs_chunked_by_default_and_equals_whole_batch(cuda, early):
     """fp16x3 (round 6): run() takes plan.CHUNKS_F16X3 = 2 depth-first halves by default, the layers'
     last tails chaining the next layers' first conv1 inside each half and across into the whole-batch
