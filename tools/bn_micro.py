@@ -41,6 +41,8 @@ def main():
     ap.add_argument('--reps', type=int, default=20)
     ap.add_argument('--rounds', type=int, default=3)
     ap.add_argument('--lib', default=None, help='another build of libposeu.so (experiments)')
+    ap.add_argument('--frames', type=int, default=128, help='batch of the shapes (32: one view of the 4)')
+    ap.add_argument('--nseg', type=int, default=NSEG)
     args = ap.parse_args()
     if args.lib:
         from posu import _native
@@ -49,6 +51,7 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     total = 0.0
     for shp in SHAPES:
+        shp = (args.frames,) + tuple(shp[1:])
         c = shp[-1]
         z = torch.randn(shp, device=dev, generator=g).to(torch.bfloat16)
         r = torch.randn(shp, device=dev, generator=g).to(torch.bfloat16)
@@ -56,18 +59,18 @@ def main():
         gamma = torch.rand(c, device=dev) + 0.5
         beta = torch.randn(c, device=dev)
         nb = z.numel() * 2
-        mean, rstd, sc, sh = T.bn_train_fwd(z, NSEG, gamma, beta, 1e-5, 0.1)
-        y = T.bn_apply(z, NSEG, sc, sh, r, True)
-        _, mask = T.bn_apply_mask(z, NSEG, sc, sh, r)
+        mean, rstd, sc, sh = T.bn_train_fwd(z, args.nseg, gamma, beta, 1e-5, 0.1)
+        y = T.bn_apply(z, args.nseg, sc, sh, r, True)
+        _, mask = T.bn_apply_mask(z, args.nseg, sc, sh, r)
         out = torch.empty_like(z)
         cases = [
-            ('stats', lambda: T.bn_train_fwd(z, NSEG, gamma, beta, 1e-5, 0.1), 1),
-            ('apply', lambda: T.bn_apply(z, NSEG, sc, sh, None, True, out=out), 2),
-            ('apply+res', lambda: T.bn_apply(z, NSEG, sc, sh, r, True, out=out), 3),
-            ('bwd(y,gres)', lambda: T.bn_train_bwd(gy, y, z, NSEG, mean, rstd, gamma, want_gres=True), 8),
-            ('bwd(mask,gres)', lambda: T.bn_train_bwd(gy, None, z, NSEG, mean, rstd, gamma, want_gres=True,
+            ('stats', lambda: T.bn_train_fwd(z, args.nseg, gamma, beta, 1e-5, 0.1), 1),
+            ('apply', lambda: T.bn_apply(z, args.nseg, sc, sh, None, True, out=out), 2),
+            ('apply+res', lambda: T.bn_apply(z, args.nseg, sc, sh, r, True, out=out), 3),
+            ('bwd(y,gres)', lambda: T.bn_train_bwd(gy, y, z, args.nseg, mean, rstd, gamma, want_gres=True), 8),
+            ('bwd(mask,gres)', lambda: T.bn_train_bwd(gy, None, z, args.nseg, mean, rstd, gamma, want_gres=True,
                                                       mask=mask), 6),
-            ('bwd(relu_from)', lambda: T.bn_train_bwd(gy, None, z, NSEG, mean, rstd, gamma, relu_from=(sc, sh)), 5),
+            ('bwd(relu_from)', lambda: T.bn_train_bwd(gy, None, z, args.nseg, mean, rstd, gamma, relu_from=(sc, sh)), 5),
         ]
         for name, fn, passes in cases:
             us = timeit(fn, args.reps, args.rounds)
