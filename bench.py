@@ -128,14 +128,14 @@ def parse():
 
 # the plan switches this round added (posu.plan): off, the plan is the previous round's -- the
 # line's `control` legs time it in the same process, so a gain shows on the driver's own box.
-# headline (bf16 R50@256): none this round (round 5's two-K-group tile 39 showed no gain in its control
-# leg and is off, plan.TILES_KSPLIT); parity_mode (fp16x3): round 6's split streamed tails (layer1-3,
+# headline (bf16 R50@256): the two-K-group tile 39 among the tuner's candidates again (plan.TILES_KSPLIT,
+# back on at the end of round 6: 1 % on the headline and configs[1] with this round's plan); parity_mode (fp16x3): round 6's split streamed tails (layer1-3,
 # layer1's down tail, the layers' first conv1 chained), staggered split tiles and the depth-first halves
 # (CHUNKS_F16X3 off: whole batches); configs4 (R152@384 fp16):
 # round 6's layer1 tails at 96-wide maps.
 # (PRECISE_HEAD stays on: it is a precision choice -- +39 us for 2x closer joints -- and the
 # control legs compare the plans at the same numerics)
-CONTROL_FLAGS = ()
+CONTROL_FLAGS = ('TILES_KSPLIT',)
 CONTROL_FLAGS_PARITY = ('SPLIT_TAILS', 'TILES_SPLIT_SG', 'CHUNKS_F16X3')   # (SPLIT_TAILS off also drops CHAIN_LAYERS)
 CONTROL_FLAGS_C4 = ('TAIL_W96',)
 

@@ -88,11 +88,14 @@ class RawViews:
 TILES_128X8 = True
 # the 128x128 tile with two K groups of four waves (39, round 5; inference plans only: its K order
 # differs from the other tiles', and the training plan relies on every candidate summing alike).
-# Off since round 6: no network-level gain on the driver's box (control leg 2.2622 vs 2.2641 ms,
-# BENCH_r05; fp16x3 5.780 / 5.847 vs 5.782 / 5.784 ms, profiles/r06/ksplit_fp16x3_ab_r6e.txt), and
-# without it every candidate tile computes the same sums -- the results no longer depend on which tile
-# the autotuner picks (bitwise reproducible without a fixed --tune-file)
-TILES_KSPLIT = False
+# bf16 / fp16 plans: on again at the end of round 6 -- with this round's plan the headline and configs[1]
+# measured 1 % faster with it (2.237 / 2.250 vs 2.267 / 2.270 ms; 1.331 / 1.327 vs 1.345 / 1.342 ms,
+# profiles/r06/ksplit_bf16_ab_r6ah.txt; round 5's plan showed no gain), and the line's `control` leg times
+# the plan without it.  Where the tuner picks it, the 2-byte plans' last bits depend on the tuned table
+# (reproducible under a fixed --tune-file); the parity mode keeps it out (TILES_KSPLIT_F16X3): every
+# candidate tile of the split dtype sums alike, so its results do not depend on the tuning
+TILES_KSPLIT = True
+TILES_KSPLIT_F16X3 = False
 # the split dtype's staggered eight-wave tiles (31, 47 / 55; round 6) among its autotuner candidates
 TILES_SPLIT_SG = True
 
@@ -135,7 +138,8 @@ def _tile_candidates(cout, code=None, ksplit=False):
         # and (round 6) staggered (47 / 55) eight-wave 128x128 tiles, the staggered 256x128 tile (31) and the
         # two-K-group tile (39)
         return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + (
-            [7, 15] + ([47, 55, 31] if TILES_SPLIT_SG else []) + ([39] if ksplit else []) if cpad % 128 == 0 else [])
+            [7, 15] + ([47, 55, 31] if TILES_SPLIT_SG else []) + ([39] if ksplit and TILES_KSPLIT_F16X3 else [])
+            if cpad % 128 == 0 else [])
     if ksplit and code in (ops.BF16, ops.F16) and cpad % 128 == 0:
         sg = sg + [39]
     return c + [t + 8 for t in c if t <= 4] + [t + 16 for t in c if t != 5] + [t + 32 for t in c if t != 0] + sg
