@@ -144,7 +144,7 @@ def apply_plan_flags(flags):
     from posu import plan as pl, train_plan as tpl
     for f in flags:
         name, _, val = f.partition('=')
-        mod = next((m for m in (pl, tpl) if isinstance(getattr(m, name, None), (bool, int))), None)
+        mod = next((m for m in (pl, tpl) if isinstance(getattr(m, name, None), (bool, int, float))), None)
         if mod is None:
             raise SystemExit('--plan-flag %s: not a switch of posu.plan / posu.train_plan' % f)
         if isinstance(getattr(mod, name), bool):
@@ -152,10 +152,11 @@ def apply_plan_flags(flags):
                 raise SystemExit('--plan-flag %s: a boolean switch takes 0 or 1' % f)
             setattr(mod, name, val == '1')
         else:
+            kind = type(getattr(mod, name))
             try:
-                setattr(mod, name, int(val))
+                setattr(mod, name, kind(val))
             except ValueError:
-                raise SystemExit('--plan-flag %s: an integer switch takes an integer' % f) from None
+                raise SystemExit('--plan-flag %s: a %s switch takes a %s' % (f, kind.__name__, kind.__name__)) from None
 
 
 # ------------------------------------------------------------------ launcher

@@ -106,6 +106,9 @@ _TUNE_TIMES = {}   # geometry key -> {tile: best ms of the reps}, the last tunin
 _REFINE_TIMES = {}  # geometry key -> {tile: ms per whole forward}, the in-context stage's measurements
 # the in-context second tuning stage (PoseResNetPlan._refine_in_context)
 REFINE_IN_CONTEXT = True
+# its candidates: the per-launch times within REFINE_WITHIN of a geometry's best, at most REFINE_TOP of them
+REFINE_WITHIN = 0.25
+REFINE_TOP = 3
 
 
 class _Tuner:
@@ -741,7 +744,7 @@ class PoseResNetPlan:
                 self._refine_in_context(x, chunks, keep_features)
         return out
 
-    def _refine_in_context(self, x, chunks, keep_features, within=0.25, top=3, forwards=6):
+    def _refine_in_context(self, x, chunks, keep_features, within=None, top=None, forwards=6):
         """Second tuning stage: for every geometry of this forward whose best per-launch
         candidates lie within 25 % of each other, run the whole forward with each of its top
         three and keep the one whose launches of that geometry took least INSIDE the forward
@@ -764,6 +767,8 @@ class PoseResNetPlan:
             finally:
                 _Tuner.probe, _Tuner.probe_events = None, []
             return ms[len(ms) // 2] if ms else float('inf')
+        within = REFINE_WITHIN if within is None else within
+        top = REFINE_TOP if top is None else top
         for key in list(_Tuner.seen):
             times = _TUNE_TIMES.get(key)
             if not times or key not in _TUNE_CACHE:
